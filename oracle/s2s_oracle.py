@@ -1,0 +1,614 @@
+"""CPU oracle for the attention-seq2seq ASR training step (forward + backward).
+
+TEST INFRASTRUCTURE ONLY.  Nothing in the product path (`seq2seq-attention-asr_amd/`,
+`libs2s_hip.so`) imports, links or calls this module.  Only `tests/`,
+`__graft_entry__.smoke()` and `bench.py`'s `cpu_baseline` leg use it, and only as
+the checker / the timed CPU baseline.
+
+What it is
+----------
+A NumPy restatement (float64 by default, float32 on request) of the reference's
+Torch7 hot path, module by module, following the Lua sources in
+Ajay-Wong/seq2seq-attention-asr.  Every function cites the reference file:line
+it restates.  The arithmetic of the un-vendored Torch7 packages (`nn`, `nngraph`)
+that those Lua files call is restated from their published semantics (marked 3p):
+`nn.Linear` y = W x + b, W (out, in); `nn.TemporalConvolution` W (out, in*kW);
+`nn.SoftMax` / `nn.LogSoftMax` max-subtracted; `nn.Sigmoid` / `nn.Tanh` backward
+from their outputs; `nn.TemporalMaxPooling` first maximum wins; `nn.Dropout`
+(v2) inverted scaling.  No Torch7 version is pinned by the reference.
+
+Parity status
+-------------
+The reference (Lua/Torch7) cannot run in this container or on the GPU box (no
+`th`/`luajit`/Torch7).  The restatement is pinned by
+  * the reference notebooks' known answers (TemporalConvolution iota layout
+    -> rows of [15, 40, 65, 90]; hybrid-attention padding shapes; the
+    "-sum(labelmask*logprobs) == ClassNLL" loss identity), see
+    tests/test_oracle.py;
+  * the batched-vs-per-utterance identity the notebooks exercise
+    (Attention.ipynb cells 43-44);
+  * an independent PyTorch-CPU autograd formulation of the same forward pass
+    and central finite differences in float64 (tests/test_oracle.py).
+It is NOT pinned against outputs of Torch7 itself: "parity unpinned against
+Torch7" in the sense of the task statement.
+
+Batch semantics
+---------------
+The reference forwards one utterance at a time as a 2-D (L x F) tensor and
+accumulates gradients over `opt.batchSize` utterances, then divides by B
+(timit/timit.lua:240-295).  Here every function takes a leading batch axis B;
+each batch row is computed exactly as the reference computes one utterance
+(rows never interact), so B=1 is the reference's own call and B>1 equals the
+per-utterance loop.
+"""
+from __future__ import annotations
+
+import dataclasses
+from typing import Dict, Optional
+
+import numpy as np
+
+Array = np.ndarray
+
+
+# ----------------------------------------------------------------------------
+# (3p) nn pointwise semantics
+# ----------------------------------------------------------------------------
+
+def sigmoid(x: Array) -> Array:
+    """nn.Sigmoid (3p): 1 / (1 + exp(-x))."""
+    return 1.0 / (1.0 + np.exp(-x))
+
+
+def softmax(x: Array, axis: int = -1) -> Array:
+    """nn.SoftMax (3p): exp(x - max) / sum(exp(x - max))."""
+    m = np.max(x, axis=axis, keepdims=True)
+    e = np.exp(x - m)
+    return e / np.sum(e, axis=axis, keepdims=True)
+
+
+def log_softmax(x: Array, axis: int = -1) -> Array:
+    """nn.LogSoftMax (3p): x - max - log(sum(exp(x - max)))."""
+    m = np.max(x, axis=axis, keepdims=True)
+    return x - m - np.log(np.sum(np.exp(x - m), axis=axis, keepdims=True))
+
+
+# ----------------------------------------------------------------------------
+# LinearZeroBias / TemporalConvolutionZeroBias
+# ----------------------------------------------------------------------------
+
+def linear_zero_bias_fwd(W: Array, x: Array) -> Array:
+    """LinearZeroBias.lua:31-48: y = W x (addmv for 1-D, addmm x W^T for 2-D)."""
+    return x @ W.T
+
+
+def linear_zero_bias_bwd(W: Array, x: Array, dy: Array, dW: Array, scale: float = 1.0) -> Array:
+    """LinearZeroBias.lua:50-74: dx = W^T dy; dW += scale * dy (x) x."""
+    dW += scale * (dy.reshape(-1, dy.shape[-1]).T @ x.reshape(-1, x.shape[-1]))
+    return dy @ W
+
+
+def temporal_conv(W: Array, b: Optional[Array], x: Array, kW: int) -> Array:
+    """nn.TemporalConvolution (3p) with dW=1, no padding, as called by
+    TemporalConvolutionZeroBias.lua:37-40 and Attention.lua:66,90.
+
+    x (..., L_in, inFrame) -> y (..., L_in - kW + 1, outFrame); W is (out, in*kW) with
+    the window laid out frame-major (pinned by Attention.ipynb cells 4-6: weights
+    1..20 row-major on ones(10,5) give rows of [15, 40, 65, 90])."""
+    L_in, fin = x.shape[-2], x.shape[-1]
+    L_out = L_in - kW + 1
+    cols = np.stack([x[..., j:j + L_out, :] for j in range(kW)], axis=-2)  # (..., L_out, kW, fin)
+    cols = cols.reshape(cols.shape[:-2] + (kW * fin,))
+    y = cols @ W.T
+    if b is not None:
+        y = y + b
+    return y
+
+
+# ----------------------------------------------------------------------------
+# GRU cell + nn.RNN unroll
+# ----------------------------------------------------------------------------
+
+def gru_seq_fwd(x: Array, Wz: Array, Wr: Array, Wh: Array, reverse: bool = False,
+                h0: Optional[Array] = None):
+    """nn.RNN(nn.GRU(D, H), reverse) forward.
+
+    GRU.lua:16-38 (cell): hx = [h; x] (h FIRST, :22); z = sig(Wz hx) (:23);
+    r = sig(Wr hx) (:24); hh = tanh(Wh [r*h; x]) (:25-26); h' = (1-z)*h + z*hh (:27-30).
+    No biases (LinearZeroBias).  Recurrent.lua:104-127 supplies zeros for the first
+    prev_h; RNN.lua:120-167 runs t = 1..L, or L..1 when reverse (:142-145), passing
+    y_{t-1} as prev_h.
+
+    x (B, L, D); W* (H, H+D).  Returns y (B, L, H) and the saved activations."""
+    B, L, D = x.shape
+    H = Wz.shape[0]
+    h = np.zeros((B, H), x.dtype) if h0 is None else h0
+    y = np.zeros((B, L, H), x.dtype)
+    sv = {k: np.zeros((B, L, H), x.dtype) for k in ("z", "r", "hh", "hprev")}
+    order = range(L - 1, -1, -1) if reverse else range(L)
+    for t in order:
+        xt = x[:, t]
+        hx = np.concatenate([h, xt], axis=1)
+        z = sigmoid(hx @ Wz.T)
+        r = sigmoid(hx @ Wr.T)
+        rhx = np.concatenate([r * h, xt], axis=1)
+        hh = np.tanh(rhx @ Wh.T)
+        sv["z"][:, t], sv["r"][:, t], sv["hh"][:, t], sv["hprev"][:, t] = z, r, hh, h
+        h = (1.0 - z) * h + z * hh
+        y[:, t] = h
+    return y, sv
+
+
+def gru_seq_bwd(x: Array, Wz: Array, Wr: Array, Wh: Array, sv: Dict[str, Array], dy: Array,
+                grads: Dict[str, Array], reverse: bool = False, scale: float = 1.0):
+    """nn.RNN:updateGradInput (RNN.lua:169-201) over nn.GRU / nn.Recurrent
+    (GRU.lua:45-51 uses only gradOutput[1]; Recurrent.lua:129-151).
+
+    BPTT: dEdy_t += dEdpy from step t+1 (RNN.lua:194); gradInput[t] = dx_t (:196).
+    Weight grads accumulate into grads['Wz'|'Wr'|'Wh'] (LinearZeroBias.lua:67-74).
+    Returns dx (B, L, D) and dh0 (grad w.r.t. the zero initial state)."""
+    B, L, D = x.shape
+    H = Wz.shape[0]
+    dx = np.zeros_like(x)
+    dnext = np.zeros((B, H), x.dtype)
+    order = range(L) if reverse else range(L - 1, -1, -1)
+    for t in order:
+        z, r, hh, hp = sv["z"][:, t], sv["r"][:, t], sv["hh"][:, t], sv["hprev"][:, t]
+        xt = x[:, t]
+        dh = dy[:, t] + dnext
+        dz = dh * (hh - hp)
+        dhh = dh * z
+        dhp = dh * (1.0 - z)
+        dah = dhh * (1.0 - hh * hh)
+        rhx = np.concatenate([r * hp, xt], axis=1)
+        grads["Wh"] += scale * (dah.T @ rhx)
+        drhx = dah @ Wh
+        drh = drhx[:, :H]
+        dxt = drhx[:, H:].copy()
+        dr = drh * hp
+        dhp += drh * r
+        daz = dz * z * (1.0 - z)
+        dar = dr * r * (1.0 - r)
+        hx = np.concatenate([hp, xt], axis=1)
+        grads["Wz"] += scale * (daz.T @ hx)
+        grads["Wr"] += scale * (dar.T @ hx)
+        dhx = daz @ Wz + dar @ Wr
+        dhp += dhx[:, :H]
+        dxt += dhx[:, H:]
+        dx[:, t] = dxt
+        dnext = dhp
+    return dx, dnext
+
+
+# ----------------------------------------------------------------------------
+# LSTM cell + nn.RNN unroll (BiLSTM variant)
+# ----------------------------------------------------------------------------
+
+LSTM_GATES = ("i", "f", "g", "o")
+
+
+def lstm_seq_fwd(x: Array, P: Dict[str, Array], reverse: bool = False, peepholes: bool = False):
+    """nn.RNN(nn.LSTM(D, H, peepholes), reverse) forward.
+
+    LSTM.lua:16-58: each gate is Linear(D,H)(x) + Linear(H,H)(prev_h) [+ Linear(H,H)(c)
+    peephole] with biases (:25-36); in_gate, forget_gate = sig (:42-43, peek prev_c);
+    in2cell = tanh (:44, never peeks); next_c = f*c + i*g (:45-46); out_gate = sig
+    peeking next_c (:47-50); next_h = o * tanh(next_c) (:51).  nn.RNN passes
+    {x, y_{t-1}, h_{t-1}} so prev_h = y_{t-1} and prev_c = the carried cell
+    (RNN.lua:155-163, LSTM.lua:100-116).
+
+    P keys: W{g}x (H,D), b{g}x (H), W{g}h (H,H), b{g}h (H), and W{g}c, b{g}c (H,H)/(H)
+    for g in i,f,o when peepholes."""
+    B, L, D = x.shape
+    H = P["Wix"].shape[0]
+    h = np.zeros((B, H), x.dtype)
+    c = np.zeros((B, H), x.dtype)
+    y = np.zeros((B, L, H), x.dtype)
+    sv = {k: np.zeros((B, L, H), x.dtype) for k in ("i", "f", "g", "o", "c", "cprev", "hprev", "tc")}
+    order = range(L - 1, -1, -1) if reverse else range(L)
+    for t in order:
+        xt = x[:, t]
+
+        def pre(gname, peek):
+            a = xt @ P[f"W{gname}x"].T + P[f"b{gname}x"] + h @ P[f"W{gname}h"].T + P[f"b{gname}h"]
+            if peepholes and peek is not None:
+                a = a + peek @ P[f"W{gname}c"].T + P[f"b{gname}c"]
+            return a
+
+        i = sigmoid(pre("i", c))
+        f = sigmoid(pre("f", c))
+        g = np.tanh(pre("g", None))
+        cn = f * c + i * g
+        o = sigmoid(pre("o", cn))
+        tc = np.tanh(cn)
+        hn = o * tc
+        for k, v in (("i", i), ("f", f), ("g", g), ("o", o), ("c", cn), ("cprev", c), ("hprev", h), ("tc", tc)):
+            sv[k][:, t] = v
+        h, c = hn, cn
+        y[:, t] = h
+    return y, sv
+
+
+def lstm_seq_bwd(x: Array, P: Dict[str, Array], sv: Dict[str, Array], dy: Array,
+                 grads: Dict[str, Array], reverse: bool = False, peepholes: bool = False,
+                 scale: float = 1.0):
+    """LSTM:updateGradInput (LSTM.lua:118-136) under nn.RNN's BPTT (RNN.lua:169-201):
+    dEdh = dy_t + d prev_h from t+1, dEdc = d prev_c from t+1."""
+    B, L, D = x.shape
+    H = P["Wix"].shape[0]
+    dx = np.zeros_like(x)
+    dh_next = np.zeros((B, H), x.dtype)
+    dc_next = np.zeros((B, H), x.dtype)
+    order = range(L) if reverse else range(L - 1, -1, -1)
+    for t in order:
+        i, f, g, o = sv["i"][:, t], sv["f"][:, t], sv["g"][:, t], sv["o"][:, t]
+        cn, cp, hp, tc = sv["c"][:, t], sv["cprev"][:, t], sv["hprev"][:, t], sv["tc"][:, t]
+        xt = x[:, t]
+        dh = dy[:, t] + dh_next
+        do = dh * tc
+        dcn = dc_next + dh * o * (1.0 - tc * tc)
+        dao = do * o * (1.0 - o)
+        dxt = np.zeros_like(xt)
+        dhp = np.zeros_like(hp)
+        dcp = np.zeros_like(cp)
+
+        def acc(gname, da, peek_val):
+            nonlocal dxt, dhp
+            grads[f"W{gname}x"] += scale * (da.T @ xt)
+            grads[f"b{gname}x"] += scale * da.sum(0)
+            grads[f"W{gname}h"] += scale * (da.T @ hp)
+            grads[f"b{gname}h"] += scale * da.sum(0)
+            dxt = dxt + da @ P[f"W{gname}x"]
+            dhp = dhp + da @ P[f"W{gname}h"]
+            if peepholes and peek_val is not None:
+                grads[f"W{gname}c"] += scale * (da.T @ peek_val)
+                grads[f"b{gname}c"] += scale * da.sum(0)
+                return da @ P[f"W{gname}c"]
+            return None
+
+        dpeek = acc("o", dao, cn)
+        if dpeek is not None:
+            dcn = dcn + dpeek
+        di = dcn * g
+        df = dcn * cp
+        dg = dcn * i
+        dcp = dcp + dcn * f
+        dai = di * i * (1.0 - i)
+        daf = df * f * (1.0 - f)
+        dag = dg * (1.0 - g * g)
+        for gname, da in (("i", dai), ("f", daf)):
+            dpk = acc(gname, da, cp)
+            if dpk is not None:
+                dcp = dcp + dpk
+        acc("g", dag, None)
+        dx[:, t] = dxt
+        dh_next, dc_next = dhp, dcp
+    return dx
+
+
+# ----------------------------------------------------------------------------
+# Bidirectional encoder (timit/model_chorowski_baseline.lua:20-34)
+# ----------------------------------------------------------------------------
+
+def encoder_fwd(x: Array, P: Dict[str, Array], nlayers: int = 3):
+    """3 x [fwd GRU || bwd GRU] joined on features, fwd first (JoinTable(2,2),
+    model_chorowski_baseline.lua:24,28,32)."""
+    caches = []
+    inp = x
+    for l in range(1, nlayers + 1):
+        yf, svf = gru_seq_fwd(inp, P[f"enc{l}f.Wz"], P[f"enc{l}f.Wr"], P[f"enc{l}f.Wh"], False)
+        yb, svb = gru_seq_fwd(inp, P[f"enc{l}b.Wz"], P[f"enc{l}b.Wr"], P[f"enc{l}b.Wh"], True)
+        caches.append((inp, svf, svb))
+        inp = np.concatenate([yf, yb], axis=2)
+    return inp, caches
+
+
+def encoder_bwd(P: Dict[str, Array], caches, dout: Array, G: Dict[str, Array], scale: float = 1.0):
+    d = dout
+    for l in range(len(caches), 0, -1):
+        inp, svf, svb = caches[l - 1]
+        H = P[f"enc{l}f.Wz"].shape[0]
+        gf = {k: G[f"enc{l}f.{k}"] for k in ("Wz", "Wr", "Wh")}
+        gb = {k: G[f"enc{l}b.{k}"] for k in ("Wz", "Wr", "Wh")}
+        dxf, _ = gru_seq_bwd(inp, P[f"enc{l}f.Wz"], P[f"enc{l}f.Wr"], P[f"enc{l}f.Wh"], svf, d[:, :, :H], gf, False, scale)
+        dxb, _ = gru_seq_bwd(inp, P[f"enc{l}b.Wz"], P[f"enc{l}b.Wr"], P[f"enc{l}b.Wh"], svb, d[:, :, H:], gb, True, scale)
+        d = dxf + dxb
+    return d
+
+
+# ----------------------------------------------------------------------------
+# Attention decoder (Attention.lua + RNNAttention.lua + MonotonicAlignment.lua)
+# ----------------------------------------------------------------------------
+
+def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfig",
+                  dropout_mask: Optional[Array] = None):
+    """nn.Attention:updateOutput (Attention.lua:305-322) = decoder gModule
+    {h, labelmask} -> RNNAttention over T steps (RNNAttention.lua:144-185).
+
+    h (B, L, A) annotations; labels (B, T) int in [0, O) (0-based; the reference is
+    1-based).  Teacher forcing: prev_y = zeros at t=1, else onehot(labels[t-1])
+    (RNNAttention.lua:172-176).  Hidden carried = {alpha, s, mem}, zeros at t=1
+    (Recurrent.lua:79-112 with dimhidden {L, S, S}, Attention.lua:318).
+
+    Per step (decoder_base_, Attention.lua:51-184):
+      ws = Ws s + bs            TemporalConvolution(1,Sc,S) on View(S,1) (:65-66)
+      Z = expand_L(ws) + Vh      ExpandAs + CAddTable (:67,98)  [hybrid off]
+      e = we . tanh(Z)           TCZB(Sc,1,1) (:104-110)
+      alpha = softmax_L(e)       (:117)
+      alpha = MonoAlign(alpha, alpha_prev) identity fwd (:122-125, MonotonicAlignment.lua:19-42)
+      c = alpha^T h              Replicate + MM + View (:132-134)
+      y_in = Wy y + by; c_in = Wc c + bc; d = Wd [c_in; y_in] + bd   (:149-151)
+      s = GRU(d, s_prev)         decoder_recurrent (model_chorowski_baseline.lua:48-51)
+      logp = LogSoftMax(Wo Maxout([s; c]) + bo)   decoder_mlp (:53-59, Maxout.lua:14-18)
+    Vh = h V^T once per utterance (TCZB(A, Sc, 1), Attention.lua:43-47,202)."""
+    B, L, A = h.shape
+    T = labels.shape[1]
+    S, Sc, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    dt = h.dtype
+    Vh = temporal_conv(P["V"], None, h, 1)                      # (B, L, Sc)
+    s = np.zeros((B, S), dt)
+    alpha_prev = np.zeros((B, L), dt)
+    cache = {key: [] for key in ("ws", "alpha", "c", "cin", "yin", "d", "sprev", "mono_ind",
+                                 "z", "r", "hh", "u", "argmax", "m", "logp", "v", "alpha_prev")}
+    logp_all = np.zeros((B, T, O), dt)
+    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    for t in range(T):
+        yprev = np.zeros((B, O), dt)
+        if t > 0:
+            yprev[np.arange(B), labels[:, t - 1]] = 1.0
+        ws = s @ P["Ws"].T + P["bs"]                               # (B, Sc)
+        Z = ws[:, None, :] + Vh
+        th = np.tanh(Z)
+        e = (th @ P["we"].T)[..., 0]                               # (B, L)
+        alpha = softmax(e, axis=1)
+        # MonotonicAlignment.lua:27-39: penalty = lambda * max(sum_j(cumsum a - cumsum a_prev), 0)
+        diff = np.sum(np.cumsum(alpha, 1) - np.cumsum(alpha_prev, 1), axis=1)
+        pen = cfg.penalty * np.maximum(diff, 0.0)
+        ind = (pen > 0).astype(dt)
+        c = np.einsum("bl,bla->ba", alpha, h)
+        yin = yprev @ P["Wy"].T + P["by"]
+        cin = c @ P["Wc"].T + P["bc"]
+        d = np.concatenate([cin, yin], 1) @ P["Wd"].T + P["bd"]
+        hx = np.concatenate([s, d], 1)
+        z = sigmoid(hx @ Wg["z"].T)
+        r = sigmoid(hx @ Wg["r"].T)
+        hh = np.tanh(np.concatenate([r * s, d], 1) @ Wg["h"].T)
+        s_new = (1.0 - z) * s + z * hh
+        v = np.concatenate([s_new, c], 1)
+        if dropout_mask is not None:
+            v = v * dropout_mask[:, t]
+        u = v @ P["Wm"].T + P["bm"]
+        ug = u.reshape(B, M, k)
+        am = np.argmax(ug, axis=2)                                 # first max wins
+        m = np.take_along_axis(ug, am[..., None], 2)[..., 0]
+        o = m @ P["Wo"].T + P["bo"]
+        logp = log_softmax(o, 1)
+        logp_all[:, t] = logp
+        for key, val in (("ws", ws), ("alpha", alpha), ("c", c), ("cin", cin), ("yin", yin), ("d", d),
+                         ("sprev", s), ("mono_ind", ind), ("z", z), ("r", r), ("hh", hh), ("u", u),
+                         ("argmax", am), ("m", m), ("logp", logp), ("v", v), ("alpha_prev", alpha_prev)):
+            cache[key].append(val)
+        s = s_new
+        alpha_prev = alpha
+    cache = {key: np.stack(vals, 1) for key, vals in cache.items()}
+    cache["Vh"] = Vh
+    cache["h"] = h
+    cache["labels"] = labels
+    return logp_all, cache
+
+
+def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, G: Dict[str, Array],
+                  scale: float = 1.0, dropout_mask: Optional[Array] = None):
+    """nn.Attention:updateGradInput (Attention.lua:324-327): RNNAttention's reverse BPTT
+    (RNNAttention.lua:203-253) accumulating d{Vh, h} over all t (:247); dy discarded
+    (:248).  MonotonicAlignment.lua:44-77 adds lambda*(L+1-j)*ind to d alpha and its
+    negation to d alpha_prev.  Returns dh (B, L, A)."""
+    h, Vh, labels = cache["h"], cache["Vh"], cache["labels"]
+    B, L, A = h.shape
+    T = dlogp.shape[1]
+    S, Sc, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    dt = h.dtype
+    dh = np.zeros_like(h)
+    dVh = np.zeros_like(Vh)
+    ds_carry = np.zeros((B, S), dt)
+    dalpha_carry = np.zeros((B, L), dt)
+    jw = (L + 1 - np.arange(1, L + 1)).astype(dt)               # (L+1-j), j 1-based
+    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    for t in range(T - 1, -1, -1):
+        g_ = lambda key: cache[key][:, t]
+        logp = g_("logp")
+        # LogSoftMax backward (3p): do = dlogp - exp(logp) * sum(dlogp)
+        dl = dlogp[:, t]
+        do = dl - np.exp(logp) * dl.sum(1, keepdims=True)
+        G["Wo"] += scale * (do.T @ g_("m"))
+        G["bo"] += scale * do.sum(0)
+        dm = do @ P["Wo"]
+        du = np.zeros((B, M * k), dt)
+        idx = np.arange(M) * k + g_("argmax")
+        np.put_along_axis(du, idx, dm, axis=1)
+        v = g_("v")
+        G["Wm"] += scale * (du.T @ v)
+        G["bm"] += scale * du.sum(0)
+        dv = du @ P["Wm"]
+        if dropout_mask is not None:
+            dv = dv * dropout_mask[:, t]
+        ds = dv[:, :S] + ds_carry
+        dc = dv[:, S:].copy()
+        # decoder GRU backward (GRU.lua:16-38), x = d, h = s_prev
+        sp, d, z, r, hh = g_("sprev"), g_("d"), g_("z"), g_("r"), g_("hh")
+        dz = ds * (hh - sp)
+        dah = ds * z * (1 - hh * hh)
+        dsp = ds * (1 - z)
+        rhx = np.concatenate([r * sp, d], 1)
+        G["dec.Wh"] += scale * (dah.T @ rhx)
+        drhx = dah @ Wg["h"]
+        dd = drhx[:, S:].copy()
+        dr = drhx[:, :S] * sp
+        dsp += drhx[:, :S] * r
+        daz = dz * z * (1 - z)
+        dar = dr * r * (1 - r)
+        hx = np.concatenate([sp, d], 1)
+        G["dec.Wz"] += scale * (daz.T @ hx)
+        G["dec.Wr"] += scale * (dar.T @ hx)
+        dhx = daz @ Wg["z"] + dar @ Wg["r"]
+        dsp += dhx[:, :S]
+        dd += dhx[:, S:]
+        # d = Wd [c_in; y_in] + bd
+        cin, yin = g_("cin"), g_("yin")
+        G["Wd"] += scale * (dd.T @ np.concatenate([cin, yin], 1))
+        G["bd"] += scale * dd.sum(0)
+        dcy = dd @ P["Wd"]
+        dcin, dyin = dcy[:, :S], dcy[:, S:]
+        c = g_("c")
+        G["Wc"] += scale * (dcin.T @ c)
+        G["bc"] += scale * dcin.sum(0)
+        dc += dcin @ P["Wc"]
+        yprev = np.zeros((B, O), dt)
+        if t > 0:
+            yprev[np.arange(B), labels[:, t - 1]] = 1.0
+        G["Wy"] += scale * (dyin.T @ yprev)
+        G["by"] += scale * dyin.sum(0)
+        # c = alpha^T h
+        alpha = g_("alpha")
+        dalpha = np.einsum("ba,bla->bl", dc, h) + dalpha_carry
+        dh += alpha[:, :, None] * dc[:, None, :]
+        # MonotonicAlignment backward
+        gdiff = cfg.penalty * jw[None, :] * g_("mono_ind")[:, None]
+        dalpha = dalpha + gdiff
+        dalpha_carry = -gdiff
+        # softmax backward (3p)
+        de = alpha * (dalpha - np.sum(alpha * dalpha, 1, keepdims=True))
+        ws = g_("ws")
+        th = np.tanh(ws[:, None, :] + Vh)
+        G["we"] += scale * np.einsum("bl,blk->k", de, th)[None, :]
+        dZ = de[:, :, None] * P["we"][0][None, None, :] * (1 - th * th)
+        dVh += dZ
+        dws = dZ.sum(1)
+        G["Ws"] += scale * (dws.T @ sp)
+        G["bs"] += scale * dws.sum(0)
+        ds_carry = dsp + dws @ P["Ws"]
+    # Vh = h V^T  (TCZB k=1)
+    G["V"] += scale * np.einsum("bls,bla->sa", dVh, h)
+    dh += dVh @ P["V"]
+    return dh
+
+
+# ----------------------------------------------------------------------------
+# Model config, init, full training step (timit/timit.lua:240-295)
+# ----------------------------------------------------------------------------
+
+@dataclasses.dataclass
+class ModelConfig:
+    """Mirrors loadmodel(opt) field names (timit/model_chorowski_baseline.lua:14-46)."""
+    inputFrameSize: int = 123
+    hiddenFrameSize: int = 256
+    outputFrameSize: int = 256
+    scoreDepth: int = 512
+    stateDepth: int = 256
+    outputDepth: int = 62          # opt.numPhonemes (TIMIT) / opt.outputDepth (LibriSpeech)
+    mlpDepth: int = 64
+    maxoutWindow: int = 7          # Maxout(..., 7) (model_chorowski_baseline.lua:56)
+    penalty: float = 0.0           # MonotonicAlignment lambda
+    numLayers: int = 3
+
+    @property
+    def annotationDepth(self) -> int:
+        return 2 * self.outputFrameSize
+
+
+def param_shapes(cfg: ModelConfig):
+    """Canonical parameter list, in flat-buffer order (see DESIGN.md §Data layout)."""
+    shapes = []
+    D = cfg.inputFrameSize
+    for l in range(1, cfg.numLayers + 1):
+        H = cfg.outputFrameSize if l == cfg.numLayers else cfg.hiddenFrameSize
+        for dname in ("f", "b"):
+            for g in ("Wz", "Wr", "Wh"):
+                shapes.append((f"enc{l}{dname}.{g}", (H, H + D)))
+        D = 2 * H
+    A, Sc, S, O, M, k = cfg.annotationDepth, cfg.scoreDepth, cfg.stateDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    shapes += [("V", (Sc, A)), ("Ws", (Sc, S)), ("bs", (Sc,)), ("we", (1, Sc)),
+               ("Wy", (S, O)), ("by", (S,)), ("Wc", (S, A)), ("bc", (S,)),
+               ("Wd", (S, 2 * S)), ("bd", (S,)),
+               ("dec.Wz", (S, 2 * S)), ("dec.Wr", (S, 2 * S)), ("dec.Wh", (S, 2 * S)),
+               ("Wm", (M * k, S + A)), ("bm", (M * k,)), ("Wo", (O, M)), ("bo", (O,))]
+    return shapes
+
+
+def fan_in(name: str, shape, cfg: ModelConfig) -> int:
+    """Default reset() stdv = 1/sqrt(fan_in): LinearZeroBias.lua:12-29 (in),
+    TemporalConvolutionZeroBias.lua:21-35 (kW*inFrame), nn.Linear / nn.TemporalConvolution (3p)."""
+    S, Sc, A, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.annotationDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    table = {"V": A, "Ws": S, "bs": S, "we": Sc, "Wy": O, "by": O, "Wc": A, "bc": A, "Wd": 2 * S, "bd": 2 * S,
+             "Wm": S + A, "bm": S + A, "Wo": M, "bo": M}
+    if name in table:
+        return table[name]
+    return shape[1]
+
+
+def init_params(cfg: ModelConfig, seed: int = 1234, dtype=np.float64) -> Dict[str, Array]:
+    rng = np.random.default_rng(seed)
+    P = {}
+    for name, shape in param_shapes(cfg):
+        stdv = 1.0 / np.sqrt(fan_in(name, shape, cfg))
+        P[name] = rng.uniform(-stdv, stdv, size=shape).astype(dtype)
+    return P
+
+
+def zeros_like_params(P: Dict[str, Array]) -> Dict[str, Array]:
+    return {k: np.zeros_like(v) for k, v in P.items()}
+
+
+def flatten(P: Dict[str, Array], cfg: ModelConfig) -> Array:
+    return np.concatenate([P[n].reshape(-1) for n, _ in param_shapes(cfg)])
+
+
+def unflatten(flat: Array, cfg: ModelConfig) -> Dict[str, Array]:
+    out, off = {}, 0
+    for n, shp in param_shapes(cfg):
+        sz = int(np.prod(shp))
+        out[n] = flat[off:off + sz].reshape(shp)
+        off += sz
+    assert off == flat.size
+    return out
+
+
+def training_step(x: Array, labels: Array, P: Dict[str, Array], cfg: ModelConfig,
+                  normalizeNLL: bool = True, dropout_mask: Optional[Array] = None):
+    """timit/timit.lua:240-295 for one optimizer step's gradient, B utterances of
+    equal length: per utterance logp = fwd({X, onehot(Y)}) (:262-265);
+    nll_b = -sum(onehot * logp) [/T] (:268-272, reporting only); dlogp = -onehot (:278);
+    backward accumulates; then nll /= B and grad /= B when B > 1 (:292-295).
+    Returns (nll, grads dict, logp, enc_out)."""
+    B, L, F = x.shape
+    T = labels.shape[1]
+    O = cfg.outputDepth
+    enc, ecache = encoder_fwd(x, P, cfg.numLayers)
+    logp, acache = attention_fwd(enc, labels, P, cfg, dropout_mask)
+    onehot = np.zeros((B, T, O), x.dtype)
+    np.put_along_axis(onehot, labels[..., None], 1.0, axis=2)
+    nll_b = -(onehot * logp).sum((1, 2))
+    if normalizeNLL:
+        nll_b = nll_b / T
+    scale = 1.0 / B if B > 1 else 1.0
+    G = zeros_like_params(P)
+    denc = attention_bwd(P, cfg, acache, -onehot, G, scale, dropout_mask)
+    encoder_bwd(P, ecache, denc, G, scale)
+    return float(nll_b.mean()), G, logp, enc
+
+
+def synthetic_batch(cfg: ModelConfig, B: int, L: int, T: int, seed: int = 1234, pad: int = 10,
+                    eos: int = 23, dtype=np.float64):
+    """x ~ N(0,1), zero pad frames each side (timit/preprocess_timit.py:274-276);
+    labels uniform over non-EOS classes, last label = EOS (TIMIT EOS = 24 1-based,
+    timit/phonemes.txt:25 -> 23 0-based)."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((B, L, cfg.inputFrameSize)).astype(dtype)
+    if pad > 0 and L > 2 * pad:
+        x[:, :pad] = 0
+        x[:, L - pad:] = 0
+    O = cfg.outputDepth
+    choices = np.array([c for c in range(O) if c != eos])
+    labels = choices[rng.integers(0, len(choices), size=(B, T))]
+    labels[:, -1] = eos
+    return x, labels.astype(np.int32)
