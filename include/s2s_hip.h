@@ -1,0 +1,135 @@
+/* libs2s_hip.so -- MI355X (gfx950) drop-in for the hot path of
+ * Ajay-Wong/seq2seq-attention-asr: the attention-seq2seq training step, forward + backward.
+ *
+ * C ABI only: plain pointers, sizes and an opaque HIP stream; no torch types.  It is what
+ * a LuaJIT `ffi.cdef` shim binds in place of the Torch7 nn.Module methods it replaces
+ * (see INTEGRATION.md), and what the Python ctypes host layer (seq2seq-attention-asr_amd/s2s_amd)
+ * binds in this repo's tests and bench.
+ *
+ * Conventions:
+ *   - every buffer is a caller-owned DEVICE pointer, fp32 unless stated, row-major;
+ *   - utterances of a call share one length L (and T); the batch axis is leading:
+ *     x (B, L, F), h (B, L, A), labels (B, T) int32, 0-based class ids;
+ *   - weight layouts are the reference's: W (out, in) row-major (LinearZeroBias.lua:8,
+ *     nn.Linear, TemporalConvolution (out, in*kW));
+ *   - gradients ACCUMULATE (dW += scale * ...), as Torch's accGradParameters; zero them
+ *     yourself (zeroGradParameters) or pass S2S_ZERO_GRADS to the model step;
+ *   - calls return 0 on success, nonzero on error, never abort; s2s_last_error() has the text;
+ *   - `stream` is a hipStream_t (NULL = legacy default stream); calls are asynchronous on it
+ *     and allocate nothing (scratch/saved buffers come from the caller, sized by the *_bytes
+ *     queries);
+ *   - one context per process/GPU; a context is not thread-safe.
+ */
+#ifndef S2S_HIP_H_
+#define S2S_HIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct s2s_ctx s2s_ctx;
+typedef void* s2s_stream_t; /* hipStream_t */
+
+/* ---------------------------------------------------------------- context */
+int s2s_version(void);
+const char* s2s_last_error(void);
+int s2s_ctx_create(int device, s2s_ctx** out);
+void s2s_ctx_destroy(s2s_ctx* ctx);
+/* flags: S2S_CTX_GRAPH = capture the model step into a hipGraph and replay it when the
+ * dims / pointers repeat (the step is ~2000 dependent launches). */
+#define S2S_CTX_GRAPH 1
+int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
+
+/* ---------------------------------------------------------------- GRU layer
+ * nn.RNN(nn.GRU(D, H), reverse)  (RNN.lua:120-201, GRU.lua:16-51, Recurrent.lua:104-151).
+ * ndir = 1: one nn.RNN.  ndir = 2: the two directions of a bidirectional encoder layer that read
+ * the same x (timit/model_chorowski_baseline.lua:22-32) in the same launches; W[d*3 + g] is
+ * direction d's gate g in (z, r, h) order, each (H, H+D) with columns [h | x] (GRU.lua:22).
+ * y[d] rows: y[d][(b*L + t)*ldy + j]; ldy = 2H with y[1] = y[0] + H reproduces JoinTable(2,2).
+ * saved[d]: s2s_gru_saved_bytes(B, L, H) each, written by fwd and read by bwd.           */
+size_t s2s_gru_saved_bytes(int B, int L, int H);
+size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H);
+int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
+                const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved,
+                void* scratch, size_t scratch_bytes);
+/* dy[d] rows with stride lddy; dx (may be NULL) = sum over directions, overwritten unless
+ * dx_accumulate; dW[d*3+g] += scale * ...  (LinearZeroBias.lua:50-74)                      */
+int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
+                const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy,
+                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch,
+                size_t scratch_bytes);
+
+/* ---------------------------------------------------------------- attention decoder
+ * nn.Attention(decoder_recurrent = GRU(S,S), decoder_mlp = Maxout(S+A, M, K) -> Linear(M, O)
+ * -> LogSoftMax, scoreDepth Sc, hybrid off, stateDepth S, annotationDepth A, outputDepth O,
+ * monoAlignPenalty true, penaltyLambda) -- Attention.lua:15-211, RNNAttention.lua:144-253,
+ * MonotonicAlignment.lua, Maxout.lua, timit/model_chorowski_baseline.lua:37-70.
+ * Parameter pointers, in this order (W = (out, in)):
+ *   0 V (Sc, A)  [Vh TCZB]     1 Ws (Sc, S)  2 bs (Sc)   [TemporalConvolution(1, Sc, S)]
+ *   3 we (1, Sc) [e TCZB]      4 Wy (S, O)   5 by (S)    6 Wc (S, A)   7 bc (S)
+ *   8 Wd (S, 2S) 9 bd (S)     10 Wz (S, 2S) 11 Wr (S, 2S) 12 Wh (S, 2S)   [decoder GRU]
+ *  13 Wm (M*K, S+A) 14 bm (M*K)   15 Wo (O, M) 16 bo (O)                                     */
+#define S2S_ATTN_NPARAMS 17
+typedef struct {
+  int B, L, T;
+  int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
+  float penalty;
+} s2s_attn_dims;
+size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
+size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
+/* Attention:updateOutput (Attention.lua:305-322): h (B, L, A), labels (B, T) -> logp (B, T, O) */
+int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
+                 const float* const* params, float* logp, void* saved, void* scratch, size_t scratch_bytes);
+/* Attention:updateGradInput (Attention.lua:324-327) + accGradParameters: dlogp (B, T, O) -> dh (B, L, A) */
+int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
+                 const float* const* params, const void* saved, const float* dlogp, float* dh, int dh_accumulate,
+                 float* const* grads, float scale, void* scratch, size_t scratch_bytes);
+/* decoder:alpha() (Attention.lua:241-243): device pointer to alpha (B, T, L) inside `saved` */
+const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
+
+/* ---------------------------------------------------------------- loss seed
+ * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
+ * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).       */
+int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,
+                 int normalize, float* nll, float* dlogp);
+
+/* ---------------------------------------------------------------- whole training step
+ * autoencoder:forward({X, labelmask}); nll; autoencoder:backward({X, labelmask}, -labelmask)
+ * for a batch of B equal-length utterances (timit/timit.lua:240-295), flat parameter and
+ * gradient buffers (timit.lua:172 getParameters).  Flat layout: see s2s_model_param_offset
+ * and DESIGN.md.                                                                             */
+typedef struct {
+  int B, L, T;
+  int inputFrameSize, hiddenFrameSize, outputFrameSize, numLayers;
+  int scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
+  float penalty;
+} s2s_model_dims;
+#define S2S_ZERO_GRADS 1
+#define S2S_NORMALIZE_NLL 2
+size_t s2s_model_param_count(const s2s_model_dims* d);
+/* offset (in floats) of parameter #i of the flat layout and its element count; -1 past the end */
+long s2s_model_param_offset(const s2s_model_dims* d, int i, long* numel);
+size_t s2s_model_workspace_bytes(const s2s_model_dims* d);
+/* grads (+)= scale * dL/dparams; logp (B, T, O) and nll (B) are outputs (may be NULL). */
+int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, const float* params, float* grads,
+                   const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
+                   void* workspace, size_t workspace_bytes);
+/* encoder output (the annotations h, B x L x 2*outputFrameSize) of the last step, inside workspace
+ * (encoder.output, timit/timit.lua:397). */
+const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace);
+
+/* ---------------------------------------------------------------- data parallel (RCCL)
+ * One process per GPU.  Rank 0 calls s2s_comm_unique_id, the bytes are shared out of band,
+ * every rank calls s2s_comm_init; s2s_allreduce_sum sums a float buffer in place over xGMI. */
+#define S2S_UNIQUE_ID_BYTES 128
+int s2s_comm_unique_id(void* out_bytes);
+int s2s_comm_init(s2s_ctx* ctx, const void* id_bytes, int nranks, int rank);
+int s2s_allreduce_sum(s2s_ctx* ctx, s2s_stream_t stream, float* buf, size_t count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* S2S_HIP_H_ */

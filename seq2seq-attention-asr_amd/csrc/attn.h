@@ -1,0 +1,45 @@
+#pragma once
+#include "s2s_common.h"
+
+namespace s2s {
+
+// Attention decoder dims: nn.Attention(decoder_recurrent, decoder_mlp, scoreDepth, ...,
+// stateDepth, annotationDepth, outputDepth, monoAlignPenalty, penaltyLambda)
+// (Attention.lua:15-24) with the Chorowski decoder_recurrent = GRU(S,S) and
+// decoder_mlp = Maxout(S+A, M, K) -> Linear(M, O) -> LogSoftMax
+// (timit/model_chorowski_baseline.lua:48-59).
+struct AttnDims {
+  int B, L, T;
+  int A;   // annotationDepth
+  int Sc;  // scoreDepth
+  int S;   // stateDepth
+  int O;   // outputDepth
+  int M;   // mlpDepth
+  int K;   // maxout window
+  float penalty;
+};
+struct AttnParams {
+  const float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
+};
+struct AttnGrads {
+  float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
+};
+
+int attn_check_dims(const AttnDims& d);
+size_t attn_saved_bytes(const AttnDims& d);
+size_t attn_scratch_bytes(const AttnDims& d);
+// h (B, L, A) contiguous; labels (B, T) int32 0-based; logp (B, T, O) out.
+int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
+             void* saved, void* scratch, size_t scratch_bytes);
+// dlogp (B, T, O); dh (B, L, A) written (accumulate_dh=0) or accumulated; grads accumulated with scale.
+int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+             const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
+             void* scratch, size_t scratch_bytes);
+// alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
+const float* attn_saved_alpha(const AttnDims& d, const void* saved);
+
+// -log p of the labels and the reference's seed dlogp = -labelmask (timit/timit.lua:262-282).
+int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
+             float* dlogp);
+
+}  // namespace s2s

@@ -1,0 +1,778 @@
+// Attention decoder forward/backward: the drop-in for nn.Attention's decoder graph
+// (Attention.lua:43-211, 305-327) unrolled by nn.RNNAttention (RNNAttention.lua:144-253)
+// with the Chorowski decoder_recurrent / decoder_mlp (timit/model_chorowski_baseline.lua:48-59).
+//
+// Per decoder step t (teacher forcing, RNNAttention.lua:172-176), one launch each:
+//   F1 ws = Ws s_{t-1} + bs                           skinny MFMA  (Attention.lua:65-66)
+//   F2 e_l = we . tanh(ws + Vh_l); local softmax stats
+//      and partial context over a 16-frame chunk       wave-dot + wave reductions (Attention.lua:98-117, 132-134)
+//   F3 combine chunks -> alpha, c, lse, MonoAlign ind  (MonotonicAlignment.lua:19-42)
+//   F4 c_in = Wc c + bc, y_in = Wy[:,y_{t-1}] + by      skinny MFMA  (Attention.lua:149-150)
+//   F5 d = Wd [c_in; y_in] + bd                        skinny MFMA  (Attention.lua:151)
+//   F6/F7 decoder GRU (GRU.lua:22-30) on [s_{t-1}; d]   skinny MFMA x2
+// The decoder MLP (Maxout -> Linear -> LogSoftMax) is not on the recurrence, so it runs
+// once for all B*T rows after the loop (one GEMM + one per-row head kernel).
+// Backward mirrors RNNAttention:updateGradInput's reverse loop (RNNAttention.lua:233-250):
+// MLP backward for all rows first, then per step GRU p1/p2, Wd^T, Wc^T, the fused
+// attention backward (softmax, tanh, dVh, dh += alpha dc), the dws combine and Ws^T;
+// every weight gradient is one GEMM over all B*T rows afterwards.
+#include "attn.h"
+
+#include "skinny.h"
+
+namespace s2s {
+
+namespace {
+
+constexpr int LC = 16;  // frames per attention workgroup (4 waves x 4 frames)
+
+struct AttnK {
+  // dims
+  int B, L, T, A, Sc, S, O, M, K, NCH, t;
+  float penalty;
+  // params
+  AttnParams P;
+  const float* h;
+  const int* labels;
+  // saved
+  float *Vh, *WS, *E, *ALPHA, *LSE, *IND, *C, *HX, *RHX, *CY, *GSV, *VV, *MM, *LOGP;
+  int* AM;
+  // fwd scratch
+  float *PM, *PL, *PC, *U;
+  // bwd scratch
+  float *DO, *DU, *DV, *DGA, *DS, *DSP, *DSPF, *DD, *DCY, *DC, *DVH, *PDWS, *DWS, *DWEACC, *YP;
+  float *WhT, *GT, *WdT, *WcT, *WsT;
+  float* dh;
+  long lddh;
+  const float* dlogp;
+  float* logp;
+};
+
+struct Layout {
+  size_t saved, fwd, bwd;
+};
+
+Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
+  const long B = d.B, L = d.L, T = d.T, A = d.A, Sc = d.Sc, S = d.S, O = d.O, M = d.M, Mk = (long)d.M * d.K;
+  const long NCH = (d.L + LC - 1) / LC, BT = B * T;
+  Bump sv{saved, 0, 0};
+  float* Vh = sv.take<float>(B * L * Sc);
+  float* WS = sv.take<float>(BT * Sc);
+  float* E = sv.take<float>(BT * L);
+  float* ALPHA = sv.take<float>(BT * L);
+  float* LSE = sv.take<float>(BT);
+  float* IND = sv.take<float>(BT);
+  float* C = sv.take<float>(BT * A);
+  float* HX = sv.take<float>(BT * 2 * S);
+  float* RHX = sv.take<float>(BT * 2 * S);
+  float* CY = sv.take<float>(BT * 2 * S);
+  float* GSV = sv.take<float>(BT * 3 * S);
+  float* VV = sv.take<float>(BT * (S + A));
+  float* MM = sv.take<float>(BT * M);
+  int* AM = sv.take<int>(BT * M);
+  float* LOGP = sv.take<float>(BT * O);
+  Bump f{scratch, 0, 0};
+  float* PM = f.take<float>(B * NCH);
+  float* PL = f.take<float>(B * NCH);
+  float* PC = f.take<float>(B * NCH * A);
+  float* U = f.take<float>(BT * Mk);
+  Bump g{scratch, 0, 0};
+  float* DO = g.take<float>(BT * O);
+  float* DU = g.take<float>(BT * Mk);
+  float* DV = g.take<float>(BT * (S + A));
+  float* DGA = g.take<float>(BT * 3 * S);
+  float* DS = g.take<float>(B * S);
+  float* DSP = g.take<float>(B * S);
+  float* DSPF = g.take<float>(B * S);
+  float* DD = g.take<float>(BT * S);
+  float* DCY = g.take<float>(BT * 2 * S);
+  float* DC = g.take<float>(BT * A);
+  float* DVH = g.take<float>(B * L * Sc);
+  float* PDWS = g.take<float>(B * NCH * Sc);
+  float* DWS = g.take<float>(BT * Sc);
+  float* DWEACC = g.take<float>(B * NCH * Sc);
+  float* YP = g.take<float>(BT * O);
+  float* WhT = g.take<float>(S * S);
+  float* GT = g.take<float>(2 * S * 3 * S);
+  float* WdT = g.take<float>(2 * S * S);
+  float* WcT = g.take<float>(A * S);
+  float* WsT = g.take<float>(S * Sc);
+  if (k) {
+    k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
+    k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
+    k->Vh = Vh; k->WS = WS; k->E = E; k->ALPHA = ALPHA; k->LSE = LSE; k->IND = IND; k->C = C; k->HX = HX;
+    k->RHX = RHX; k->CY = CY; k->GSV = GSV; k->VV = VV; k->MM = MM; k->AM = AM; k->LOGP = LOGP;
+    k->PM = PM; k->PL = PL; k->PC = PC; k->U = U;
+    k->DO = DO; k->DU = DU; k->DV = DV; k->DGA = DGA; k->DS = DS; k->DSP = DSP; k->DSPF = DSPF; k->DD = DD;
+    k->DCY = DCY; k->DC = DC; k->DVH = DVH; k->PDWS = PDWS; k->DWS = DWS; k->DWEACC = DWEACC; k->YP = YP;
+    k->WhT = WhT; k->GT = GT; k->WdT = WdT; k->WcT = WcT; k->WsT = WsT;
+  }
+  return Layout{sv.off + 256, f.off + 256, g.off + 256};
+}
+
+__device__ __forceinline__ int brow(int b0, int lane, int B) { return min(b0 + (lane & 15), B - 1); }
+
+// ------------------------------------------------------------------ forward step kernels
+
+// F1: ws[b] = Ws s_{t-1}[b] + bs  (N = Sc, K = S)
+__global__ __launch_bounds__(256) void dec_f1_ws(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (t > 0)
+    acc = skinny_wave(k.HX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S, k.P.Ws + (long)(n0 + (lane & 15)) * S,
+                      S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b < k.B) k.WS[((long)b * k.T + t) * k.Sc + n] = s + k.P.bs[n];
+}
+
+// F2: scores + chunk-local softmax stats + partial context.  grid (NCH, B)
+__global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
+  __shared__ float sc[LC];
+  __shared__ float pw[LC];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = blockIdx.x, b = blockIdx.y, t = k.t;
+  const int L = k.L, Sc = k.Sc, A = k.A;
+  const float* ws = k.WS + ((long)b * k.T + t) * Sc;
+  const float* we = k.P.we;
+  for (int i = 0; i < 4; ++i) {
+    const int li = wave * 4 + i, l = ch * LC + li;
+    float part = 0.f;
+    if (l < L) {
+      const float* vh = k.Vh + ((long)b * L + l) * Sc;
+      for (int c4 = lane; c4 < Sc / 4; c4 += 64) {
+        const float4 v = reinterpret_cast<const float4*>(vh)[c4];
+        const float4 w = reinterpret_cast<const float4*>(ws)[c4];
+        const float4 e = reinterpret_cast<const float4*>(we)[c4];
+        part += e.x * tanhf(w.x + v.x) + e.y * tanhf(w.y + v.y) + e.z * tanhf(w.z + v.z) + e.w * tanhf(w.w + v.w);
+      }
+    }
+    part = wave_sum(part);
+    if (lane == 0) sc[li] = l < L ? part : -INFINITY;
+  }
+  __syncthreads();
+  float m = -INFINITY;
+  for (int i = 0; i < LC; ++i) m = fmaxf(m, sc[i]);
+  if (tid < LC) {
+    const int l = ch * LC + tid;
+    const float p = l < L ? expf(sc[tid] - m) : 0.f;
+    pw[tid] = p;
+    if (l < L) k.E[((long)b * k.T + t) * L + l] = sc[tid];
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int i = 0; i < LC; ++i) s += pw[i];
+    k.PM[b * k.NCH + ch] = m;
+    k.PL[b * k.NCH + ch] = s;
+  }
+  float* pc = k.PC + ((long)b * k.NCH + ch) * A;
+  const int lend = min(LC, L - ch * LC);
+  for (int a4 = tid; a4 < A / 4; a4 += 256) {
+    float4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < lend; ++i) {
+      const float4 hv = reinterpret_cast<const float4*>(k.h + ((long)b * L + ch * LC + i) * A)[a4];
+      const float p = pw[i];
+      acc.x += p * hv.x; acc.y += p * hv.y; acc.z += p * hv.z; acc.w += p * hv.w;
+    }
+    reinterpret_cast<float4*>(pc)[a4] = acc;
+  }
+}
+
+// F3: combine chunks (grid B): lse, alpha, c, MonoAlign indicator
+__global__ __launch_bounds__(256) void dec_f3_combine(AttnK k) {
+  __shared__ float wj[64];
+  __shared__ float red[4];
+  __shared__ float stat[2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, b = blockIdx.x, t = k.t;
+  const int L = k.L, A = k.A, S = k.S, NCH = k.NCH;
+  const long row = (long)b * k.T + t;
+  if (tid == 0) {
+    float m = -INFINITY;
+    for (int j = 0; j < NCH; ++j) m = fmaxf(m, k.PM[b * NCH + j]);
+    float den = 0.f;
+    for (int j = 0; j < NCH; ++j) {
+      const float w = expf(k.PM[b * NCH + j] - m);
+      if (j < 64) wj[j] = w;
+      den += w * k.PL[b * NCH + j];
+    }
+    stat[0] = m;
+    stat[1] = den;
+    k.LSE[row] = m + logf(den);
+  }
+  __syncthreads();
+  const float m = stat[0], inv = 1.0f / stat[1];
+  // context c = sum_j w_j pc_j / den  -> C and the MLP input VV[:, S:]
+  for (int a = tid; a < A; a += 256) {
+    float acc = 0.f;
+    for (int j = 0; j < NCH; ++j) {
+      const float w = j < 64 ? wj[j] : expf(k.PM[b * NCH + j] - m);
+      acc += w * k.PC[((long)b * NCH + j) * A + a];
+    }
+    const float c = acc * inv;
+    k.C[row * A + a] = c;
+    k.VV[row * (S + A) + S + a] = c;
+  }
+  // alpha_l = exp(e_l - lse) and sum_l (L - l)(alpha_l - alpha_prev_l)   (MonotonicAlignment.lua:27-35)
+  const float lse = m + logf(stat[1]);
+  float diff = 0.f;
+  for (int l = tid; l < L; l += 256) {
+    const float a = expf(k.E[row * L + l] - lse);
+    k.ALPHA[row * L + l] = a;
+    const float ap = t > 0 ? k.ALPHA[(row - 1) * L + l] : 0.f;  // alpha_{t-1} (written by step t-1)
+    diff += (float)(L - l) * (a - ap);
+  }
+  diff = wave_sum(diff);
+  if (lane == 0) red[wave] = diff;
+  __syncthreads();
+  if (tid == 0) {
+    const float d = ((red[0] + red[1]) + red[2]) + red[3];
+    const float pen = k.penalty * fmaxf(d, 0.f);
+    k.IND[row] = pen > 0.f ? 1.f : 0.f;
+  }
+}
+
+// F4: c_in = Wc c + bc (N = S, K = A); y_in = Wy[:, y_{t-1}] + by   -> CY = [c_in | y_in]
+__global__ __launch_bounds__(256) void dec_f4_cin(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S, A = k.A;
+  floatx4 acc = skinny_wave(k.C + ((long)brow(b0, lane, k.B) * k.T + t) * A, k.P.Wc + (long)(n0 + (lane & 15)) * A,
+                            A, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  k.CY[row * 2 * S + n] = s + k.P.bc[n];
+  float yin = k.P.by[n];
+  if (t > 0) yin += k.P.Wy[(long)n * k.O + k.labels[(long)b * k.T + t - 1]];
+  k.CY[row * 2 * S + S + n] = yin;
+}
+
+// F5: d = Wd [c_in; y_in] + bd (N = S, K = 2S) -> HX[:, S:] and RHX[:, S:]
+__global__ __launch_bounds__(256) void dec_f5_d(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.CY + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
+                            k.P.Wd + (long)(n0 + (lane & 15)) * 2 * S, 2 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float d = s + k.P.bd[n];
+  k.HX[row * 2 * S + S + n] = d;
+  k.RHX[row * 2 * S + S + n] = d;
+}
+
+// F6: [z|r] = sig(W{z,r} [s_{t-1}; d])  (N = 2S, K = 2S)
+__global__ __launch_bounds__(256) void dec_f6_gru1(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  const float* W = n0 < S ? k.P.Wz + (long)n0 * 2 * S : k.P.Wr + (long)(n0 - S) * 2 * S;
+  floatx4 acc = skinny_wave(k.HX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S, W + (long)(lane & 15) * 2 * S,
+                            2 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float g = sigmoidf_(s);
+  if (n < S) {
+    k.GSV[row * 3 * S + n] = g;
+  } else {
+    const int j = n - S;
+    k.GSV[row * 3 * S + S + j] = g;
+    k.RHX[row * 2 * S + j] = g * k.HX[row * 2 * S + j];
+  }
+}
+
+// F7: hh = tanh(Wh [r*s; d]); s_t = (1-z) s_{t-1} + z hh  (N = S, K = 2S)
+__global__ __launch_bounds__(256) void dec_f7_gru2(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.RHX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
+                            k.P.Wh + (long)(n0 + (lane & 15)) * 2 * S, 2 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float hh = tanhf(s);
+  const float z = k.GSV[row * 3 * S + n], sp = k.HX[row * 2 * S + n];
+  k.GSV[row * 3 * S + 2 * S + n] = hh;
+  const float snew = (-z + 1.0f) * sp + z * hh;
+  k.VV[row * (S + k.A) + n] = snew;
+  if (t + 1 < k.T) k.HX[(row + 1) * 2 * S + n] = snew;
+}
+
+__global__ void dec_init_fwd(AttnK k) {
+  // s_0 = 0 (Recurrent.lua:112 zeros_hidden)
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < k.B * k.S) {
+    const int b = i / k.S, n = i - b * k.S;
+    k.HX[((long)b * k.T) * 2 * k.S + n] = 0.f;
+  }
+}
+
+// MLP head (per row b*T+t, one wave each): maxout (first max wins), Linear(M,O), LogSoftMax.
+__global__ __launch_bounds__(256) void dec_mlp_head(AttnK k, int rows) {
+  extern __shared__ float sm[];  // 4 * M
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = blockIdx.x * 4 + wave;
+  const int M = k.M, Kw = k.K, O = k.O;
+  float* mv = sm + wave * M;
+  if (r < rows) {
+    const float* u = k.U + (long)r * M * Kw;
+    for (int j = lane; j < M; j += 64) {
+      float best = u[j * Kw];
+      int bi = 0;
+      for (int i = 1; i < Kw; ++i) {
+        const float v = u[j * Kw + i];
+        if (v > best) { best = v; bi = i; }
+      }
+      mv[j] = best;
+      k.MM[(long)r * M + j] = best;
+      k.AM[(long)r * M + j] = bi;
+    }
+  }
+  __syncthreads();
+  if (r >= rows) return;
+  float mx = -INFINITY;
+  for (int n = lane; n < O; n += 64) {
+    float o = k.P.bo[n];
+    const float* w = k.P.Wo + (long)n * M;
+    for (int j = 0; j < M; ++j) o += w[j] * mv[j];
+    k.LOGP[(long)r * O + n] = o;
+    mx = fmaxf(mx, o);
+  }
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int n = lane; n < O; n += 64) se += expf(k.LOGP[(long)r * O + n] - mx);
+  se = wave_sum(se);
+  const float lz = mx + logf(se);
+  for (int n = lane; n < O; n += 64) {
+    const float v = k.LOGP[(long)r * O + n] - lz;
+    k.LOGP[(long)r * O + n] = v;
+    if (k.logp) k.logp[(long)r * O + n] = v;
+  }
+}
+
+// ------------------------------------------------------------------ backward kernels
+
+// per row: do = dlogp - exp(logp) sum(dlogp) (LogSoftMax bwd); dm = Wo^T do; du = scatter(dm, argmax)
+__global__ __launch_bounds__(256) void dec_mlp_head_bwd(AttnK k, int rows) {
+  extern __shared__ float sm[];  // 4 * O
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int r = blockIdx.x * 4 + wave;
+  const int M = k.M, Kw = k.K, O = k.O;
+  float* dov = sm + wave * O;
+  float sd = 0.f;
+  if (r < rows)
+    for (int n = lane; n < O; n += 64) sd += k.dlogp[(long)r * O + n];
+  sd = wave_sum(sd);
+  if (r < rows)
+    for (int n = lane; n < O; n += 64) {
+      const float v = k.dlogp[(long)r * O + n] - expf(k.LOGP[(long)r * O + n]) * sd;
+      dov[n] = v;
+      k.DO[(long)r * O + n] = v;
+    }
+  __syncthreads();
+  if (r >= rows) return;
+  float* du = k.DU + (long)r * M * Kw;
+  for (int j = lane; j < M; j += 64) {
+    float dm = 0.f;
+    for (int n = 0; n < O; ++n) dm += k.P.Wo[(long)n * M + j] * dov[n];
+    const int am = k.AM[(long)r * M + j];
+    for (int i = 0; i < Kw; ++i) du[j * Kw + i] = i == am ? dm : 0.f;
+  }
+}
+
+__device__ __forceinline__ void dec_gate_grads(const AttnK& k, int b, int t, int n, float ds) {
+  const int S = k.S;
+  const long row = (long)b * k.T + t;
+  const float z = k.GSV[row * 3 * S + n], hh = k.GSV[row * 3 * S + 2 * S + n], sp = k.HX[row * 2 * S + n];
+  k.DS[b * S + n] = ds;
+  k.DGA[row * 3 * S + n] = ds * (hh - sp) * (z * (1.0f - z));
+  k.DGA[row * 3 * S + 2 * S + n] = (ds * z) * (1.0f - hh * hh);
+}
+
+__global__ void dec_bwd_init(AttnK k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= k.B * k.S) return;
+  const int b = i / k.S, n = i - b * k.S, t = k.T - 1;
+  dec_gate_grads(k, b, t, n, k.DV[((long)b * k.T + t) * (k.S + k.A) + n]);
+}
+
+// K2: dq = Wh[:, :S]^T da_h (N = S, K = S) -> da_r, DSP = ds(1-z) + dq r
+__global__ __launch_bounds__(256) void dec_b2_gru1(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DGA + ((long)brow(b0, lane, k.B) * k.T + t) * 3 * S + 2 * S,
+                            k.WhT + (long)(n0 + (lane & 15)) * S, S, wave, lane);
+  const float dq = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float z = k.GSV[row * 3 * S + n], r = k.GSV[row * 3 * S + S + n], sp = k.HX[row * 2 * S + n];
+  k.DGA[row * 3 * S + S + n] = (dq * sp) * (r * (1.0f - r));
+  k.DSP[b * S + n] = k.DS[b * S + n] * (-z + 1.0f) + dq * r;
+}
+
+// K3: [ds_prev | dd] = GT [da_z; da_r; da_h]  (N = 2S, K = 3S)
+__global__ __launch_bounds__(256) void dec_b3_gru2(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DGA + ((long)brow(b0, lane, k.B) * k.T + t) * 3 * S,
+                            k.GT + (long)(n0 + (lane & 15)) * 3 * S, 3 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  if (n < S) k.DSPF[b * S + n] = k.DSP[b * S + n] + s;
+  else k.DD[((long)b * k.T + t) * S + n - S] = s;
+}
+
+// K4: [dc_in | dy_in] = Wd^T dd  (N = 2S, K = S)
+__global__ __launch_bounds__(256) void dec_b4_wd(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DD + ((long)brow(b0, lane, k.B) * k.T + t) * S, k.WdT + (long)(n0 + (lane & 15)) * S,
+                            S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b < k.B) k.DCY[((long)b * k.T + t) * 2 * S + n] = s;
+}
+
+// K5: dc = dv_c + Wc^T dc_in  (N = A, K = S)
+__global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DCY + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
+                            k.WcT + (long)(n0 + (lane & 15)) * S, S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  k.DC[row * k.A + n] = k.DV[row * (S + k.A) + S + n] + s;
+}
+
+// K6: fused attention backward for one 16-frame chunk.  grid (NCH, B)
+//   d alpha_l = dc . h_l + carry_l + gdiff_l      (MM bwd + MonotonicAlignment.lua:44-77)
+//   de_l = alpha_l (d alpha_l - sum_j alpha_j d alpha_j)   with sum = dc . c + sum alpha (carry + gdiff)
+//   dh_l += alpha_l dc;  dZ = de_l we (1 - tanh^2);  dVh_l += dZ;  partial dws, dwe
+__global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
+  __shared__ float redv[4];
+  __shared__ float pws[4][1024];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int ch = blockIdx.x, b = blockIdx.y, t = k.t;
+  const int L = k.L, A = k.A, Sc = k.Sc, T = k.T;
+  const long row = (long)b * T + t;
+  const float* dc = k.DC + row * A;
+  const float* c = k.C + row * A;
+  const float* alpha = k.ALPHA + row * L;
+  const float lam = k.penalty;
+  const float ind = k.IND[row], indn = t + 1 < T ? k.IND[row + 1] : 0.f;
+  // sum_j alpha_j d alpha_j
+  float part = 0.f;
+  for (int a = tid; a < A; a += 256) part += dc[a] * c[a];
+  for (int l = tid; l < L; l += 256) part += alpha[l] * (lam * (float)(L - l) * (ind - indn));
+  part = wave_sum(part);
+  if (lane == 0) redv[wave] = part;
+  __syncthreads();
+  const float ssum = ((redv[0] + redv[1]) + redv[2]) + redv[3];
+  const float* ws = k.WS + row * Sc;
+  const float* we = k.P.we;
+  // Sc <= 1024 asserted on the host: each lane owns k = 4*(lane + 64 i)
+  float dwsp[16], dwep[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) { dwsp[i] = 0.f; dwep[i] = 0.f; }
+  for (int i4 = 0; i4 < 4; ++i4) {
+    const int l = ch * LC + wave * 4 + i4;
+    if (l >= L) break;
+    const float* hl = k.h + ((long)b * L + l) * A;
+    float dd = 0.f;
+    for (int a4 = lane; a4 < A / 4; a4 += 64) {
+      const float4 hv = reinterpret_cast<const float4*>(hl)[a4];
+      const float4 dv = reinterpret_cast<const float4*>(dc)[a4];
+      dd += hv.x * dv.x + hv.y * dv.y + hv.z * dv.z + hv.w * dv.w;
+    }
+    dd = wave_sum(dd);
+    const float al = alpha[l];
+    const float dal = dd + lam * (float)(L - l) * (ind - indn);
+    const float de = al * (dal - ssum);
+    float* dhl = k.dh + ((long)b * L + l) * k.lddh;
+    for (int a = lane; a < A; a += 64) dhl[a] += al * dc[a];
+    const float* vh = k.Vh + ((long)b * L + l) * Sc;
+    float* dvh = k.DVH + ((long)b * L + l) * Sc;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < Sc / 4) {
+        const float4 v = reinterpret_cast<const float4*>(vh)[c4];
+        const float4 w = reinterpret_cast<const float4*>(ws)[c4];
+        const float4 e = reinterpret_cast<const float4*>(we)[c4];
+        float4 o = reinterpret_cast<float4*>(dvh)[c4];
+        const float th0 = tanhf(w.x + v.x), th1 = tanhf(w.y + v.y), th2 = tanhf(w.z + v.z), th3 = tanhf(w.w + v.w);
+        const float z0 = de * e.x * (1.f - th0 * th0), z1 = de * e.y * (1.f - th1 * th1);
+        const float z2 = de * e.z * (1.f - th2 * th2), z3 = de * e.w * (1.f - th3 * th3);
+        o.x += z0; o.y += z1; o.z += z2; o.w += z3;
+        reinterpret_cast<float4*>(dvh)[c4] = o;
+        dwsp[4 * i] += z0; dwsp[4 * i + 1] += z1; dwsp[4 * i + 2] += z2; dwsp[4 * i + 3] += z3;
+        dwep[4 * i] += de * th0; dwep[4 * i + 1] += de * th1; dwep[4 * i + 2] += de * th2; dwep[4 * i + 3] += de * th3;
+      }
+    }
+  }
+  // cross-wave sums of the per-wave partials (fixed order), dws then dwe
+  float* pd = k.PDWS + ((long)b * k.NCH + ch) * Sc;
+  float* pe = k.DWEACC + ((long)b * k.NCH + ch) * Sc;
+#pragma unroll
+  for (int pass = 0; pass < 2; ++pass) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < Sc / 4) {
+        float* dst = &pws[wave][4 * c4];
+        const float* src = pass == 0 ? &dwsp[4 * i] : &dwep[4 * i];
+        dst[0] = src[0]; dst[1] = src[1]; dst[2] = src[2]; dst[3] = src[3];
+      }
+    }
+    __syncthreads();
+    for (int kk = tid; kk < Sc; kk += 256) {
+      const float v = ((pws[0][kk] + pws[1][kk]) + pws[2][kk]) + pws[3][kk];
+      if (pass == 0) pd[kk] = v; else pe[kk] += v;
+    }
+  }
+}
+
+// K7: DWS[b][t] = sum over chunks (grid B)
+__global__ void dec_b7_dws(AttnK k) {
+  const int b = blockIdx.x, t = k.t, Sc = k.Sc, NCH = k.NCH;
+  for (int kk = threadIdx.x; kk < Sc; kk += blockDim.x) {
+    float s = 0.f;
+    for (int j = 0; j < NCH; ++j) s += k.PDWS[((long)b * NCH + j) * Sc + kk];
+    k.DWS[((long)b * k.T + t) * Sc + kk] = s;
+  }
+}
+
+// K8: ds_{t-1} = DSPF + Ws^T dws (N = S, K = Sc); then gate grads of step t-1
+__global__ __launch_bounds__(256) void dec_b8_ws(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DWS + ((long)brow(b0, lane, k.B) * k.T + t) * k.Sc,
+                            k.WsT + (long)(n0 + (lane & 15)) * k.Sc, k.Sc, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B || t == 0) return;
+  const float carry = k.DSPF[b * S + n] + s;
+  dec_gate_grads(k, b, t - 1, n, k.DV[((long)b * k.T + t - 1) * (S + k.A) + n] + carry);
+}
+
+__global__ void dec_onehot_prev(AttnK k) {
+  // YP[b][t] = onehot(y_{t-1}), zeros at t = 0 (RNNAttention.lua:172-176)
+  const long n = (long)k.B * k.T * k.O;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / k.O;
+    const int o = (int)(i - row * k.O);
+    const int t = (int)(row % k.T);
+    k.YP[i] = (t > 0 && k.labels[row - 1] == o) ? 1.f : 0.f;
+  }
+}
+
+__global__ void transpose_kernel(const float* __restrict__ src, long lds, int rows, int cols, float* __restrict__ dst,
+                                 long ldd) {
+  // dst[c*ldd + r] = src[r*lds + c]
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + threadIdx.x;
+    if (r < rows && c < cols) tile[i][threadIdx.x] = src[(long)r * lds + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + threadIdx.x;
+    if (r < rows && c < cols) dst[(long)c * ldd + r] = tile[threadIdx.x][i];
+  }
+}
+
+int transpose(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd) {
+  hipLaunchKernelGGL(transpose_kernel, dim3((cols + 31) / 32, (rows + 31) / 32), dim3(32, 8), 0, st, src, lds, rows,
+                     cols, dst, ldd);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+__global__ void fill2d_kernel(float* dst, long ldd, int rows, int cols, float v) {
+  const long n = (long)rows * cols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / cols, c = i - r * cols;
+    dst[r * ldd + c] = v;
+  }
+}
+
+__global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
+                                float* dlogp) {
+  const int b = blockIdx.x;
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < T * O; i += blockDim.x) {
+    const int t = i / O, o = i - t * O;
+    const bool hit = labels[b * T + t] == o;
+    if (hit) s += logp[((long)b * T + t) * O + o];
+    if (dlogp) dlogp[((long)b * T + t) * O + o] = hit ? -1.f : 0.f;
+  }
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = -(((red[0] + red[1]) + red[2]) + red[3]);
+    nll[b] = normalize ? v / (float)T : v;
+  }
+}
+
+}  // namespace
+
+int attn_check_dims(const AttnDims& d) {
+  S2S_REQUIRE(d.B > 0 && d.L > 0 && d.T > 0, "attn: empty B/L/T");
+  S2S_REQUIRE(d.S % 16 == 0 && d.A % 16 == 0 && d.Sc % 16 == 0, "attn: S, A, scoreDepth must be multiples of 16");
+  S2S_REQUIRE(d.Sc <= 1024, "attn: scoreDepth > 1024 not supported");
+  S2S_REQUIRE(d.O > 0 && d.M > 0 && d.K > 0, "attn: bad output/mlp dims");
+  return 0;
+}
+
+size_t attn_saved_bytes(const AttnDims& d) { return carve(d, nullptr, nullptr, nullptr).saved; }
+size_t attn_scratch_bytes(const AttnDims& d) {
+  Layout l = carve(d, nullptr, nullptr, nullptr);
+  return l.fwd > l.bwd ? l.fwd : l.bwd;
+}
+const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.ALPHA;
+}
+
+int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
+             void* saved, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(attn_check_dims(d));
+  S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
+  AttnK k{};
+  carve(d, &k, (char*)saved, (char*)scratch);
+  k.P = P;
+  k.h = h;
+  k.labels = labels;
+  k.logp = logp;
+  const int B = d.B, L = d.L, T = d.T, S = d.S;
+  const int bt = (B + 15) / 16;
+  // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
+  S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc));
+  hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  for (int t = 0; t < T; ++t) {
+    k.t = t;
+    hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, B), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f3_combine, dim3(B), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
+  const int rows = B * T;
+  S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
+                (long)d.M * d.K, P.bm));
+  hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+             const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
+             void* scratch, size_t scratch_bytes) {
+  S2S_TRY(attn_check_dims(d));
+  S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
+  AttnK k{};
+  carve(d, &k, (char*)saved, (char*)scratch);
+  k.P = P;
+  k.h = h;
+  k.labels = labels;
+  k.dlogp = dlogp;
+  k.dh = dh;
+  k.lddh = d.A;
+  const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
+  const int rows = B * T, bt = (B + 15) / 16;
+  if (!accumulate_dh) S2S_CHECK_HIP(hipMemsetAsync(dh, 0, sizeof(float) * (size_t)B * L * A, st));
+  S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
+  S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
+  // packed transposes for the backward products
+  S2S_TRY(transpose(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
+  S2S_TRY(transpose(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
+  S2S_TRY(transpose(st, P.Wr, 2L * S, S, 2 * S, k.GT + S, 3L * S));
+  S2S_TRY(transpose(st, P.Wh, 2L * S, S, 2 * S, k.GT + 2 * S, 3L * S));
+  // the h-half of Wh reaches ds_{t-1} through dq = Wh[:, :S]^T da_h (K2), not through GT
+  hipLaunchKernelGGL(fill2d_kernel, dim3(64), dim3(256), 0, st, k.GT + 2 * S, 3L * S, S, S, 0.f);
+  S2S_TRY(transpose(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
+  S2S_TRY(transpose(st, P.Wc, A, S, A, k.WcT, S));
+  S2S_TRY(transpose(st, P.Ws, S, Sc, S, k.WsT, Sc));
+  // MLP backward for all rows (not on the recurrence)
+  hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
+  S2S_CHECK_HIP(hipGetLastError());
+  // dV = dU Wm  ->  [ds_mlp | dc_mlp]
+  S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A));
+  hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  for (int t = T - 1; t >= 0; --t) {
+    k.t = t;
+    hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b6_attn, dim3(k.NCH, B), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b7_dws, dim3(B), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  hipLaunchKernelGGL(dec_onehot_prev, dim3(256), dim3(256), 0, st, k);
+  S2S_CHECK_HIP(hipGetLastError());
+  // weight gradients: one GEMM per parameter over all B*T rows (accumulate, alpha = scale)
+  {
+    GemmProblem pr[16];
+    int n = 0;
+    pr[n++] = GemmProblem{k.DO, k.MM, G.Wo, nullptr, O, d.M, d.M, O, d.M, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DU, k.VV, G.Wm, nullptr, Mk, S + A, S + A, Mk, S + A, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DGA, k.HX, G.Wz, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DGA + S, k.HX, G.Wr, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DGA + 2 * S, k.RHX, G.Wh, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DD, k.CY, G.Wd, nullptr, S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DCY, k.C, G.Wc, nullptr, 2L * S, A, A, S, A, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DCY + S, k.YP, G.Wy, nullptr, 2L * S, O, O, S, O, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DWS, k.HX, G.Ws, nullptr, Sc, 2L * S, S, Sc, S, rows, scale, 1.f};
+    pr[n++] = GemmProblem{k.DVH, h, G.V, nullptr, Sc, A, A, Sc, A, B * L, scale, 1.f};
+    S2S_TRY(gemm_f32(st, pr, n, true, false));
+  }
+  S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo));
+  S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));
+  S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd));
+  S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc));
+  S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));
+  S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs));
+  S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we));
+  // dh += dVh V   (Vh = h V^T)
+  S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A));
+  return 0;
+}
+
+int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
+             float* dlogp) {
+  hipLaunchKernelGGL(nll_seed_kernel, dim3(B), dim3(256), 0, st, B, T, O, logp, labels, normalize, nll, dlogp);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace s2s

@@ -1,0 +1,462 @@
+// C-ABI surface of libs2s_hip.so (include/s2s_hip.h): argument checking, the model-level
+// training step (encoder -> attention decoder -> NLL seed -> backward), hipGraph capture
+// of that step, and RCCL data-parallel gradient sums.
+#include "../../include/s2s_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "attn.h"
+#include "gru.h"
+#include "s2s_common.h"
+
+namespace s2s {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+const char* get_error() { return g_err.c_str(); }
+
+}  // namespace s2s
+
+using namespace s2s;
+
+struct GraphKey {
+  s2s_model_dims d;
+  const void* ptrs[7];
+  float scale;
+  int flags;
+  void* stream;
+  bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
+};
+
+struct s2s_ctx {
+  int device = 0;
+  int flags = 0;
+  bool have_graph = false;
+  GraphKey key{};
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  ncclComm_t comm = nullptr;
+};
+
+namespace {
+
+int set_device(s2s_ctx* ctx) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  S2S_CHECK_HIP(hipSetDevice(ctx->device));
+  return 0;
+}
+
+AttnDims to_attn(const s2s_attn_dims* d) {
+  return AttnDims{d->B, d->L, d->T, d->annotationDepth, d->scoreDepth, d->stateDepth, d->outputDepth, d->mlpDepth,
+                  d->maxoutWindow, d->penalty};
+}
+
+// ------------------------------------------------------------ model layout
+struct LayerDims {
+  int D, H;
+};
+std::vector<LayerDims> enc_layers(const s2s_model_dims* d) {
+  std::vector<LayerDims> v;
+  int D = d->inputFrameSize;
+  for (int l = 1; l <= d->numLayers; ++l) {
+    const int H = l == d->numLayers ? d->outputFrameSize : d->hiddenFrameSize;
+    v.push_back({D, H});
+    D = 2 * H;
+  }
+  return v;
+}
+AttnDims model_attn(const s2s_model_dims* d) {
+  return AttnDims{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
+                  d->mlpDepth, d->maxoutWindow, d->penalty};
+}
+std::vector<long> param_sizes(const s2s_model_dims* d) {
+  std::vector<long> s;
+  for (auto& ld : enc_layers(d))
+    for (int i = 0; i < 6; ++i) s.push_back((long)ld.H * (ld.H + ld.D));
+  const long A = 2L * d->outputFrameSize, Sc = d->scoreDepth, S = d->stateDepth, O = d->outputDepth,
+             M = d->mlpDepth, Mk = (long)d->mlpDepth * d->maxoutWindow;
+  const long dec[S2S_ATTN_NPARAMS] = {Sc * A, Sc * S, Sc, Sc, S * O, S, S * A, S, S * 2 * S, S,
+                                      S * 2 * S, S * 2 * S, S * 2 * S, Mk * (S + A), Mk, O * M, O};
+  for (long v : dec) s.push_back(v);
+  return s;
+}
+
+struct ModelWs {
+  std::vector<float*> saved;  // 2 per layer
+  std::vector<float*> Y;      // per layer output (B, L, 2H)
+  void* attn_saved;
+  void* scratch;
+  size_t scratch_bytes;
+  float *dlogp, *nll, *logp, *dY0, *dY1;
+  size_t total;
+};
+ModelWs model_ws(const s2s_model_dims* d, void* base) {
+  ModelWs w{};
+  Bump bp{static_cast<char*>(base), 0, 0};
+  const long B = d->B, L = d->L, T = d->T, O = d->outputDepth;
+  size_t scr = 0;
+  long hmax = 0;
+  for (auto& ld : enc_layers(d)) {
+    w.saved.push_back(bp.take<float>(B * L * 5 * ld.H));
+    w.saved.push_back(bp.take<float>(B * L * 5 * ld.H));
+    w.Y.push_back(bp.take<float>(B * L * 2 * ld.H));
+    size_t s = gru_layer_scratch_bytes(2, d->B, d->L, ld.D, ld.H);
+    scr = s > scr ? s : scr;
+    hmax = ld.H > hmax ? ld.H : hmax;
+  }
+  const AttnDims ad = model_attn(d);
+  w.attn_saved = bp.take<char>(attn_saved_bytes(ad));
+  const size_t as = attn_scratch_bytes(ad);
+  scr = as > scr ? as : scr;
+  w.scratch = bp.take<char>(scr);
+  w.scratch_bytes = scr;
+  w.dlogp = bp.take<float>(B * T * O);
+  w.nll = bp.take<float>(B);
+  w.logp = bp.take<float>(B * T * O);
+  w.dY0 = bp.take<float>(B * L * 2 * hmax);
+  w.dY1 = bp.take<float>(B * L * 2 * hmax);
+  w.total = bp.off + 256;
+  return w;
+}
+
+int check_model_dims(const s2s_model_dims* d) {
+  S2S_REQUIRE(d != nullptr, "null dims");
+  S2S_REQUIRE(d->B > 0 && d->L > 0 && d->T > 0, "model: empty B/L/T");
+  S2S_REQUIRE(d->numLayers >= 1 && d->inputFrameSize > 0, "model: bad encoder dims");
+  S2S_REQUIRE(d->hiddenFrameSize % 16 == 0 && d->outputFrameSize % 16 == 0, "model: hidden sizes must be multiples of 16");
+  S2S_TRY(attn_check_dims(model_attn(d)));
+  return 0;
+}
+
+int model_step_impl(hipStream_t st, const s2s_model_dims* d, const float* params, float* grads, const float* x,
+                    const int* labels, float scale, int flags, float* logp, float* nll, void* workspace) {
+  ModelWs w = model_ws(d, workspace);
+  const std::vector<LayerDims> layers = enc_layers(d);
+  const std::vector<long> sizes = param_sizes(d);
+  std::vector<const float*> P;
+  std::vector<float*> G;
+  long off = 0;
+  for (long s : sizes) {
+    P.push_back(params + off);
+    G.push_back(grads + off);
+    off += s;
+  }
+  if (flags & S2S_ZERO_GRADS) S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, st));
+  const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
+  const int nl = (int)layers.size();
+  // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
+  const float* inp = x;
+  long ldin = d->inputFrameSize;
+  for (int l = 0; l < nl; ++l) {
+    const int H = layers[l].H;
+    GruLayerIO io{};
+    io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
+    io.x = inp; io.ldx = ldin;
+    for (int dd = 0; dd < 2; ++dd) {
+      for (int g = 0; g < 3; ++g) io.W[dd][g] = P[6 * l + 3 * dd + g];
+      io.reverse[dd] = dd;
+      io.y[dd] = w.Y[l] + dd * H;
+      io.saved[dd] = w.saved[2 * l + dd];
+    }
+    io.ldy = 2L * H;
+    S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
+    inp = w.Y[l];
+    ldin = 2L * H;
+  }
+  // ---- attention decoder forward
+  const AttnDims ad = model_attn(d);
+  AttnParams ap;
+  AttnGrads ag;
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  float** gp = reinterpret_cast<float**>(&ag);
+  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+    pp[i] = P[6 * nl + i];
+    gp[i] = G[6 * nl + i];
+  }
+  float* lp = logp ? logp : w.logp;
+  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.scratch, w.scratch_bytes));
+  // ---- loss seed: dlogp = -labelmask
+  S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
+  // ---- decoder backward -> dh
+  float* dYcur = w.dY0;
+  float* dYnext = w.dY1;
+  S2S_TRY(attn_bwd(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, ag, scale, w.scratch,
+                   w.scratch_bytes));
+  // ---- encoder backward
+  for (int l = nl - 1; l >= 0; --l) {
+    const int H = layers[l].H;
+    GruLayerIO io{};
+    io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
+    io.x = l == 0 ? x : w.Y[l - 1];
+    io.ldx = l == 0 ? d->inputFrameSize : 2L * layers[l - 1].H;
+    io.ldy = 2L * H;
+    GruLayerGrad gr{};
+    for (int dd = 0; dd < 2; ++dd) {
+      for (int g = 0; g < 3; ++g) {
+        io.W[dd][g] = P[6 * l + 3 * dd + g];
+        gr.dW[dd][g] = G[6 * l + 3 * dd + g];
+      }
+      io.reverse[dd] = dd;
+      io.y[dd] = w.Y[l] + dd * H;
+      io.saved[dd] = w.saved[2 * l + dd];
+      gr.dy[dd] = dYcur + dd * H;
+    }
+    gr.lddy = 2L * H;
+    gr.dx = l == 0 ? nullptr : dYnext;
+    gr.lddx = io.ldx;
+    gr.dx_accumulate = 0;
+    gr.scale = scale;
+    S2S_TRY(gru_layer_bwd(st, io, gr, w.scratch, w.scratch_bytes));
+    float* tmp = dYcur;
+    dYcur = dYnext;
+    dYnext = tmp;
+  }
+  return 0;
+}
+
+}  // namespace
+
+// ================================================================== C ABI
+extern "C" {
+
+int s2s_version(void) { return 1; }
+const char* s2s_last_error(void) { return s2s::get_error(); }
+
+int s2s_ctx_create(int device, s2s_ctx** out) {
+  S2S_REQUIRE(out != nullptr, "null out");
+  int n = 0;
+  S2S_CHECK_HIP(hipGetDeviceCount(&n));
+  S2S_REQUIRE(device >= 0 && device < n, "device index out of range");
+  auto* c = new s2s_ctx();
+  c->device = device;
+  *out = c;
+  return 0;
+}
+
+void s2s_ctx_destroy(s2s_ctx* ctx) {
+  if (!ctx) return;
+  if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
+  if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  delete ctx;
+}
+
+int s2s_ctx_set_flags(s2s_ctx* ctx, int flags) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  ctx->flags = flags;
+  return 0;
+}
+
+size_t s2s_gru_saved_bytes(int B, int L, int H) { return sizeof(float) * (size_t)B * L * 5 * H; }
+size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H) {
+  return gru_layer_scratch_bytes(ndir, B, L, D, H);
+}
+
+static int fill_gru_io(GruLayerIO& io, int ndir, int B, int L, int D, int H, const int* reverse, const float* x,
+                       long ldx, const float* const* W, float* const* y, long ldy, void* const* saved) {
+  S2S_REQUIRE(ndir == 1 || ndir == 2, "gru: ndir must be 1 or 2");
+  S2S_REQUIRE(reverse && x && W && saved, "gru: null argument");
+  S2S_REQUIRE(ldx >= D, "gru: ldx < D");
+  io.ndir = ndir; io.B = B; io.L = L; io.D = D; io.H = H; io.x = x; io.ldx = ldx; io.ldy = ldy;
+  for (int d = 0; d < ndir; ++d) {
+    for (int g = 0; g < 3; ++g) {
+      io.W[d][g] = W[3 * d + g];
+      S2S_REQUIRE(io.W[d][g] != nullptr, "gru: null weight");
+    }
+    io.reverse[d] = reverse[d] ? 1 : 0;
+    io.y[d] = y ? y[d] : nullptr;
+    io.saved[d] = static_cast<float*>(saved[d]);
+    S2S_REQUIRE(io.saved[d] != nullptr, "gru: null saved buffer");
+  }
+  return 0;
+}
+
+int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
+                const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved,
+                void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  GruLayerIO io{};
+  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, y, ldy, saved));
+  S2S_REQUIRE(y != nullptr, "gru: null y");
+  for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "gru: null y");
+  S2S_REQUIRE(ldy >= H, "gru: ldy < H");
+  return gru_layer_fwd(static_cast<hipStream_t>(stream), io, scratch, scratch_bytes);
+}
+
+int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
+                const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy,
+                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch,
+                size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  GruLayerIO io{};
+  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, nullptr, H, saved));
+  S2S_REQUIRE(dy && dW, "gru: null dy/dW");
+  GruLayerGrad gr{};
+  for (int d = 0; d < ndir; ++d) {
+    gr.dy[d] = dy[d];
+    S2S_REQUIRE(gr.dy[d] != nullptr, "gru: null dy");
+    for (int g = 0; g < 3; ++g) {
+      gr.dW[d][g] = dW[3 * d + g];
+      S2S_REQUIRE(gr.dW[d][g] != nullptr, "gru: null dW");
+    }
+  }
+  gr.lddy = lddy;
+  gr.dx = dx;
+  gr.lddx = lddx;
+  gr.dx_accumulate = dx_accumulate;
+  gr.scale = scale;
+  return gru_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
+}
+
+size_t s2s_attn_saved_bytes(const s2s_attn_dims* d) { return d ? attn_saved_bytes(to_attn(d)) : 0; }
+size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d) { return d ? attn_scratch_bytes(to_attn(d)) : 0; }
+const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_alpha(to_attn(d), saved) : nullptr;
+}
+
+int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
+                 const float* const* params, float* logp, void* saved, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && h && labels && params && logp && saved, "attn: null argument");
+  AttnParams ap;
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+    pp[i] = params[i];
+    S2S_REQUIRE(pp[i] != nullptr, "attn: null parameter");
+  }
+  return attn_fwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, logp, saved, scratch, scratch_bytes);
+}
+
+int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
+                 const float* const* params, const void* saved, const float* dlogp, float* dh, int dh_accumulate,
+                 float* const* grads, float scale, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && h && labels && params && saved && dlogp && dh && grads, "attn: null argument");
+  AttnParams ap;
+  AttnGrads ag;
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  float** gp = reinterpret_cast<float**>(&ag);
+  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+    pp[i] = params[i];
+    gp[i] = grads[i];
+    S2S_REQUIRE(pp[i] != nullptr && gp[i] != nullptr, "attn: null parameter/grad");
+  }
+  return attn_bwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, saved, dlogp, dh, dh_accumulate, ag,
+                  scale, scratch, scratch_bytes);
+}
+
+int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,
+                 int normalize, float* nll, float* dlogp) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(logp && labels && nll, "nll: null argument");
+  S2S_REQUIRE(B > 0 && T > 0 && O > 0, "nll: empty dims");
+  return nll_seed(static_cast<hipStream_t>(stream), B, T, O, logp, labels, normalize, nll, dlogp);
+}
+
+size_t s2s_model_param_count(const s2s_model_dims* d) {
+  if (!d) return 0;
+  size_t n = 0;
+  for (long s : param_sizes(d)) n += (size_t)s;
+  return n;
+}
+
+long s2s_model_param_offset(const s2s_model_dims* d, int i, long* numel) {
+  if (!d) return -1;
+  const std::vector<long> s = param_sizes(d);
+  if (i < 0 || i >= (int)s.size()) return -1;
+  long off = 0;
+  for (int j = 0; j < i; ++j) off += s[j];
+  if (numel) *numel = s[i];
+  return off;
+}
+
+size_t s2s_model_workspace_bytes(const s2s_model_dims* d) {
+  if (check_model_dims(d) != 0) return 0;
+  return model_ws(d, nullptr).total;
+}
+
+const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace) {
+  if (!d || !workspace) return nullptr;
+  ModelWs w = model_ws(d, const_cast<void*>(workspace));
+  return w.Y.back();
+}
+
+int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, const float* params, float* grads,
+                   const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
+                   void* workspace, size_t workspace_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_TRY(check_model_dims(d));
+  S2S_REQUIRE(params && grads && x && labels && workspace, "model: null argument");
+  S2S_REQUIRE(workspace_bytes >= model_ws(d, nullptr).total, "model: workspace too small");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
+    return model_step_impl(st, d, params, grads, x, labels, scale, flags, logp, nll, workspace);
+  GraphKey key;
+  std::memset(&key, 0, sizeof(key));
+  key.d = *d;
+  const void* ptrs[7] = {params, grads, x, labels, logp, nll, workspace};
+  std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
+  key.scale = scale;
+  key.flags = flags;
+  key.stream = stream;
+  if (!(ctx->have_graph && ctx->key == key)) {
+    if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
+    if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+    ctx->exec = nullptr;
+    ctx->graph = nullptr;
+    ctx->have_graph = false;
+    S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = model_step_impl(st, d, params, grads, x, labels, scale, flags, logp, nll, workspace);
+    hipGraph_t g = nullptr;
+    const hipError_t ec = hipStreamEndCapture(st, &g);
+    if (rc != 0) {
+      if (g) (void)hipGraphDestroy(g);
+      return rc;
+    }
+    S2S_CHECK_HIP(ec);
+    ctx->graph = g;
+    S2S_CHECK_HIP(hipGraphInstantiate(&ctx->exec, g, nullptr, nullptr, 0));
+    ctx->key = key;
+    ctx->have_graph = true;
+  }
+  S2S_CHECK_HIP(hipGraphLaunch(ctx->exec, st));
+  return 0;
+}
+
+int s2s_comm_unique_id(void* out_bytes) {
+  S2S_REQUIRE(out_bytes != nullptr, "null out");
+  ncclUniqueId id;
+  const ncclResult_t r = ncclGetUniqueId(&id);
+  S2S_REQUIRE(r == ncclSuccess, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+  std::memcpy(out_bytes, &id, sizeof(id));
+  return 0;
+}
+
+int s2s_comm_init(s2s_ctx* ctx, const void* id_bytes, int nranks, int rank) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(id_bytes && nranks > 0 && rank >= 0 && rank < nranks, "comm: bad arguments");
+  ncclUniqueId id;
+  std::memcpy(&id, id_bytes, sizeof(id));
+  if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  ctx->comm = nullptr;
+  const ncclResult_t r = ncclCommInitRank(&ctx->comm, nranks, id, rank);
+  S2S_REQUIRE(r == ncclSuccess, std::string("ncclCommInitRank: ") + ncclGetErrorString(r));
+  return 0;
+}
+
+int s2s_allreduce_sum(s2s_ctx* ctx, s2s_stream_t stream, float* buf, size_t count) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(ctx->comm != nullptr, "allreduce: s2s_comm_init first");
+  const ncclResult_t r =
+      ncclAllReduce(buf, buf, count, ncclFloat32, ncclSum, ctx->comm, static_cast<hipStream_t>(stream));
+  S2S_REQUIRE(r == ncclSuccess, std::string("ncclAllReduce: ") + ncclGetErrorString(r));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,32 @@
+#pragma once
+#include "s2s_common.h"
+
+namespace s2s {
+
+// One GRU layer, 1 or 2 directions sharing the same input x (the bidirectional
+// encoder layer of timit/model_chorowski_baseline.lua:22-32 runs both in each launch).
+struct GruLayerIO {
+  int ndir, B, L, D, H;
+  const float* x;  // x[(b*L + t)*ldx + c], c < D
+  long ldx;
+  const float* W[2][3];  // per direction Wz, Wr, Wh, each (H, H+D) row-major
+  int reverse[2];
+  float* y[2];  // y[d][(b*L + t)*ldy + j]
+  long ldy;
+  float* saved[2];  // per direction (B, L, 5H)
+};
+struct GruLayerGrad {
+  const float* dy[2];  // dy[d][(b*L+t)*lddy + j]
+  long lddy;
+  float* dx;  // may be null; dx[(b*L+t)*lddx + c]
+  long lddx;
+  int dx_accumulate;
+  float* dW[2][3];  // accumulated: dW += scale * ...
+  float scale;
+};
+
+size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
+int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes);
+int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes);
+
+}  // namespace s2s

@@ -1,0 +1,334 @@
+// GRU layer sequence forward/backward: the drop-in for nn.RNN(nn.GRU(D,H), reverse)
+// (RNN.lua:120-201 over GRU.lua:16-51 / Recurrent.lua:104-151).
+//
+// Reference cell (GRU.lua:22-30), no biases, hx = [h; x] (h first):
+//   z = sig(Wz hx), r = sig(Wr hx), hh = tanh(Wh [r*h; x]), h' = (1-z)*h + z*hh
+// MI355X decomposition:
+//   * the x-half of all three gates for every (b, t) is ONE hoisted MFMA GEMM
+//     (B*L x D) x (D x 3H) -- both directions of a layer in the same launch;
+//   * per time step two dependent skinny MFMA launches (r gates the candidate):
+//       p1: [z|r] = sig(Uzr h_{t-1} + xp)  ->  z, r, q = r*h_{t-1}
+//       p2: hh = tanh(Uh q + xp_h), h_t = (1-z) h_{t-1} + z hh
+//   * BPTT: two skinny launches per step (dq = Uh^T da_h; dh_{t-1} = Uzr^T [da_z; da_r] + ...),
+//     with the next step's gate gradients computed in p2's epilogue;
+//   * dW (the reference's per-step rank-1 GER, LinearZeroBias.lua:70) and dx are
+//     GEMMs over all B*L rows after the sweep.
+// Saved activations per direction: sv (B, L, 5H) = z | r | hh | h_{t-1} | q.
+#include "gru.h"
+
+#include "skinny.h"
+
+namespace s2s {
+
+namespace {
+
+struct GruFwdDir {
+  const float* xp;  // (B, L, ldxp): [z | r | h] x-projections at offset 0
+  long ldxp;
+  const float* Uzr;  // (2H, H)
+  const float* Uh;   // (H, H)
+  float* y;          // y[(b*L + t)*ldy + j]
+  long ldy;
+  float* sv;  // (B, L, 5H)
+  int reverse;
+};
+struct GruFwdArgs {
+  GruFwdDir d[2];
+  int B, L, H, step;
+};
+
+__global__ __launch_bounds__(256) void gru_fwd_p1(GruFwdArgs a) {
+  __shared__ SkinnyRed red;
+  const GruFwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tp = g.reverse ? t + 1 : t - 1;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (step > 0) {
+    const int br = min(b0 + (lane & 15), B - 1);
+    acc = skinny_wave(g.y + ((long)br * L + tp) * g.ldy, g.Uzr + (long)(n0 + (lane & 15)) * H, H, wave, lane);
+  }
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= B) return;
+  const long row = (long)b * L + t;
+  const float gate = sigmoidf_(s + g.xp[row * g.ldxp + n]);
+  float* sv = g.sv + row * 5 * H;
+  if (n < H) {
+    sv[n] = gate;  // z
+  } else {
+    const int j = n - H;
+    const float hp = step > 0 ? g.y[((long)b * L + tp) * g.ldy + j] : 0.f;
+    sv[H + j] = gate;          // r
+    sv[3 * H + j] = hp;        // h_{t-1}
+    sv[4 * H + j] = gate * hp; // q = r*h  (CMulTable, GRU.lua:25)
+  }
+}
+
+__global__ __launch_bounds__(256) void gru_fwd_p2(GruFwdArgs a) {
+  __shared__ SkinnyRed red;
+  const GruFwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (step > 0) {
+    const int br = min(b0 + (lane & 15), B - 1);
+    acc = skinny_wave(g.sv + ((long)br * L + t) * 5 * H + 4 * H, g.Uh + (long)(n0 + (lane & 15)) * H, H, wave,
+                      lane);
+  }
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= B) return;
+  const long row = (long)b * L + t;
+  const float hh = tanhf(s + g.xp[row * g.ldxp + 2 * H + n]);
+  float* sv = g.sv + row * 5 * H;
+  const float z = sv[n], hp = sv[3 * H + n];
+  sv[2 * H + n] = hh;
+  // GRU.lua:27-30: v1 = (-z)+1; v2 = v1*h; h' = v2 + z*hh
+  g.y[row * g.ldy + n] = (-z + 1.0f) * hp + z * hh;
+}
+
+struct GruBwdDir {
+  const float* dy;  // dy[(b*L+t)*lddy + j]
+  long lddy;
+  const float* sv;    // (B, L, 5H)
+  const float* UhT;   // (H, H)   UhT[k][n]  = Uh[n][k]
+  const float* UzrT;  // (H, 2H)  UzrT[k][n] = Uzr[n][k]
+  float* dA;          // dA[(b*L+t)*ldA + {0,H,2H}] = da_z | da_r | da_h
+  long ldA;
+  float* dhc;  // (B, H) carried dL/dh_t from step t+1
+  float* dhp;  // (B, H) partial dL/dh_{t-1} from p1
+  int reverse;
+};
+struct GruBwdArgs {
+  GruBwdDir d[2];
+  int B, L, H, step;  // step = forward step index being back-propagated (L-1 .. 0)
+};
+
+__device__ __forceinline__ void gru_gate_grads(const GruBwdDir& g, int B, int L, int H, int b, int t, int k,
+                                               float dhcarry) {
+  const long row = (long)b * L + t;
+  const float* sv = g.sv + row * 5 * H;
+  const float dh = g.dy[row * g.lddy + k] + dhcarry;
+  const float z = sv[k], hh = sv[2 * H + k], hp = sv[3 * H + k];
+  float* dA = g.dA + row * g.ldA;
+  dA[k] = dh * (hh - hp) * (z * (1.0f - z));          // da_z
+  dA[2 * H + k] = (dh * z) * (1.0f - hh * hh);        // da_h
+}
+
+// gate gradients for the last forward step (carry = 0)
+__global__ void gru_bwd_init(GruBwdArgs a) {
+  const GruBwdDir& g = a.d[blockIdx.y];
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= a.B * a.H) return;
+  const int b = idx / a.H, k = idx - b * a.H;
+  const int t = g.reverse ? 0 : a.L - 1;
+  g.dhc[idx] = 0.f;
+  gru_gate_grads(g, a.B, a.L, a.H, b, t, k, 0.f);
+}
+
+__global__ __launch_bounds__(256) void gru_bwd_p1(GruBwdArgs a) {
+  __shared__ SkinnyRed red;
+  const GruBwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  const int br = min(b0 + (lane & 15), B - 1);
+  floatx4 acc = skinny_wave(g.dA + ((long)br * L + t) * g.ldA + 2 * H, g.UhT + (long)(n0 + (lane & 15)) * H, H,
+                            wave, lane);
+  const float dq = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), k = n0 + (tid & 15);
+  if (b >= B) return;
+  const long row = (long)b * L + t;
+  const float* sv = g.sv + row * 5 * H;
+  const float z = sv[k], r = sv[H + k], hp = sv[3 * H + k];
+  g.dA[row * g.ldA + H + k] = (dq * hp) * (r * (1.0f - r));  // da_r
+  const float dh = g.dy[row * g.lddy + k] + g.dhc[b * H + k];
+  g.dhp[b * H + k] = dh * (-z + 1.0f) + dq * r;
+}
+
+__global__ __launch_bounds__(256) void gru_bwd_p2(GruBwdArgs a) {
+  __shared__ SkinnyRed red;
+  const GruBwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  const int br = min(b0 + (lane & 15), B - 1);
+  floatx4 acc = skinny_wave(g.dA + ((long)br * L + t) * g.ldA, g.UzrT + (long)(n0 + (lane & 15)) * 2 * H, 2 * H,
+                            wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), k = n0 + (tid & 15);
+  if (b >= B || step == 0) return;
+  const float dhprev = g.dhp[b * H + k] + s;
+  g.dhc[b * H + k] = dhprev;
+  const int tn = g.reverse ? t + 1 : t - 1;
+  gru_gate_grads(g, B, L, H, b, tn, k, dhprev);
+}
+
+// Pack W{z,r,h} (H, H+D) into kernel layouts.
+//   Uzr (2H,H), Uh (H,H), UhT (H,H), UzrT (H,2H), Wx rows [z;r;h] (3H, D) at Wx + xrow0*D
+struct PackArgs {
+  const float* W[3];
+  float *Uzr, *Uh, *UhT, *UzrT, *Wx;
+  int H, D;
+};
+__global__ void gru_pack(PackArgs p) {
+  const int H = p.H, D = p.D, HD = H + D;
+  const long nU = 3L * H * H, nX = 3L * H * D;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nU + nX; i += (long)gridDim.x * blockDim.x) {
+    if (i < nU) {
+      const int g = (int)(i / ((long)H * H));
+      const int rem = (int)(i - (long)g * H * H);
+      const int n = rem / H, k = rem - n * H;
+      const float w = p.W[g][(long)n * HD + k];
+      if (g < 2) {
+        if (p.Uzr) p.Uzr[(long)(g * H + n) * H + k] = w;
+        if (p.UzrT) p.UzrT[(long)k * 2 * H + g * H + n] = w;
+      } else {
+        if (p.Uh) p.Uh[(long)n * H + k] = w;
+        if (p.UhT) p.UhT[(long)k * H + n] = w;
+      }
+    } else if (p.Wx) {
+      const long j = i - nU;
+      const int g = (int)(j / ((long)H * D));
+      const long rem = j - (long)g * H * D;
+      const int n = (int)(rem / D), c = (int)(rem - (long)n * D);
+      p.Wx[(long)(g * H + n) * D + c] = p.W[g][(long)n * HD + H + c];
+    }
+  }
+}
+
+int launch_pack(hipStream_t st, const float* Wz, const float* Wr, const float* Wh, int H, int D, float* Uzr,
+                float* Uh, float* UhT, float* UzrT, float* Wx) {
+  PackArgs p{{Wz, Wr, Wh}, Uzr, Uh, UhT, UzrT, Wx, H, D};
+  long n = 3L * H * (H + D);
+  int blocks = (int)((n + 255) / 256);
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(gru_pack, dim3(blocks), dim3(256), 0, st, p);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
+  Bump bp{nullptr, 0, 0};
+  for (int d = 0; d < ndir; ++d) {
+    bp.take<float>(2L * H * H);
+    bp.take<float>((long)H * H);
+    bp.take<float>((long)H * H);
+    bp.take<float>(2L * H * H);
+    bp.take<float>((long)B * H);
+    bp.take<float>((long)B * H);
+  }
+  bp.take<float>(3L * ndir * H * D);             // Wx (both dirs)
+  bp.take<float>((long)B * L * 3 * ndir * H);    // xp or dA (both dirs)
+  return bp.off + 256;
+}
+
+int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes) {
+  const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
+  S2S_REQUIRE(nd == 1 || nd == 2, "gru: ndir must be 1 or 2");
+  S2S_REQUIRE(B > 0 && L > 0 && D > 0 && H > 0, "gru: empty dims");
+  S2S_REQUIRE(H % 16 == 0, "gru: H must be a multiple of 16");
+  S2S_REQUIRE(io.ldy % 4 == 0, "gru: ldy must be a multiple of 4");
+  S2S_REQUIRE(scratch_bytes >= gru_layer_scratch_bytes(nd, B, L, D, H), "gru: scratch too small");
+  Bump bp{static_cast<char*>(scratch), 0, scratch_bytes};
+  float *Uzr[2], *Uh[2];
+  for (int d = 0; d < nd; ++d) {
+    Uzr[d] = bp.take<float>(2L * H * H);
+    Uh[d] = bp.take<float>((long)H * H);
+    bp.take<float>((long)H * H);
+    bp.take<float>(2L * H * H);
+    bp.take<float>((long)B * H);
+    bp.take<float>((long)B * H);
+  }
+  float* Wx = bp.take<float>(3L * nd * H * D);
+  float* xp = bp.take<float>((long)B * L * 3 * nd * H);
+  for (int d = 0; d < nd; ++d)
+    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Uzr[d], Uh[d], nullptr, nullptr,
+                        Wx + 3L * d * H * D));
+  // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, D) . Wx^T
+  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, D, 1.f, io.x, io.ldx, Wx, D, 0.f, xp, 3L * nd * H));
+  GruFwdArgs a{};
+  for (int d = 0; d < nd; ++d)
+    a.d[d] = GruFwdDir{xp + 3L * d * H, 3L * nd * H, Uzr[d], Uh[d], io.y[d], io.ldy, io.saved[d], io.reverse[d]};
+  a.B = B;
+  a.L = L;
+  a.H = H;
+  const dim3 g1(2 * H / 16, (B + 15) / 16, nd), g2(H / 16, (B + 15) / 16, nd);
+  for (int s = 0; s < L; ++s) {
+    a.step = s;
+    hipLaunchKernelGGL(gru_fwd_p1, g1, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gru_fwd_p2, g2, dim3(256), 0, st, a);
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes) {
+  const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
+  S2S_REQUIRE(nd == 1 || nd == 2, "gru: ndir must be 1 or 2");
+  S2S_REQUIRE(H % 16 == 0, "gru: H must be a multiple of 16");
+  S2S_REQUIRE(scratch_bytes >= gru_layer_scratch_bytes(nd, B, L, D, H), "gru: scratch too small");
+  Bump bp{static_cast<char*>(scratch), 0, scratch_bytes};
+  float *UhT[2], *UzrT[2], *dhc[2], *dhp[2];
+  for (int d = 0; d < nd; ++d) {
+    bp.take<float>(2L * H * H);
+    bp.take<float>((long)H * H);
+    UhT[d] = bp.take<float>((long)H * H);
+    UzrT[d] = bp.take<float>(2L * H * H);
+    dhc[d] = bp.take<float>((long)B * H);
+    dhp[d] = bp.take<float>((long)B * H);
+  }
+  float* Wx = bp.take<float>(3L * nd * H * D);
+  float* dA = bp.take<float>((long)B * L * 3 * nd * H);
+  const long ldA = 3L * nd * H;
+  for (int d = 0; d < nd; ++d)
+    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, nullptr, nullptr, UhT[d], UzrT[d],
+                        Wx + 3L * d * H * D));
+  GruBwdArgs a{};
+  for (int d = 0; d < nd; ++d)
+    a.d[d] = GruBwdDir{gr.dy[d], gr.lddy, io.saved[d], UhT[d], UzrT[d], dA + 3L * d * H, ldA, dhc[d], dhp[d],
+                       io.reverse[d]};
+  a.B = B;
+  a.L = L;
+  a.H = H;
+  hipLaunchKernelGGL(gru_bwd_init, dim3((B * H + 255) / 256, nd), dim3(256), 0, st, a);
+  const dim3 g1(H / 16, (B + 15) / 16, nd);
+  for (int s = L - 1; s >= 0; --s) {
+    a.step = s;
+    hipLaunchKernelGGL(gru_bwd_p1, g1, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(gru_bwd_p2, g1, dim3(256), 0, st, a);
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  // dx (+)= dA (B*L, 3*nd*H) . Wx (3*nd*H, D)   (RNN.lua:196 gradInput; both directions summed,
+  // which is what the encoder graph's fan-out of the layer input accumulates)
+  if (gr.dx)
+    S2S_TRY(gemm1(st, false, false, B * L, D, 3 * nd * H, 1.f, dA, ldA, Wx, D, gr.dx_accumulate ? 1.f : 0.f, gr.dx,
+                  gr.lddx));
+  // dW += scale * dA_g^T . [h_{t-1} | q ; x]   (LinearZeroBias.lua:67-74 summed over all steps)
+  GemmProblem probs[12];
+  int np = 0;
+  for (int d = 0; d < nd; ++d) {
+    for (int g = 0; g < 3; ++g) {
+      const float* dAg = dA + 3L * d * H + (long)g * H;
+      float* dW = gr.dW[d][g];
+      // h-part columns [0, H): z,r use h_{t-1} (sv + 3H), h-gate uses q = r*h (sv + 4H)
+      probs[np++] = GemmProblem{dAg, io.saved[d] + (g == 2 ? 4 : 3) * H, dW, nullptr, ldA, 5L * H, (long)H + D,
+                                H, H, B * L, gr.scale, 1.f};
+      // x-part columns [H, H+D)
+      probs[np++] = GemmProblem{dAg, io.x, dW + H, nullptr, ldA, io.ldx, (long)H + D, H, D, B * L, gr.scale, 1.f};
+    }
+  }
+  S2S_TRY(gemm_f32(st, probs, np, true, false));
+  return 0;
+}
+
+}  // namespace s2s

@@ -1,0 +1,102 @@
+// Shared internals of libs2s_hip.so (MI355X / gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace s2s {
+
+// ---------------------------------------------------------------- errors
+// C-ABI calls never abort: they record a message and return nonzero
+// (SURVEY.md §8b "Errors": Lua error() on nonzero status).
+void set_error(const std::string& msg);
+const char* get_error();
+
+#define S2S_CHECK_HIP(expr)                                                                  \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) {                                                                  \
+      ::s2s::set_error(std::string(#expr) + ": " + hipGetErrorString(_e) + " @" __FILE__ ":" \
+                       + std::to_string(__LINE__));                                          \
+      return 1;                                                                              \
+    }                                                                                        \
+  } while (0)
+
+#define S2S_REQUIRE(cond, msg)                          \
+  do {                                                  \
+    if (!(cond)) {                                      \
+      ::s2s::set_error(std::string("s2s: ") + (msg));   \
+      return 2;                                         \
+    }                                                   \
+  } while (0)
+
+#define S2S_TRY(expr)          \
+  do {                         \
+    int _rc = (expr);          \
+    if (_rc != 0) return _rc;  \
+  } while (0)
+
+// ---------------------------------------------------------------- device helpers
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---------------------------------------------------------------- big GEMM (gemm_f32.hip)
+// Row-major C[M x N] = alpha * op(A) * op(B) + beta * C (+ bias[n] if bias).
+//   op(A)(i,k) = transA ? A[k*lda + i] : A[i*lda + k]
+//   op(B)(k,j) = transB ? B[j*ldb + k] : B[k*ldb + j]
+// beta == 0 overwrites C without reading it.
+struct GemmProblem {
+  const float* A;
+  const float* B;
+  float* C;
+  const float* bias;
+  long lda, ldb, ldc;
+  int M, N, K;
+  float alpha, beta;
+};
+constexpr int kMaxGemmBatch = 16;
+// All problems of one call share transA/transB.
+int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB);
+inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
+                 const float* B, long ldb, float beta, float* C, long ldc, const float* bias = nullptr) {
+  GemmProblem p{A, B, C, bias, lda, ldb, ldc, M, N, K, alpha, beta};
+  return gemm_f32(st, &p, 1, tA, tB);
+}
+
+// Column sums: out[j] = beta*out[j] + alpha * sum_i X[i*ldx + j], i < M, j < N.
+int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out);
+// Strided 2-D copy (rows x cols) dst[r*ldd + c] = src[r*lds + c]  (+ optional accumulate).
+int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd, int rows, int cols, bool accumulate);
+// dst[i] = alpha * src[i] + beta * dst[i]
+int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alpha, float beta);
+
+// ---------------------------------------------------------------- workspace bump allocator
+struct Bump {
+  char* base;
+  size_t off;
+  size_t cap;
+  template <class T>
+  T* take(size_t n) {
+    size_t a = (off + 255) & ~size_t(255);
+    T* p = reinterpret_cast<T*>(base ? base + a : nullptr);
+    off = a + n * sizeof(T);
+    return p;
+  }
+};
+
+}  // namespace s2s

@@ -1,0 +1,62 @@
+// Per-time-step "skinny" products of the recurrences: out[b][n] = sum_k X[b][k] * W[n][k]
+// with b the utterance (batch) row -- B is 32..64, so the step GEMM is (B x K) x (K x N).
+//
+// One workgroup = 4 waves computes a 16 (batch rows) x 16 (units) tile; K is split
+// across the 4 waves (16-wide chunks round-robin), each wave runs
+// v_mfma_f32_16x16x4_f32 (exact f32) on float4 operand loads (lane l holds rows
+// l&15 and k-quad l>>4; element e of the float4 feeds MFMA e, the same
+// permutation of k on both operands), and the 4 partial tiles are summed through
+// LDS in a fixed order.  Thread tid of the workgroup then owns output
+// (row tid>>4, unit tid&15) for the fused epilogue.
+#pragma once
+#include "s2s_common.h"
+
+namespace s2s {
+
+struct SkinnyRed {
+  float v[4][16][17];
+};
+
+// xrow / wrow: this lane's operand rows (already offset to the lane's batch row /
+// output unit); both 16-byte aligned; K % 16 == 0.
+__device__ __forceinline__ floatx4 skinny_wave(const float* __restrict__ xrow, const float* __restrict__ wrow,
+                                               int K, int wave, int lane) {
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int kq = 4 * (lane >> 4);
+  int kc = wave * 16;
+  for (; kc + 64 < K; kc += 128) {
+    const float4 a0 = *reinterpret_cast<const float4*>(xrow + kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    const float4 a1 = *reinterpret_cast<const float4*>(xrow + kc + 64 + kq);
+    const float4 b1 = *reinterpret_cast<const float4*>(wrow + kc + 64 + kq);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+  }
+  for (; kc < K; kc += 64) {
+    const float4 a0 = *reinterpret_cast<const float4*>(xrow + kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
+// Writes this wave's partial tile and returns (after the barrier) the summed value
+// of output (tid>>4, tid&15).  Must be called by all 256 threads.
+__device__ __forceinline__ float skinny_reduce(SkinnyRed& red, floatx4 acc, int wave, int lane, int tid) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red.v[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  const int i = tid >> 4, j = tid & 15;
+  return ((red.v[0][i][j] + red.v[1][i][j]) + red.v[2][i][j]) + red.v[3][i][j];
+}
+
+}  // namespace s2s

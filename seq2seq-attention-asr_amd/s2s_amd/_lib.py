@@ -1,0 +1,98 @@
+"""ctypes binding of libs2s_hip.so (include/s2s_hip.h).
+
+The product path: every compute call goes through this library.  If the shared object
+is missing or fails to load, importing the host layer raises -- there is no CPU
+fallback (the CPU oracle under oracle/ is test infrastructure only).
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libs2s_hip.so")
+
+c_int, c_long, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
+P = ctypes.POINTER
+
+
+class s2s_attn_dims(ctypes.Structure):
+    _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("annotationDepth", c_int), ("scoreDepth", c_int),
+                ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
+                ("penalty", c_float)]
+
+
+class s2s_model_dims(ctypes.Structure):
+    _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("inputFrameSize", c_int), ("hiddenFrameSize", c_int),
+                ("outputFrameSize", c_int), ("numLayers", c_int), ("scoreDepth", c_int), ("stateDepth", c_int),
+                ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int), ("penalty", c_float)]
+
+
+# every symbol include/s2s_hip.h declares: (name, restype, argtypes)
+SIGNATURES = [
+    ("s2s_version", c_int, []),
+    ("s2s_last_error", ctypes.c_char_p, []),
+    ("s2s_ctx_create", c_int, [c_int, P(c_void_p)]),
+    ("s2s_ctx_destroy", None, [c_void_p]),
+    ("s2s_ctx_set_flags", c_int, [c_void_p, c_int]),
+    ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),
+    ("s2s_gru_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    ("s2s_gru_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
+                            P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_size_t]),
+    ("s2s_gru_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
+                            P(c_void_p), P(c_void_p), P(c_void_p), c_long, c_void_p, c_long, c_int, P(c_void_p),
+                            c_float, c_void_p, c_size_t]),
+    ("s2s_attn_saved_bytes", c_size_t, [P(s2s_attn_dims)]),
+    ("s2s_attn_scratch_bytes", c_size_t, [P(s2s_attn_dims)]),
+    ("s2s_attn_fwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,
+                             c_void_p, c_void_p, c_size_t]),
+    ("s2s_attn_bwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,
+                             c_void_p, c_void_p, c_int, P(c_void_p), c_float, c_void_p, c_size_t]),
+    ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
+                             c_void_p]),
+    ("s2s_model_param_count", c_size_t, [P(s2s_model_dims)]),
+    ("s2s_model_param_offset", c_long, [P(s2s_model_dims), c_int, P(c_long)]),
+    ("s2s_model_workspace_bytes", c_size_t, [P(s2s_model_dims)]),
+    ("s2s_model_step", c_int, [c_void_p, c_void_p, P(s2s_model_dims), c_void_p, c_void_p, c_void_p, c_void_p,
+                               c_float, c_int, c_void_p, c_void_p, c_void_p, c_size_t]),
+    ("s2s_model_encoder_output", c_void_p, [P(s2s_model_dims), c_void_p]),
+    ("s2s_comm_unique_id", c_int, [c_void_p]),
+    ("s2s_comm_init", c_int, [c_void_p, c_void_p, c_int, c_int]),
+    ("s2s_allreduce_sum", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+]
+
+S2S_CTX_GRAPH = 1
+S2S_ZERO_GRADS = 1
+S2S_NORMALIZE_NLL = 2
+S2S_ATTN_NPARAMS = 17
+S2S_UNIQUE_ID_BYTES = 128
+
+
+class S2SError(RuntimeError):
+    pass
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} is missing: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                          "(the HIP extension is required; there is no CPU fallback)")
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+lib = _load()
+
+
+def check(rc: int):
+    if rc != 0:
+        raise S2SError(lib.s2s_last_error().decode(errors="replace"))
+
+
+def ptr_array(ptrs, ctype=c_void_p):
+    arr = (ctype * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = p
+    return arr

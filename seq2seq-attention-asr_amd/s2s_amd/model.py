@@ -1,0 +1,171 @@
+"""The Chorowski TIMIT baseline autoencoder (timit/model_chorowski_baseline.lua:10-83) as one
+flat-buffer training step on libs2s_hip.so (s2s_model_step).
+
+`loadmodel(opt)` field names are kept in ModelConfig; the flat parameter/gradient buffers
+play the role of `parameters, gradients = autoencoder:getParameters()` (timit/timit.lua:172).
+"""
+import ctypes
+import dataclasses
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+from .nn import _bytes, dptr, get_context, stream_ptr
+
+
+@dataclasses.dataclass
+class ModelConfig:
+    inputFrameSize: int = 123
+    hiddenFrameSize: int = 256
+    outputFrameSize: int = 256
+    scoreDepth: int = 512
+    stateDepth: int = 256
+    outputDepth: int = 62        # opt.numPhonemes (TIMIT, incl. EOS) / opt.outputDepth (LibriSpeech chars)
+    mlpDepth: int = 64
+    maxoutWindow: int = 7
+    penalty: float = 0.0
+    numLayers: int = 3
+
+    @property
+    def annotationDepth(self):
+        return 2 * self.outputFrameSize
+
+    @classmethod
+    def from_opt(cls, opt: dict):
+        """loadmodel(opt) defaults (timit/model_chorowski_baseline.lua:14-46)."""
+        return cls(inputFrameSize=opt.get("inputFrameSize", 123), hiddenFrameSize=opt.get("hiddenFrameSize", 256),
+                   outputFrameSize=opt.get("outputFrameSize", 256), scoreDepth=opt.get("scoreDepth", 512),
+                   stateDepth=opt.get("stateDepth", 256),
+                   outputDepth=opt.get("numPhonemes", opt.get("outputDepth", 62)),
+                   mlpDepth=opt.get("mlpDepth", 64), penalty=opt.get("penalty", 0.0))
+
+
+def param_shapes(cfg: ModelConfig):
+    """Flat layout (DESIGN.md §Data layout): encoder layers x (fwd, bwd) x (Wz, Wr, Wh), then the
+    decoder in s2s_attn parameter order."""
+    out = []
+    D = cfg.inputFrameSize
+    for l in range(1, cfg.numLayers + 1):
+        H = cfg.outputFrameSize if l == cfg.numLayers else cfg.hiddenFrameSize
+        for d in ("f", "b"):
+            for g in ("Wz", "Wr", "Wh"):
+                out.append((f"enc{l}{d}.{g}", (H, H + D)))
+        D = 2 * H
+    A, Sc, S, O, M, k = (cfg.annotationDepth, cfg.scoreDepth, cfg.stateDepth, cfg.outputDepth, cfg.mlpDepth,
+                         cfg.maxoutWindow)
+    out += [("V", (Sc, A)), ("Ws", (Sc, S)), ("bs", (Sc,)), ("we", (1, Sc)), ("Wy", (S, O)), ("by", (S,)),
+            ("Wc", (S, A)), ("bc", (S,)), ("Wd", (S, 2 * S)), ("bd", (S,)), ("dec.Wz", (S, 2 * S)),
+            ("dec.Wr", (S, 2 * S)), ("dec.Wh", (S, 2 * S)), ("Wm", (M * k, S + A)), ("bm", (M * k,)),
+            ("Wo", (O, M)), ("bo", (O,))]
+    return out
+
+
+def _fan_in(name, shape, cfg):
+    S, Sc, A, O, M = cfg.stateDepth, cfg.scoreDepth, cfg.annotationDepth, cfg.outputDepth, cfg.mlpDepth
+    table = {"V": A, "Ws": S, "bs": S, "we": Sc, "Wy": O, "by": O, "Wc": A, "bc": A, "Wd": 2 * S, "bd": 2 * S,
+             "Wm": S + A, "bm": S + A, "Wo": M, "bo": M}
+    return table.get(name, shape[1] if len(shape) > 1 else shape[0])
+
+
+class ChorowskiBaseline:
+    """autoencoder = decoder({encoder(x), labelmask}) with flat params/grads on one device."""
+
+    def __init__(self, cfg: ModelConfig = None, device=None, seed: int = 1234, graph: bool = False):
+        self.cfg = cfg or ModelConfig()
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        shapes = param_shapes(self.cfg)
+        self.shapes = shapes
+        n = sum(math.prod(s) for _, s in shapes)
+        g = torch.Generator().manual_seed(seed)
+        flat = torch.empty(n, dtype=torch.float32)
+        off = 0
+        for name, shp in shapes:
+            sz = math.prod(shp)
+            stdv = 1.0 / math.sqrt(_fan_in(name, shp, self.cfg))
+            flat[off:off + sz] = (torch.rand(sz, generator=g, dtype=torch.float64) * 2 - 1).mul_(stdv).float()
+            off += sz
+        self.params = flat.to(self.device)
+        self.grads = torch.zeros_like(self.params)
+        self.ctx = get_context(self.device.index) if not graph else None
+        if graph:
+            from .nn import Context
+            self.ctx = Context(self.device.index, graph=True)
+        self._ws = {}
+        self._check_layout()
+
+    def dims(self, B, L, T):
+        c = self.cfg
+        return _lib.s2s_model_dims(B, L, T, c.inputFrameSize, c.hiddenFrameSize, c.outputFrameSize, c.numLayers,
+                                   c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty)
+
+    def _check_layout(self):
+        d = self.dims(1, 1, 1)
+        assert lib.s2s_model_param_count(ctypes.byref(d)) == self.params.numel()
+        off = 0
+        for i, (_, shp) in enumerate(self.shapes):
+            numel = ctypes.c_long()
+            assert lib.s2s_model_param_offset(ctypes.byref(d), i, ctypes.byref(numel)) == off
+            assert numel.value == math.prod(shp)
+            off += numel.value
+
+    def getParameters(self):
+        return self.params, self.grads
+
+    def views(self, flat=None):
+        flat = self.params if flat is None else flat
+        out, off = {}, 0
+        for name, shp in self.shapes:
+            sz = math.prod(shp)
+            out[name] = flat[off:off + sz].view(shp)
+            off += sz
+        return out
+
+    def workspace(self, B, L, T):
+        key = (B, L, T)
+        if key not in self._ws:
+            d = self.dims(B, L, T)
+            nbytes = lib.s2s_model_workspace_bytes(ctypes.byref(d))
+            if nbytes == 0:
+                check(1)
+            self._ws[key] = _bytes(nbytes, self.device)
+        return self._ws[key]
+
+    def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None):
+        """One training-step gradient (timit/timit.lua:240-295): grads (+)= scale * d(sum_b nll_b)/dparams,
+        scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O))."""
+        if x.dim() == 2:
+            x = x[None]
+        if labels.dim() == 1:
+            labels = labels[None]
+        B, L, F = x.shape
+        T = labels.shape[1]
+        if F != self.cfg.inputFrameSize:
+            raise ValueError(f"input frame size {F} != {self.cfg.inputFrameSize}")
+        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
+            raise ValueError("x must be a contiguous float32 CUDA tensor")
+        lab = labels.to(torch.int32).contiguous()
+        if scale is None:
+            scale = 1.0 / B if B > 1 else 1.0
+        if logp is None:
+            logp = torch.empty((B, T, self.cfg.outputDepth), device=self.device, dtype=torch.float32)
+        if nll is None:
+            nll = torch.empty(B, device=self.device, dtype=torch.float32)
+        ws = self.workspace(B, L, T)
+        d = self.dims(B, L, T)
+        flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        check(lib.s2s_model_step(self.ctx.handle, st, ctypes.byref(d), dptr(self.params), dptr(self.grads), dptr(x),
+                                 dptr(lab), float(scale), flags, dptr(logp), dptr(nll), dptr(ws), ws.numel()))
+        self._last = (B, L, T)
+        return nll, logp
+
+    def encoder_output(self):
+        B, L, T = self._last
+        d = self.dims(B, L, T)
+        ws = self._ws[(B, L, T)]
+        p = lib.s2s_model_encoder_output(ctypes.byref(d), dptr(ws))
+        off = p - ws.data_ptr()
+        n = B * L * self.cfg.annotationDepth
+        return ws[off:off + 4 * n].view(torch.float32).view(B, L, self.cfg.annotationDepth)

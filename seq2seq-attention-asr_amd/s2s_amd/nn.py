@@ -1,0 +1,358 @@
+"""nn.Module-protocol mirrors of the reference's hot-path modules, on libs2s_hip.so.
+
+Protocol kept from Torch7: `forward(input)` = `updateOutput`,
+`backward(input, gradOutput, scale)` = `updateGradInput` + `accGradParameters`,
+`parameters()` -> ([weights], [gradWeights]), `zeroGradParameters()`, gradients
+accumulate, `training()` / `evaluate()`.  2-D inputs are one utterance (the reference's
+SGD mode, Recurrent.lua:67-77); 3-D inputs are a batch of equal-length utterances.
+"""
+import ctypes
+import math
+
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr_array
+
+
+# --------------------------------------------------------------------------- context / memory
+
+class Context:
+    """One s2s_ctx per device (s2s_ctx_create)."""
+
+    def __init__(self, device: int = 0, graph: bool = False):
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib.s2s_ctx_create(device, ctypes.byref(h)))
+        self.handle = h
+        if graph:
+            check(lib.s2s_ctx_set_flags(h, _lib.S2S_CTX_GRAPH))
+
+    def __del__(self):
+        try:
+            if self.handle:
+                lib.s2s_ctx_destroy(self.handle)
+        except Exception:
+            pass
+
+
+_CTX = {}
+
+
+def get_context(device=None) -> Context:
+    dev = torch.cuda.current_device() if device is None else int(device)
+    if dev not in _CTX:
+        _CTX[dev] = Context(dev)
+    return _CTX[dev]
+
+
+def stream_ptr():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def _bytes(n, device):
+    return torch.empty(max(int(n), 1), dtype=torch.uint8, device=device)
+
+
+def _require_cuda_f32(t, name):
+    if not (t.is_cuda and t.dtype == torch.float32 and t.is_contiguous()):
+        raise S2SArgumentError(f"{name} must be a contiguous float32 CUDA tensor")
+
+
+class S2SArgumentError(ValueError):
+    pass
+
+
+def _uniform(shape, stdv, gen=None):
+    return (torch.rand(shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(stdv).float()
+
+
+class Module:
+    def __init__(self):
+        self.output = None
+        self.gradInput = None
+        self.train = True
+
+    def parameters(self):
+        return [], []
+
+    def zeroGradParameters(self):
+        for g in self.parameters()[1]:
+            g.zero_()
+
+    def forward(self, input):
+        return self.updateOutput(input)
+
+    def backward(self, input, gradOutput, scale=1.0):
+        self.updateGradInput(input, gradOutput, scale)
+        return self.gradInput
+
+    def training(self):
+        self.train = True
+
+    def evaluate(self):
+        self.train = False
+
+    def cuda(self, device=None):
+        dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+        ws, gs = self.parameters()
+        for t in ws + gs:
+            t.data = t.data.to(dev)
+        return self
+
+
+# --------------------------------------------------------------------------- GRU / RNN
+
+class GRU(Module):
+    """nn.GRU(diminput, dimoutput) cell parameters (GRU.lua:8-43): three LinearZeroBias
+    (dimoutput, diminput+dimoutput) for z, r, h, columns [h | x]; reset U(+-1/sqrt(in))
+    (LinearZeroBias.lua:12-29).  The cell runs inside RNN / Attention sequence kernels."""
+
+    def __init__(self, diminput, dimoutput, generator=None):
+        super().__init__()
+        assert diminput is not None, "diminput must be specified"
+        assert dimoutput is not None, "dimoutput must be specified"
+        self.diminput, self.dimoutput = diminput, dimoutput
+        stdv = 1.0 / math.sqrt(diminput + dimoutput)
+        self.weight = [_uniform((dimoutput, diminput + dimoutput), stdv, generator) for _ in range(3)]
+        self.gradWeight = [torch.zeros_like(w) for w in self.weight]
+
+    def parameters(self):
+        return list(self.weight), list(self.gradWeight)
+
+
+class _GruSeq(Module):
+    """Shared driver of s2s_gru_fwd / s2s_gru_bwd for 1 or 2 directions over the same input."""
+
+    def __init__(self, cells, reverses):
+        super().__init__()
+        self.cells = cells
+        self.reverses = reverses
+        self.dimoutput = cells[0].dimoutput
+        for c in cells:
+            if c.dimoutput % 16 != 0:
+                raise S2SArgumentError("GRU dimoutput must be a multiple of 16 on this path")
+
+    def parameters(self):
+        ws, gs = [], []
+        for c in self.cells:
+            w, g = c.parameters()
+            ws += w
+            gs += g
+        return ws, gs
+
+    def _shape(self, input):
+        if input.dim() == 2:
+            return 1, input.shape[0], input.shape[1]
+        if input.dim() == 3:
+            return input.shape
+        raise S2SArgumentError("input dimension must be 2D or 3D")  # RNN.lua:128
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        B, L, D = self._shape(input)
+        H, nd = self.dimoutput, len(self.cells)
+        if D != self.cells[0].diminput:
+            raise S2SArgumentError(f"input frame size {D} != diminput {self.cells[0].diminput}")
+        dev = input.device
+        out = torch.empty((B, L, nd * H), device=dev, dtype=torch.float32)
+        self._saved = [_bytes(lib.s2s_gru_saved_bytes(B, L, H), dev) for _ in range(nd)]
+        scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
+        W = ptr_array([w.data_ptr() for c in self.cells for w in c.weight])
+        y = ptr_array([out.data_ptr() + 4 * H * d for d in range(nd)])
+        sv = ptr_array([s.data_ptr() for s in self._saved])
+        rev = ptr_array([int(r) for r in self.reverses], ctypes.c_int)
+        check(lib.s2s_gru_fwd(get_context(dev.index).handle, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, y,
+                              nd * H, sv, dptr(scr), scr.numel()))
+        self._dims = (B, L, D)
+        self.output = out if input.dim() == 3 else out[0]
+        return self.output
+
+    def updateGradInput(self, input, gradOutput, scale=1.0):
+        B, L, D = self._dims
+        H, nd = self.dimoutput, len(self.cells)
+        dev = input.device
+        go = gradOutput.contiguous()
+        dx = torch.empty((B, L, D), device=dev, dtype=torch.float32)
+        scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
+        W = ptr_array([w.data_ptr() for c in self.cells for w in c.weight])
+        dW = ptr_array([g.data_ptr() for c in self.cells for g in c.gradWeight])
+        dy = ptr_array([go.data_ptr() + 4 * H * d for d in range(nd)])
+        sv = ptr_array([s.data_ptr() for s in self._saved])
+        rev = ptr_array([int(r) for r in self.reverses], ctypes.c_int)
+        check(lib.s2s_gru_bwd(get_context(dev.index).handle, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv,
+                              dy, nd * H, dptr(dx), D, 0, dW, float(scale), dptr(scr), scr.numel()))
+        self.gradInput = dx if input.dim() == 3 else dx[0]
+        return self.gradInput
+
+    def accGradParameters(self, input, gradOutput, scale=1.0):
+        pass  # accumulated inside updateGradInput, as Recurrent's inner gModule:backward does
+
+
+class RNN(_GruSeq):
+    """nn.RNN(nn.GRU(D, H), reverse) (RNN.lua:3-201)."""
+
+    def __init__(self, recurrent, reverse=False):
+        assert recurrent is not None, "recurrent cannot be nil"
+        assert getattr(recurrent, "dimoutput", None) is not None, "recurrent must specify dimoutput"
+        if not isinstance(recurrent, GRU):
+            raise S2SArgumentError("this path runs nn.GRU cells (LSTM cells: next row)")
+        super().__init__([recurrent], [bool(reverse)])
+        self.recurrent = recurrent
+        self.reverse = bool(reverse)
+
+
+class BiRNN(_GruSeq):
+    """JoinTable(2,2)({RNN(GRU, false)(x), RNN(GRU, true)(x)}) -- one bidirectional encoder layer
+    (timit/model_chorowski_baseline.lua:22-24) with both directions in the same launches."""
+
+    def __init__(self, fwd_cell, bwd_cell):
+        super().__init__([fwd_cell, bwd_cell], [False, True])
+
+
+# --------------------------------------------------------------------------- Attention decoder
+
+class MaxoutMLP(Module):
+    """decoder_mlp of timit/model_chorowski_baseline.lua:53-59:
+    Maxout(inDim, mlpDepth, window) -> Linear(mlpDepth, outputDepth) -> LogSoftMax.
+    Maxout = Linear(in, out*window) + TemporalMaxPooling(window, window) over consecutive groups
+    (Maxout.lua:14-18)."""
+
+    def __init__(self, inputDimension, mlpDepth, window, outputDepth, generator=None):
+        super().__init__()
+        self.inputDim, self.mlpDepth, self.window, self.outputDepth = inputDimension, mlpDepth, window, outputDepth
+        s1 = 1.0 / math.sqrt(inputDimension)
+        s2 = 1.0 / math.sqrt(mlpDepth)
+        self.weight = [_uniform((mlpDepth * window, inputDimension), s1, generator),
+                       _uniform((mlpDepth * window,), s1, generator),
+                       _uniform((outputDepth, mlpDepth), s2, generator),
+                       _uniform((outputDepth,), s2, generator)]
+        self.gradWeight = [torch.zeros_like(w) for w in self.weight]
+
+    def parameters(self):
+        return list(self.weight), list(self.gradWeight)
+
+
+class Attention(Module):
+    """nn.Attention (Attention.lua:15-211) for the Chorowski decoder: decoder_recurrent = GRU(S,S)
+    (model_chorowski_baseline.lua:48-51), decoder_mlp = MaxoutMLP.  Input {h, y}: h (L, A) or
+    (B, L, A) annotations, y the (T, O)/(B, T, O) labelmask or (B, T) int labels."""
+
+    PARAM_NAMES = ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "Wz", "Wr", "Wh", "Wm", "bm", "Wo",
+                   "bo")
+
+    def __init__(self, decoder_recurrent, decoder_mlp, scoreDepth, hybridAttendFilterSize, hybridAttendFeatureMaps,
+                 stateDepth, annotationDepth, outputDepth, monoAlignPenalty=False, penaltyLambda=0.0,
+                 generator=None):
+        super().__init__()
+        if hybridAttendFeatureMaps and hybridAttendFeatureMaps > 0:
+            raise NotImplementedError("hybrid (location-aware) attention is a 'next' row (SURVEY.md §8f.4)")
+        if not isinstance(decoder_recurrent, GRU) or decoder_recurrent.dimoutput != stateDepth:
+            raise S2SArgumentError("decoder_recurrent must be GRU(stateDepth, stateDepth)")
+        if not isinstance(decoder_mlp, MaxoutMLP) or decoder_mlp.inputDim != stateDepth + annotationDepth:
+            raise S2SArgumentError("decoder_mlp must be MaxoutMLP(stateDepth + annotationDepth, ...)")
+        self.scoreDepth, self.stateDepth, self.annotationDepth, self.outputDepth = (scoreDepth, stateDepth,
+                                                                                    annotationDepth, outputDepth)
+        self.hybridAttendFilterSize, self.hybridAttendFeatureMaps = hybridAttendFilterSize, hybridAttendFeatureMaps
+        self.MonotonicAlignmentPenalty = bool(monoAlignPenalty)
+        self.penalty = float(penaltyLambda or 0.0) if monoAlignPenalty else 0.0
+        self.decoder_recurrent, self.decoder_mlp = decoder_recurrent, decoder_mlp
+        Sc, S, A, O = scoreDepth, stateDepth, annotationDepth, outputDepth
+        g = generator
+        own = {"V": _uniform((Sc, A), 1 / math.sqrt(A), g),            # TCZB(A, Sc, 1)
+               "Ws": _uniform((Sc, S), 1 / math.sqrt(S), g),           # TemporalConvolution(1, Sc, S)
+               "bs": _uniform((Sc,), 1 / math.sqrt(S), g),
+               "we": _uniform((1, Sc), 1 / math.sqrt(Sc), g),          # TCZB(Sc, 1, 1)
+               "Wy": _uniform((S, O), 1 / math.sqrt(O), g), "by": _uniform((S,), 1 / math.sqrt(O), g),
+               "Wc": _uniform((S, A), 1 / math.sqrt(A), g), "bc": _uniform((S,), 1 / math.sqrt(A), g),
+               "Wd": _uniform((S, 2 * S), 1 / math.sqrt(2 * S), g), "bd": _uniform((S,), 1 / math.sqrt(2 * S), g)}
+        self.own = own
+        self.own_grad = {k: torch.zeros_like(v) for k, v in own.items()}
+
+    def _tensors(self, grads=False):
+        o = self.own_grad if grads else self.own
+        r = self.decoder_recurrent.gradWeight if grads else self.decoder_recurrent.weight
+        m = self.decoder_mlp.gradWeight if grads else self.decoder_mlp.weight
+        return [o["V"], o["Ws"], o["bs"], o["we"], o["Wy"], o["by"], o["Wc"], o["bc"], o["Wd"], o["bd"],
+                r[0], r[1], r[2], m[0], m[1], m[2], m[3]]
+
+    def parameters(self):
+        return self._tensors(False), self._tensors(True)
+
+    def _dims(self, h, T):
+        B, L = (1, h.shape[0]) if h.dim() == 2 else (h.shape[0], h.shape[1])
+        m = self.decoder_mlp
+        return _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
+                                  m.mlpDepth, m.window, self.penalty)
+
+    @staticmethod
+    def labels_from(y, O):
+        if y.dtype in (torch.int32, torch.int64):
+            return y.to(torch.int32).contiguous()
+        # labelmask: one-hot rows (timit/timit.lua:262)
+        return y.argmax(-1).to(torch.int32).contiguous()
+
+    def updateOutput(self, input):
+        h, y = input
+        if h.dim() not in (2, 3):
+            raise S2SArgumentError("x must be 2d or 3d")  # Attention.lua:316
+        _require_cuda_f32(h, "h")
+        lab = self.labels_from(y, self.outputDepth)
+        if lab.dim() == 1:
+            lab = lab[None]
+        T = lab.shape[1]
+        d = self._dims(h, T)
+        dev = h.device
+        self._d = d
+        self._labels = lab
+        self._saved = _bytes(lib.s2s_attn_saved_bytes(ctypes.byref(d)), dev)
+        scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
+        out = torch.empty((d.B, T, self.outputDepth), device=dev, dtype=torch.float32)
+        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
+        check(lib.s2s_attn_fwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h), dptr(lab),
+                               params, dptr(out), dptr(self._saved), dptr(scr), scr.numel()))
+        self.output = out if h.dim() == 3 else out[0]
+        return self.output
+
+    def updateGradInput(self, input, gradOutput, scale=1.0):
+        h, _ = input
+        d = self._d
+        dev = h.device
+        go = gradOutput.contiguous()
+        if go.dim() == 2:
+            go = go[None]
+        dh = torch.empty((d.B, d.L, self.annotationDepth), device=dev, dtype=torch.float32)
+        scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
+        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
+        grads = ptr_array([t.data_ptr() for t in self._tensors(True)])
+        check(lib.s2s_attn_bwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h),
+                               dptr(self._labels), params, dptr(self._saved), dptr(go), dptr(dh), 0, grads,
+                               float(scale), dptr(scr), scr.numel()))
+        self.gradInput = [dh if h.dim() == 3 else dh[0], None]
+        return self.gradInput
+
+    def accGradParameters(self, input, gradOutput, scale=1.0):
+        pass
+
+    def alpha(self):
+        """Attention:alpha() (Attention.lua:241-243): (B, T, L) attention weights of the last forward."""
+        d = self._d
+        p = lib.s2s_attn_alpha(ctypes.byref(d), dptr(self._saved))
+        off = p - self._saved.data_ptr()
+        n = d.B * d.T * d.L
+        return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T, d.L)
+
+
+def nll_seed(logp, labels, normalize=False):
+    """timit/timit.lua:262-282: per-utterance nll and dlogp = -labelmask."""
+    B, T, O = logp.shape
+    lab = labels.to(torch.int32).contiguous()
+    nll = torch.empty(B, device=logp.device, dtype=torch.float32)
+    dlogp = torch.empty_like(logp)
+    check(lib.s2s_nll_seed(get_context(logp.device.index).handle, stream_ptr(), B, T, O, dptr(logp), dptr(lab),
+                           int(normalize), dptr(nll), dptr(dlogp)))
+    return nll, dlogp

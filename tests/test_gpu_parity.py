@@ -1,0 +1,202 @@
+"""GPU parity: libs2s_hip.so (through the C ABI / the host mirror) against the CPU oracle.
+
+Tolerance (fp32 vs the oracle's float64): for every output / gradient tensor,
+max|gpu - ref| <= RTOL * max|ref| with RTOL = 1e-4 (BASELINE.json north star: "outputs
+within 1e-4 rel of the Torch7 CPU reference").
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import s2s_oracle as orc
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-4
+
+
+def rel_err(g, r):
+    g = np.asarray(g, dtype=np.float64)
+    r = np.asarray(r, dtype=np.float64)
+    assert g.shape == r.shape, (g.shape, r.shape)
+    denom = max(np.abs(r).max(), 1e-30)
+    return float(np.abs(g - r).max() / denom)
+
+
+def assert_rel(g, r, name, rtol=RTOL):
+    e = rel_err(g, r)
+    assert np.isfinite(g).all(), f"{name}: non-finite values"
+    assert e <= rtol, f"{name}: max rel err {e:.3e} > {rtol:.0e}"
+
+
+@pytest.fixture(scope="module")
+def s2s():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import s2s_amd
+    return s2s_amd
+
+
+def cu(a, dtype=torch.float32):
+    return torch.tensor(np.ascontiguousarray(a), dtype=dtype, device="cuda")
+
+
+# --------------------------------------------------------------------------- GRU layer
+
+@pytest.mark.parametrize("B,L,D,H", [(3, 7, 20, 32), (5, 16, 123, 64), (17, 9, 64, 16)])
+@pytest.mark.parametrize("bidir", [False, True])
+def test_gru_layer_matches_oracle(s2s, B, L, D, H, bidir):
+    rng = np.random.default_rng(B * 100 + L)
+    x = rng.standard_normal((B, L, D))
+    cells = [s2s.GRU(D, H) for _ in range(2 if bidir else 1)]
+    Ws = [[w.double().numpy() for w in c.weight] for c in cells]
+    if bidir:
+        mod = s2s.BiRNN(cells[0], cells[1])
+    else:
+        mod = s2s.RNN(cells[0], reverse=(L % 2 == 1))
+    mod.cuda()
+    xs = cu(x)
+    y = mod.forward(xs).cpu().numpy()
+    dy = rng.standard_normal(y.shape)
+    mod.zeroGradParameters()
+    dx = mod.backward(xs, cu(dy), 0.5).cpu().numpy()
+    torch.cuda.synchronize()
+    revs = [False, True] if bidir else [mod.reverse]
+    dx_ref = np.zeros_like(x)
+    for i, (W, rev) in enumerate(zip(Ws, revs)):
+        yr, sv = orc.gru_seq_fwd(x, W[0], W[1], W[2], rev)
+        assert_rel(y[:, :, i * H:(i + 1) * H], yr, f"y[{i}]")
+        G = {k: np.zeros_like(v) for k, v in zip(("Wz", "Wr", "Wh"), W)}
+        dxr, _ = orc.gru_seq_bwd(x, W[0], W[1], W[2], sv, dy[:, :, i * H:(i + 1) * H], G, rev, 0.5)
+        dx_ref += dxr
+        for k, g in zip(("Wz", "Wr", "Wh"), cells[i].gradWeight):
+            assert_rel(g.cpu().numpy(), G[k], f"d{k}[{i}]")
+    assert_rel(dx, dx_ref, "dx")
+
+
+def test_gru_single_utterance_2d(s2s):
+    """2-D input = the reference's SGD mode (RNN.lua:122-124)."""
+    rng = np.random.default_rng(0)
+    cell = s2s.GRU(12, 16)
+    mod = s2s.RNN(cell, reverse=True).cuda()
+    x = rng.standard_normal((6, 12))
+    y = mod.forward(cu(x)).cpu().numpy()
+    W = [w.cpu().double().numpy() for w in cell.weight]
+    yr, _ = orc.gru_seq_fwd(x[None], *W, True)
+    assert y.shape == (6, 16)
+    assert_rel(y, yr[0], "y")
+
+
+# --------------------------------------------------------------------------- attention decoder
+
+ATT_CASES = [
+    # B, L, T, A, Sc, S, O, M, K, penalty
+    (3, 20, 5, 32, 48, 32, 7, 4, 3, 0.0),
+    (4, 33, 6, 64, 64, 48, 29, 8, 7, 0.0),
+    (2, 16, 4, 32, 32, 16, 5, 3, 2, 0.25),
+    (19, 8, 3, 16, 16, 16, 62, 5, 7, 0.0),
+]
+
+
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O,M,K,pen", ATT_CASES)
+def test_attention_decoder_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen):
+    rng = np.random.default_rng(L * 7 + T)
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=K, penalty=pen, numLayers=1)
+    dec_gru = s2s.GRU(S, S)
+    mlp = s2s.MaxoutMLP(S + A, M, K, O)
+    att = s2s.Attention(dec_gru, mlp, Sc, 10, 0, S, A, O, True, pen).cuda()
+    P = {n: t.cpu().double().numpy() for n, t in zip(
+        ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "dec.Wz", "dec.Wr", "dec.Wh", "Wm", "bm", "Wo",
+         "bo"), att.parameters()[0])}
+    h = rng.standard_normal((B, L, A)) * 0.5
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    hs = cu(h)
+    logp = att.forward([hs, cu(labels, torch.int32)]).cpu().numpy()
+    lref, cache = orc.attention_fwd(h, labels, P, cfg)
+    assert_rel(logp, lref, "logp")
+    assert_rel(att.alpha().cpu().numpy(), cache["alpha"], "alpha")
+    dlogp = rng.standard_normal(logp.shape)
+    att.zeroGradParameters()
+    dh = att.backward([hs, None], cu(dlogp), 0.5)[0].cpu().numpy()
+    G = orc.zeros_like_params(P)
+    dhr = orc.attention_bwd(P, cfg, cache, dlogp, G, 0.5)
+    assert_rel(dh, dhr, "dh")
+    for name, g in zip(P.keys(), att.parameters()[1]):
+        assert_rel(g.cpu().numpy(), G[name], "d" + name)
+
+
+def test_labelmask_input_equals_int_labels(s2s):
+    rng = np.random.default_rng(5)
+    B, L, T, A, Sc, S, O = 2, 12, 4, 32, 32, 16, 9
+    att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, 4, 3, O), Sc, 10, 0, S, A, O, True, 0.0).cuda()
+    h = cu(rng.standard_normal((B, L, A)))
+    labels = rng.integers(0, O, (B, T))
+    mask = np.zeros((B, T, O), np.float32)
+    np.put_along_axis(mask, labels[..., None], 1.0, 2)
+    a = att.forward([h, cu(labels, torch.int32)]).clone()
+    b = att.forward([h, cu(mask)])
+    assert torch.equal(a, b)
+
+
+# --------------------------------------------------------------------------- whole training step
+
+def _model_case(s2s, cfg_kw, B, L, T, seed=1234, graph=False):
+    cfg_o = orc.ModelConfig(**cfg_kw)
+    model = s2s.ChorowskiBaseline(s2s.ModelConfig(**cfg_kw), graph=graph)
+    P = orc.unflatten(model.params.cpu().double().numpy(), cfg_o)
+    x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=seed, pad=min(10, L // 4), eos=min(23, cfg_o.outputDepth - 1))
+    return cfg_o, model, P, x, labels
+
+
+def _check_step(model, cfg_o, P, x, labels, stream=None):
+    nll, logp = model.step(cu(x), cu(labels, torch.int32), stream=stream)
+    torch.cuda.synchronize()
+    nll_ref, G, lref, enc = orc.training_step(x, labels, P, cfg_o)
+    assert_rel(logp.cpu().numpy(), lref, "logp")
+    assert_rel(model.encoder_output().cpu().numpy(), enc, "encoder.output")
+    assert abs(float(nll.mean()) - nll_ref) <= RTOL * abs(nll_ref)
+    Gg = orc.unflatten(model.grads.cpu().double().numpy(), cfg_o)
+    for k in G:
+        assert_rel(Gg[k], G[k], "grad " + k)
+
+
+def test_model_step_small(s2s):
+    kw = dict(inputFrameSize=20, hiddenFrameSize=32, outputFrameSize=32, scoreDepth=48, stateDepth=32,
+              outputDepth=11, mlpDepth=6, maxoutWindow=3, numLayers=2)
+    cfg_o, model, P, x, labels = _model_case(s2s, kw, 5, 24, 7)
+    _check_step(model, cfg_o, P, x, labels)
+
+
+def test_model_step_chorowski_config2(s2s):
+    """BASELINE config 2 at full size: B=32, L=128, T=40, F=123, 3x BiGRU(256), Sc=512, O=62."""
+    cfg_o, model, P, x, labels = _model_case(s2s, {}, 32, 128, 40)
+    _check_step(model, cfg_o, P, x, labels)
+
+
+def test_model_step_librispeech_shape(s2s):
+    """config 4 shape class (F=80, O=29 chars), reduced L/T so the oracle stays in seconds."""
+    kw = dict(inputFrameSize=80, outputDepth=29)
+    cfg_o, model, P, x, labels = _model_case(s2s, kw, 4, 100, 30, seed=7)
+    _check_step(model, cfg_o, P, x, labels)
+
+
+def test_model_step_graph_replay_bitwise(s2s):
+    kw = dict(inputFrameSize=20, hiddenFrameSize=32, outputFrameSize=32, scoreDepth=48, stateDepth=32,
+              outputDepth=11, mlpDepth=6, maxoutWindow=3, numLayers=2)
+    cfg_o, model, P, x, labels = _model_case(s2s, kw, 4, 20, 6, graph=True)
+    st = torch.cuda.Stream()
+    xs, ls = cu(x), cu(labels, torch.int32)
+    with torch.cuda.stream(st):
+        outs = []
+        for _ in range(3):
+            nll, logp = model.step(xs, ls, stream=st)
+            outs.append((nll.clone(), logp.clone(), model.grads.clone()))
+    st.synchronize()
+    for o in outs[1:]:
+        for a, b in zip(outs[0], o):
+            assert torch.equal(a, b)
+    eager = s2s.ChorowskiBaseline(s2s.ModelConfig(**kw))
+    eager.params.copy_(model.params)
+    nll2, logp2 = eager.step(xs, ls)
+    torch.cuda.synchronize()
+    assert torch.equal(logp2, outs[0][1]) and torch.equal(eager.grads, outs[0][2])
