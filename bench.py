@@ -1,0 +1,174 @@
+"""Throughput of the attention-seq2seq training step (forward + NLL seed + backward) on MI355X.
+
+Metric (BASELINE.json): log-mel frames/s fwd+bwd, Chorowski TIMIT baseline; frames = N_gpu * B * L
+per step.  Workload = BASELINE config 2: B=32 utterances/GPU, L=128 frames,
+T=40 labels, F=123 (40 log-mel + energy, +d +dd), 3 x BiGRU(256), scoreDepth 512, GRU(256) decoder,
+Maxout(768 -> 64, 7), 62 classes, fp32 (random-init weights, synthetic N(0,1) features).
+Data parallel: one process per GPU, each its own B utterances (weak scaling); the flat fp32
+gradient is summed over ranks with RCCL all-reduce inside the timed step (§8e).  The optimizer
+step is excluded (§8d).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, os.path.join(ROOT, "seq2seq-attention-asr_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+CONFIGS = {
+    # name: (model kwargs, B per GPU, L, T)
+    "timit_chorowski_b32": (dict(), 32, 128, 40),
+    "librispeech_chorowski_b32": (dict(inputFrameSize=80, outputDepth=29), 32, 400, 200),
+}
+PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
+PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def flops_per_utterance(cfg, L, T):
+    """fwd = 2 [L (P_enc + A Sc) + T P_step + T L (2 Sc + A)], fwd+bwd = 3 x fwd."""
+    H = [cfg.hiddenFrameSize] * (cfg.numLayers - 1) + [cfg.outputFrameSize]
+    D = [cfg.inputFrameSize] + [2 * h for h in H[:-1]]
+    p_enc = sum(2 * 3 * h * (h + d) for h, d in zip(H, D))
+    A, Sc, S, O, M, k = cfg.annotationDepth, cfg.scoreDepth, cfg.stateDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    p_step = S * Sc + O * S + A * S + 2 * S * S + 3 * S * 2 * S + (S + A) * M * k + M * O
+    fwd = 2 * (L * (p_enc + A * Sc) + T * p_step + T * L * (2 * Sc + A))
+    return 3 * fwd
+
+
+def cpu_worker(args):
+    """One reference-semantics utterance (B=1, 2-D, fp32) through the oracle on one core."""
+    seed, L, T, kw = args
+    import numpy as np
+    from oracle import s2s_oracle as orc
+    cfg = orc.ModelConfig(**kw)
+    P = orc.init_params(cfg, seed=1234, dtype=np.float32)
+    x, lab = orc.synthetic_batch(cfg, 1, L, T, seed=seed, dtype=np.float32)
+    t = time.perf_counter()
+    orc.training_step(x, lab, P, cfg)
+    return time.perf_counter() - t
+
+
+def cpu_baseline(kw, L, T, seconds_budget):
+    """CPU restatement (oracle/, numpy fp32, per-utterance like timit/timit.lua:240-295) on the host's
+    cores: one single-threaded worker process per core, each running whole utterances."""
+    import multiprocessing as mp
+    for v in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS"):
+        os.environ[v] = "1"
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    ctx = mp.get_context("spawn")
+    with ctx.Pool(cores) as pool:
+        pool.map(cpu_worker, [(0, 16, 4, kw)] * cores)          # warm-up (imports)
+        t1 = pool.map(cpu_worker, [(1, L, T, kw)])[0]            # one utterance alone -> size the sample
+        per_core = max(1, int(seconds_budget / max(t1, 1e-3)))
+        n = per_core * cores
+        t = time.perf_counter()
+        pool.map(cpu_worker, [(i + 2, L, T, kw) for i in range(n)])
+        wall = time.perf_counter() - t
+    return {"value": round(n * L / wall, 1), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{n} utterances (L={L}, T={T}, B=1 each, fp32) of the same model, oracle/s2s_oracle.py "
+                      f"(numpy restatement of the Torch7 path, not Torch7), {cores} single-threaded processes, "
+                      f"{wall:.1f} s wall"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="timit_chorowski_b32", choices=sorted(CONFIGS))
+    ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import s2s_amd
+    from s2s_amd import profile as s2s_profile
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    kw, B, L, T = CONFIGS[args.config]
+    cfg = s2s_amd.ModelConfig(**kw)
+    model = s2s_amd.ChorowskiBaseline(cfg, graph=not args.no_graph, seed=1234)
+    g = torch.Generator(device="cpu").manual_seed(1234 + rank)
+    x = torch.randn((B, L, cfg.inputFrameSize), generator=g)
+    x[:, :10] = 0
+    x[:, L - 10:] = 0
+    eos = 23 if cfg.outputDepth > 23 else cfg.outputDepth - 1
+    labels = torch.randint(0, cfg.outputDepth - 1, (B, T), generator=g)
+    labels[labels >= eos] += 1
+    labels[:, -1] = eos
+    x = x.cuda()
+    labels = labels.to(torch.int32).cuda()
+    stream = torch.cuda.Stream()
+    scale = 1.0 / (B * world)
+
+    def step():
+        model.step(x, labels, scale=scale, stream=stream)
+        if world > 1:
+            dist.all_reduce(model.grads)
+
+    with torch.cuda.stream(stream):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / args.steps
+    frames_per_step = world * B * L
+    value = frames_per_step / (ms / 1000.0)
+
+    flop_step = flops_per_utterance(cfg, L, T) * B
+    out = {
+        "metric": "log-mel frames/sec fwd+bwd, Chorowski TIMIT baseline",
+        "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp32", "data": "synthetic (N(0,1) log-mel-shaped features, uniform labels, random-init weights)",
+        "config": {"workload": f"BASELINE config 2: {args.config}", "model": "timit/model_chorowski_baseline.lua",
+                   "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
+                   "feat_dim": cfg.inputFrameSize, "parallelism": f"dp{world}",
+                   "launch": "eager" if args.no_graph else "hipGraph replay",
+                   "flop_per_step_per_gpu": flop_step},
+        "step_tflops_per_gpu": round(flop_step / (ms / 1000.0) / 1e12, 3),
+    }
+    if rank == 0 and not args.no_kernel_timing:
+        with torch.cuda.stream(stream):
+            out["roofline"], out["kernels"] = s2s_profile.dominant_kernel_roofline(
+                model, x, labels, stream, PEAK_FP32_MFMA_TFLOPS, PEAK_HBM_GBS)
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(kw, L, T, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -121,6 +121,13 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
  * (encoder.output, timit/timit.lua:397). */
 const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace);
 
+/* ---------------------------------------------------------------- live kernel timing
+ * s2s_prof_enable(1): every subsequent eager (non-captured) launch is bracketed by two
+ * hipEvents on its stream and tagged with its kernel family's algorithmic flops/bytes.
+ * s2s_prof_collect: synchronises, writes "name\tlaunches\ttotal_us\tflops\tbytes\n" per family. */
+int s2s_prof_enable(int on);
+int s2s_prof_collect(char* buf, size_t cap);
+
 /* ---------------------------------------------------------------- data parallel (RCCL)
  * One process per GPU.  Rank 0 calls s2s_comm_unique_id, the bytes are shared out of band,
  * every rank calls s2s_comm_init; s2s_allreduce_sum sums a float buffer in place over xGMI. */

@@ -673,6 +673,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc));
   hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  ProfScope ps(st, "dec_fwd_steps", 0.0, 0.0);
   for (int t = 0; t < T; ++t) {
     k.t = t;
     hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
@@ -727,6 +728,7 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A));
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  ProfScope ps(st, "dec_bwd_steps", 0.0, 0.0);
   for (int t = T - 1; t >= 0; --t) {
     k.t = t;
     hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -20,6 +21,52 @@ namespace s2s {
 static thread_local std::string g_err;
 void set_error(const std::string& msg) { g_err = msg; }
 const char* get_error() { return g_err.c_str(); }
+
+// ------------------------------------------------------------ live kernel timing
+struct ProfRec {
+  const char* name;
+  double flops, bytes;
+  hipEvent_t a, b;
+};
+static bool g_prof = false;
+static std::vector<ProfRec> g_recs;
+static std::vector<hipEvent_t> g_pool;
+static std::mutex g_prof_mu;
+
+static hipEvent_t prof_event() {
+  if (!g_pool.empty()) {
+    hipEvent_t e = g_pool.back();
+    g_pool.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  if (hipEventCreate(&e) != hipSuccess) return nullptr;
+  return e;
+}
+static bool capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return true;
+  return cs != hipStreamCaptureStatusNone;
+}
+bool prof_on() { return g_prof; }
+void prof_begin(hipStream_t st, const char* name, double flops, double bytes) {
+  if (capturing(st)) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  ProfRec r{name, flops, bytes, prof_event(), nullptr};
+  if (!r.a) return;
+  (void)hipEventRecord(r.a, st);
+  g_recs.push_back(r);
+}
+void prof_end(hipStream_t st) {
+  if (capturing(st)) return;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  for (auto it = g_recs.rbegin(); it != g_recs.rend(); ++it)
+    if (it->b == nullptr) {
+      it->b = prof_event();
+      if (it->b) (void)hipEventRecord(it->b, st);
+      return;
+    }
+}
 
 }  // namespace s2s
 
@@ -226,6 +273,54 @@ int model_step_impl(hipStream_t st, const s2s_model_dims* d, const float* params
 extern "C" {
 
 int s2s_version(void) { return 1; }
+
+int s2s_prof_enable(int on) {
+  s2s::g_prof = on != 0;
+  return 0;
+}
+
+// Aggregates every recorded launch per kernel family (after synchronising on its events):
+// one line per family "name<TAB>launches<TAB>total_us<TAB>flops<TAB>bytes\n", then clears.
+int s2s_prof_collect(char* buf, size_t cap) {
+  using namespace s2s;
+  std::lock_guard<std::mutex> lk(g_prof_mu);
+  struct Agg {
+    std::string name;
+    long n;
+    double us, flops, bytes;
+  };
+  std::vector<Agg> aggs;
+  for (auto& r : g_recs) {
+    float ms = 0.f;
+    if (r.b) {
+      S2S_CHECK_HIP(hipEventSynchronize(r.b));
+      S2S_CHECK_HIP(hipEventElapsedTime(&ms, r.a, r.b));
+    }
+    Agg* a = nullptr;
+    for (auto& x : aggs)
+      if (x.name == r.name) a = &x;
+    if (!a) {
+      aggs.push_back({r.name, 0, 0.0, 0.0, 0.0});
+      a = &aggs.back();
+    }
+    a->n += 1;
+    a->us += 1000.0 * ms;
+    a->flops += r.flops;
+    a->bytes += r.bytes;
+    g_pool.push_back(r.a);
+    if (r.b) g_pool.push_back(r.b);
+  }
+  g_recs.clear();
+  std::string out;
+  for (auto& a : aggs) {
+    char line[256];
+    snprintf(line, sizeof(line), "%s\t%ld\t%.3f\t%.6e\t%.6e\n", a.name.c_str(), a.n, a.us, a.flops, a.bytes);
+    out += line;
+  }
+  S2S_REQUIRE(buf != nullptr && cap > out.size(), "prof: buffer too small");
+  std::memcpy(buf, out.c_str(), out.size() + 1);
+  return 0;
+}
 const char* s2s_last_error(void) { return s2s::get_error(); }
 
 int s2s_ctx_create(int device, s2s_ctx** out) {

@@ -161,6 +161,13 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
     gn = gn > (q.N + BN - 1) / BN ? gn : (q.N + BN - 1) / BN;
   }
   if (used == 0) return 0;
+  double flops = 0, bytes = 0;
+  for (int i = 0; i < used; ++i) {
+    const GemmProblem& q = args.p[i];
+    flops += 2.0 * q.M * q.N * q.K;
+    bytes += 4.0 * ((double)q.M * q.K + (double)q.K * q.N + (double)q.M * q.N * (q.beta != 0.f ? 2 : 1));
+  }
+  ProfScope ps(st, "gemm_f32", flops, bytes);
   dim3 grid(gn, gm, used);
   if (!transA && !transB) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, st, args);
   else if (!transA && transB) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, st, args);

@@ -16,6 +16,10 @@
 // Saved activations per direction: sv (B, L, 5H) = z | r | hh | h_{t-1} | q.
 #include "gru.h"
 
+#include <cstdlib>
+#include <cstring>
+
+#include "gru_persist.h"
 #include "skinny.h"
 
 namespace s2s {
@@ -217,6 +221,14 @@ int launch_pack(hipStream_t st, const float* Wz, const float* Wr, const float* W
 
 }  // namespace
 
+// S2S_GRU_MODE=step forces the per-step launch path (A/B and fallback); default: persistent
+// whenever the shape is supported.
+static bool use_persistent(int nd, int B, int H) {
+  const char* m = std::getenv("S2S_GRU_MODE");
+  if (m && std::strcmp(m, "step") == 0) return false;
+  return gru_persist_supported(nd, B, H);
+}
+
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   Bump bp{nullptr, 0, 0};
   for (int d = 0; d < ndir; ++d) {
@@ -229,6 +241,7 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   }
   bp.take<float>(3L * ndir * H * D);             // Wx (both dirs)
   bp.take<float>((long)B * L * 3 * ndir * H);    // xp or dA (both dirs)
+  bp.take<char>(gru_persist_sync_bytes(B, H));   // persistent-kernel granule buffers
   return bp.off + 256;
 }
 
@@ -251,6 +264,7 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   }
   float* Wx = bp.take<float>(3L * nd * H * D);
   float* xp = bp.take<float>((long)B * L * 3 * nd * H);
+  char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   for (int d = 0; d < nd; ++d)
     S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Uzr[d], Uh[d], nullptr, nullptr,
                         Wx + 3L * d * H * D));
@@ -262,7 +276,17 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   a.B = B;
   a.L = L;
   a.H = H;
+  if (use_persistent(nd, B, H)) {
+    GruPersistFwd f{};
+    f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 3L * nd * H; f.ldy = io.ldy;
+    for (int d = 0; d < nd; ++d) {
+      f.xp[d] = xp + 3L * d * H; f.Uzr[d] = Uzr[d]; f.Uh[d] = Uh[d]; f.y[d] = io.y[d]; f.sv[d] = io.saved[d];
+      f.reverse[d] = io.reverse[d];
+    }
+    return gru_persist_fwd(st, f, sync);
+  }
   const dim3 g1(2 * H / 16, (B + 15) / 16, nd), g2(H / 16, (B + 15) / 16, nd);
+  ProfScope ps(st, "gru_fwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);
   for (int s = 0; s < L; ++s) {
     a.step = s;
     hipLaunchKernelGGL(gru_fwd_p1, g1, dim3(256), 0, st, a);
@@ -289,6 +313,7 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
   }
   float* Wx = bp.take<float>(3L * nd * H * D);
   float* dA = bp.take<float>((long)B * L * 3 * nd * H);
+  char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   const long ldA = 3L * nd * H;
   for (int d = 0; d < nd; ++d)
     S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, nullptr, nullptr, UhT[d], UzrT[d],
@@ -300,14 +325,25 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
   a.B = B;
   a.L = L;
   a.H = H;
-  hipLaunchKernelGGL(gru_bwd_init, dim3((B * H + 255) / 256, nd), dim3(256), 0, st, a);
-  const dim3 g1(H / 16, (B + 15) / 16, nd);
-  for (int s = L - 1; s >= 0; --s) {
-    a.step = s;
-    hipLaunchKernelGGL(gru_bwd_p1, g1, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(gru_bwd_p2, g1, dim3(256), 0, st, a);
+  if (use_persistent(nd, B, H)) {
+    GruPersistBwd f{};
+    f.ndir = nd; f.B = B; f.L = L; f.H = H; f.lddy = gr.lddy; f.ldA = ldA;
+    for (int d = 0; d < nd; ++d) {
+      f.UhT[d] = UhT[d]; f.UzrT[d] = UzrT[d]; f.sv[d] = io.saved[d]; f.dy[d] = gr.dy[d]; f.dA[d] = dA + 3L * d * H;
+      f.reverse[d] = io.reverse[d];
+    }
+    S2S_TRY(gru_persist_bwd(st, f, sync));
+  } else {
+    ProfScope ps(st, "gru_bwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);
+    hipLaunchKernelGGL(gru_bwd_init, dim3((B * H + 255) / 256, nd), dim3(256), 0, st, a);
+    const dim3 g1(H / 16, (B + 15) / 16, nd);
+    for (int s = L - 1; s >= 0; --s) {
+      a.step = s;
+      hipLaunchKernelGGL(gru_bwd_p1, g1, dim3(256), 0, st, a);
+      hipLaunchKernelGGL(gru_bwd_p2, g1, dim3(256), 0, st, a);
+    }
+    S2S_CHECK_HIP(hipGetLastError());
   }
-  S2S_CHECK_HIP(hipGetLastError());
   // dx (+)= dA (B*L, 3*nd*H) . Wx (3*nd*H, D)   (RNN.lua:196 gradInput; both directions summed,
   // which is what the encoder graph's fan-out of the layer input accumulates)
   if (gr.dx)

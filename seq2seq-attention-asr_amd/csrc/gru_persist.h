@@ -1,0 +1,34 @@
+#pragma once
+#include "s2s_common.h"
+
+namespace s2s {
+
+struct GruPersistFwd {
+  int ndir, B, L, H;
+  const float* xp[2];
+  long ldxp;
+  const float* Uzr[2];
+  const float* Uh[2];
+  float* y[2];
+  long ldy;
+  float* sv[2];
+  int reverse[2];
+};
+struct GruPersistBwd {
+  int ndir, B, L, H;
+  const float* UhT[2];
+  const float* UzrT[2];
+  float* sv[2];
+  const float* dy[2];
+  long lddy;
+  float* dA[2];
+  long ldA;
+  int reverse[2];
+};
+
+bool gru_persist_supported(int ndir, int B, int H);
+size_t gru_persist_sync_bytes(int B, int H);
+int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync);
+int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync);
+
+}  // namespace s2s

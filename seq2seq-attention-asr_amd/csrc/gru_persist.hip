@@ -1,0 +1,382 @@
+// Persistent GRU layer recurrence: the whole L-step sweep of one bidirectional layer
+// (both directions) in ONE launch instead of 2*L launches.
+//
+// Same arithmetic and summation order as the per-step kernels in gru.hip (bitwise-equal
+// results, tested), reorganised for MI355X:
+//   * workgroup = one fixed (16-unit column tile, 16-utterance row tile) task for the whole
+//     sweep; its weight slices live in VGPRs (per wave: its K-quarter of 16 rows, H/64 float4
+//     per matrix), so no weight byte is re-read per step;
+//   * the two all-to-all seams of a GRU step (h_{t-1} -> [z|r], q = r*h -> hh) are in-launch
+//     hand-offs in the "data is the flag" form (MI355X guide §6 Guideline 16, R2): every
+//     handed-off fp32 value travels as ONE 8-byte {value, tag} granule stored write-through
+//     (sc1); a consumer wave re-reads exactly the granules its MFMA operands need (16-byte sc1
+//     loads) until every tag equals the step's epoch -- no flags, fences or counters;
+//   * 16-utterance row tiles are independent chains (a tile only waits on its own rows);
+//     granule buffers are double-buffered by step parity (a slot is rewritten two steps later,
+//     which the dependency chain orders after every read of it) and zeroed by a memset node
+//     before each launch; epochs are 1 + step index within the launch;
+//   * operands that come from earlier kernels (x-projections, saved activations, dy) are
+//     loaded before the wait so their latency hides under it;
+//   * every wait is bounded: on timeout a wave raises the launch's abort word, every waiting
+//     wave sees it within 64 polls, all workgroups leave at their next barrier.
+#include "gru.h"
+#include "gru_persist.h"
+#include "skinny.h"
+
+namespace s2s {
+
+namespace {
+
+constexpr unsigned kSpinLimit = 1u << 21;
+
+struct PDir {
+  const float* xp;
+  long ldxp;
+  const float* Wa;  // fwd: Uzr (2H,H)   bwd: UhT (H,H)
+  const float* Wb;  // fwd: Uh  (H,H)    bwd: UzrT (H,2H)
+  float* y;
+  long ldy;
+  float* sv;  // (B, L, 5H)
+  const float* dy;
+  long lddy;
+  float* dA;
+  long ldA;
+  int reverse;
+  // granule buffers, each [2 slots][B][H] x 8 bytes
+  unsigned long long* g0;  // fwd: h      bwd: da_z
+  unsigned long long* g1;  // fwd: q      bwd: da_r
+  unsigned long long* g2;  //             bwd: da_h
+};
+struct PArgs {
+  PDir d[2];
+  int B, L, H, MT, nwg;  // nwg = workgroups per direction
+  unsigned* abort_word;
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ void put_granule(unsigned long long* g, float v, unsigned tag) {
+  const unsigned long long x = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
+  __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float get_granule(const unsigned long long* g) {
+  return __uint_as_float((unsigned)__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+// Sweep: load this lane's operand granules (NC chunks x 4 consecutive k) of one row until
+// every tag == tag.  rs/off: buffer + byte offset of granule (row, k = 0).  Returns false on
+// abort/timeout (the operands are then garbage; the caller leaves at its next barrier).
+template <int NC>
+__device__ __forceinline__ bool sweep(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, unsigned tag,
+                                      int wave, int lane, unsigned* abort_word) {
+  const long kq = 4 * (lane >> 4);
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const long off = row_off + 8 * (wave * 16 + 64 * i + kq);
+      const uint4 p0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+      const uint4 p1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off + 16, 0, 16));
+      ok = ok && p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
+      a[i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z));
+    }
+    if (__all(ok)) return true;
+    ++spins;
+    if ((spins & 63u) == 0) {
+      if (spins > kSpinLimit ||
+          __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// same chunk order / accumulator split as skinny_wave (bitwise-equal sums)
+template <int NC>
+__device__ __forceinline__ floatx4 mfma_chunks(const float4 (&a)[NC], const float4 (&w)[NC]) {
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i + 1 < NC; i += 2) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].x, w[i + 1].x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].y, w[i + 1].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].z, w[i + 1].z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].w, w[i + 1].w, acc1, 0, 0, 0);
+  }
+  if (NC & 1) {
+    constexpr int i = NC - 1;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
+template <int NC>
+__device__ __forceinline__ void load_w(float4 (&w)[NC], const float* row, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    w[i] = *reinterpret_cast<const float4*>(row + wave * 16 + 64 * i + 4 * (lane >> 4));
+}
+
+// cross-wave sum + abort agreement at the same barrier
+__device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds, bool ok, floatx4 acc, int wave,
+                                                 int lane, int tid, bool* aborted) {
+  if (!ok) *abort_lds = 1;
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  *aborted = *abort_lds != 0;
+  return s;
+}
+
+// ------------------------------------------------------------------------------ forward
+// grid = ndir * nwg, nwg = (2H/16) * MT; task (c1, mt) = (w % (2H/16), w / (2H/16)).
+// z-column workgroups (c1 < H/16) also own the candidate tile of the same units.
+template <int NC>  // NC = H / 64
+__global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
+  __shared__ SkinnyRed red;
+  __shared__ int abort_lds;
+  const int H = a.H, B = a.B, L = a.L;
+  const int dir = blockIdx.x / a.nwg, w = blockIdx.x % a.nwg;
+  const PDir& g = a.d[dir];
+  const int ncol = 2 * H / 16;
+  const int c1 = w % ncol, mt = w / ncol;
+  const bool isz = c1 < H / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = mt * 16;
+  if (tid == 0) abort_lds = 0;
+
+  float4 w1[NC], w2[NC];
+  load_w(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
+  if (isz) load_w(w2, g.Wb + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
+
+  const __amdgpu_buffer_rsrc_t hg = rsrc_of(g.g0), qg = rsrc_of(g.g1);
+  const long slot = (long)B * H;  // granules per slot
+  const int br = min(b0 + (lane & 15), B - 1);
+  const int ob = b0 + (tid >> 4), on = c1 * 16 + (tid & 15);  // this thread's output
+  const bool live = ob < B;
+  float zreg = 0.f, hreg = 0.f;
+  bool aborted = false;
+
+  for (int s = 0; s < L; ++s) {
+    const int t = g.reverse ? L - 1 - s : s;
+    const long row = (long)ob * L + t;
+    // ---- p1: [z | r] = sig(Uzr h_{t-1} + xp)
+    const float xpv = live ? g.xp[row * g.ldxp + on] : 0.f;
+    floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+    bool ok = true;
+    if (s > 0) {
+      float4 av[NC];
+      ok = sweep<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
+      acc = mfma_chunks<NC>(av, w1);
+    }
+    float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
+    if (aborted) return;
+    if (live) {
+      const float gate = sigmoidf_(sum + xpv);
+      float* sv = g.sv + row * 5 * H;
+      if (isz) {
+        sv[on] = gate;
+        zreg = gate;
+      } else {
+        const int j = on - H;
+        const float hp = s > 0 ? get_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
+        const float q = gate * hp;
+        sv[H + j] = gate;
+        sv[3 * H + j] = hp;
+        sv[4 * H + j] = q;
+        put_granule(g.g1 + (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1));
+      }
+    }
+    if (!isz) continue;
+    // ---- p2: hh = tanh(Uh q + xp_h); h = (1-z) h_{t-1} + z hh
+    const float xph = live ? g.xp[row * g.ldxp + 2 * H + on] : 0.f;
+    acc = floatx4{0.f, 0.f, 0.f, 0.f};
+    ok = true;
+    if (s > 0) {
+      float4 av[NC];
+      ok = sweep<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), (unsigned)(s + 1), wave, lane, a.abort_word);
+      acc = mfma_chunks<NC>(av, w2);
+    }
+    sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
+    if (aborted) return;
+    if (live) {
+      const float hh = tanhf(sum + xph);
+      const float hp = hreg;
+      g.sv[row * 5 * H + 2 * H + on] = hh;
+      hreg = (-zreg + 1.0f) * hp + zreg * hh;
+      g.y[row * g.ldy + on] = hreg;
+      put_granule(g.g0 + (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1));
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ backward
+// grid = ndir * nwg, nwg = (H/16) * MT; task (c, mt) for both seams.
+template <int NC>
+__global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
+  __shared__ SkinnyRed red;
+  __shared__ int abort_lds;
+  const int H = a.H, B = a.B, L = a.L;
+  const int dir = blockIdx.x / a.nwg, w = blockIdx.x % a.nwg;
+  const PDir& g = a.d[dir];
+  const int ncol = H / 16;
+  const int c = w % ncol, mt = w / ncol;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = mt * 16;
+  if (tid == 0) abort_lds = 0;
+
+  float4 wh[NC], wzr[2 * NC];
+  load_w(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
+  load_w(wzr, g.Wb + (long)(c * 16 + (lane & 15)) * 2 * H, wave, lane);
+  const __amdgpu_buffer_rsrc_t zg = rsrc_of(g.g0), rg = rsrc_of(g.g1), hg = rsrc_of(g.g2);
+  const long slot = (long)B * H;
+  const int br = min(b0 + (lane & 15), B - 1);
+  const int ob = b0 + (tid >> 4), ok_ = c * 16 + (tid & 15);
+  const bool live = ob < B;
+  float dhc = 0.f, dhp = 0.f;
+  bool aborted = false;
+
+  // gate gradients of dh = dy_t + carry at time t, published with epoch `tag` into slot `sl`
+  auto gate = [&](int t, float dh, unsigned tag, int sl) {
+    const long row = (long)ob * L + t;
+    const float* sv = g.sv + row * 5 * H;
+    const float z = sv[ok_], hh = sv[2 * H + ok_], hp = sv[3 * H + ok_];
+    const float daz = dh * (hh - hp) * (z * (1.0f - z));
+    const float dah = (dh * z) * (1.0f - hh * hh);
+    g.dA[row * g.ldA + ok_] = daz;
+    g.dA[row * g.ldA + 2 * H + ok_] = dah;
+    put_granule(g.g0 + sl * slot + (long)ob * H + ok_, daz, tag);
+    put_granule(g.g2 + sl * slot + (long)ob * H + ok_, dah, tag);
+  };
+
+  const int tl = g.reverse ? 0 : L - 1;
+  if (live) gate(tl, g.dy[((long)ob * L + tl) * g.lddy + ok_], 1u, 0);
+
+  for (int p = 0; p < L; ++p) {
+    const int s = L - 1 - p;
+    const int t = g.reverse ? L - 1 - s : s;
+    const long row = (long)ob * L + t;
+    const unsigned tag = (unsigned)(p + 1);
+    const int sl = p & 1;
+    // ---- p1: dq = Uh^T da_h -> da_r, partial dh_{t-1}
+    float z = 0.f, r = 0.f, hp = 0.f, dyv = 0.f;
+    if (live) {
+      const float* sv = g.sv + row * 5 * H;
+      z = sv[ok_]; r = sv[H + ok_]; hp = sv[3 * H + ok_];
+      dyv = g.dy[row * g.lddy + ok_];
+    }
+    float4 av[NC];
+    bool ok = sweep<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+    floatx4 acc = mfma_chunks<NC>(av, wh);
+    const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
+    if (aborted) return;
+    if (live) {
+      const float dar = (dq * hp) * (r * (1.0f - r));
+      g.dA[row * g.ldA + H + ok_] = dar;
+      put_granule(g.g1 + sl * slot + (long)ob * H + ok_, dar, tag);
+      const float dh = dyv + dhc;
+      dhp = dh * (-z + 1.0f) + dq * r;
+    }
+    // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
+    const int tn = g.reverse ? t + 1 : t - 1;
+    const float dyn = (live && s > 0) ? g.dy[((long)ob * L + tn) * g.lddy + ok_] : 0.f;
+    float4 azr[2 * NC];
+    {
+      float4 az[NC], ar[NC];
+      ok = sweep<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      ok = ok && sweep<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      // chunk i of the K = 2H product: i < NC reads da_z, i >= NC reads da_r (H % 64 == 0)
+#pragma unroll
+      for (int i = 0; i < NC; ++i) { azr[i] = az[i]; azr[NC + i] = ar[i]; }
+    }
+    acc = mfma_chunks<2 * NC>(azr, wzr);
+    const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
+    if (aborted) return;
+    if (live && s > 0) {
+      dhc = dhp + sm;
+      gate(tn, dyn + dhc, tag + 1, sl ^ 1);
+    }
+  }
+}
+
+template <int NC>
+int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
+  const dim3 grid(ndir * a.nwg);
+  if (fwd) hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(256), 0, st, a);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int launch(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
+  switch (a.H / 64) {
+    case 1: return launch_nc<1>(st, a, ndir, fwd);
+    case 2: return launch_nc<2>(st, a, ndir, fwd);
+    case 4: return launch_nc<4>(st, a, ndir, fwd);
+    case 8: return launch_nc<8>(st, a, ndir, fwd);
+  }
+  set_error("gru persistent: unsupported H");
+  return 2;
+}
+
+}  // namespace
+
+bool gru_persist_supported(int ndir, int B, int H) {
+  if (!(H == 64 || H == 128 || H == 256 || H == 512)) return false;
+  const int MT = (B + 15) / 16;
+  const long wgs = (long)ndir * (2 * H / 16) * MT;
+  return wgs <= 512;  // all workgroups must be co-resident (256 CUs, >= 2 per CU at this footprint)
+}
+
+size_t gru_persist_sync_bytes(int B, int H) { return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H; }
+
+static void carve_granules(char* sync, int B, int H, unsigned** abort_word, unsigned long long* (&g)[2][3]) {
+  *abort_word = reinterpret_cast<unsigned*>(sync);
+  unsigned long long* p = reinterpret_cast<unsigned long long*>(sync + 256);
+  for (int d = 0; d < 2; ++d)
+    for (int k = 0; k < 3; ++k) {
+      g[d][k] = p;
+      p += 2L * B * H;
+    }
+}
+
+int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
+  PArgs a{};
+  const int MT = (f.B + 15) / 16;
+  unsigned long long* gr[2][3];
+  carve_granules(static_cast<char*>(sync), f.B, f.H, &a.abort_word, gr);
+  for (int d = 0; d < f.ndir; ++d)
+    a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
+                  gr[d][0], gr[d][1], gr[d][2]};
+  a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
+  S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(f.B, f.H), st));
+  ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
+               4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
+  return launch(st, a, f.ndir, true);
+}
+
+int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
+  PArgs a{};
+  const int MT = (b.B + 15) / 16;
+  unsigned long long* gr[2][3];
+  carve_granules(static_cast<char*>(sync), b.B, b.H, &a.abort_word, gr);
+  for (int d = 0; d < b.ndir; ++d)
+    a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
+                  b.reverse[d], gr[d][0], gr[d][1], gr[d][2]};
+  a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
+  S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(b.B, b.H), st));
+  ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
+               4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
+  return launch(st, a, b.ndir, false);
+}
+
+}  // namespace s2s

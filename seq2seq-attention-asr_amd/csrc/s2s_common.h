@@ -85,6 +85,24 @@ int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd,
 // dst[i] = alpha * src[i] + beta * dst[i]
 int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alpha, float beta);
 
+// ---------------------------------------------------------------- live kernel timing
+// When enabled (s2s_prof_enable) and the stream is not being captured, every launch site
+// brackets its kernel with two hipEvents and records the kernel family's ALGORITHMIC flops
+// and bytes for that launch; s2s_prof_collect aggregates per family.  Off by default.
+bool prof_on();
+void prof_begin(hipStream_t st, const char* name, double flops, double bytes);
+void prof_end(hipStream_t st);
+struct ProfScope {
+  hipStream_t st;
+  bool on;
+  ProfScope(hipStream_t s, const char* name, double flops, double bytes) : st(s), on(prof_on()) {
+    if (on) prof_begin(st, name, flops, bytes);
+  }
+  ~ProfScope() {
+    if (on) prof_end(st);
+  }
+};
+
 // ---------------------------------------------------------------- workspace bump allocator
 struct Bump {
   char* base;

@@ -55,6 +55,8 @@ SIGNATURES = [
     ("s2s_model_step", c_int, [c_void_p, c_void_p, P(s2s_model_dims), c_void_p, c_void_p, c_void_p, c_void_p,
                                c_float, c_int, c_void_p, c_void_p, c_void_p, c_size_t]),
     ("s2s_model_encoder_output", c_void_p, [P(s2s_model_dims), c_void_p]),
+    ("s2s_prof_enable", c_int, [c_int]),
+    ("s2s_prof_collect", c_int, [ctypes.c_char_p, c_size_t]),
     ("s2s_comm_unique_id", c_int, [c_void_p]),
     ("s2s_comm_init", c_int, [c_void_p, c_void_p, c_int, c_int]),
     ("s2s_allreduce_sum", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),

@@ -1,0 +1,64 @@
+"""Live per-kernel timing (HIP events inside libs2s_hip.so, s2s_prof_*) for bench.py's roofline."""
+import ctypes
+
+from ._lib import check, lib
+from .nn import Context
+
+# kernel family -> roofline it is priced against
+BOUND = {"gemm_f32": "mfma", "gru_fwd_persist": "mfma", "gru_bwd_persist": "mfma"}
+
+
+def collect():
+    buf = ctypes.create_string_buffer(1 << 16)
+    check(lib.s2s_prof_collect(buf, len(buf)))
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, n, us, flops, nbytes = line.split("\t")
+        out[name] = {"launches": int(n), "total_us": float(us), "flops": float(flops), "bytes": float(nbytes)}
+    return out
+
+
+def profile_step(model, x, labels, stream, reps=3):
+    """Eager (un-captured) training steps with event timing on; returns per-family aggregates
+    averaged over `reps` steps."""
+    graph_ctx = model.ctx
+    model.ctx = Context(model.device.index, graph=False)
+    try:
+        model.step(x, labels, stream=stream)  # warm
+        stream.synchronize()
+        check(lib.s2s_prof_enable(1))
+        collect()
+        for _ in range(reps):
+            model.step(x, labels, stream=stream)
+        stream.synchronize()
+        agg = collect()
+    finally:
+        lib.s2s_prof_enable(0)
+        model.ctx = graph_ctx
+    for v in agg.values():
+        for k in ("launches", "total_us", "flops", "bytes"):
+            v[k] = v[k] / reps
+    return agg
+
+
+def dominant_kernel_roofline(model, x, labels, stream, peak_tflops, peak_gbs):
+    agg = profile_step(model, x, labels, stream)
+    kernels = {k: {"launches_per_step": round(v["launches"], 2), "us_per_step": round(v["total_us"], 2),
+                   "avg_us": round(v["total_us"] / max(v["launches"], 1e-9), 3)} for k, v in agg.items()}
+    single = {k: v for k, v in agg.items() if not k.endswith("_steps") and v["flops"] > 0}
+    if not single:
+        return None, kernels
+    name, v = max(single.items(), key=lambda kv: kv[1]["total_us"])
+    avg_us = v["total_us"] / v["launches"]
+    bound = BOUND.get(name, "hbm")
+    if bound == "mfma":
+        achieved = v["flops"] / v["launches"] / (avg_us * 1e-6) / 1e12
+        peak, unit = peak_tflops, "TFLOP/s"
+    else:
+        achieved = v["bytes"] / v["launches"] / (avg_us * 1e-6) / 1e9
+        peak, unit = peak_gbs, "GB/s"
+    roof = {"kernel": name, "bound": bound, "achieved": round(achieved, 3), "peak": peak, "unit": unit,
+            "frac": round(achieved / peak, 4), "traffic": None, "avg_launch_us": round(avg_us, 2),
+            "algorithmic_flops_per_launch": v["flops"] / v["launches"],
+            "algorithmic_bytes_per_launch": v["bytes"] / v["launches"]}
+    return roof, kernels

@@ -200,3 +200,32 @@ def test_model_step_graph_replay_bitwise(s2s):
     nll2, logp2 = eager.step(xs, ls)
     torch.cuda.synchronize()
     assert torch.equal(logp2, outs[0][1]) and torch.equal(eager.grads, outs[0][2])
+
+
+def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch):
+    """The persistent layer kernel (in-launch sc1 hand-offs) must reproduce the per-step launch
+    path bit for bit -- same arithmetic, same summation order -- over repeated launches."""
+    rng = np.random.default_rng(11)
+    B, L, D, H = 32, 40, 48, 256
+    x = cu(rng.standard_normal((B, L, D)))
+    f, b = s2s.GRU(D, H), s2s.GRU(D, H)
+    outs = {}
+    for mode in ("step", "persistent"):
+        monkeypatch.setenv("S2S_GRU_MODE", mode)
+        mod = s2s.BiRNN(f, b).cuda()
+        res = []
+        for rep in range(3):
+            y = mod.forward(x).clone()
+            mod.zeroGradParameters()
+            dy = torch.ones_like(y) * 0.01 + y * 0.5
+            dx = mod.backward(x, dy).clone()
+            res.append((y, dx, [g.clone() for g in f.gradWeight + b.gradWeight]))
+        torch.cuda.synchronize()
+        outs[mode] = res
+    for rep in range(3):
+        ys, dxs, gs = outs["step"][rep]
+        yp, dxp, gp = outs["persistent"][rep]
+        assert torch.equal(ys, yp), f"y differs (rep {rep})"
+        assert torch.equal(dxs, dxp), f"dx differs (rep {rep})"
+        for i, (a, c) in enumerate(zip(gs, gp)):
+            assert torch.equal(a, c), f"grad {i} differs (rep {rep})"
