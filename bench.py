@@ -93,6 +93,7 @@ def main():
     import torch.distributed as dist
 
     import s2s_amd
+    from s2s_amd import dist as s2s_dist
     from s2s_amd import profile as s2s_profile
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -115,12 +116,12 @@ def main():
     x = x.cuda()
     labels = labels.to(torch.int32).cuda()
     stream = torch.cuda.Stream()
-    scale = 1.0 / (B * world)
+    scale = s2s_dist.step_scale(B)
 
     def step():
         model.step(x, labels, scale=scale, stream=stream)
         if world > 1:
-            dist.all_reduce(model.grads)
+            s2s_dist.allreduce_gradients(model.grads)
 
     with torch.cuda.stream(stream):
         for _ in range(args.warmup):

@@ -41,6 +41,10 @@ void s2s_ctx_destroy(s2s_ctx* ctx);
 /* flags: S2S_CTX_GRAPH = capture the model step into a hipGraph and replay it when the
  * dims / pointers repeat (the step is ~2000 dependent launches). */
 #define S2S_CTX_GRAPH 1
+/* S2S_CTX_OVERLAP = run the weight-gradient GEMMs on a side stream beside the next layer's BPTT
+ * (off by default: on MI355X the GEMM workgroups share CUs with the persistent recurrence and
+ * both slow down; measured 9.66 vs 9.23 ms per config-2 step). */
+#define S2S_CTX_OVERLAP 2
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
 
 /* ---------------------------------------------------------------- GRU layer

@@ -35,6 +35,12 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
 int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
              const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
              void* scratch, size_t scratch_bytes);
+// split form used by the model step (wgrad may run on a side stream after core)
+int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+                  const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
+                  size_t scratch_bytes);
+int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const void* saved,
+                   const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
 

@@ -694,9 +694,9 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   return 0;
 }
 
-int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
-             const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
-             void* scratch, size_t scratch_bytes) {
+int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+                  const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
+                  size_t scratch_bytes) {
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
@@ -740,9 +740,23 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
   S2S_CHECK_HIP(hipGetLastError());
+  // dh += dVh V   (Vh = h V^T)
+  S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A));
+  return 0;
+}
+
+// Weight gradients: one GEMM per parameter over all B*T rows (accumulate, alpha = scale), then
+// the bias column sums.  Reads only the saved buffer and attn_bwd_core's scratch, so the model
+// step runs it on a side stream beside the encoder BPTT.
+int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const void* saved,
+                   const AttnGrads& G, float scale, void* scratch) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, (char*)scratch);
+  k.labels = labels;
+  const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
+  const int rows = B * T;
   hipLaunchKernelGGL(dec_onehot_prev, dim3(256), dim3(256), 0, st, k);
   S2S_CHECK_HIP(hipGetLastError());
-  // weight gradients: one GEMM per parameter over all B*T rows (accumulate, alpha = scale)
   {
     GemmProblem pr[16];
     int n = 0;
@@ -765,9 +779,14 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));
   S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs));
   S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we));
-  // dh += dVh V   (Vh = h V^T)
-  S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A));
   return 0;
+}
+
+int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+             const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
+             void* scratch, size_t scratch_bytes) {
+  S2S_TRY(attn_bwd_core(st, d, h, labels, P, saved, dlogp, dh, accumulate_dh, scratch, scratch_bytes));
+  return attn_bwd_wgrad(st, d, h, labels, saved, G, scale, scratch);
 }
 
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,

@@ -84,6 +84,8 @@ struct GraphKey {
 struct s2s_ctx {
   int device = 0;
   int flags = 0;
+  hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
+  hipEvent_t ev[16] = {};
   bool have_graph = false;
   GraphKey key{};
   hipGraph_t graph = nullptr;
@@ -137,7 +139,10 @@ std::vector<long> param_sizes(const s2s_model_dims* d) {
 struct ModelWs {
   std::vector<float*> saved;  // 2 per layer
   std::vector<float*> Y;      // per layer output (B, L, 2H)
+  std::vector<float*> dA;     // per layer gate gradients (B, L, 6H), read by the side-stream dW GEMMs
   void* attn_saved;
+  void* attn_scratch;
+  size_t attn_scratch_bytes;
   void* scratch;
   size_t scratch_bytes;
   float *dlogp, *nll, *logp, *dY0, *dY1;
@@ -153,14 +158,15 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
     w.saved.push_back(bp.take<float>(B * L * 5 * ld.H));
     w.saved.push_back(bp.take<float>(B * L * 5 * ld.H));
     w.Y.push_back(bp.take<float>(B * L * 2 * ld.H));
+    w.dA.push_back(bp.take<float>(B * L * 6 * ld.H));
     size_t s = gru_layer_scratch_bytes(2, d->B, d->L, ld.D, ld.H);
     scr = s > scr ? s : scr;
     hmax = ld.H > hmax ? ld.H : hmax;
   }
   const AttnDims ad = model_attn(d);
   w.attn_saved = bp.take<char>(attn_saved_bytes(ad));
-  const size_t as = attn_scratch_bytes(ad);
-  scr = as > scr ? as : scr;
+  w.attn_scratch_bytes = attn_scratch_bytes(ad);
+  w.attn_scratch = bp.take<char>(w.attn_scratch_bytes);
   w.scratch = bp.take<char>(scr);
   w.scratch_bytes = scr;
   w.dlogp = bp.take<float>(B * T * O);
@@ -181,8 +187,17 @@ int check_model_dims(const s2s_model_dims* d) {
   return 0;
 }
 
-int model_step_impl(hipStream_t st, const s2s_model_dims* d, const float* params, float* grads, const float* x,
-                    const int* labels, float scale, int flags, float* logp, float* nll, void* workspace) {
+// fork: `side` waits for everything issued so far on `st`
+int fork_to(hipStream_t st, hipStream_t side, hipEvent_t ev) {
+  S2S_CHECK_HIP(hipEventRecord(ev, st));
+  S2S_CHECK_HIP(hipStreamWaitEvent(side, ev, 0));
+  return 0;
+}
+
+int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_model_dims* d, const float* params,
+                    float* grads, const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
+                    void* workspace) {
+  const bool split = side != nullptr;
   ModelWs w = model_ws(d, workspace);
   const std::vector<LayerDims> layers = enc_layers(d);
   const std::vector<long> sizes = param_sizes(d);
@@ -227,14 +242,16 @@ int model_step_impl(hipStream_t st, const s2s_model_dims* d, const float* params
     gp[i] = G[6 * nl + i];
   }
   float* lp = logp ? logp : w.logp;
-  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.scratch, w.scratch_bytes));
+  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes));
   // ---- loss seed: dlogp = -labelmask
   S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
   // ---- decoder backward -> dh
   float* dYcur = w.dY0;
   float* dYnext = w.dY1;
-  S2S_TRY(attn_bwd(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, ag, scale, w.scratch,
-                   w.scratch_bytes));
+  S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
+                        w.attn_scratch_bytes));
+  if (split) S2S_TRY(fork_to(st, side, ev[0]));
+  S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, w.attn_saved, ag, scale, w.attn_scratch));
   // ---- encoder backward
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
@@ -259,10 +276,16 @@ int model_step_impl(hipStream_t st, const s2s_model_dims* d, const float* params
     gr.lddx = io.ldx;
     gr.dx_accumulate = 0;
     gr.scale = scale;
-    S2S_TRY(gru_layer_bwd(st, io, gr, w.scratch, w.scratch_bytes));
+    S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
+    if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
+    S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l]));
     float* tmp = dYcur;
     dYcur = dYnext;
     dYnext = tmp;
+  }
+  if (split) {  // join: the step ends when the side stream's gradient GEMMs are done
+    S2S_CHECK_HIP(hipEventRecord(ev[15], side));
+    S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[15], 0));
   }
   return 0;
 }
@@ -328,8 +351,15 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
   int n = 0;
   S2S_CHECK_HIP(hipGetDeviceCount(&n));
   S2S_REQUIRE(device >= 0 && device < n, "device index out of range");
+  S2S_CHECK_HIP(hipSetDevice(device));
   auto* c = new s2s_ctx();
   c->device = device;
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+  for (auto& e : c->ev)
+    if (c->side && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
+      (void)hipStreamDestroy(c->side);
+      c->side = nullptr;
+    }
   *out = c;
   return 0;
 }
@@ -339,6 +369,9 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
   if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
+  for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
 }
 
@@ -491,7 +524,8 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   S2S_REQUIRE(workspace_bytes >= model_ws(d, nullptr).total, "model: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
-    return model_step_impl(st, d, params, grads, x, labels, scale, flags, logp, nll, workspace);
+    return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, d, params,
+                           grads, x, labels, scale, flags, logp, nll, workspace);
   GraphKey key;
   std::memset(&key, 0, sizeof(key));
   key.d = *d;
@@ -507,7 +541,8 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     ctx->graph = nullptr;
     ctx->have_graph = false;
     S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    const int rc = model_step_impl(st, d, params, grads, x, labels, scale, flags, logp, nll, workspace);
+    const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, d, params,
+                                   grads, x, labels, scale, flags, logp, nll, workspace);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(st, &g);
     if (rc != 0) {

@@ -28,5 +28,11 @@ struct GruLayerGrad {
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
 int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes);
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes);
+// split form used by the model step: core = weight packing + BPTT + dx (critical path), writing the
+// gate gradients into dA (B, L, 3*ndir*H) (dA == nullptr: inside scratch); wgrad = the dW GEMMs.
+int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, float* dA, void* scratch,
+                       size_t scratch_bytes);
+int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA);
+float* gru_layer_dA(const GruLayerIO& io, void* scratch);
 
 }  // namespace s2s

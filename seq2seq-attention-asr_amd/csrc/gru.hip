@@ -296,7 +296,8 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   return 0;
 }
 
-int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes) {
+int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, float* dA_ext, void* scratch,
+                       size_t scratch_bytes) {
   const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
   S2S_REQUIRE(nd == 1 || nd == 2, "gru: ndir must be 1 or 2");
   S2S_REQUIRE(H % 16 == 0, "gru: H must be a multiple of 16");
@@ -312,7 +313,8 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
     dhp[d] = bp.take<float>((long)B * H);
   }
   float* Wx = bp.take<float>(3L * nd * H * D);
-  float* dA = bp.take<float>((long)B * L * 3 * nd * H);
+  float* dA_int = bp.take<float>((long)B * L * 3 * nd * H);
+  float* dA = dA_ext ? dA_ext : dA_int;
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   const long ldA = 3L * nd * H;
   for (int d = 0; d < nd; ++d)
@@ -349,7 +351,28 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
   if (gr.dx)
     S2S_TRY(gemm1(st, false, false, B * L, D, 3 * nd * H, 1.f, dA, ldA, Wx, D, gr.dx_accumulate ? 1.f : 0.f, gr.dx,
                   gr.lddx));
-  // dW += scale * dA_g^T . [h_{t-1} | q ; x]   (LinearZeroBias.lua:67-74 summed over all steps)
+  return 0;
+}
+
+float* gru_layer_dA(const GruLayerIO& io, void* scratch) {
+  Bump bp{static_cast<char*>(scratch), 0, 0};
+  for (int d = 0; d < io.ndir; ++d) {
+    bp.take<float>(2L * io.H * io.H);
+    bp.take<float>((long)io.H * io.H);
+    bp.take<float>((long)io.H * io.H);
+    bp.take<float>(2L * io.H * io.H);
+    bp.take<float>((long)io.B * io.H);
+    bp.take<float>((long)io.B * io.H);
+  }
+  bp.take<float>(3L * io.ndir * io.H * io.D);
+  return bp.take<float>((long)io.B * io.L * 3 * io.ndir * io.H);
+}
+
+// dW += scale * dA_g^T . [h_{t-1} | q ; x]   (LinearZeroBias.lua:67-74 summed over all steps).
+// Off the recurrence: the model step runs it on a side stream beside the next layer's BPTT.
+int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA) {
+  const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
+  const long ldA = 3L * nd * H;
   GemmProblem probs[12];
   int np = 0;
   for (int d = 0; d < nd; ++d) {
@@ -363,8 +386,12 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
       probs[np++] = GemmProblem{dAg, io.x, dW + H, nullptr, ldA, io.ldx, (long)H + D, H, D, B * L, gr.scale, 1.f};
     }
   }
-  S2S_TRY(gemm_f32(st, probs, np, true, false));
-  return 0;
+  return gemm_f32(st, probs, np, true, false);
+}
+
+int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(gru_layer_bwd_core(st, io, gr, nullptr, scratch, scratch_bytes));
+  return gru_layer_wgrad(st, io, gr, gru_layer_dA(io, scratch));
 }
 
 }  // namespace s2s

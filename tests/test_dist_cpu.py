@@ -1,0 +1,72 @@
+"""world_size-2 gloo test of the data-parallel step semantics on CPU:
+per-rank local gradients (oracle, reference per-utterance semantics) scaled by 1/(B*world) and
+all-reduced equal the single-process gradient over the global batch (timit/timit.lua:292-295)."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _cfg():
+    from oracle import s2s_oracle as orc
+    return orc.ModelConfig(inputFrameSize=6, hiddenFrameSize=4, outputFrameSize=4, scoreDepth=5, stateDepth=4,
+                           outputDepth=7, mlpDepth=3, maxoutWindow=2, numLayers=2)
+
+
+def _worker(rank, world, port, B, out_path, buckets):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "seq2seq-attention-asr_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from oracle import s2s_oracle as orc
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "s2s_dist", os.path.join(ROOT, "seq2seq-attention-asr_amd", "s2s_amd", "dist.py"))
+    sd = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sd)
+    cfg = _cfg()
+    P = orc.init_params(cfg, seed=5)
+    x, labels = orc.synthetic_batch(cfg, B * world, 6, 4, seed=9, pad=1, eos=2)
+    xs, ls = x[rank * B:(rank + 1) * B], labels[rank * B:(rank + 1) * B]
+    # local per-utterance gradient sum (reference semantics), scaled for the global mean
+    G = orc.zeros_like_params(P)
+    for b in range(B):
+        _, g1, _, _ = orc.training_step(xs[b:b + 1], ls[b:b + 1], P, cfg)
+        for k in G:
+            G[k] += g1[k]
+    flat = torch.tensor(orc.flatten(G, cfg)) * (sd.step_scale(B) * 1.0)
+    sd.allreduce_gradients(flat, bucket_elems=buckets)
+    if rank == 0:
+        np.save(out_path, flat.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("buckets", [0, 37])
+def test_dp_allreduce_equals_global_batch(tmp_path, buckets):
+    from oracle import s2s_oracle as orc
+    world, B = 2, 2
+    out = str(tmp_path / "g.npy")
+    mp.start_processes(_worker, args=(world, _free_port(), B, out, buckets), nprocs=world, start_method="spawn")
+    got = np.load(out)
+    cfg = _cfg()
+    P = orc.init_params(cfg, seed=5)
+    x, labels = orc.synthetic_batch(cfg, B * world, 6, 4, seed=9, pad=1, eos=2)
+    _, G, _, _ = orc.training_step(x, labels, P, cfg)
+    np.testing.assert_allclose(got, orc.flatten(G, cfg), rtol=1e-10, atol=1e-13)
