@@ -18,6 +18,10 @@
 // every weight gradient is one GEMM over all B*T rows afterwards.
 #include "attn.h"
 
+#include <cstdlib>
+#include <cstring>
+
+#include "handoff.h"
 #include "skinny.h"
 
 namespace s2s {
@@ -42,6 +46,12 @@ struct AttnK {
   // bwd scratch
   float *DO, *DU, *DV, *DGA, *DS, *DSP, *DSPF, *DD, *DCY, *DC, *DVH, *PDWS, *DWS, *DWEACC, *YP;
   float *WhT, *GT, *WdT, *WcT, *WsT;
+  // persistent-kernel granule buffers ([2 slots][...]) and abort word; one zeroed region each
+  granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gCY, *gD, *gQ;           // forward
+  granule_t *gZ, *gR, *gH, *gDD, *gDCY, *gDC, *gPDWS, *gDWS;           // backward
+  char *fsync, *bsync;
+  size_t fsync_bytes, bsync_bytes;
+  unsigned long long* stamps;  // diagnostic phase stamps (nullptr = off)
   float* dh;
   long lddh;
   const float* dlogp;
@@ -97,6 +107,33 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
   float* WdT = g.take<float>(2 * S * S);
   float* WcT = g.take<float>(A * S);
   float* WsT = g.take<float>(S * Sc);
+  // granule regions (256-byte header = abort word), zeroed by one memset before each persistent launch
+  char* fsync = f.take<char>(256);
+  granule_t* gS = f.take<granule_t>(2 * B * S);
+  granule_t* gWS = f.take<granule_t>(2 * B * Sc);
+  granule_t* gPM = f.take<granule_t>(2 * B * NCH);
+  granule_t* gPL = f.take<granule_t>(2 * B * NCH);
+  granule_t* gPC = f.take<granule_t>(2 * B * NCH * A);
+  granule_t* gC = f.take<granule_t>(2 * B * A);
+  granule_t* gCY = f.take<granule_t>(2 * B * 2 * S);
+  granule_t* gD = f.take<granule_t>(2 * B * S);
+  granule_t* gQ = f.take<granule_t>(2 * B * S);
+  const size_t fsync_bytes = f.off - (size_t)(fsync - scratch);
+  char* bsync = g.take<char>(256);
+  granule_t* gZ = g.take<granule_t>(2 * B * S);
+  granule_t* gR = g.take<granule_t>(2 * B * S);
+  granule_t* gH = g.take<granule_t>(2 * B * S);
+  granule_t* gDD = g.take<granule_t>(2 * B * S);
+  granule_t* gDCY = g.take<granule_t>(2 * B * S);
+  granule_t* gDC = g.take<granule_t>(2 * B * A);
+  granule_t* gPDWS = g.take<granule_t>(2 * B * NCH * Sc);
+  granule_t* gDWS = g.take<granule_t>(2 * B * Sc);
+  const size_t bsync_bytes = g.off - (size_t)(bsync - scratch);
+  if (k) {
+    k->gS = gS; k->gWS = gWS; k->gPM = gPM; k->gPL = gPL; k->gPC = gPC; k->gC = gC; k->gCY = gCY; k->gD = gD;
+    k->gQ = gQ; k->gZ = gZ; k->gR = gR; k->gH = gH; k->gDD = gDD; k->gDCY = gDCY; k->gDC = gDC; k->gPDWS = gPDWS;
+    k->gDWS = gDWS; k->fsync = fsync; k->bsync = bsync; k->fsync_bytes = fsync_bytes; k->bsync_bytes = bsync_bytes;
+  }
   if (k) {
     k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
     k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
@@ -637,6 +674,8 @@ __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const in
   }
 }
 
+#include "attn_persist.inc"
+
 }  // namespace
 
 int attn_check_dims(const AttnDims& d) {
@@ -658,6 +697,20 @@ const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
   return k.ALPHA;
 }
 
+// S2S_DEC_MODE=step forces the per-step launch path (A/B and fallback); default: the persistent
+// decoder kernels whenever the shape has an instantiation.
+static unsigned long long* g_dec_stamps[2] = {nullptr, nullptr};
+
+static int dec_persist_variant(const AttnDims& d) {
+  const char* m = std::getenv("S2S_DEC_MODE");
+  if (m && std::strcmp(m, "step") == 0) return 0;
+  if ((d.B + 15) / 16 * kDecWG > 512) return 0;
+  if ((d.L + LC - 1) / LC > 256) return 0;
+  if (d.S == 256 && d.A == 512 && d.Sc == 512) return 1;
+  if (d.S == 64 && d.A == 128 && d.Sc == 128) return 2;
+  return 0;
+}
+
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
              void* saved, void* scratch, size_t scratch_bytes) {
   S2S_TRY(attn_check_dims(d));
@@ -668,11 +721,23 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   k.h = h;
   k.labels = labels;
   k.logp = logp;
+  k.stamps = g_dec_stamps[0];
   const int B = d.B, L = d.L, T = d.T, S = d.S;
   const int bt = (B + 15) / 16;
   // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc));
   hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  if (const int var = dec_persist_variant(d)) {
+    S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
+    const dim3 grid(kDecWG * ((B + 15) / 16));
+    {
+      ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
+      if (var == 1) hipLaunchKernelGGL((dec_fwd_persist<4, 8, 2>), grid, dim3(256), 0, st, k);
+      else hipLaunchKernelGGL((dec_fwd_persist<1, 2, 1>), grid, dim3(256), 0, st, k);
+    }
+    hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, st, k);
+    S2S_CHECK_HIP(hipGetLastError());
+  } else {
   ProfScope ps(st, "dec_fwd_steps", 0.0, 0.0);
   for (int t = 0; t < T; ++t) {
     k.t = t;
@@ -685,6 +750,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
   S2S_CHECK_HIP(hipGetLastError());
+  }
   // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
   const int rows = B * T;
   S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
@@ -705,6 +771,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   k.h = h;
   k.labels = labels;
   k.dlogp = dlogp;
+  k.stamps = g_dec_stamps[1];
   k.dh = dh;
   k.lddh = d.A;
   const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
@@ -727,6 +794,14 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_CHECK_HIP(hipGetLastError());
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A));
+  if (const int var = dec_persist_variant(d)) {
+    S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
+    const dim3 grid(kDecWG * ((B + 15) / 16));
+    ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
+    if (var == 1) hipLaunchKernelGGL((dec_bwd_persist<4, 8>), grid, dim3(256), 0, st, k);
+    else hipLaunchKernelGGL((dec_bwd_persist<1, 2>), grid, dim3(256), 0, st, k);
+    S2S_CHECK_HIP(hipGetLastError());
+  } else {
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   ProfScope ps(st, "dec_bwd_steps", 0.0, 0.0);
   for (int t = T - 1; t >= 0; --t) {
@@ -740,6 +815,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
   S2S_CHECK_HIP(hipGetLastError());
+  }
   // dh += dVh V   (Vh = h V^T)
   S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A));
   return 0;
@@ -797,3 +873,11 @@ int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* 
 }
 
 }  // namespace s2s
+
+// Diagnostic (not part of the C ABI header): device buffers of (grid * T * 8) uint64 that the
+// persistent decoder kernels fill with s_memrealtime stamps at phase ends; nullptr turns it off.
+extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
+  s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
+  s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);
+  return 0;
+}

@@ -21,13 +21,12 @@
 //     wave sees it within 64 polls, all workgroups leave at their next barrier.
 #include "gru.h"
 #include "gru_persist.h"
+#include "handoff.h"
 #include "skinny.h"
 
 namespace s2s {
 
 namespace {
-
-constexpr unsigned kSpinLimit = 1u << 21;
 
 struct PDir {
   const float* xp;
@@ -43,90 +42,15 @@ struct PDir {
   long ldA;
   int reverse;
   // granule buffers, each [2 slots][B][H] x 8 bytes
-  unsigned long long* g0;  // fwd: h      bwd: da_z
-  unsigned long long* g1;  // fwd: q      bwd: da_r
-  unsigned long long* g2;  //             bwd: da_h
+  granule_t* g0;  // fwd: h      bwd: da_z
+  granule_t* g1;  // fwd: q      bwd: da_r
+  granule_t* g2;  //             bwd: da_h
 };
 struct PArgs {
   PDir d[2];
   int B, L, H, MT, nwg;  // nwg = workgroups per direction
   unsigned* abort_word;
 };
-
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
-}
-
-__device__ __forceinline__ void put_granule(unsigned long long* g, float v, unsigned tag) {
-  const unsigned long long x = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
-  __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ float get_granule(const unsigned long long* g) {
-  return __uint_as_float((unsigned)__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
-// Sweep: load this lane's operand granules (NC chunks x 4 consecutive k) of one row until
-// every tag == tag.  rs/off: buffer + byte offset of granule (row, k = 0).  Returns false on
-// abort/timeout (the operands are then garbage; the caller leaves at its next barrier).
-template <int NC>
-__device__ __forceinline__ bool sweep(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, unsigned tag,
-                                      int wave, int lane, unsigned* abort_word) {
-  const long kq = 4 * (lane >> 4);
-  unsigned spins = 0;
-  while (true) {
-    bool ok = true;
-#pragma unroll
-    for (int i = 0; i < NC; ++i) {
-      const long off = row_off + 8 * (wave * 16 + 64 * i + kq);
-      const uint4 p0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
-      const uint4 p1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off + 16, 0, 16));
-      ok = ok && p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
-      a[i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z));
-    }
-    if (__all(ok)) return true;
-    ++spins;
-    if ((spins & 63u) == 0) {
-      if (spins > kSpinLimit ||
-          __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
-
-// same chunk order / accumulator split as skinny_wave (bitwise-equal sums)
-template <int NC>
-__device__ __forceinline__ floatx4 mfma_chunks(const float4 (&a)[NC], const float4 (&w)[NC]) {
-  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int i = 0; i + 1 < NC; i += 2) {
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].x, w[i + 1].x, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].y, w[i + 1].y, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].z, w[i + 1].z, acc1, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
-    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].w, w[i + 1].w, acc1, 0, 0, 0);
-  }
-  if (NC & 1) {
-    constexpr int i = NC - 1;
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
-    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
-  }
-  return acc0 + acc1;
-}
-
-template <int NC>
-__device__ __forceinline__ void load_w(float4 (&w)[NC], const float* row, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < NC; ++i)
-    w[i] = *reinterpret_cast<const float4*>(row + wave * 16 + 64 * i + 4 * (lane >> 4));
-}
 
 // cross-wave sum + abort agreement at the same barrier
 __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds, bool ok, floatx4 acc, int wave,
@@ -155,8 +79,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   if (tid == 0) abort_lds = 0;
 
   float4 w1[NC], w2[NC];
-  load_w(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
-  if (isz) load_w(w2, g.Wb + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
+  load_wfrag(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
+  if (isz) load_wfrag(w2, g.Wb + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
 
   const __amdgpu_buffer_rsrc_t hg = rsrc_of(g.g0), qg = rsrc_of(g.g1);
   const long slot = (long)B * H;  // granules per slot
@@ -175,7 +99,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     bool ok = true;
     if (s > 0) {
       float4 av[NC];
-      ok = sweep<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
+      ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
       acc = mfma_chunks<NC>(av, w1);
     }
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
@@ -188,7 +112,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
         zreg = gate;
       } else {
         const int j = on - H;
-        const float hp = s > 0 ? get_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
+        const float hp = s > 0 ? peek_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
         const float q = gate * hp;
         sv[H + j] = gate;
         sv[3 * H + j] = hp;
@@ -203,7 +127,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     ok = true;
     if (s > 0) {
       float4 av[NC];
-      ok = sweep<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), (unsigned)(s + 1), wave, lane, a.abort_word);
+      ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), (unsigned)(s + 1), wave, lane, a.abort_word);
       acc = mfma_chunks<NC>(av, w2);
     }
     sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
@@ -235,8 +159,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   if (tid == 0) abort_lds = 0;
 
   float4 wh[NC], wzr[2 * NC];
-  load_w(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
-  load_w(wzr, g.Wb + (long)(c * 16 + (lane & 15)) * 2 * H, wave, lane);
+  load_wfrag(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
+  load_wfrag(wzr, g.Wb + (long)(c * 16 + (lane & 15)) * 2 * H, wave, lane);
   const __amdgpu_buffer_rsrc_t zg = rsrc_of(g.g0), rg = rsrc_of(g.g1), hg = rsrc_of(g.g2);
   const long slot = (long)B * H;
   const int br = min(b0 + (lane & 15), B - 1);
@@ -275,7 +199,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
       dyv = g.dy[row * g.lddy + ok_];
     }
     float4 av[NC];
-    bool ok = sweep<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+    bool ok = sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
@@ -292,8 +216,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     float4 azr[2 * NC];
     {
       float4 az[NC], ar[NC];
-      ok = sweep<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
-      ok = ok && sweep<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      ok = sweep_skinny<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      ok = ok && sweep_skinny<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
       // chunk i of the K = 2H product: i < NC reads da_z, i >= NC reads da_r (H % 64 == 0)
 #pragma unroll
       for (int i = 0; i < NC; ++i) { azr[i] = az[i]; azr[NC + i] = ar[i]; }
@@ -339,9 +263,9 @@ bool gru_persist_supported(int ndir, int B, int H) {
 
 size_t gru_persist_sync_bytes(int B, int H) { return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H; }
 
-static void carve_granules(char* sync, int B, int H, unsigned** abort_word, unsigned long long* (&g)[2][3]) {
+static void carve_granules(char* sync, int B, int H, unsigned** abort_word, granule_t* (&g)[2][3]) {
   *abort_word = reinterpret_cast<unsigned*>(sync);
-  unsigned long long* p = reinterpret_cast<unsigned long long*>(sync + 256);
+  granule_t* p = reinterpret_cast<granule_t*>(sync + 256);
   for (int d = 0; d < 2; ++d)
     for (int k = 0; k < 3; ++k) {
       g[d][k] = p;
@@ -352,7 +276,7 @@ static void carve_granules(char* sync, int B, int H, unsigned** abort_word, unsi
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   PArgs a{};
   const int MT = (f.B + 15) / 16;
-  unsigned long long* gr[2][3];
+  granule_t* gr[2][3];
   carve_granules(static_cast<char*>(sync), f.B, f.H, &a.abort_word, gr);
   for (int d = 0; d < f.ndir; ++d)
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
@@ -367,7 +291,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   PArgs a{};
   const int MT = (b.B + 15) / 16;
-  unsigned long long* gr[2][3];
+  granule_t* gr[2][3];
   carve_granules(static_cast<char*>(sync), b.B, b.H, &a.abort_word, gr);
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,

@@ -1,0 +1,154 @@
+// In-launch hand-offs between workgroups of a persistent kernel (MI355X guide §6 Guideline 16,
+// form R2 "the data is the flag"): every handed-off fp32 value is ONE 8-byte granule
+// {value, tag} stored write-through (sc1); consumers re-read the granules they need with sc1
+// loads until every tag equals the expected epoch.  Buffers are zeroed (memset node) before each
+// launch; epochs are 1-based step counters within the launch.  Every wait is bounded: on timeout
+// (or when another wave already gave up) the abort word is raised and the wait returns false.
+#pragma once
+#include "s2s_common.h"
+
+namespace s2s {
+
+constexpr unsigned kSpinLimit = 1u << 21;
+typedef unsigned long long granule_t;
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
+}
+
+__device__ __forceinline__ void put_granule(granule_t* g, float v, unsigned tag) {
+  const granule_t x = ((granule_t)tag << 32) | (granule_t)__float_as_uint(v);
+  __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// value of a granule already known to carry the right tag (validated by a sweep of this workgroup)
+__device__ __forceinline__ float peek_granule(const granule_t* g) {
+  return __uint_as_float((unsigned)__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+__device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_word) {
+  ++spins;
+  if ((spins & 63u) == 0) {
+    if (spins > kSpinLimit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+      __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return true;
+    }
+  }
+  __builtin_amdgcn_s_sleep(1);
+  return false;
+}
+
+// one thread waits for one granule
+__device__ __forceinline__ float wait_granule(const granule_t* g, unsigned tag, unsigned* abort_word, bool& ok) {
+  unsigned spins = 0;
+  while (true) {
+    const granule_t x = __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((unsigned)(x >> 32) == tag) return __uint_as_float((unsigned)x);
+    if (spin_give_up(spins, abort_word)) {
+      ok = false;
+      return 0.f;
+    }
+  }
+}
+
+// one thread waits for n <= N granules base[j * stride], j < n: all loads are issued before any
+// tag is checked (one round trip per pass instead of n dependent ones)
+template <int N>
+__device__ __forceinline__ bool wait_granules(const granule_t* base, long stride, int n, unsigned tag, float (&v)[N],
+                                              unsigned* abort_word) {
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < N; ++j) {
+      if (j < n) {
+        const granule_t x = __hip_atomic_load(base + j * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = ok && (unsigned)(x >> 32) == tag;
+        v[j] = __uint_as_float((unsigned)x);
+      }
+    }
+    if (ok) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
+// Skinny-operand sweep: this lane's NC chunks (chunk i = k in [wave*16 + 64 i + 4*(lane>>4), +4))
+// of one granule row starting at byte offset row_off.  Matches skinny_wave's operand layout.
+template <int NC>
+__device__ __forceinline__ bool sweep_skinny(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, unsigned tag,
+                                             int wave, int lane, unsigned* abort_word) {
+  const long kq = 4 * (lane >> 4);
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const long off = row_off + 8 * (wave * 16 + 64 * i + kq);
+      const uint4 p0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+      const uint4 p1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off + 16, 0, 16));
+      ok = ok && p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
+      a[i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z));
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
+// Vector sweep: float4 index c4 = lane + 64 i (i < NV) of one granule row (row_off bytes);
+// lanes with c4 >= n4 read nothing.  Matches the "for (c4 = lane; c4 < n4; c4 += 64)" loops.
+template <int NV>
+__device__ __forceinline__ bool sweep_vec(float4 (&a)[NV], __amdgpu_buffer_rsrc_t rs, long row_off, int n4,
+                                          unsigned tag, int lane, unsigned* abort_word) {
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < n4) {
+        const long off = row_off + 32L * c4;
+        const uint4 p0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+        const uint4 p1 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off + 16, 0, 16));
+        ok = ok && p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
+        a[i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x),
+                           __uint_as_float(p1.z));
+      }
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
+// same chunk order / accumulator split as skinny_wave (bitwise-equal sums)
+template <int NC>
+__device__ __forceinline__ floatx4 mfma_chunks(const float4 (&a)[NC], const float4 (&w)[NC]) {
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i + 1 < NC; i += 2) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].x, w[i + 1].x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].y, w[i + 1].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].z, w[i + 1].z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].w, w[i + 1].w, acc1, 0, 0, 0);
+  }
+  if (NC & 1) {
+    constexpr int i = NC - 1;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+
+// W operand fragments of one output-unit row (chunk i at wave*16 + 64 i), kept in VGPRs
+template <int NC>
+__device__ __forceinline__ void load_wfrag(float4 (&w)[NC], const float* row, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    w[i] = *reinterpret_cast<const float4*>(row + wave * 16 + 64 * i + 4 * (lane >> 4));
+}
+
+}  // namespace s2s

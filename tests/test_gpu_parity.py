@@ -94,6 +94,9 @@ ATT_CASES = [
     (4, 33, 6, 64, 64, 48, 29, 8, 7, 0.0),
     (2, 16, 4, 32, 32, 16, 5, 3, 2, 0.25),
     (19, 8, 3, 16, 16, 16, 62, 5, 7, 0.0),
+    # shapes served by the persistent decoder kernels (S=64, A=128, Sc=128), ragged B and L
+    (5, 37, 6, 128, 128, 64, 29, 4, 7, 0.3),
+    (18, 16, 4, 128, 128, 64, 62, 8, 7, 0.0),
 ]
 
 
@@ -229,3 +232,30 @@ def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch):
         assert torch.equal(dxs, dxp), f"dx differs (rep {rep})"
         for i, (a, c) in enumerate(zip(gs, gp)):
             assert torch.equal(a, c), f"grad {i} differs (rep {rep})"
+
+
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O", [(32, 40, 12, 512, 512, 256, 62), (21, 50, 9, 128, 128, 64, 29)])
+def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B, L, T, A, Sc, S, O):
+    """The persistent decoder kernels (granule hand-offs, 128 workgroups per 16-row tile) must
+    reproduce the per-step launch path bit for bit, forward and backward, over repeated launches."""
+    rng = np.random.default_rng(3)
+    att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, 8, 7, O), Sc, 10, 0, S, A, O, True, 0.2).cuda()
+    h = cu(rng.standard_normal((B, L, A)) * 0.5)
+    labels = cu(rng.integers(0, O, (B, T)), torch.int32)
+    dlogp = cu(rng.standard_normal((B, T, O)))
+    outs = {}
+    for mode in ("step", "persistent"):
+        monkeypatch.setenv("S2S_DEC_MODE", mode)
+        res = []
+        for _ in range(2):
+            logp = att.forward([h, labels]).clone()
+            alpha = att.alpha().clone()
+            att.zeroGradParameters()
+            dh = att.backward([h, None], dlogp)[0].clone()
+            res.append([logp, alpha, dh] + [g.clone() for g in att.parameters()[1]])
+        torch.cuda.synchronize()
+        outs[mode] = res
+    names = ["logp", "alpha", "dh"] + ["d" + n for n in s2s.Attention.PARAM_NAMES]
+    for rep in range(2):
+        for name, a, b in zip(names, outs["step"][rep], outs["persistent"][rep]):
+            assert torch.equal(a, b), f"{name} differs (rep {rep}): max |d| = {(a - b).abs().max().item():.3e}"
