@@ -704,10 +704,66 @@ static unsigned long long* g_dec_stamps[2] = {nullptr, nullptr};
 static int dec_persist_variant(const AttnDims& d) {
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && std::strcmp(m, "step") == 0) return 0;
-  if ((d.B + 15) / 16 * kDecWG > 512) return 0;
   if ((d.L + LC - 1) / LC > 256) return 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) return 1;
   if (d.S == 64 && d.A == 128 && d.Sc == 128) return 2;
+  return 0;
+}
+
+// A persistent launch must be fully co-resident (its workgroups wait on each other).
+static bool co_resident(const void* fn, int grid, size_t dyn_lds) {
+  int dev = 0, cus = 0, per_cu = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return false;
+  if (dyn_lds > 0 && hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)dyn_lds) != hipSuccess)
+    return false;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, dyn_lds) != hipSuccess) return false;
+  return (long)per_cu * cus >= grid;
+}
+
+// resident-chunk variant (attn_persist.inc) unless S2S_DEC_RES=0
+static bool dec_res_enabled(const AttnDims& d) {
+  const char* m = std::getenv("S2S_DEC_RES");
+  if (m && std::strcmp(m, "0") == 0) return false;
+  return 16 * ((d.L + LC - 1) / LC) <= kDecWG;
+}
+
+struct PersistLaunch {
+  const void* fn = nullptr;
+  size_t lds = 0;
+};
+
+static PersistLaunch pick_dec_fwd(int var, const AttnDims& d, int grid) {
+  PersistLaunch c[2];
+  if (var == 1) {
+    c[0] = {(const void*)dec_fwd_persist<4, 8, 2, true>, dec_fwd_res_lds(d.A, d.Sc)};
+    c[1] = {(const void*)dec_fwd_persist<4, 8, 2, false>, 0};
+  } else {
+    c[0] = {(const void*)dec_fwd_persist<1, 2, 1, true>, dec_fwd_res_lds(d.A, d.Sc)};
+    c[1] = {(const void*)dec_fwd_persist<1, 2, 1, false>, 0};
+  }
+  for (int i = dec_res_enabled(d) ? 0 : 1; i < 2; ++i)
+    if (co_resident(c[i].fn, grid, c[i].lds)) return c[i];
+  return {};
+}
+
+static PersistLaunch pick_dec_bwd(int var, const AttnDims& d, int grid) {
+  PersistLaunch c[2];
+  if (var == 1) {
+    c[0] = {(const void*)dec_bwd_persist<4, 8, true>, dec_bwd_res_lds(d.A, d.Sc)};
+    c[1] = {(const void*)dec_bwd_persist<4, 8, false>, 0};
+  } else {
+    c[0] = {(const void*)dec_bwd_persist<1, 2, true>, dec_bwd_res_lds(d.A, d.Sc)};
+    c[1] = {(const void*)dec_bwd_persist<1, 2, false>, 0};
+  }
+  for (int i = dec_res_enabled(d) ? 0 : 1; i < 2; ++i)
+    if (co_resident(c[i].fn, grid, c[i].lds)) return c[i];
+  return {};
+}
+
+static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, AttnK& k) {
+  void* args[] = {&k};
+  S2S_CHECK_HIP(hipLaunchKernel(p.fn, dim3(grid), dim3(256), args, p.lds, st));
   return 0;
 }
 
@@ -727,13 +783,14 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc));
   hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
-  if (const int var = dec_persist_variant(d)) {
+  const int pgrid = kDecWG * ((B + 15) / 16);
+  const int pvar = dec_persist_variant(d);
+  const PersistLaunch pf = pvar ? pick_dec_fwd(pvar, d, pgrid) : PersistLaunch{};
+  if (pf.fn) {
     S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
-    const dim3 grid(kDecWG * ((B + 15) / 16));
     {
       ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
-      if (var == 1) hipLaunchKernelGGL((dec_fwd_persist<4, 8, 2>), grid, dim3(256), 0, st, k);
-      else hipLaunchKernelGGL((dec_fwd_persist<1, 2, 1>), grid, dim3(256), 0, st, k);
+      S2S_TRY(launch_persist(pf, pgrid, st, k));
     }
     hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, st, k);
     S2S_CHECK_HIP(hipGetLastError());
@@ -794,12 +851,13 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_CHECK_HIP(hipGetLastError());
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A));
-  if (const int var = dec_persist_variant(d)) {
+  const int pgrid = kDecWG * ((B + 15) / 16);
+  const int pvar = dec_persist_variant(d);
+  const PersistLaunch pb = pvar ? pick_dec_bwd(pvar, d, pgrid) : PersistLaunch{};
+  if (pb.fn) {
     S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
-    const dim3 grid(kDecWG * ((B + 15) / 16));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
-    if (var == 1) hipLaunchKernelGGL((dec_bwd_persist<4, 8>), grid, dim3(256), 0, st, k);
-    else hipLaunchKernelGGL((dec_bwd_persist<1, 2>), grid, dim3(256), 0, st, k);
+    S2S_TRY(launch_persist(pb, pgrid, st, k));
     S2S_CHECK_HIP(hipGetLastError());
   } else {
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
