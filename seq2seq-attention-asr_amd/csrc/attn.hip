@@ -687,9 +687,14 @@ int attn_check_dims(const AttnDims& d) {
 }
 
 size_t attn_saved_bytes(const AttnDims& d) { return carve(d, nullptr, nullptr, nullptr).saved; }
-size_t attn_scratch_bytes(const AttnDims& d) {
+// scratch = [forward | backward working sets (overlapping)] + split-K slabs of the GEMMs
+static size_t attn_ws_offset(const AttnDims& d) {
   Layout l = carve(d, nullptr, nullptr, nullptr);
-  return l.fwd > l.bwd ? l.fwd : l.bwd;
+  return ((l.fwd > l.bwd ? l.fwd : l.bwd) + 255) & ~size_t(255);
+}
+size_t attn_scratch_bytes(const AttnDims& d) { return attn_ws_offset(d) + sizeof(float) * kGemmWsFloats; }
+static GemmWs attn_gemm_ws(const AttnDims& d, void* scratch) {
+  return GemmWs{reinterpret_cast<float*>(static_cast<char*>(scratch) + attn_ws_offset(d)), kGemmWsFloats};
 }
 const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
   AttnK k{};
@@ -781,7 +786,8 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   const int B = d.B, L = d.L, T = d.T, S = d.S;
   const int bt = (B + 15) / 16;
   // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
-  S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc));
+  const GemmWs gws = attn_gemm_ws(d, scratch);
+  S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
   hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   const int pgrid = kDecWG * ((B + 15) / 16);
   const int pvar = dec_persist_variant(d);
@@ -811,7 +817,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
   const int rows = B * T;
   S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
-                (long)d.M * d.K, P.bm));
+                (long)d.M * d.K, P.bm, gws));
   hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
@@ -850,7 +856,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
-  S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A));
+  const GemmWs gws = attn_gemm_ws(d, scratch);
+  S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A, nullptr, gws));
   const int pgrid = kDecWG * ((B + 15) / 16);
   const int pvar = dec_persist_variant(d);
   const PersistLaunch pb = pvar ? pick_dec_bwd(pvar, d, pgrid) : PersistLaunch{};
@@ -875,7 +882,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_CHECK_HIP(hipGetLastError());
   }
   // dh += dVh V   (Vh = h V^T)
-  S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A));
+  S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A, nullptr, gws));
   return 0;
 }
 
@@ -904,7 +911,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
     pr[n++] = GemmProblem{k.DCY + S, k.YP, G.Wy, nullptr, 2L * S, O, O, S, O, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DWS, k.HX, G.Ws, nullptr, Sc, 2L * S, S, Sc, S, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DVH, h, G.V, nullptr, Sc, A, A, Sc, A, B * L, scale, 1.f};
-    S2S_TRY(gemm_f32(st, pr, n, true, false));
+    S2S_TRY(gemm_f32(st, pr, n, true, false, attn_gemm_ws(d, scratch)));
   }
   S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo));
   S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));

@@ -146,6 +146,7 @@ struct ModelWs {
   void* scratch;
   size_t scratch_bytes;
   float *dlogp, *nll, *logp, *dY0, *dY1;
+  GemmWs gws_side;  // split-K slabs of the encoder weight-gradient GEMMs (may run on the side stream)
   size_t total;
 };
 ModelWs model_ws(const s2s_model_dims* d, void* base) {
@@ -174,6 +175,7 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
   w.logp = bp.take<float>(B * T * O);
   w.dY0 = bp.take<float>(B * L * 2 * hmax);
   w.dY1 = bp.take<float>(B * L * 2 * hmax);
+  w.gws_side = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
   w.total = bp.off + 256;
   return w;
 }
@@ -278,7 +280,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
     gr.scale = scale;
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
     if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
-    S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l]));
+    S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
     float* tmp = dYcur;
     dYcur = dYnext;
     dYnext = tmp;

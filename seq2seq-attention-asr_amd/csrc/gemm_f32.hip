@@ -1,5 +1,5 @@
-// fp32 GEMM on the gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32,
-// one rounding per product, bit-identical to a k-ordered fmaf chain).
+// fp32 GEMM on the gfx950 f32-input MFMA (v_mfma_f32_32x32x2_f32: exact f32 products,
+// fp32 accumulation in a fixed k order -> deterministic, run to run and graph replay).
 //
 // Used for every "plain" contraction of the training step that is hoisted out of
 // the recurrences: encoder input projections (the x-half of every GRU gate
@@ -9,105 +9,267 @@
 // GEMMs that the reference accumulates one rank-1 GER per time step
 // (LinearZeroBias.lua:67-74) -- here one GEMM over all B*L rows.
 //
-// Tile 64x64x32, 256 threads = 4 waves in 2x2, each wave one 32x32 accumulator.
-// LDS k-major [32][64+1] for both operands (column reads conflict-free), two LDS
-// buffers, next tile prefetched into registers while the current one computes.
+// Tiles BM x BN x 32 (BM, BN in {128, 64}), 256 threads = 4 waves in 2 x 2, each wave
+// (BM/64) x (BN/64) 32x32 accumulators.  Both operands are staged row-major in LDS with k
+// contiguous ([r][32 + 4]); MFMA step ks of a K-tile pairs k = ks (lanes 0-31) with
+// k = 16 + ks (lanes 32-63), so each lane's operands for the whole tile are 16 contiguous
+// floats = 4 ds_read_b128 per fragment (row stride 36 floats: conflict-free per 16-lane group).
+// Global reads are float4 whenever rows are 16-B aligned: k-contiguous operands go to LDS with
+// ds_write_b128, row-contiguous ones (A of TN, B of NN) are transposed by ds_write_b32 with
+// lanes running along k (conflict-free).
+// Batched problems are flattened into one 1-D grid; logical blocks are dealt XCD-contiguously
+// (hardware deals blockIdx round-robin over the 8 XCDs), so neighbouring output tiles that
+// share an A panel share an L2.  When the output has too few tiles to fill 256 CUs, K is cut
+// into equal slices (split-K): each slice writes a partial slab and one reduce kernel sums the
+// slabs in slice order (deterministic) and applies alpha / bias / beta.
 #include "s2s_common.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 
 namespace s2s {
 
 namespace {
 
-constexpr int BM = 64, BN = 64, BK = 32, LDSP = BM + 1;
+constexpr int BK = 32, LDK = BK + 4;
 
-struct GemmBatchArgs {
-  GemmProblem p[kMaxGemmBatch];
+struct GemmTile {
+  GemmProblem p;
+  float* part;  // split-K partial slabs (splits x M x N) or nullptr
+  int tiles_n, tiles_m, splits, kslice;
+  int base;  // first logical block of this problem
+  int vecA, vecB;
+};
+struct GemmLaunch {
+  GemmTile q[kMaxGemmBatch];
+  int nprob, nblocks;
 };
 
-template <bool TA, bool TB>
-__global__ __launch_bounds__(256) void gemm_f32_kernel(GemmBatchArgs args) {
-  const GemmProblem& p = args.p[blockIdx.z];
-  const int M = p.M, N = p.N, K = p.K;
-  const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  if (m0 >= M || n0 >= N) return;
-
-  __shared__ float As[2][BK][LDSP];
-  __shared__ float Bs[2][BK][LDSP];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
-  const float* __restrict__ A = p.A;
-  const float* __restrict__ Bm = p.B;
-  const long lda = p.lda, ldb = p.ldb;
-
-  float ra[8], rb[8];
-  auto load = [&](int k0) {
+// k-contiguous operand (element (r, k) at X[r * ld + k]): f -> row f / 8, k quad f % 8.
+// FAST: interior tile, aligned rows -> unguarded float4.  Otherwise branch-free scalar loads
+// from clamped addresses, zeroed outside the problem (no divergent waits between loads).
+template <int R, bool FAST>
+__device__ __forceinline__ void load_kc(floatx4 (&v)[R / 32], const float* X, long ld, int r0, int rmax, int k0,
+                                        int kend) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i;
-      int kk, mm;
-      if (TA) { kk = e >> 6; mm = e & 63; } else { kk = e & 31; mm = e >> 5; }
-      const int gm = m0 + mm, gk = k0 + kk;
-      float v = 0.f;
-      if (gm < M && gk < K) v = TA ? A[(long)gk * lda + gm] : A[(long)gm * lda + gk];
-      ra[i] = v;
-      int kb, nn;
-      if (TB) { kb = e & 31; nn = e >> 5; } else { kb = e >> 6; nn = e & 63; }
-      const int gn = n0 + nn, gkb = k0 + kb;
-      float w = 0.f;
-      if (gn < N && gkb < K) w = TB ? Bm[(long)gn * ldb + gkb] : Bm[(long)gkb * ldb + gn];
-      rb[i] = w;
+  for (int j = 0; j < R / 32; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    const int gr = r0 + (f >> 3), k = k0 + 4 * (f & 7);
+    if (FAST) {
+      v[j] = *reinterpret_cast<const floatx4*>(X + (long)gr * ld + k);
+    } else {
+      const float* row = X + (long)min(gr, rmax - 1) * ld;
+      float e[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = row[min(k + c, kend - 1)];
+        e[c] = (gr < rmax && k + c < kend) ? x : 0.f;
+      }
+      v[j] = floatx4{e[0], e[1], e[2], e[3]};
     }
-  };
-  auto store = [&](int buf) {
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_kc(float* Xs, const floatx4 (&v)[R / 32]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int e = tid + 256 * i;
-      int kk, mm;
-      if (TA) { kk = e >> 6; mm = e & 63; } else { kk = e & 31; mm = e >> 5; }
-      As[buf][kk][mm] = ra[i];
-      int kb, nn;
-      if (TB) { kb = e & 31; nn = e >> 5; } else { kb = e >> 6; nn = e & 63; }
-      Bs[buf][kb][nn] = rb[i];
+  for (int j = 0; j < R / 32; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    *reinterpret_cast<floatx4*>(Xs + (f >> 3) * LDK + 4 * (f & 7)) = v[j];
+  }
+}
+// row-contiguous operand (element (r, k) at X[k * ld + r]): f -> k = f % 32, row quad f / 32
+template <int R, bool FAST>
+__device__ __forceinline__ void load_rc(floatx4 (&v)[R / 32], const float* X, long ld, int r0, int rmax, int k0,
+                                        int kend) {
+#pragma unroll
+  for (int j = 0; j < R / 32; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    const int k = k0 + (f & 31), r = r0 + 4 * (f >> 5);
+    if (FAST) {
+      v[j] = *reinterpret_cast<const floatx4*>(X + (long)k * ld + r);
+    } else {
+      const float* row = X + (long)min(k, kend - 1) * ld;
+      float e[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = row[min(r + c, rmax - 1)];
+        e[c] = (k < kend && r + c < rmax) ? x : 0.f;
+      }
+      v[j] = floatx4{e[0], e[1], e[2], e[3]};
     }
-  };
-
-  floatx16 acc;
+  }
+}
+template <int R>
+__device__ __forceinline__ void store_rc(float* Xs, const floatx4 (&v)[R / 32]) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+  for (int j = 0; j < R / 32; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    float* p = Xs + (4 * (f >> 5)) * LDK + (f & 31);
+    p[0] = v[j][0];
+    p[LDK] = v[j][1];
+    p[2 * LDK] = v[j][2];
+    p[3 * LDK] = v[j][3];
+  }
+}
 
-  const int nk = (K + BK - 1) / BK;
-  load(0);
-  store(0);
+// Double-buffered K loop: the next K-tile's global loads are in flight (registers) while the
+// current tile's 16 x FM x FN MFMAs run; one barrier per K-tile.  No lambdas here: captured
+// prefetch arrays were left in scratch memory by the compiler.
+template <bool TA, bool TB, int BM, int BN, bool FAST>
+__device__ __forceinline__ void gemm_mainloop(floatx16 (&acc)[BM / 64][BN / 64], float (&As)[2][BM * LDK],
+                                              float (&Bs)[2][BN * LDK], const float* __restrict__ A,
+                                              const float* __restrict__ Bm, long lda, long ldb, int m0, int n0, int M,
+                                              int N, int kbeg, int kend, int nk, int wy, int wx, int li, int lk) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
+  floatx4 ra[BM / 32], rb[BN / 32];
+  if (TA) load_rc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend); else load_kc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend);
+  if (TB) load_kc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend); else load_rc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend);
+  if (TA) store_rc<BM>(As[0], ra); else store_kc<BM>(As[0], ra);
+  if (TB) store_kc<BN>(Bs[0], rb); else store_rc<BN>(Bs[0], rb);
   __syncthreads();
-  const int li = lane & 31, lk = lane >> 5;
   for (int kt = 0; kt < nk; ++kt) {
     const int buf = kt & 1;
-    if (kt + 1 < nk) load((kt + 1) * BK);
-#pragma unroll
-    for (int kp = 0; kp < BK / 2; ++kp) {
-      const float a = As[buf][2 * kp + lk][wm + li];
-      const float b = Bs[buf][2 * kp + lk][wn + li];
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, acc, 0, 0, 0);
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * BK;
+      if (TA) load_rc<BM, FAST>(ra, A, lda, m0, M, k0, kend); else load_kc<BM, FAST>(ra, A, lda, m0, M, k0, kend);
+      if (TB) load_kc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend); else load_rc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend);
     }
-    if (kt + 1 < nk) store(buf ^ 1);
+    floatx4 a[FM][4], b[FN][4];
+#pragma unroll
+    for (int f = 0; f < FM; ++f) {
+      const float* p = As[buf] + (wy * WM + 32 * f + li) * LDK + 16 * lk;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) a[f][c] = *reinterpret_cast<const floatx4*>(p + 4 * c);
+    }
+#pragma unroll
+    for (int g = 0; g < FN; ++g) {
+      const float* p = Bs[buf] + (wx * WN + 32 * g + li) * LDK + 16 * lk;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[g][c] = *reinterpret_cast<const floatx4*>(p + 4 * c);
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int g = 0; g < FN; ++g)
+            acc[f][g] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[f][c][e], b[g][c][e], acc[f][g], 0, 0, 0);
+      }
+    }
+    if (more) {
+      if (TA) store_rc<BM>(As[buf ^ 1], ra); else store_kc<BM>(As[buf ^ 1], ra);
+      if (TB) store_kc<BN>(Bs[buf ^ 1], rb); else store_rc<BN>(Bs[buf ^ 1], rb);
+    }
     __syncthreads();
   }
+}
 
-  const float alpha = p.alpha, beta = p.beta;
-  const float* __restrict__ bias = p.bias;
-  float* __restrict__ C = p.C;
-  const int col = n0 + wn + li;
+template <bool TA, bool TB, int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
+  __shared__ __attribute__((aligned(16))) float As[2][BM * LDK];
+  __shared__ __attribute__((aligned(16))) float Bs[2][BN * LDK];
+
+  const int lin = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (lin >= Lc.nblocks) return;
+  int pi = 0;
+  while (pi + 1 < Lc.nprob && lin >= Lc.q[pi + 1].base) ++pi;
+  const GemmTile& q = Lc.q[pi];
+  int loc = lin - q.base;
+  const int tn = loc % q.tiles_n;
+  loc /= q.tiles_n;
+  const int tm = loc % q.tiles_m, s = loc / q.tiles_m;
+  const int M = q.p.M, N = q.p.N, K = q.p.K;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = s * q.kslice, kend = min(K, kbeg + q.kslice);
+  const float* __restrict__ A = q.p.A;
+  const float* __restrict__ Bm = q.p.B;
+  const long lda = q.p.lda, ldb = q.p.ldb;
+
+  floatx16 acc[FM][FN];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int row = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * lk;
-    if (row < M && col < N) {
-      float v = alpha * acc[r];
-      if (bias) v += bias[col];
-      float* c = C + (long)row * p.ldc + col;
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][g][r] = 0.f;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wy = wave >> 1, wx = wave & 1, li = lane & 31, lk = lane >> 5;
+  const int nk = (kend - kbeg + BK - 1) / BK;
+
+  if (nk > 0) {
+    const bool fast = q.vecA && q.vecB && m0 + BM <= M && n0 + BN <= N && (kend - kbeg) % BK == 0;
+    if (fast)
+      gemm_mainloop<TA, TB, BM, BN, true>(acc, As, Bs, A, Bm, lda, ldb, m0, n0, M, N, kbeg, kend, nk, wy, wx, li, lk);
+    else
+      gemm_mainloop<TA, TB, BM, BN, false>(acc, As, Bs, A, Bm, lda, ldb, m0, n0, M, N, kbeg, kend, nk, wy, wx, li, lk);
+  }
+
+  const float alpha = q.p.alpha, beta = q.p.beta;
+  const float* __restrict__ bias = q.p.bias;
+  float* __restrict__ C = q.p.C;
+  float* __restrict__ part = q.part;
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g) {
+      const int col = n0 + wx * WN + 32 * g + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = m0 + wy * WM + 32 * f + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        if (row < M && col < N) {
+          if (part) {
+            part[((long)s * M + row) * N + col] = acc[f][g][r];
+          } else {
+            float v = alpha * acc[f][g][r];
+            if (bias) v += bias[col];
+            float* c = C + (long)row * q.p.ldc + col;
+            if (beta != 0.f) v += beta * *c;
+            *c = v;
+          }
+        }
+      }
+    }
+}
+
+// C = alpha * (sum of the split slabs in slice order) (+ bias) + beta * C; blockIdx.y = problem.
+// Four consecutive columns per thread (float4) when rows allow it.
+__global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
+  const GemmTile& q = Lc.q[blockIdx.y];
+  if (q.part == nullptr) return;
+  const int M = q.p.M, N = q.p.N;
+  const long mn = (long)M * N;
+  const float alpha = q.p.alpha, beta = q.p.beta;
+  const float* __restrict__ bias = q.p.bias;
+  const bool vec = (N % 4 == 0) && (q.p.ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.p.C) & 15) == 0) &&
+                   ((reinterpret_cast<uintptr_t>(q.part) & 15) == 0);
+  if (vec) {
+    for (long e = 4 * (blockIdx.x * 256L + threadIdx.x); e < mn; e += 4L * gridDim.x * 256) {
+      floatx4 sum = {0.f, 0.f, 0.f, 0.f};
+      for (int s = 0; s < q.splits; ++s) sum += *reinterpret_cast<const floatx4*>(q.part + s * mn + e);
+      const int row = (int)(e / N), col = (int)(e % N);
+      floatx4 v = alpha * sum;
+      if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
+      floatx4* c = reinterpret_cast<floatx4*>(q.p.C + (long)row * q.p.ldc + col);
       if (beta != 0.f) v += beta * *c;
       *c = v;
     }
+    return;
+  }
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < mn; e += (long)gridDim.x * 256) {
+    float sum = 0.f;
+    for (int s = 0; s < q.splits; ++s) sum += q.part[s * mn + e];
+    const int row = (int)(e / N), col = (int)(e % N);
+    float v = alpha * sum;
+    if (bias) v += bias[col];
+    float* c = q.p.C + (long)row * q.p.ldc + col;
+    if (beta != 0.f) v += beta * *c;
+    *c = v;
   }
 }
 
@@ -148,31 +310,114 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 
 }  // namespace
 
-int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB) {
+struct GemmPlan {
+  int bm = 64, bn = 64, kslice = 0, nblocks = 0;
+};
+
+// Pick the tile shape and a uniform K slice for the batch from a simple time model: every CU
+// (256) works through ceil(blocks / 256) blocks of bm*bn*kslice MACs at a per-shape efficiency,
+// plus the split slabs' HBM round trip and the reduce launch.
+static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats) {
+  int kmax = 0;
+  for (int i = 0; i < n; ++i) kmax = p[i].K > kmax ? p[i].K : kmax;
+  const int kfull = (kmax + BK - 1) / BK * BK;
+  auto count = [&](GemmPlan& pl) {  // blocks and slab floats of a plan; false if the slabs do not fit
+    long blocks = 0;
+    double slab = 0;
+    for (int i = 0; i < n; ++i) {
+      const long t = (long)((p[i].M + pl.bm - 1) / pl.bm) * ((p[i].N + pl.bn - 1) / pl.bn);
+      const int sp = p[i].K > 0 && pl.kslice > 0 ? (p[i].K + pl.kslice - 1) / pl.kslice : 1;
+      blocks += t * sp;
+      if (sp > 1) slab += (double)sp * p[i].M * p[i].N;
+    }
+    pl.nblocks = (int)blocks;
+    return slab <= (double)ws_floats;
+  };
+  GemmPlan pl;
+  if (const char* o = std::getenv("S2S_GEMM_PLAN")) {  // "bm:bn:kslice" (diagnostics)
+    int bm = 0, bn = 0, ks = 0;
+    if (std::sscanf(o, "%d:%d:%d", &bm, &bn, &ks) == 3 && (bm == 128 || bm == 64) && (bn == 128 || bn == 64) &&
+        !(bm == 64 && bn == 128) && ks % BK == 0) {
+      pl.bm = bm; pl.bn = bn; pl.kslice = ks > 0 ? ks : kfull;
+      if (count(pl)) return pl;
+    }
+  }
+  // Measured on MI355X (tools/gemm_bench.cpp, every GEMM shape of the training step): 64 x 64
+  // tiles are the fastest or within a few % everywhere at these sizes (more blocks per CU hide
+  // the global->LDS latency); split-K pays only while the output has fewer than 512 tiles
+  // (2 per CU), and only down to 512-long K slices, until there are >= 1024 blocks.
+  pl.bm = 64; pl.bn = 64; pl.kslice = kfull;
+  count(pl);
+  const int tiles = pl.nblocks;
+  while (tiles < 512 && pl.nblocks < 1024 && pl.kslice / 2 >= 512) {
+    GemmPlan nx = pl;
+    nx.kslice = (pl.kslice / 2 + BK - 1) / BK * BK;
+    if (!count(nx)) break;
+    pl = nx;
+  }
+  return pl;
+}
+
+template <bool TA, bool TB>
+static void launch_tiles(hipStream_t st, const GemmPlan& pl, dim3 grid, const GemmLaunch& L) {
+  if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 128, 128>), grid, dim3(256), 0, st, L);
+  else if (pl.bm == 128) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 128, 64>), grid, dim3(256), 0, st, L);
+  else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 64, 64>), grid, dim3(256), 0, st, L);
+}
+
+int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB, GemmWs ws) {
   S2S_REQUIRE(nprob >= 1 && nprob <= kMaxGemmBatch, "gemm_f32: bad batch count");
-  GemmBatchArgs args;
-  int gm = 0, gn = 0, used = 0;
+  GemmProblem use[kMaxGemmBatch];
+  int used = 0;
   for (int i = 0; i < nprob; ++i) {
     const GemmProblem& q = probs[i];
     if (q.M <= 0 || q.N <= 0) continue;
     S2S_REQUIRE(q.K >= 0 && q.C != nullptr, "gemm_f32: bad problem");
-    args.p[used++] = q;
-    gm = gm > (q.M + BM - 1) / BM ? gm : (q.M + BM - 1) / BM;
-    gn = gn > (q.N + BN - 1) / BN ? gn : (q.N + BN - 1) / BN;
+    use[used++] = q;
   }
   if (used == 0) return 0;
+  const GemmPlan pl = plan_gemm(use, used, ws.p ? ws.n : 0);
+  GemmLaunch L{};
+  L.nprob = used;
+  int base = 0;
+  size_t woff = 0;
+  bool split = false;
   double flops = 0, bytes = 0;
   for (int i = 0; i < used; ++i) {
-    const GemmProblem& q = args.p[i];
-    flops += 2.0 * q.M * q.N * q.K;
-    bytes += 4.0 * ((double)q.M * q.K + (double)q.K * q.N + (double)q.M * q.N * (q.beta != 0.f ? 2 : 1));
+    GemmTile& t = L.q[i];
+    t.p = use[i];
+    t.tiles_m = (t.p.M + pl.bm - 1) / pl.bm;
+    t.tiles_n = (t.p.N + pl.bn - 1) / pl.bn;
+    t.kslice = t.p.K > 0 ? pl.kslice : BK;
+    t.splits = t.p.K > 0 ? (t.p.K + pl.kslice - 1) / pl.kslice : 1;
+    if (t.p.K == 0) t.kslice = 0;
+    t.part = nullptr;
+    if (t.splits > 1) {
+      t.part = ws.p + woff;
+      woff += (size_t)t.splits * t.p.M * t.p.N;
+      split = true;
+    }
+    t.base = base;
+    base += t.tiles_m * t.tiles_n * t.splits;
+    t.vecA = (t.p.lda % 4 == 0 && (reinterpret_cast<uintptr_t>(t.p.A) & 15) == 0) ? 1 : 0;
+    t.vecB = (t.p.ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(t.p.B) & 15) == 0) ? 1 : 0;
+    flops += 2.0 * t.p.M * t.p.N * t.p.K;
+    bytes += 4.0 * ((double)t.p.M * t.p.K + (double)t.p.K * t.p.N + (double)t.p.M * t.p.N * (t.p.beta != 0.f ? 2 : 1));
   }
+  L.nblocks = base;
   ProfScope ps(st, "gemm_f32", flops, bytes);
-  dim3 grid(gn, gm, used);
-  if (!transA && !transB) hipLaunchKernelGGL((gemm_f32_kernel<false, false>), grid, dim3(256), 0, st, args);
-  else if (!transA && transB) hipLaunchKernelGGL((gemm_f32_kernel<false, true>), grid, dim3(256), 0, st, args);
-  else if (transA && !transB) hipLaunchKernelGGL((gemm_f32_kernel<true, false>), grid, dim3(256), 0, st, args);
-  else hipLaunchKernelGGL((gemm_f32_kernel<true, true>), grid, dim3(256), 0, st, args);
+  const dim3 grid((unsigned)((base + 7) / 8 * 8));
+  if (!transA && !transB) launch_tiles<false, false>(st, pl, grid, L);
+  else if (!transA && transB) launch_tiles<false, true>(st, pl, grid, L);
+  else if (transA && !transB) launch_tiles<true, false>(st, pl, grid, L);
+  else launch_tiles<true, true>(st, pl, grid, L);
+  if (split) {
+    long mn_max = 0;
+    for (int i = 0; i < used; ++i)
+      if (L.q[i].part) mn_max = std::max(mn_max, (long)L.q[i].p.M * L.q[i].p.N);
+    const unsigned gx = (unsigned)std::min<long>(1024, (mn_max + 1023) / 1024);
+    hipLaunchKernelGGL(splitk_reduce_kernel, dim3(gx, used), dim3(256), 0, st, L);
+  }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

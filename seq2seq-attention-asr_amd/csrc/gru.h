@@ -32,7 +32,7 @@ int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, 
 // gate gradients into dA (B, L, 3*ndir*H) (dA == nullptr: inside scratch); wgrad = the dW GEMMs.
 int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, float* dA, void* scratch,
                        size_t scratch_bytes);
-int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA);
+int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws);
 float* gru_layer_dA(const GruLayerIO& io, void* scratch);
 
 }  // namespace s2s

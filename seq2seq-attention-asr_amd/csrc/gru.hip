@@ -242,7 +242,14 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   bp.take<float>(3L * ndir * H * D);             // Wx (both dirs)
   bp.take<float>((long)B * L * 3 * ndir * H);    // xp or dA (both dirs)
   bp.take<char>(gru_persist_sync_bytes(B, H));   // persistent-kernel granule buffers
+  bp.take<float>(kGemmWsFloats);                 // split-K slabs of this layer's GEMMs
   return bp.off + 256;
+}
+
+// the split-K region at the tail of a layer scratch (gru_layer_scratch_bytes)
+static GemmWs layer_gemm_ws(void* scratch, int ndir, int B, int L, int D, int H) {
+  const size_t tail = gru_layer_scratch_bytes(ndir, B, L, D, H) - 256 - sizeof(float) * kGemmWsFloats;
+  return GemmWs{reinterpret_cast<float*>(static_cast<char*>(scratch) + tail), kGemmWsFloats};
 }
 
 int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes) {
@@ -269,7 +276,8 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
     S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Uzr[d], Uh[d], nullptr, nullptr,
                         Wx + 3L * d * H * D));
   // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, D) . Wx^T
-  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, D, 1.f, io.x, io.ldx, Wx, D, 0.f, xp, 3L * nd * H));
+  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, D, 1.f, io.x, io.ldx, Wx, D, 0.f, xp, 3L * nd * H, nullptr,
+                layer_gemm_ws(scratch, nd, B, L, D, H)));
   GruFwdArgs a{};
   for (int d = 0; d < nd; ++d)
     a.d[d] = GruFwdDir{xp + 3L * d * H, 3L * nd * H, Uzr[d], Uh[d], io.y[d], io.ldy, io.saved[d], io.reverse[d]};
@@ -350,7 +358,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   // which is what the encoder graph's fan-out of the layer input accumulates)
   if (gr.dx)
     S2S_TRY(gemm1(st, false, false, B * L, D, 3 * nd * H, 1.f, dA, ldA, Wx, D, gr.dx_accumulate ? 1.f : 0.f, gr.dx,
-                  gr.lddx));
+                  gr.lddx, nullptr, layer_gemm_ws(scratch, nd, B, L, D, H)));
   return 0;
 }
 
@@ -370,7 +378,7 @@ float* gru_layer_dA(const GruLayerIO& io, void* scratch) {
 
 // dW += scale * dA_g^T . [h_{t-1} | q ; x]   (LinearZeroBias.lua:67-74 summed over all steps).
 // Off the recurrence: the model step runs it on a side stream beside the next layer's BPTT.
-int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA) {
+int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws) {
   const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
   const long ldA = 3L * nd * H;
   GemmProblem probs[12];
@@ -386,12 +394,13 @@ int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr
       probs[np++] = GemmProblem{dAg, io.x, dW + H, nullptr, ldA, io.ldx, (long)H + D, H, D, B * L, gr.scale, 1.f};
     }
   }
-  return gemm_f32(st, probs, np, true, false);
+  return gemm_f32(st, probs, np, true, false, ws);
 }
 
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes) {
   S2S_TRY(gru_layer_bwd_core(st, io, gr, nullptr, scratch, scratch_bytes));
-  return gru_layer_wgrad(st, io, gr, gru_layer_dA(io, scratch));
+  return gru_layer_wgrad(st, io, gr, gru_layer_dA(io, scratch),
+                         layer_gemm_ws(scratch, io.ndir, io.B, io.L, io.D, io.H));
 }
 
 }  // namespace s2s

@@ -70,12 +70,20 @@ struct GemmProblem {
   float alpha, beta;
 };
 constexpr int kMaxGemmBatch = 16;
+// Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs
+// fit; without a workspace every problem runs unsplit.  Concurrent calls need disjoint ones.
+struct GemmWs {
+  float* p = nullptr;
+  size_t n = 0;
+};
+constexpr size_t kGemmWsFloats = size_t(8) << 20;  // 32 MiB
 // All problems of one call share transA/transB.
-int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB);
+int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB, GemmWs ws = GemmWs{});
 inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
-                 const float* B, long ldb, float beta, float* C, long ldc, const float* bias = nullptr) {
+                 const float* B, long ldb, float beta, float* C, long ldc, const float* bias = nullptr,
+                 GemmWs ws = GemmWs{}) {
   GemmProblem p{A, B, C, bias, lda, ldb, ldc, M, N, K, alpha, beta};
-  return gemm_f32(st, &p, 1, tA, tB);
+  return gemm_f32(st, &p, 1, tA, tB, ws);
 }
 
 // Column sums: out[j] = beta*out[j] + alpha * sum_i X[i*ldx + j], i < M, j < N.
