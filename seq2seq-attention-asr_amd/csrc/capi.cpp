@@ -147,6 +147,8 @@ struct ModelWs {
   size_t scratch_bytes;
   float *dlogp, *nll, *logp, *dY0, *dY1;
   GemmWs gws_side;  // split-K slabs of the encoder weight-gradient GEMMs (may run on the side stream)
+  float* xpad;      // (B*L, Dp) zero-padded copy of the input when inputFrameSize % 32 != 0, else null
+  int Dp;
   size_t total;
 };
 ModelWs model_ws(const s2s_model_dims* d, void* base) {
@@ -176,6 +178,8 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
   w.dY0 = bp.take<float>(B * L * 2 * hmax);
   w.dY1 = bp.take<float>(B * L * 2 * hmax);
   w.gws_side = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
+  w.Dp = (d->inputFrameSize + 31) / 32 * 32;
+  w.xpad = d->inputFrameSize % 32 != 0 ? bp.take<float>(B * L * w.Dp) : nullptr;
   w.total = bp.off + 256;
   return w;
 }
@@ -215,13 +219,22 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
-  const float* inp = x;
-  long ldin = d->inputFrameSize;
+  // layer-1 input padded to a multiple of 32 columns: its GEMMs then run on aligned full tiles
+  const float* x0 = x;
+  long ldx0 = d->inputFrameSize;
+  if (w.xpad) {
+    S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
+    x0 = w.xpad;
+    ldx0 = w.Dp;
+  }
+  const float* inp = x0;
+  long ldin = ldx0;
   for (int l = 0; l < nl; ++l) {
     const int H = layers[l].H;
     GruLayerIO io{};
     io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
     io.x = inp; io.ldx = ldin;
+    io.Dx = (l == 0 && w.xpad) ? w.Dp : 0;
     for (int dd = 0; dd < 2; ++dd) {
       for (int g = 0; g < 3; ++g) io.W[dd][g] = P[6 * l + 3 * dd + g];
       io.reverse[dd] = dd;
@@ -259,8 +272,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
     const int H = layers[l].H;
     GruLayerIO io{};
     io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
-    io.x = l == 0 ? x : w.Y[l - 1];
-    io.ldx = l == 0 ? d->inputFrameSize : 2L * layers[l - 1].H;
+    io.x = l == 0 ? x0 : w.Y[l - 1];
+    io.ldx = l == 0 ? ldx0 : 2L * layers[l - 1].H;
+    io.Dx = (l == 0 && w.xpad) ? w.Dp : 0;
     io.ldy = 2L * H;
     GruLayerGrad gr{};
     for (int dd = 0; dd < 2; ++dd) {

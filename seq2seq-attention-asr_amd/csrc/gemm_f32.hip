@@ -203,7 +203,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
   const int nk = (kend - kbeg + BK - 1) / BK;
 
   if (nk > 0) {
-    const bool fast = q.vecA && q.vecB && m0 + BM <= M && n0 + BN <= N && (kend - kbeg) % BK == 0;
+    const int Mr = max(M, q.p.Mread), Nr = max(N, q.p.Nread);
+    const bool fast = q.vecA && q.vecB && m0 + BM <= Mr && n0 + BN <= Nr && (kend - kbeg) % BK == 0;
     if (fast)
       gemm_mainloop<TA, TB, BM, BN, true>(acc, As, Bs, A, Bm, lda, ldb, m0, n0, M, N, kbeg, kend, nk, wy, wx, li, lk);
     else
@@ -299,6 +300,15 @@ __global__ void copy2d_kernel(const float* __restrict__ src, long lds, float* __
     const long r = i / cols, c = i - r * cols;
     const float v = src[r * lds + c];
     if (accumulate) dst[r * ldd + c] += v; else dst[r * ldd + c] = v;
+  }
+}
+
+__global__ void pad_cols_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, int rows, int cols,
+                                int dcols) {
+  const long n = (long)rows * dcols;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / dcols, c = i - r * dcols;
+    dst[i] = c < cols ? src[r * lds + c] : 0.f;
   }
 }
 
@@ -435,6 +445,15 @@ int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd,
   int blocks = (int)((n + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(copy2d_kernel, dim3(blocks), dim3(256), 0, st, src, lds, dst, ldd, rows, cols, acc ? 1 : 0);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int pad_cols_f32(hipStream_t st, const float* src, long lds, float* dst, int rows, int cols, int dcols) {
+  if (rows <= 0 || dcols <= 0) return 0;
+  const long n = (long)rows * dcols;
+  const int blocks = (int)std::min<long>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(pad_cols_kernel, dim3(blocks), dim3(256), 0, st, src, lds, dst, rows, cols, dcols);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -14,6 +14,8 @@ struct GruLayerIO {
   float* y[2];  // y[d][(b*L + t)*ldy + j]
   long ldy;
   float* saved[2];  // per direction (B, L, 5H)
+  int Dx = 0;       // x columns [D, Dx) are readable zeros (0 = D; Dx <= round_up(D, 32)):
+                    // the input GEMMs then run over K = Dx on aligned, unguarded tiles
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]

@@ -180,11 +180,11 @@ __global__ __launch_bounds__(256) void gru_bwd_p2(GruBwdArgs a) {
 struct PackArgs {
   const float* W[3];
   float *Uzr, *Uh, *UhT, *UzrT, *Wx;
-  int H, D;
+  int H, D, Kx;  // Wx rows have stride Kx >= D, columns [D, Kx) zero
 };
 __global__ void gru_pack(PackArgs p) {
-  const int H = p.H, D = p.D, HD = H + D;
-  const long nU = 3L * H * H, nX = 3L * H * D;
+  const int H = p.H, D = p.D, HD = H + D, Kx = p.Kx;
+  const long nU = 3L * H * H, nX = 3L * H * Kx;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nU + nX; i += (long)gridDim.x * blockDim.x) {
     if (i < nU) {
       const int g = (int)(i / ((long)H * H));
@@ -200,18 +200,18 @@ __global__ void gru_pack(PackArgs p) {
       }
     } else if (p.Wx) {
       const long j = i - nU;
-      const int g = (int)(j / ((long)H * D));
-      const long rem = j - (long)g * H * D;
-      const int n = (int)(rem / D), c = (int)(rem - (long)n * D);
-      p.Wx[(long)(g * H + n) * D + c] = p.W[g][(long)n * HD + H + c];
+      const int g = (int)(j / ((long)H * Kx));
+      const long rem = j - (long)g * H * Kx;
+      const int n = (int)(rem / Kx), c = (int)(rem - (long)n * Kx);
+      p.Wx[(long)(g * H + n) * Kx + c] = c < D ? p.W[g][(long)n * HD + H + c] : 0.f;
     }
   }
 }
 
-int launch_pack(hipStream_t st, const float* Wz, const float* Wr, const float* Wh, int H, int D, float* Uzr,
+int launch_pack(hipStream_t st, const float* Wz, const float* Wr, const float* Wh, int H, int D, int Kx, float* Uzr,
                 float* Uh, float* UhT, float* UzrT, float* Wx) {
-  PackArgs p{{Wz, Wr, Wh}, Uzr, Uh, UhT, UzrT, Wx, H, D};
-  long n = 3L * H * (H + D);
+  PackArgs p{{Wz, Wr, Wh}, Uzr, Uh, UhT, UzrT, Wx, H, D, Kx};
+  long n = 3L * H * (H + Kx);
   int blocks = (int)((n + 255) / 256);
   if (blocks > 1024) blocks = 1024;
   hipLaunchKernelGGL(gru_pack, dim3(blocks), dim3(256), 0, st, p);
@@ -239,7 +239,7 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
     bp.take<float>((long)B * H);
     bp.take<float>((long)B * H);
   }
-  bp.take<float>(3L * ndir * H * D);             // Wx (both dirs)
+  bp.take<float>(3L * ndir * H * ((D + 31) / 32 * 32));  // Wx (both dirs, rows padded)
   bp.take<float>((long)B * L * 3 * ndir * H);    // xp or dA (both dirs)
   bp.take<char>(gru_persist_sync_bytes(B, H));   // persistent-kernel granule buffers
   bp.take<float>(kGemmWsFloats);                 // split-K slabs of this layer's GEMMs
@@ -269,14 +269,16 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
     bp.take<float>((long)B * H);
     bp.take<float>((long)B * H);
   }
-  float* Wx = bp.take<float>(3L * nd * H * D);
+  const int Kx = io.Dx > D ? io.Dx : D;
+  S2S_REQUIRE(Kx <= (D + 31) / 32 * 32 && io.ldx >= Kx, "gru: Dx must be <= round_up(D, 32) and <= ldx");
+  float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* xp = bp.take<float>((long)B * L * 3 * nd * H);
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   for (int d = 0; d < nd; ++d)
-    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Uzr[d], Uh[d], nullptr, nullptr,
-                        Wx + 3L * d * H * D));
-  // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, D) . Wx^T
-  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, D, 1.f, io.x, io.ldx, Wx, D, 0.f, xp, 3L * nd * H, nullptr,
+    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, Uzr[d], Uh[d], nullptr, nullptr,
+                        Wx + 3L * d * H * Kx));
+  // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, Kx) . Wx^T
+  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, Kx, 1.f, io.x, io.ldx, Wx, Kx, 0.f, xp, 3L * nd * H, nullptr,
                 layer_gemm_ws(scratch, nd, B, L, D, H)));
   GruFwdArgs a{};
   for (int d = 0; d < nd; ++d)
@@ -320,14 +322,16 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     dhc[d] = bp.take<float>((long)B * H);
     dhp[d] = bp.take<float>((long)B * H);
   }
-  float* Wx = bp.take<float>(3L * nd * H * D);
+  const int Kx = io.Dx > D ? io.Dx : D;
+  S2S_REQUIRE(Kx <= (D + 31) / 32 * 32 && io.ldx >= Kx, "gru: Dx must be <= round_up(D, 32) and <= ldx");
+  float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* dA_int = bp.take<float>((long)B * L * 3 * nd * H);
   float* dA = dA_ext ? dA_ext : dA_int;
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   const long ldA = 3L * nd * H;
   for (int d = 0; d < nd; ++d)
-    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, nullptr, nullptr, UhT[d], UzrT[d],
-                        Wx + 3L * d * H * D));
+    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, nullptr, nullptr, UhT[d], UzrT[d],
+                        Wx + 3L * d * H * Kx));
   GruBwdArgs a{};
   for (int d = 0; d < nd; ++d)
     a.d[d] = GruBwdDir{gr.dy[d], gr.lddy, io.saved[d], UhT[d], UzrT[d], dA + 3L * d * H, ldA, dhc[d], dhp[d],
@@ -356,9 +360,11 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   }
   // dx (+)= dA (B*L, 3*nd*H) . Wx (3*nd*H, D)   (RNN.lua:196 gradInput; both directions summed,
   // which is what the encoder graph's fan-out of the layer input accumulates)
-  if (gr.dx)
-    S2S_TRY(gemm1(st, false, false, B * L, D, 3 * nd * H, 1.f, dA, ldA, Wx, D, gr.dx_accumulate ? 1.f : 0.f, gr.dx,
-                  gr.lddx, nullptr, layer_gemm_ws(scratch, nd, B, L, D, H)));
+  if (gr.dx) {
+    GemmProblem p{dA, Wx, gr.dx, nullptr, ldA, Kx, gr.lddx, B * L, D, 3 * nd * H, 1.f, gr.dx_accumulate ? 1.f : 0.f};
+    p.Nread = Kx;  // Wx's zero columns
+    S2S_TRY(gemm_f32(st, &p, 1, false, false, layer_gemm_ws(scratch, nd, B, L, D, H)));
+  }
   return 0;
 }
 
@@ -372,7 +378,7 @@ float* gru_layer_dA(const GruLayerIO& io, void* scratch) {
     bp.take<float>((long)io.B * io.H);
     bp.take<float>((long)io.B * io.H);
   }
-  bp.take<float>(3L * io.ndir * io.H * io.D);
+  bp.take<float>(3L * io.ndir * io.H * ((io.D + 31) / 32 * 32));  // Wx (padded rows), as in the layer calls
   return bp.take<float>((long)io.B * io.L * 3 * io.ndir * io.H);
 }
 
@@ -391,7 +397,8 @@ int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr
       probs[np++] = GemmProblem{dAg, io.saved[d] + (g == 2 ? 4 : 3) * H, dW, nullptr, ldA, 5L * H, (long)H + D,
                                 H, H, B * L, gr.scale, 1.f};
       // x-part columns [H, H+D)
-      probs[np++] = GemmProblem{dAg, io.x, dW + H, nullptr, ldA, io.ldx, (long)H + D, H, D, B * L, gr.scale, 1.f};
+      probs[np] = GemmProblem{dAg, io.x, dW + H, nullptr, ldA, io.ldx, (long)H + D, H, D, B * L, gr.scale, 1.f};
+      probs[np++].Nread = io.Dx > D ? io.Dx : D;  // x's zero columns
     }
   }
   return gemm_f32(st, probs, np, true, false, ws);

@@ -60,6 +60,8 @@ __device__ __forceinline__ float wave_max(float v) {
 //   op(A)(i,k) = transA ? A[k*lda + i] : A[i*lda + k]
 //   op(B)(k,j) = transB ? B[j*ldb + k] : B[k*ldb + j]
 // beta == 0 overwrites C without reading it.
+// Mread / Nread (0 = M / N): rows of op(A) / columns of op(B) that may be READ (zero padding
+// the caller guarantees), so tiles straddling M / N can still take the unguarded load path.
 struct GemmProblem {
   const float* A;
   const float* B;
@@ -68,6 +70,7 @@ struct GemmProblem {
   long lda, ldb, ldc;
   int M, N, K;
   float alpha, beta;
+  int Mread = 0, Nread = 0;
 };
 constexpr int kMaxGemmBatch = 16;
 // Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs
@@ -90,6 +93,8 @@ inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float al
 int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out);
 // Strided 2-D copy (rows x cols) dst[r*ldd + c] = src[r*lds + c]  (+ optional accumulate).
 int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd, int rows, int cols, bool accumulate);
+// dst (rows x dcols, ld dcols) = src (rows x cols, ld lds) with columns [cols, dcols) zeroed
+int pad_cols_f32(hipStream_t st, const float* src, long lds, float* dst, int rows, int cols, int dcols);
 // dst[i] = alpha * src[i] + beta * dst[i]
 int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alpha, float beta);
 
