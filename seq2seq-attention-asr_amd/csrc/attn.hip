@@ -623,29 +623,6 @@ __global__ void dec_onehot_prev(AttnK k) {
   }
 }
 
-__global__ void transpose_kernel(const float* __restrict__ src, long lds, int rows, int cols, float* __restrict__ dst,
-                                 long ldd) {
-  // dst[c*ldd + r] = src[r*lds + c]
-  __shared__ float tile[32][33];
-  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
-  for (int i = threadIdx.y; i < 32; i += 8) {
-    const int r = r0 + i, c = c0 + threadIdx.x;
-    if (r < rows && c < cols) tile[i][threadIdx.x] = src[(long)r * lds + c];
-  }
-  __syncthreads();
-  for (int i = threadIdx.y; i < 32; i += 8) {
-    const int c = c0 + i, r = r0 + threadIdx.x;
-    if (r < rows && c < cols) dst[(long)c * ldd + r] = tile[threadIdx.x][i];
-  }
-}
-
-int transpose(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd) {
-  hipLaunchKernelGGL(transpose_kernel, dim3((cols + 31) / 32, (rows + 31) / 32), dim3(32, 8), 0, st, src, lds, rows,
-                     cols, dst, ldd);
-  S2S_CHECK_HIP(hipGetLastError());
-  return 0;
-}
-
 __global__ void fill2d_kernel(float* dst, long ldd, int rows, int cols, float v) {
   const long n = (long)rows * cols;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -843,15 +820,15 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
   S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
   // packed transposes for the backward products
-  S2S_TRY(transpose(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
-  S2S_TRY(transpose(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
-  S2S_TRY(transpose(st, P.Wr, 2L * S, S, 2 * S, k.GT + S, 3L * S));
-  S2S_TRY(transpose(st, P.Wh, 2L * S, S, 2 * S, k.GT + 2 * S, 3L * S));
+  S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
+  S2S_TRY(transpose_f32(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
+  S2S_TRY(transpose_f32(st, P.Wr, 2L * S, S, 2 * S, k.GT + S, 3L * S));
+  S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, 2 * S, k.GT + 2 * S, 3L * S));
   // the h-half of Wh reaches ds_{t-1} through dq = Wh[:, :S]^T da_h (K2), not through GT
   hipLaunchKernelGGL(fill2d_kernel, dim3(64), dim3(256), 0, st, k.GT + 2 * S, 3L * S, S, S, 0.f);
-  S2S_TRY(transpose(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
-  S2S_TRY(transpose(st, P.Wc, A, S, A, k.WcT, S));
-  S2S_TRY(transpose(st, P.Ws, S, Sc, S, k.WsT, Sc));
+  S2S_TRY(transpose_f32(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
+  S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
+  S2S_TRY(transpose_f32(st, P.Ws, S, Sc, S, k.WsT, Sc));
   // MLP backward for all rows (not on the recurrence)
   hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());

@@ -303,6 +303,22 @@ __global__ void copy2d_kernel(const float* __restrict__ src, long lds, float* __
   }
 }
 
+__global__ void transpose_kernel(const float* __restrict__ src, long lds, int rows, int cols, float* __restrict__ dst,
+                                 long ldd) {
+  // dst[c*ldd + r] = src[r*lds + c]
+  __shared__ float tile[32][33];
+  const int r0 = blockIdx.y * 32, c0 = blockIdx.x * 32;
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int r = r0 + i, c = c0 + threadIdx.x;
+    if (r < rows && c < cols) tile[i][threadIdx.x] = src[(long)r * lds + c];
+  }
+  __syncthreads();
+  for (int i = threadIdx.y; i < 32; i += 8) {
+    const int c = c0 + i, r = r0 + threadIdx.x;
+    if (r < rows && c < cols) dst[(long)c * ldd + r] = tile[threadIdx.x][i];
+  }
+}
+
 __global__ void pad_cols_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, int rows, int cols,
                                 int dcols) {
   const long n = (long)rows * dcols;
@@ -445,6 +461,13 @@ int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd,
   int blocks = (int)((n + 255) / 256);
   if (blocks > 2048) blocks = 2048;
   hipLaunchKernelGGL(copy2d_kernel, dim3(blocks), dim3(256), 0, st, src, lds, dst, ldd, rows, cols, acc ? 1 : 0);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int transpose_f32(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd) {
+  hipLaunchKernelGGL(transpose_kernel, dim3((cols + 31) / 32, (rows + 31) / 32), dim3(32, 8), 0, st, src, lds, rows,
+                     cols, dst, ldd);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

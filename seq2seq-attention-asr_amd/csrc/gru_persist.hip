@@ -50,7 +50,17 @@ struct PArgs {
   PDir d[2];
   int B, L, H, MT, nwg;  // nwg = workgroups per direction
   unsigned* abort_word;
+  unsigned long long* stamps;  // diagnostic: [grid][L][6] s_memrealtime, or nullptr
 };
+
+// diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
+// end and p2 sweep start / done / end
+#define GRU_STAMP(ph)                                                                      \
+  do {                                                                                     \
+    if (a.stamps && threadIdx.x == 0)                                                      \
+      a.stamps[((long)blockIdx.x * a.L + s) * 6 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+unsigned long long* g_gru_stamps[2] = {nullptr, nullptr};
 
 // cross-wave sum + abort agreement at the same barrier
 __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds, bool ok, floatx4 acc, int wave,
@@ -97,49 +107,59 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     const float xpv = live ? g.xp[row * g.ldxp + on] : 0.f;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     bool ok = true;
+    GRU_STAMP(0);
     if (s > 0) {
       float4 av[NC];
       ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
+      GRU_STAMP(1);
       acc = mfma_chunks<NC>(av, w1);
     }
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    if (live) {
+    {
       const float gate = sigmoidf_(sum + xpv);
       float* sv = g.sv + row * 5 * H;
       if (isz) {
-        sv[on] = gate;
+        if (live) sv[on] = gate;
         zreg = gate;
       } else {
         const int j = on - H;
-        const float hp = s > 0 ? peek_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
+        const float hp = (s > 0 && live) ? peek_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
         const float q = gate * hp;
-        sv[H + j] = gate;
-        sv[3 * H + j] = hp;
-        sv[4 * H + j] = q;
-        put_granule(g.g1 + (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1));
+        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1), live);  // critical first
+        if (live) {
+          sv[H + j] = gate;
+          sv[3 * H + j] = hp;
+          sv[4 * H + j] = q;
+        }
       }
     }
+    GRU_STAMP(2);
     if (!isz) continue;
     // ---- p2: hh = tanh(Uh q + xp_h); h = (1-z) h_{t-1} + z hh
     const float xph = live ? g.xp[row * g.ldxp + 2 * H + on] : 0.f;
     acc = floatx4{0.f, 0.f, 0.f, 0.f};
     ok = true;
+    GRU_STAMP(3);
     if (s > 0) {
       float4 av[NC];
       ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), (unsigned)(s + 1), wave, lane, a.abort_word);
+      GRU_STAMP(4);
       acc = mfma_chunks<NC>(av, w2);
     }
     sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    if (live) {
+    {
       const float hh = tanhf(sum + xph);
       const float hp = hreg;
-      g.sv[row * 5 * H + 2 * H + on] = hh;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
-      g.y[row * g.ldy + on] = hreg;
-      put_granule(g.g0 + (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1));
+      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1), live);  // first
+      if (live) {
+        g.sv[row * 5 * H + 2 * H + on] = hh;
+        g.y[row * g.ldy + on] = hreg;
+      }
     }
+    GRU_STAMP(5);
   }
 }
 
@@ -169,21 +189,28 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   float dhc = 0.f, dhp = 0.f;
   bool aborted = false;
 
-  // gate gradients of dh = dy_t + carry at time t, published with epoch `tag` into slot `sl`
-  auto gate = [&](int t, float dh, unsigned tag, int sl) {
+  // gate gradients of dh = dy_t + carry at time t (rows that are live), published with epoch `tag`
+  // into slot `sl` when `pub`; every lane of the workgroup calls it (pair stores)
+  auto gate = [&](int t, float dh, unsigned tag, int sl, bool pub) {
     const long row = (long)ob * L + t;
-    const float* sv = g.sv + row * 5 * H;
-    const float z = sv[ok_], hh = sv[2 * H + ok_], hp = sv[3 * H + ok_];
+    float z = 0.f, hh = 0.f, hp = 0.f;
+    if (pub) {
+      const float* sv = g.sv + row * 5 * H;
+      z = sv[ok_]; hh = sv[2 * H + ok_]; hp = sv[3 * H + ok_];
+    }
     const float daz = dh * (hh - hp) * (z * (1.0f - z));
     const float dah = (dh * z) * (1.0f - hh * hh);
-    g.dA[row * g.ldA + ok_] = daz;
-    g.dA[row * g.ldA + 2 * H + ok_] = dah;
-    put_granule(g.g0 + sl * slot + (long)ob * H + ok_, daz, tag);
-    put_granule(g.g2 + sl * slot + (long)ob * H + ok_, dah, tag);
+    const long off = sl * slot + (long)ob * H + ok_;
+    put_granule_pair(g.g2, off, dah, tag, pub);  // da_h gates the next p1: first
+    put_granule_pair(g.g0, off, daz, tag, pub);
+    if (pub) {
+      g.dA[row * g.ldA + ok_] = daz;
+      g.dA[row * g.ldA + 2 * H + ok_] = dah;
+    }
   };
 
   const int tl = g.reverse ? 0 : L - 1;
-  if (live) gate(tl, g.dy[((long)ob * L + tl) * g.lddy + ok_], 1u, 0);
+  gate(tl, live ? g.dy[((long)ob * L + tl) * g.lddy + ok_] : 0.f, 1u, 0, live);
 
   for (int p = 0; p < L; ++p) {
     const int s = L - 1 - p;
@@ -199,25 +226,32 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
       dyv = g.dy[row * g.lddy + ok_];
     }
     float4 av[NC];
+    GRU_STAMP(0);
     bool ok = sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+    GRU_STAMP(1);
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
+    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * hp) * (r * (1.0f - r)), tag, live);
     if (live) {
       const float dar = (dq * hp) * (r * (1.0f - r));
       g.dA[row * g.ldA + H + ok_] = dar;
-      put_granule(g.g1 + sl * slot + (long)ob * H + ok_, dar, tag);
       const float dh = dyv + dhc;
       dhp = dh * (-z + 1.0f) + dq * r;
     }
+    GRU_STAMP(2);
     // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
     const int tn = g.reverse ? t + 1 : t - 1;
     const float dyn = (live && s > 0) ? g.dy[((long)ob * L + tn) * g.lddy + ok_] : 0.f;
     float4 azr[2 * NC];
+    GRU_STAMP(3);
     {
+      // da_z (ready since the previous step) first, then poll da_r (this step's p1) alone: a
+      // merged poll of both rows re-reads da_z while waiting for da_r (measured slower)
       float4 az[NC], ar[NC];
       ok = sweep_skinny<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
       ok = ok && sweep_skinny<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      GRU_STAMP(4);
       // chunk i of the K = 2H product: i < NC reads da_z, i >= NC reads da_r (H % 64 == 0)
 #pragma unroll
       for (int i = 0; i < NC; ++i) { azr[i] = az[i]; azr[NC + i] = ar[i]; }
@@ -225,10 +259,9 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     acc = mfma_chunks<2 * NC>(azr, wzr);
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    if (live && s > 0) {
-      dhc = dhp + sm;
-      gate(tn, dyn + dhc, tag + 1, sl ^ 1);
-    }
+    if (live && s > 0) dhc = dhp + sm;
+    if (s > 0) gate(tn, dyn + dhc, tag + 1, sl ^ 1, live);
+    GRU_STAMP(5);
   }
 }
 
@@ -282,6 +315,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
                   gr[d][0], gr[d][1], gr[d][2]};
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
+  a.stamps = g_gru_stamps[0];
   S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(f.B, f.H), st));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
@@ -297,6 +331,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
                   b.reverse[d], gr[d][0], gr[d][1], gr[d][2]};
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
+  a.stamps = g_gru_stamps[1];
   S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(b.B, b.H), st));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
@@ -304,3 +339,10 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
 }
 
 }  // namespace s2s
+
+// diagnostic: the next persistent GRU launches fill these with stamps (tools/gru_stamps.py);
+// nullptr turns it off.  Not part of the C ABI header.
+extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
+  s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
+  s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);
+}

@@ -20,6 +20,36 @@ __device__ __forceinline__ void put_granule(granule_t* g, float v, unsigned tag)
   const granule_t x = ((granule_t)tag << 32) | (granule_t)__float_as_uint(v);
   __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// Publish granule base[idx] of this lane when `active` (base is wave-uniform).  Lanes l and l^1
+// own adjacent granules j, j+1 (j even at the even lane) at every call site, so
+// S2S_PAIRED_GRANULES=1 lets the even lane write both in one 16-byte sc1 buffer store after a
+// lane shuffle (every lane must then call it).  Measured on MI355X (same-box A/B): slower than
+// one 8-byte global sc1 store per lane, and buffer-form 8-byte stores are slower than the
+// global form -- so the default is put_granule's global_store_dwordx2 sc1.
+#ifndef S2S_PAIRED_GRANULES
+#define S2S_PAIRED_GRANULES 0
+#endif
+__device__ __forceinline__ void put_granule_pair(granule_t* base, long idx, float v, unsigned tag, bool active) {
+#if S2S_PAIRED_GRANULES
+  const float vn = __shfl_xor(v, 1, 64);
+  if (active && (threadIdx.x & 1) == 0) {
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 d = {__float_as_uint(v), tag, __float_as_uint(vn), tag};
+    __builtin_amdgcn_raw_buffer_store_b128(d, rsrc_of(base), (int)(8 * idx), 0, 16);
+  }
+#else
+  if (active) put_granule(base + idx, v, tag);
+#endif
+}
+// four adjacent granules j..j+3 of one lane (j % 2 == 0) as two 16-byte write-through stores
+__device__ __forceinline__ void put_granule4(__amdgpu_buffer_rsrc_t rs, long byte_off, float v0, float v1, float v2,
+                                             float v3, unsigned tag) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 d0 = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
+  const u32x4 d1 = {__float_as_uint(v2), tag, __float_as_uint(v3), tag};
+  __builtin_amdgcn_raw_buffer_store_b128(d0, rs, (int)byte_off, 0, 16);
+  __builtin_amdgcn_raw_buffer_store_b128(d1, rs, (int)byte_off + 16, 0, 16);
+}
 // value of a granule already known to carry the right tag (validated by a sweep of this workgroup)
 __device__ __forceinline__ float peek_granule(const granule_t* g) {
   return __uint_as_float((unsigned)__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -88,6 +118,34 @@ __device__ __forceinline__ bool sweep_skinny(float4 (&a)[NC], __amdgpu_buffer_rs
       ok = ok && p0.y == tag && p0.w == tag && p1.y == tag && p1.w == tag;
       a[i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x), __uint_as_float(p1.z));
     }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
+// Several granule rows (R of them, each NC chunks in sweep_skinny's layout) polled in ONE loop:
+// every pass issues all R * NC * 2 loads before any tag check, so a phase that consumes R
+// hand-offs pays one round trip, not R.  a[r][i] = chunk i of row r.
+template <int NC, int R>
+__device__ __forceinline__ bool sweep_skinny_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],
+                                                  const long (&row_off)[R], const unsigned (&tag)[R], int wave,
+                                                  int lane, unsigned* abort_word) {
+  const long kq = 4 * (lane >> 4);
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const long off = row_off[r] + 8 * (wave * 16 + 64 * i + kq);
+        const uint4 p0 = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[r], (int)off, 0, 16));
+        const uint4 p1 =
+            __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[r], (int)off + 16, 0, 16));
+        ok = ok && p0.y == tag[r] && p0.w == tag[r] && p1.y == tag[r] && p1.w == tag[r];
+        a[r][i] = make_float4(__uint_as_float(p0.x), __uint_as_float(p0.z), __uint_as_float(p1.x),
+                              __uint_as_float(p1.z));
+      }
     if (__all(ok)) return true;
     if (spin_give_up(spins, abort_word)) return false;
   }

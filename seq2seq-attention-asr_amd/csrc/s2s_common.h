@@ -93,6 +93,8 @@ inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float al
 int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out);
 // Strided 2-D copy (rows x cols) dst[r*ldd + c] = src[r*lds + c]  (+ optional accumulate).
 int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd, int rows, int cols, bool accumulate);
+// dst[c*ldd + r] = src[r*lds + c] for the rows x cols block
+int transpose_f32(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd);
 // dst (rows x dcols, ld dcols) = src (rows x cols, ld lds) with columns [cols, dcols) zeroed
 int pad_cols_f32(hipStream_t st, const float* src, long lds, float* dst, int rows, int cols, int dcols);
 // dst[i] = alpha * src[i] + beta * dst[i]

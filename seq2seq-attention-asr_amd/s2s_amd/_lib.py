@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libs2s_hip.so")
+# S2S_HIP_LIB overrides the in-tree library (same-box A/B comparisons of two builds)
+LIB_PATH = os.environ.get("S2S_HIP_LIB") or os.path.join(_HERE, "libs2s_hip.so")
 
 c_int, c_long, c_float, c_size_t, c_void_p = ctypes.c_int, ctypes.c_long, ctypes.c_float, ctypes.c_size_t, ctypes.c_void_p
 P = ctypes.POINTER

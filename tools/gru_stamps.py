@@ -1,0 +1,72 @@
+"""Diagnostic: hand-off vs compute latency inside the persistent GRU layer kernels, from in-kernel
+s_memrealtime stamps (100 MHz).  Run on a GPU box:  python tools/gru_stamps.py [B L H]
+
+Per step of one chain (direction, 16-row tile):
+  forward   h_{t-1} -> [z|r] (p1, 2H/16 workgroups)  ->  q = r*h -> hh, h_t (p2, H/16 workgroups)
+  backward  da_h -> dq, da_r (p1, H/16)  ->  [da_z; da_r] -> dh_{t-1}, gates (p2, H/16)
+hand-off = consumer sweep done - last producer's phase end; compute = phase end - sweep done."""
+import ctypes
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "seq2seq-attention-asr_amd"))
+import s2s_amd  # noqa: E402
+from s2s_amd import _lib  # noqa: E402
+
+
+def analyse(name, st, nwg, ndir, ntile, prod1, cons1, prod2, cons2):
+    """st: (grid, L, 6) stamps in us; prodX / consX: workgroup offsets within a chain."""
+    L = st.shape[1]
+    rows = []
+    for d in range(ndir):
+        for m in range(ntile):
+            base = d * nwg + m * (nwg // ntile)
+            c = st[base:base + nwg // ntile]
+            for s in range(2, L):
+                h1 = c[cons1, s, 1].mean() - c[prod1, s - 1, 5].max()
+                k1 = c[prod2, s, 2].max() - c[cons1, s, 1].mean()
+                h2 = c[cons2, s, 4].mean() - c[prod2, s, 2].max()
+                k2 = c[prod1, s, 5].max() - c[cons2, s, 4].mean()
+                per = c[prod1, s, 5].max() - c[prod1, s - 1, 5].max()
+                rows.append((per, h1, k1, h2, k2))
+    r = np.array(rows).mean(0)
+    print(f"{name}: step {r[0]:.2f} us = hand-off1 {r[1]:.2f} + compute1 {r[2]:.2f} + hand-off2 {r[3]:.2f} "
+          f"+ compute2 {r[4]:.2f}")
+
+
+def main():
+    B, L, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (32, 128, 256)
+    D = 2 * H
+    ndir = 2
+    ntile = (B + 15) // 16
+    nf, nb = ndir * (2 * H // 16) * ntile, ndir * (H // 16) * ntile
+    sf = torch.zeros(nf * L * 6, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(nb * L * 6, dtype=torch.int64, device="cuda")
+    fn = _lib.lib.s2s_debug_gru_stamps
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    x = torch.randn(B, L, D, device="cuda")
+    cfg = s2s_amd.ModelConfig(inputFrameSize=D, hiddenFrameSize=H, outputFrameSize=H, numLayers=1)
+    model = s2s_amd.ChorowskiBaseline(cfg, graph=False)
+    lab = torch.randint(0, cfg.outputDepth, (B, 8), device="cuda", dtype=torch.int32)
+    fn(sf.data_ptr(), sb.data_ptr())
+    model.step(x, lab)
+    torch.cuda.synchronize()
+    fn(None, None)
+    tf = sf.cpu().numpy().reshape(nf, L, 6).astype(np.float64) * 0.01
+    tb = sb.cpu().numpy().reshape(nb, L, 6).astype(np.float64) * 0.01
+    z = list(range(H // 16))
+    zr = list(range(2 * H // 16))
+    r = list(range(H // 16, 2 * H // 16))
+    analyse("gru forward ", tf, nf // ndir, ndir, ntile, prod1=z, cons1=zr, prod2=r, cons2=z)
+    # backward stamps are indexed by time step s (processed L-1 .. 0): flip to processing order
+    tbp = tb[:, ::-1, :].copy()
+    allc = list(range(H // 16))
+    analyse("gru backward", tbp, nb // ndir, ndir, ntile, prod1=allc, cons1=allc, prod2=allc, cons2=allc)
+
+
+if __name__ == "__main__":
+    main()
