@@ -66,6 +66,25 @@ int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
                 long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch,
                 size_t scratch_bytes);
 
+/* ---------------------------------------------------------------- LSTM layer
+ * nn.RNN(nn.LSTM(D, H, peepholes), reverse) for ndir directions -- LSTM.lua:6-136 (gates i, f, g, o,
+ * each Linear(D,H)(x) + Linear(H,H)(h) with biases; peepholes add full Linear(H,H)(c) terms, the o
+ * gate peeking the new cell) under RNN.lua:120-201.  Replaces the per-step clone graph the
+ * reference runs for the conv+BiLSTM encoder (timit/timit.lua:108-125).
+ * W[d*NP + p], NP = 16 (22 with peepholes), W = (out, in):
+ *   for q in (i, f, g, o): Wqx (H, D), bqx (H), Wqh (H, H), bqh (H)
+ *   peepholes:             Wic (H, H), bic (H), Wfc (H, H), bfc (H), Woc (H, H), boc (H)
+ * y / saved / dy / dx / dW conventions as the GRU calls; dW and the bias grads accumulate. */
+size_t s2s_lstm_saved_bytes(int B, int L, int H);
+size_t s2s_lstm_scratch_bytes(int ndir, int B, int L, int D, int H, int peepholes);
+int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
+                 const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy,
+                 void* const* saved, void* scratch, size_t scratch_bytes);
+int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
+                 const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved,
+                 const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW,
+                 float scale, void* scratch, size_t scratch_bytes);
+
 /* ---------------------------------------------------------------- attention decoder
  * nn.Attention(decoder_recurrent = GRU(S,S), decoder_mlp = Maxout(S+A, M, K) -> Linear(M, O)
  * -> LogSoftMax, scoreDepth Sc, hybrid off, stateDepth S, annotationDepth A, outputDepth O,

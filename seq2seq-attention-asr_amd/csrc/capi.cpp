@@ -14,6 +14,7 @@
 
 #include "attn.h"
 #include "gru.h"
+#include "lstm.h"
 #include "s2s_common.h"
 
 namespace s2s {
@@ -456,6 +457,59 @@ int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
   gr.dx_accumulate = dx_accumulate;
   gr.scale = scale;
   return gru_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
+}
+
+size_t s2s_lstm_saved_bytes(int B, int L, int H) { return lstm_saved_bytes(B, L, H); }
+size_t s2s_lstm_scratch_bytes(int ndir, int B, int L, int D, int H, int peepholes) {
+  return lstm_scratch_bytes(ndir, B, L, D, H, peepholes);
+}
+
+static int fill_lstm_io(LstmLayerIO& io, int ndir, int B, int L, int D, int H, int peep, const int* reverse,
+                        const float* x, long ldx, const float* const* W, float* const* y, long ldy,
+                        void* const* saved) {
+  S2S_REQUIRE(ndir == 1 || ndir == 2, "lstm: ndir must be 1 or 2");
+  S2S_REQUIRE(reverse && x && W && saved, "lstm: null argument");
+  S2S_REQUIRE(ldx >= D, "lstm: ldx < D");
+  io.ndir = ndir; io.B = B; io.L = L; io.D = D; io.H = H; io.peep = peep ? 1 : 0;
+  io.x = x; io.ldx = ldx; io.W = W; io.ldy = ldy;
+  for (int d = 0; d < ndir; ++d) {
+    for (int p = 0; p < lstm_nparams(io.peep); ++p) S2S_REQUIRE(W[d * lstm_nparams(io.peep) + p], "lstm: null weight");
+    io.reverse[d] = reverse[d] ? 1 : 0;
+    io.y[d] = y ? y[d] : nullptr;
+    io.saved[d] = static_cast<float*>(saved[d]);
+    S2S_REQUIRE(io.saved[d] != nullptr, "lstm: null saved buffer");
+  }
+  return 0;
+}
+
+int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
+                 const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy,
+                 void* const* saved, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  LstmLayerIO io{};
+  S2S_TRY(fill_lstm_io(io, ndir, B, L, D, H, peepholes, reverse, x, ldx, W, y, ldy, saved));
+  S2S_REQUIRE(y != nullptr, "lstm: null y");
+  for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "lstm: null y");
+  return lstm_layer_fwd(static_cast<hipStream_t>(stream), io, scratch, scratch_bytes);
+}
+
+int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
+                 const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved,
+                 const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW,
+                 float scale, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  LstmLayerIO io{};
+  S2S_TRY(fill_lstm_io(io, ndir, B, L, D, H, peepholes, reverse, x, ldx, W, nullptr, H, saved));
+  S2S_REQUIRE(dy && dW, "lstm: null dy/dW");
+  LstmLayerGrad gr{};
+  for (int d = 0; d < ndir; ++d) {
+    gr.dy[d] = dy[d];
+    S2S_REQUIRE(gr.dy[d] != nullptr, "lstm: null dy");
+    for (int p = 0; p < lstm_nparams(io.peep); ++p)
+      S2S_REQUIRE(dW[d * lstm_nparams(io.peep) + p], "lstm: null dW");
+  }
+  gr.lddy = lddy; gr.dx = dx; gr.lddx = lddx; gr.dx_accumulate = dx_accumulate; gr.dW = dW; gr.scale = scale;
+  return lstm_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
 }
 
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d) { return d ? attn_saved_bytes(to_attn(d)) : 0; }

@@ -41,6 +41,13 @@ SIGNATURES = [
     ("s2s_gru_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
                             P(c_void_p), P(c_void_p), P(c_void_p), c_long, c_void_p, c_long, c_int, P(c_void_p),
                             c_float, c_void_p, c_size_t]),
+    ("s2s_lstm_saved_bytes", c_size_t, [c_int, c_int, c_int]),
+    ("s2s_lstm_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
+    ("s2s_lstm_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p,
+                             c_long, P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_size_t]),
+    ("s2s_lstm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p,
+                             c_long, P(c_void_p), P(c_void_p), P(c_void_p), c_long, c_void_p, c_long, c_int,
+                             P(c_void_p), c_float, c_void_p, c_size_t]),
     ("s2s_attn_saved_bytes", c_size_t, [P(s2s_attn_dims)]),
     ("s2s_attn_scratch_bytes", c_size_t, [P(s2s_attn_dims)]),
     ("s2s_attn_fwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,

@@ -125,17 +125,55 @@ class GRU(Module):
         return list(self.weight), list(self.gradWeight)
 
 
+class LSTM(Module):
+    """nn.LSTM(inputSize, outputSize, peepholes) cell parameters (LSTM.lua:6-60): for each gate
+    q in (i, f, g, o) a Linear(D, H) on x and a Linear(H, H) on h (both with bias); peepholes add
+    Linear(H, H) on the cell for i, f (previous cell) and o (new cell).  nn.Linear reset:
+    U(+-1/sqrt(in)) for weight and bias.  Flat order = the C ABI's (include/s2s_hip.h)."""
+
+    GATES = ("i", "f", "g", "o")
+
+    def __init__(self, inputSize, outputSize, peepholes=False, generator=None):
+        super().__init__()
+        self.diminput, self.dimoutput, self.peepholes = inputSize, outputSize, bool(peepholes)
+        D, H = inputSize, outputSize
+        sx, sh = 1.0 / math.sqrt(D), 1.0 / math.sqrt(H)
+        self.names, self.weight = [], []
+        for q in self.GATES:
+            for name, shape, sd in ((f"W{q}x", (H, D), sx), (f"b{q}x", (H,), sx), (f"W{q}h", (H, H), sh),
+                                    (f"b{q}h", (H,), sh)):
+                self.names.append(name)
+                self.weight.append(_uniform(shape, sd, generator))
+        if self.peepholes:
+            for q in ("i", "f", "o"):
+                for name, shape in ((f"W{q}c", (H, H)), (f"b{q}c", (H,))):
+                    self.names.append(name)
+                    self.weight.append(_uniform(shape, sh, generator))
+        self.gradWeight = [torch.zeros_like(w) for w in self.weight]
+
+    def parameters(self):
+        return list(self.weight), list(self.gradWeight)
+
+    def named(self, grads=False):
+        return dict(zip(self.names, self.gradWeight if grads else self.weight))
+
+
 class _GruSeq(Module):
-    """Shared driver of s2s_gru_fwd / s2s_gru_bwd for 1 or 2 directions over the same input."""
+    """Shared driver of s2s_{gru,lstm}_{fwd,bwd} for 1 or 2 directions over the same input (all
+    cells GRU, or all LSTM with the same peephole setting)."""
 
     def __init__(self, cells, reverses):
         super().__init__()
         self.cells = cells
         self.reverses = reverses
         self.dimoutput = cells[0].dimoutput
+        self.lstm = isinstance(cells[0], LSTM)
+        self.peep = int(self.lstm and cells[0].peepholes)
         for c in cells:
             if c.dimoutput % 16 != 0:
-                raise S2SArgumentError("GRU dimoutput must be a multiple of 16 on this path")
+                raise S2SArgumentError("recurrent dimoutput must be a multiple of 16 on this path")
+            if isinstance(c, LSTM) != self.lstm or (self.lstm and int(c.peepholes) != self.peep):
+                raise S2SArgumentError("all directions must use the same cell type")
 
     def parameters(self):
         ws, gs = [], []
@@ -160,14 +198,22 @@ class _GruSeq(Module):
             raise S2SArgumentError(f"input frame size {D} != diminput {self.cells[0].diminput}")
         dev = input.device
         out = torch.empty((B, L, nd * H), device=dev, dtype=torch.float32)
-        self._saved = [_bytes(lib.s2s_gru_saved_bytes(B, L, H), dev) for _ in range(nd)]
-        scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
         W = ptr_array([w.data_ptr() for c in self.cells for w in c.weight])
         y = ptr_array([out.data_ptr() + 4 * H * d for d in range(nd)])
-        sv = ptr_array([s.data_ptr() for s in self._saved])
         rev = ptr_array([int(r) for r in self.reverses], ctypes.c_int)
-        check(lib.s2s_gru_fwd(get_context(dev.index).handle, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, y,
-                              nd * H, sv, dptr(scr), scr.numel()))
+        ctx = get_context(dev.index).handle
+        if self.lstm:
+            self._saved = [_bytes(lib.s2s_lstm_saved_bytes(B, L, H), dev) for _ in range(nd)]
+            scr = _bytes(lib.s2s_lstm_scratch_bytes(nd, B, L, D, H, self.peep), dev)
+            sv = ptr_array([s.data_ptr() for s in self._saved])
+            check(lib.s2s_lstm_fwd(ctx, stream_ptr(), nd, B, L, D, H, self.peep, rev, dptr(input), D, W, y, nd * H, sv,
+                                   dptr(scr), scr.numel()))
+        else:
+            self._saved = [_bytes(lib.s2s_gru_saved_bytes(B, L, H), dev) for _ in range(nd)]
+            scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
+            sv = ptr_array([s.data_ptr() for s in self._saved])
+            check(lib.s2s_gru_fwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, y, nd * H, sv, dptr(scr),
+                                  scr.numel()))
         self._dims = (B, L, D)
         self.output = out if input.dim() == 3 else out[0]
         return self.output
@@ -178,14 +224,20 @@ class _GruSeq(Module):
         dev = input.device
         go = gradOutput.contiguous()
         dx = torch.empty((B, L, D), device=dev, dtype=torch.float32)
-        scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
         W = ptr_array([w.data_ptr() for c in self.cells for w in c.weight])
         dW = ptr_array([g.data_ptr() for c in self.cells for g in c.gradWeight])
         dy = ptr_array([go.data_ptr() + 4 * H * d for d in range(nd)])
         sv = ptr_array([s.data_ptr() for s in self._saved])
         rev = ptr_array([int(r) for r in self.reverses], ctypes.c_int)
-        check(lib.s2s_gru_bwd(get_context(dev.index).handle, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv,
-                              dy, nd * H, dptr(dx), D, 0, dW, float(scale), dptr(scr), scr.numel()))
+        ctx = get_context(dev.index).handle
+        if self.lstm:
+            scr = _bytes(lib.s2s_lstm_scratch_bytes(nd, B, L, D, H, self.peep), dev)
+            check(lib.s2s_lstm_bwd(ctx, stream_ptr(), nd, B, L, D, H, self.peep, rev, dptr(input), D, W, sv, dy, nd * H,
+                                   dptr(dx), D, 0, dW, float(scale), dptr(scr), scr.numel()))
+        else:
+            scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
+            check(lib.s2s_gru_bwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv, dy, nd * H, dptr(dx),
+                                  D, 0, dW, float(scale), dptr(scr), scr.numel()))
         self.gradInput = dx if input.dim() == 3 else dx[0]
         return self.gradInput
 
@@ -194,21 +246,22 @@ class _GruSeq(Module):
 
 
 class RNN(_GruSeq):
-    """nn.RNN(nn.GRU(D, H), reverse) (RNN.lua:3-201)."""
+    """nn.RNN(recurrent, reverse) (RNN.lua:3-201) over an nn.GRU or nn.LSTM cell."""
 
     def __init__(self, recurrent, reverse=False):
         assert recurrent is not None, "recurrent cannot be nil"
         assert getattr(recurrent, "dimoutput", None) is not None, "recurrent must specify dimoutput"
-        if not isinstance(recurrent, GRU):
-            raise S2SArgumentError("this path runs nn.GRU cells (LSTM cells: next row)")
+        if not isinstance(recurrent, (GRU, LSTM)):
+            raise S2SArgumentError("this path runs nn.GRU and nn.LSTM cells")
         super().__init__([recurrent], [bool(reverse)])
         self.recurrent = recurrent
         self.reverse = bool(reverse)
 
 
 class BiRNN(_GruSeq):
-    """JoinTable(2,2)({RNN(GRU, false)(x), RNN(GRU, true)(x)}) -- one bidirectional encoder layer
-    (timit/model_chorowski_baseline.lua:22-24) with both directions in the same launches."""
+    """JoinTable(2,2)({RNN(cell, false)(x), RNN(cell, true)(x)}) -- one bidirectional encoder layer
+    (timit/model_chorowski_baseline.lua:22-24; BiLSTM: timit/timit.lua:108-125) with both
+    directions in the same launches."""
 
     def __init__(self, fwd_cell, bwd_cell):
         super().__init__([fwd_cell, bwd_cell], [False, True])

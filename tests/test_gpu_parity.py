@@ -86,6 +86,41 @@ def test_gru_single_utterance_2d(s2s):
     assert_rel(y, yr[0], "y")
 
 
+# --------------------------------------------------------------------------- LSTM layer (§8 A7)
+
+@pytest.mark.parametrize("B,L,D,H", [(3, 7, 20, 32), (17, 9, 64, 16), (5, 12, 40, 48)])
+@pytest.mark.parametrize("bidir", [False, True])
+@pytest.mark.parametrize("peep", [False, True])
+def test_lstm_layer_matches_oracle(s2s, B, L, D, H, bidir, peep):
+    """nn.RNN(nn.LSTM(D, H, peepholes)) fwd + BPTT through s2s_lstm_{fwd,bwd} vs the oracle
+    (LSTM.lua:16-58, 118-136): y, dx and every weight / bias gradient (accumulated, scale 0.5)."""
+    rng = np.random.default_rng(B * 1000 + L * 10 + H)
+    x = rng.standard_normal((B, L, D))
+    cells = [s2s.LSTM(D, H, peepholes=peep) for _ in range(2 if bidir else 1)]
+    Ps = [{k: v.double().numpy() for k, v in c.named().items()} for c in cells]
+    mod = s2s.BiRNN(cells[0], cells[1]) if bidir else s2s.RNN(cells[0], reverse=(L % 2 == 1))
+    mod.cuda()
+    xs = cu(x)
+    y = mod.forward(xs).cpu().numpy()
+    dy = rng.standard_normal(y.shape)
+    mod.zeroGradParameters()
+    for c in cells:  # gradients accumulate onto what is already there
+        for g in c.gradWeight:
+            g.fill_(0.25)
+    dx = mod.backward(xs, cu(dy), 0.5).cpu().numpy()
+    torch.cuda.synchronize()
+    revs = [False, True] if bidir else [mod.reverse]
+    dx_ref = np.zeros_like(x)
+    for i, (P, rev) in enumerate(zip(Ps, revs)):
+        yr, sv = orc.lstm_seq_fwd(x, P, rev, peep)
+        assert_rel(y[:, :, i * H:(i + 1) * H], yr, f"y[{i}]")
+        G = {k: np.full_like(v, 0.25) for k, v in P.items()}
+        dx_ref += orc.lstm_seq_bwd(x, P, sv, dy[:, :, i * H:(i + 1) * H], G, rev, peep, 0.5)
+        for k, g in cells[i].named(grads=True).items():
+            assert_rel(g.cpu().numpy(), G[k], f"d{k}[{i}]")
+    assert_rel(dx, dx_ref, "dx")
+
+
 # --------------------------------------------------------------------------- attention decoder
 
 ATT_CASES = [
