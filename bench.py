@@ -84,6 +84,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="timit_chorowski_b32", choices=sorted(CONFIGS))
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of hipGraph replay")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="weight-gradient GEMMs on the main stream (default: S2S_CTX_OVERLAP, a side stream "
+                         "beside the next layer's BPTT)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
@@ -104,7 +107,8 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     kw, B, L, T = CONFIGS[args.config]
     cfg = s2s_amd.ModelConfig(**kw)
-    model = s2s_amd.ChorowskiBaseline(cfg, graph=not args.no_graph, seed=1234)
+    model = s2s_amd.ChorowskiBaseline(cfg, graph=not args.no_graph, seed=1234,
+                                     overlap=not args.no_overlap)
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
     x = torch.randn((B, L, cfg.inputFrameSize), generator=g)
     x[:, :10] = 0

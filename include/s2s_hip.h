@@ -41,9 +41,9 @@ void s2s_ctx_destroy(s2s_ctx* ctx);
 /* flags: S2S_CTX_GRAPH = capture the model step into a hipGraph and replay it when the
  * dims / pointers repeat (the step is ~2000 dependent launches). */
 #define S2S_CTX_GRAPH 1
-/* S2S_CTX_OVERLAP = run the weight-gradient GEMMs on a side stream beside the next layer's BPTT
- * (off by default: on MI355X the GEMM workgroups share CUs with the persistent recurrence and
- * both slow down; measured 9.66 vs 9.23 ms per config-2 step). */
+/* S2S_CTX_OVERLAP = run the weight-gradient GEMMs on a side stream beside the next layer's BPTT;
+ * the persistent GRU workgroups then reserve their CU (unused dynamic LDS) so GEMM workgroups
+ * only fill the idle CUs (config-2 step 7.39 vs 7.61 ms on MI355X; bitwise-equal results). */
 #define S2S_CTX_OVERLAP 2
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
 

@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "attn.h"
+#include "gru_persist.h"
 #include "gru.h"
 #include "lstm.h"
 #include "s2s_common.h"
@@ -205,6 +206,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
                     float* grads, const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
                     void* workspace) {
   const bool split = side != nullptr;
+  gru_persist_set_exclusive(split ? 1 : 0);
   ModelWs w = model_ws(d, workspace);
   const std::vector<LayerDims> layers = enc_layers(d);
   const std::vector<long> sizes = param_sizes(d);

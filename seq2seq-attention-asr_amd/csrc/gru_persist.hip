@@ -265,11 +265,26 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   }
 }
 
+// Exclusive-CU mode (set while weight-gradient GEMMs run on a side stream beside the recurrence):
+// each persistent workgroup reserves kExclLds bytes of dynamic LDS it never touches, so no GEMM
+// workgroup (37 KB of LDS) can share its CU; the GEMMs fill the CUs the recurrence leaves idle.
+constexpr int kExclLds = 124 * 1024;
+int g_excl = 0;
+
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
   const dim3 grid(ndir * a.nwg);
-  if (fwd) hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(256), 0, st, a);
+  const bool excl = g_excl && grid.x <= 256;
+  const unsigned shm = excl ? kExclLds : 0;
+  if (fwd) {
+    if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
+    hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(256), shm, st, a);
+  } else {
+    if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persist<NC>),
+                                                hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
+    hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(256), shm, st, a);
+  }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -286,6 +301,8 @@ int launch(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
 }
 
 }  // namespace
+
+void gru_persist_set_exclusive(int on) { g_excl = on; }
 
 bool gru_persist_supported(int ndir, int B, int H) {
   if (!(H == 64 || H == 128 || H == 256 || H == 512)) return false;

@@ -71,6 +71,7 @@ SIGNATURES = [
 ]
 
 S2S_CTX_GRAPH = 1
+S2S_CTX_OVERLAP = 2
 S2S_ZERO_GRADS = 1
 S2S_NORMALIZE_NLL = 2
 S2S_ATTN_NPARAMS = 17

@@ -72,7 +72,8 @@ def _fan_in(name, shape, cfg):
 class ChorowskiBaseline:
     """autoencoder = decoder({encoder(x), labelmask}) with flat params/grads on one device."""
 
-    def __init__(self, cfg: ModelConfig = None, device=None, seed: int = 1234, graph: bool = False):
+    def __init__(self, cfg: ModelConfig = None, device=None, seed: int = 1234, graph: bool = False,
+                 overlap: bool = False):
         self.cfg = cfg or ModelConfig()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         shapes = param_shapes(self.cfg)
@@ -88,10 +89,11 @@ class ChorowskiBaseline:
             off += sz
         self.params = flat.to(self.device)
         self.grads = torch.zeros_like(self.params)
-        self.ctx = get_context(self.device.index) if not graph else None
-        if graph:
+        if graph or overlap:
             from .nn import Context
-            self.ctx = Context(self.device.index, graph=True)
+            self.ctx = Context(self.device.index, graph=graph, overlap=overlap)
+        else:
+            self.ctx = get_context(self.device.index)
         self._ws = {}
         self._check_layout()
 

@@ -20,13 +20,14 @@ from ._lib import check, lib, ptr_array
 class Context:
     """One s2s_ctx per device (s2s_ctx_create)."""
 
-    def __init__(self, device: int = 0, graph: bool = False):
+    def __init__(self, device: int = 0, graph: bool = False, overlap: bool = False):
         self.device = device
         h = ctypes.c_void_p()
         check(lib.s2s_ctx_create(device, ctypes.byref(h)))
         self.handle = h
-        if graph:
-            check(lib.s2s_ctx_set_flags(h, _lib.S2S_CTX_GRAPH))
+        flags = (_lib.S2S_CTX_GRAPH if graph else 0) | (_lib.S2S_CTX_OVERLAP if overlap else 0)
+        if flags:
+            check(lib.s2s_ctx_set_flags(h, flags))
 
     def __del__(self):
         try:

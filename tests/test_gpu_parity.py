@@ -240,6 +240,29 @@ def test_model_step_graph_replay_bitwise(s2s):
     assert torch.equal(logp2, outs[0][1]) and torch.equal(eager.grads, outs[0][2])
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_model_step_overlap_bitwise(s2s, graph):
+    """S2S_CTX_OVERLAP (weight-gradient GEMMs on a side stream, persistent GRU workgroups on
+    exclusive CUs) must give the same bits as the single-stream step, at config-2 size."""
+    cfg = s2s.ModelConfig()
+    ref = s2s.ChorowskiBaseline(cfg)
+    ovl = s2s.ChorowskiBaseline(cfg, graph=graph, overlap=True)
+    ovl.params.copy_(ref.params)
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(32, 128, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (32, 40), generator=g).to(torch.int32).cuda()
+    nll_r, logp_r = ref.step(x, lab)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        for _ in range(3):
+            nll_o, logp_o = ovl.step(x, lab, stream=st)
+    st.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(logp_o, logp_r) and torch.equal(nll_o, nll_r)
+    assert torch.equal(ovl.grads, ref.grads)
+
+
 def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch):
     """The persistent layer kernel (in-launch sc1 hand-offs) must reproduce the per-step launch
     path bit for bit -- same arithmetic, same summation order -- over repeated launches."""
