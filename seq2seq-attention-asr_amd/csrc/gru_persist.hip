@@ -49,7 +49,10 @@ struct PDir {
 struct PArgs {
   PDir d[2];
   int B, L, H, MT, nwg;  // nwg = workgroups per direction
+  int nmem, nchains;     // chains = (direction, 16-row tile); members = column tiles
+  int allow_local;       // 0 forces write-through (sc1) hand-offs even on an XCD-local chain
   unsigned* abort_word;
+  unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   unsigned long long* stamps;  // diagnostic: [grid][L][6] s_memrealtime, or nullptr
 };
 
@@ -58,7 +61,7 @@ struct PArgs {
 #define GRU_STAMP(ph)                                                                      \
   do {                                                                                     \
     if (a.stamps && threadIdx.x == 0)                                                      \
-      a.stamps[((long)blockIdx.x * a.L + s) * 6 + (ph)] = __builtin_amdgcn_s_memrealtime(); \
+      a.stamps[((long)lw * a.L + s) * 6 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 unsigned long long* g_gru_stamps[2] = {nullptr, nullptr};
 
@@ -72,21 +75,26 @@ __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds,
 }
 
 // ------------------------------------------------------------------------------ forward
-// grid = ndir * nwg, nwg = (2H/16) * MT; task (c1, mt) = (w % (2H/16), w / (2H/16)).
-// z-column workgroups (c1 < H/16) also own the candidate tile of the same units.
+// chain (dir, mt) has nmem = 2H/16 members c1 (chain_slot placement, handoff.h); z-column
+// workgroups (c1 < H/16) also own the candidate tile of the same units.
 template <int NC>  // NC = H / 64
 __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
-  __shared__ int abort_lds;
+  __shared__ int abort_lds, local_lds;
+  __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
   const int H = a.H, B = a.B, L = a.L;
-  const int dir = blockIdx.x / a.nwg, w = blockIdx.x % a.nwg;
+  const ChainSlot cs = chain_slot(a.nmem);
+  if (cs.chain >= a.nchains) return;  // idle slot of the placement grid
+  const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
   const PDir& g = a.d[dir];
   const int ncol = 2 * H / 16;
-  const int c1 = w % ncol, mt = w / ncol;
+  const int c1 = cs.member;
+  const int lw = dir * a.nwg + mt * ncol + c1;  // logical workgroup id (stamps)
   const bool isz = c1 < H / 16;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
+  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds);
 
   float4 w1[NC], w2[NC];
   load_wfrag(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
@@ -97,6 +105,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), on = c1 * 16 + (tid & 15);  // this thread's output
   const bool live = ob < B;
+  // r tiles: units [jt, jt + 16) of h_{t-1} are chunk it of wave wt in the sweep layout
+  const int jt = c1 * 16 - H, wt = (jt % 64) / 16, it = jt / 64;
   float zreg = 0.f, hreg = 0.f;
   bool aborted = false;
 
@@ -113,6 +123,13 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
       ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
       GRU_STAMP(1);
       acc = mfma_chunks<NC>(av, w1);
+      // r tiles: the swept operand already holds h_{t-1} of this tile's 16 units (chunk it of
+      // wave wt); park it in LDS for the q = r * h epilogue (read after the reduce barrier)
+      if (!isz && wave == wt) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i)
+          if (i == it) *reinterpret_cast<float4*>(&hprev[lane & 15][4 * (lane >> 4)]) = av[i];
+      }
     }
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
@@ -124,9 +141,9 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
         zreg = gate;
       } else {
         const int j = on - H;
-        const float hp = (s > 0 && live) ? peek_granule(g.g0 + ((s - 1) & 1) * slot + (long)ob * H + j) : 0.f;
+        const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
         const float q = gate * hp;
-        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1), live);  // critical first
+        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1), live, loc);  // critical first
         if (live) {
           sv[H + j] = gate;
           sv[3 * H + j] = hp;
@@ -153,7 +170,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
       const float hh = tanhf(sum + xph);
       const float hp = hreg;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
-      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1), live);  // first
+      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1), live, loc);  // first
       if (live) {
         g.sv[row * 5 * H + 2 * H + on] = hh;
         g.y[row * g.ldy + on] = hreg;
@@ -164,19 +181,23 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
 }
 
 // ------------------------------------------------------------------------------ backward
-// grid = ndir * nwg, nwg = (H/16) * MT; task (c, mt) for both seams.
+// chain (dir, mt) has nmem = H/16 members c, each the same column tile in both seams.
 template <int NC>
 __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
-  __shared__ int abort_lds;
+  __shared__ int abort_lds, local_lds;
   const int H = a.H, B = a.B, L = a.L;
-  const int dir = blockIdx.x / a.nwg, w = blockIdx.x % a.nwg;
+  const ChainSlot cs = chain_slot(a.nmem);
+  if (cs.chain >= a.nchains) return;  // idle slot of the placement grid
+  const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
   const PDir& g = a.d[dir];
   const int ncol = H / 16;
-  const int c = w % ncol, mt = w / ncol;
+  const int c = cs.member;
+  const int lw = dir * a.nwg + mt * ncol + c;  // logical workgroup id (stamps)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
+  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds);
 
   float4 wh[NC], wzr[2 * NC];
   load_wfrag(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
@@ -201,8 +222,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     const float daz = dh * (hh - hp) * (z * (1.0f - z));
     const float dah = (dh * z) * (1.0f - hh * hh);
     const long off = sl * slot + (long)ob * H + ok_;
-    put_granule_pair(g.g2, off, dah, tag, pub);  // da_h gates the next p1: first
-    put_granule_pair(g.g0, off, daz, tag, pub);
+    put_granule_pair(g.g2, off, dah, tag, pub, loc);  // da_h gates the next p1: first
+    put_granule_pair(g.g0, off, daz, tag, pub, loc);
     if (pub) {
       g.dA[row * g.ldA + ok_] = daz;
       g.dA[row * g.ldA + 2 * H + ok_] = dah;
@@ -232,7 +253,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * hp) * (r * (1.0f - r)), tag, live);
+    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * hp) * (r * (1.0f - r)), tag, live, loc);
     if (live) {
       const float dar = (dq * hp) * (r * (1.0f - r));
       g.dA[row * g.ldA + H + ok_] = dar;
@@ -271,10 +292,14 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
 constexpr int kExclLds = 124 * 1024;
 int g_excl = 0;
 
+int g_allow_local = 1;
+
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
-  const dim3 grid(ndir * a.nwg);
-  const bool excl = g_excl && grid.x <= 256;
+  (void)ndir;
+  const dim3 grid(chain_grid(a.nchains, a.nmem));
+  // exclusive only while one chain per XCD fits one workgroup per CU (32 CUs per XCD)
+  const bool excl = g_excl && a.nchains <= 8 && a.nmem <= 32;
   const unsigned shm = excl ? kExclLds : 0;
   if (fwd) {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
@@ -307,13 +332,19 @@ void gru_persist_set_exclusive(int on) { g_excl = on; }
 bool gru_persist_supported(int ndir, int B, int H) {
   if (!(H == 64 || H == 128 || H == 256 || H == 512)) return false;
   const int MT = (B + 15) / 16;
-  const long wgs = (long)ndir * (2 * H / 16) * MT;
-  return wgs <= 512;  // all workgroups must be co-resident (256 CUs, >= 2 per CU at this footprint)
+  // the chains placed on one XCD must be co-resident there (32 CUs, >= 2 workgroups per CU at
+  // this footprint): forward members 2H/16 per chain, chains (dir, tile) dealt 8 per round
+  return (2 * H / 16) * ((ndir * MT + 7) / 8) <= 64;
 }
 
-size_t gru_persist_sync_bytes(int B, int H) { return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H; }
+static size_t census_bytes(int B, int H) { return 4 * (size_t)(2 * ((B + 15) / 16)) * (2 * H / 16); }
 
-static void carve_granules(char* sync, int B, int H, unsigned** abort_word, granule_t* (&g)[2][3]) {
+size_t gru_persist_sync_bytes(int B, int H) {
+  return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H);
+}
+
+static void carve_granules(char* sync, int B, int H, unsigned** abort_word, granule_t* (&g)[2][3],
+                           unsigned** census) {
   *abort_word = reinterpret_cast<unsigned*>(sync);
   granule_t* p = reinterpret_cast<granule_t*>(sync + 256);
   for (int d = 0; d < 2; ++d)
@@ -321,17 +352,19 @@ static void carve_granules(char* sync, int B, int H, unsigned** abort_word, gran
       g[d][k] = p;
       p += 2L * B * H;
     }
+  *census = reinterpret_cast<unsigned*>(p);
 }
 
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   PArgs a{};
   const int MT = (f.B + 15) / 16;
   granule_t* gr[2][3];
-  carve_granules(static_cast<char*>(sync), f.B, f.H, &a.abort_word, gr);
+  carve_granules(static_cast<char*>(sync), f.B, f.H, &a.abort_word, gr, &a.census);
   for (int d = 0; d < f.ndir; ++d)
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
                   gr[d][0], gr[d][1], gr[d][2]};
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
+  a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
   S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(f.B, f.H), st));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
@@ -343,11 +376,12 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   PArgs a{};
   const int MT = (b.B + 15) / 16;
   granule_t* gr[2][3];
-  carve_granules(static_cast<char*>(sync), b.B, b.H, &a.abort_word, gr);
+  carve_granules(static_cast<char*>(sync), b.B, b.H, &a.abort_word, gr, &a.census);
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
                   b.reverse[d], gr[d][0], gr[d][1], gr[d][2]};
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
+  a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
   S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(b.B, b.H), st));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
@@ -359,6 +393,8 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
 
 // diagnostic: the next persistent GRU launches fill these with stamps (tools/gru_stamps.py);
 // nullptr turns it off.  Not part of the C ABI header.
+// diagnostic: 0 forces write-through (sc1) hand-offs in every chain (tests cover both forms)
+extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);

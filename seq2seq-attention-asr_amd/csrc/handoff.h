@@ -16,9 +16,14 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_of(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, 0x7fffffff, 0x00020000);
 }
 
-__device__ __forceinline__ void put_granule(granule_t* g, float v, unsigned tag) {
+// local = every consumer runs on this workgroup's XCD (chain_is_local): the granule may then stay
+// in that XCD's L2 (plain store, sc0) -- the consumers' sc1 loads are served from the same L2, one
+// hop ~0.22 us instead of ~0.55 us through the fabric with write-through (sc1) stores (measured on
+// MI355X, tools/pingpong.hip).  Cross-XCD consumers need local = false.
+__device__ __forceinline__ void put_granule(granule_t* g, float v, unsigned tag, bool local = false) {
   const granule_t x = ((granule_t)tag << 32) | (granule_t)__float_as_uint(v);
-  __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (local) __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else __hip_atomic_store(g, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Publish granule base[idx] of this lane when `active` (base is wave-uniform).  Lanes l and l^1
 // own adjacent granules j, j+1 (j even at the even lane) at every call site, so
@@ -29,7 +34,8 @@ __device__ __forceinline__ void put_granule(granule_t* g, float v, unsigned tag)
 #ifndef S2S_PAIRED_GRANULES
 #define S2S_PAIRED_GRANULES 0
 #endif
-__device__ __forceinline__ void put_granule_pair(granule_t* base, long idx, float v, unsigned tag, bool active) {
+__device__ __forceinline__ void put_granule_pair(granule_t* base, long idx, float v, unsigned tag, bool active,
+                                                 bool local = false) {
 #if S2S_PAIRED_GRANULES
   const float vn = __shfl_xor(v, 1, 64);
   if (active && (threadIdx.x & 1) == 0) {
@@ -38,17 +44,22 @@ __device__ __forceinline__ void put_granule_pair(granule_t* base, long idx, floa
     __builtin_amdgcn_raw_buffer_store_b128(d, rsrc_of(base), (int)(8 * idx), 0, 16);
   }
 #else
-  if (active) put_granule(base + idx, v, tag);
+  if (active) put_granule(base + idx, v, tag, local);
 #endif
 }
 // four adjacent granules j..j+3 of one lane (j % 2 == 0) as two 16-byte write-through stores
 __device__ __forceinline__ void put_granule4(__amdgpu_buffer_rsrc_t rs, long byte_off, float v0, float v1, float v2,
-                                             float v3, unsigned tag) {
+                                             float v3, unsigned tag, bool local = false) {
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   const u32x4 d0 = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
   const u32x4 d1 = {__float_as_uint(v2), tag, __float_as_uint(v3), tag};
-  __builtin_amdgcn_raw_buffer_store_b128(d0, rs, (int)byte_off, 0, 16);
-  __builtin_amdgcn_raw_buffer_store_b128(d1, rs, (int)byte_off + 16, 0, 16);
+  if (local) {
+    __builtin_amdgcn_raw_buffer_store_b128(d0, rs, (int)byte_off, 0, 1);
+    __builtin_amdgcn_raw_buffer_store_b128(d1, rs, (int)byte_off + 16, 0, 1);
+  } else {
+    __builtin_amdgcn_raw_buffer_store_b128(d0, rs, (int)byte_off, 0, 16);
+    __builtin_amdgcn_raw_buffer_store_b128(d1, rs, (int)byte_off + 16, 0, 16);
+  }
 }
 // value of a granule already known to carry the right tag (validated by a sweep of this workgroup)
 __device__ __forceinline__ float peek_granule(const granule_t* g) {
@@ -65,6 +76,41 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
   }
   __builtin_amdgcn_s_sleep(1);
   return false;
+}
+
+// ---- XCD-local chains
+// A chain = the workgroups that hand data to each other (independent of other chains).  Launches
+// place chain c's members at blockIdx = 8 * (member + nmem * (c / 8)) + c % 8, which the MI355X
+// dispatcher deals to ONE XCD (blocks b and b + 8 share an XCD; speed only, never assumed):
+// chain_is_local() checks it at run time -- every member publishes HW_REG_XCC_ID and reads all of
+// its chain's -- so a chain uses L2-resident hand-offs only when it really shares one L2.
+constexpr int kXccIdHwreg = 20 | (0 << 6) | (3 << 11);  // hwreg(HW_REG_XCC_ID, 0, 4)
+struct ChainSlot {
+  int chain, member;
+};
+__device__ __forceinline__ ChainSlot chain_slot(int nmem) {
+  const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+  return ChainSlot{x + 8 * (j / nmem), j % nmem};
+}
+__host__ __device__ constexpr int chain_grid(int nchains, int nmem) { return 8 * nmem * ((nchains + 7) / 8); }
+// census: zeroed u32 per (chain, member); flag: a __shared__ int; all 256 threads call it
+__device__ __forceinline__ bool chain_is_local(unsigned* census, int chain, int nmem, int member, bool allow,
+                                               unsigned* abort_word, int* flag) {
+  const unsigned me = 0x100u | (__builtin_amdgcn_s_getreg(kXccIdHwreg) & 15u);
+  unsigned* row = census + (long)chain * nmem;
+  if (threadIdx.x == 0) {
+    *flag = allow ? 1 : 0;
+    __hip_atomic_store(row + member, me, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < nmem) {
+    unsigned spins = 0, v;
+    while (((v = __hip_atomic_load(row + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0x100u) == 0u)
+      if (spin_give_up(spins, abort_word)) break;
+    if (v != me) *flag = 0;
+  }
+  __syncthreads();
+  return *flag != 0;
 }
 
 // one thread waits for one granule

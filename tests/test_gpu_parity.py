@@ -263,14 +263,23 @@ def test_model_step_overlap_bitwise(s2s, graph):
     assert torch.equal(ovl.grads, ref.grads)
 
 
-def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch):
-    """The persistent layer kernel (in-launch sc1 hand-offs) must reproduce the per-step launch
-    path bit for bit -- same arithmetic, same summation order -- over repeated launches."""
+@pytest.mark.parametrize("local", [1, 0])
+@pytest.mark.parametrize("B,H", [(32, 256), (45, 128)])
+def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, B, H):
+    """The persistent layer kernel (in-launch granule hand-offs; XCD-local L2-resident chains when
+    local=1 and the census finds them on one XCD, write-through sc1 when local=0) must reproduce
+    the per-step launch path bit for bit -- same arithmetic, same summation order -- over
+    repeated launches."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_gru_local
+    fn.argtypes = [ctypes.c_int]
     rng = np.random.default_rng(11)
-    B, L, D, H = 32, 40, 48, 256
+    L, D = 40, 48
     x = cu(rng.standard_normal((B, L, D)))
     f, b = s2s.GRU(D, H), s2s.GRU(D, H)
     outs = {}
+    fn(local)
     for mode in ("step", "persistent"):
         monkeypatch.setenv("S2S_GRU_MODE", mode)
         mod = s2s.BiRNN(f, b).cuda()
@@ -283,6 +292,7 @@ def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch):
             res.append((y, dx, [g.clone() for g in f.gradWeight + b.gradWeight]))
         torch.cuda.synchronize()
         outs[mode] = res
+    fn(1)
     for rep in range(3):
         ys, dxs, gs = outs["step"][rep]
         yp, dxp, gp = outs["persistent"][rep]
