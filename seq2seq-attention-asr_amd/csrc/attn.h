@@ -30,7 +30,11 @@ size_t attn_saved_bytes(const AttnDims& d);
 size_t attn_scratch_bytes(const AttnDims& d);
 // h (B, L, A) contiguous; labels (B, T) int32 0-based; logp (B, T, O) out.
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
-             void* saved, void* scratch, size_t scratch_bytes);
+             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done = false);
+// The decoder's parameter folds / teacher-forced constants (needs only P and labels): the model
+// step issues it beside the encoder and then calls attn_fwd(..., prologue_done = true).
+int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, const AttnParams& P, void* saved,
+                      void* scratch);
 // dlogp (B, T, O); dh (B, L, A) written (accumulate_dh=0) or accumulated; grads accumulated with scale.
 int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
              const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
@@ -39,8 +43,8 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
 int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                   const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
                   size_t scratch_bytes);
-int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const void* saved,
-                   const AttnGrads& G, float scale, void* scratch);
+int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+                   const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
 

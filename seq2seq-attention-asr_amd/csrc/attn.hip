@@ -18,6 +18,7 @@
 // every weight gradient is one GEMM over all B*T rows afterwards.
 #include "attn.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -62,7 +63,58 @@ struct Layout {
   size_t saved, fwd, bwd;
 };
 
-Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
+// operands of the XCD-local decoder kernels (dec_xcd.inc)
+struct XArgs {
+  int U, nchains, allow_local, XLC, NCH;
+  float* WX;    // (3S, A)  Wx' = [Wz_d; Wr_d; Wh_d] Wd_c Wc          (saved)
+  float* WXT;   // (A, 3S)  Wx'^T                                    (saved)
+  float* WXD;   // (3S, S)  [Wz_d; Wr_d; Wh_d] packed                (saved)
+  float* WDC;   // (S, A)   Wd_c Wc                                  (fwd scratch)
+  float* KX;    // (B*T, 3S) d-part constants of the gates            (fwd scratch)
+  float* KD;    // (B*T, S)  Wd_c bc + Wd_y y_in + bd                 (fwd scratch)
+  float* BKD;   // (S)       Wd_c bc + bd                             (fwd scratch)
+  float* DE;    // (B*T, L)  de_{t,l}                                 (bwd scratch)
+  float* DCS;   // (B*T, A)  dc_t (= AttnK::DC)                       (bwd scratch)
+  float* VBAR;  // (B, Sc)   mean Vh row per utterance                 (bwd scratch)
+  // granule buffers, [2 slots][...]
+  granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gQ;     // forward (inside fsync)
+  granule_t *gDGZ, *gDGR, *gDGH, *gDC, *gPDWS, *gDWS;  // backward (inside bsync)
+  unsigned *fcensus, *bcensus;
+};
+constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder
+constexpr int kXMaxCh = 16;  // chunks per utterance
+constexpr int kXChains = 8;  // chains per launch (one per XCD)
+constexpr int kXWG = 32;     // workgroups per chain
+
+// ---- XCD-local decoder (dec_xcd.inc) plan: chains of U utterances, one per XCD (U as small as
+// 8 chains allow, so the attention work spreads over as many XCDs as possible), each utterance cut
+// into NCH chunks of XLC frames (U * NCH <= 32 workgroups).  var = 0: the shape is served by the
+// older kernels (S2S_DEC_MODE=persist / step force those).
+struct XPlan {
+  int var = 0, U = 0, nchains = 0, XLC = 0, NCH = 0;
+};
+XPlan dec_xcd_plan(const AttnDims& d) {
+  XPlan p;
+  const char* m = std::getenv("S2S_DEC_MODE");
+  if (m && (std::strcmp(m, "step") == 0 || std::strcmp(m, "persist") == 0)) return p;
+  int var = 0;
+  if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
+  else if (d.S == 64 && d.A == 128 && d.Sc == 128) var = 2;
+  if (!var) return p;
+  const int U = (d.B + kXChains - 1) / kXChains;
+  if (U > 16) return p;
+  const int nmax = std::min(kXMaxCh, kXWG / U);
+  const int xlc = ((d.L + nmax - 1) / nmax + 3) / 4 * 4;
+  if (xlc > kXLC) return p;
+  p.var = var;
+  p.U = U;
+  p.nchains = (d.B + U - 1) / U;
+  p.XLC = xlc;
+  p.NCH = (d.L + xlc - 1) / xlc;
+  return p;
+}
+
+Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x = nullptr) {
   const long B = d.B, L = d.L, T = d.T, A = d.A, Sc = d.Sc, S = d.S, O = d.O, M = d.M, Mk = (long)d.M * d.K;
   const long NCH = (d.L + LC - 1) / LC, BT = B * T;
   Bump sv{saved, 0, 0};
@@ -81,11 +133,19 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
   float* MM = sv.take<float>(BT * M);
   int* AM = sv.take<int>(BT * M);
   float* LOGP = sv.take<float>(BT * O);
+  float* WX = sv.take<float>(3 * S * A);
+  float* WXT = sv.take<float>(3 * S * A);
+  float* WXD = sv.take<float>(3 * S * S);
+  const long NX = std::max(1, dec_xcd_plan(d).NCH);
   Bump f{scratch, 0, 0};
   float* PM = f.take<float>(B * NCH);
   float* PL = f.take<float>(B * NCH);
   float* PC = f.take<float>(B * NCH * A);
   float* U = f.take<float>(BT * Mk);
+  float* WDC = f.take<float>(S * A);
+  float* KX = f.take<float>(BT * 3 * S);
+  float* KD = f.take<float>(BT * S);
+  float* BKD = f.take<float>(S);
   Bump g{scratch, 0, 0};
   float* DO = g.take<float>(BT * O);
   float* DU = g.take<float>(BT * Mk);
@@ -107,6 +167,8 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
   float* WdT = g.take<float>(2 * S * S);
   float* WcT = g.take<float>(A * S);
   float* WsT = g.take<float>(S * Sc);
+  float* DE = g.take<float>(BT * L);
+  float* VBAR = g.take<float>(B * Sc);
   // granule regions (256-byte header = abort word), zeroed by one memset before each persistent launch
   char* fsync = f.take<char>(256);
   granule_t* gS = f.take<granule_t>(2 * B * S);
@@ -118,6 +180,14 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
   granule_t* gCY = f.take<granule_t>(2 * B * 2 * S);
   granule_t* gD = f.take<granule_t>(2 * B * S);
   granule_t* gQ = f.take<granule_t>(2 * B * S);
+  granule_t* xgS = f.take<granule_t>(2 * B * S);
+  granule_t* xgWS = f.take<granule_t>(2 * B * Sc);
+  granule_t* xgPM = f.take<granule_t>(2 * B * NX);
+  granule_t* xgPL = f.take<granule_t>(2 * B * NX);
+  granule_t* xgPC = f.take<granule_t>(2 * B * NX * A);
+  granule_t* xgC = f.take<granule_t>(2 * B * A);
+  granule_t* xgQ = f.take<granule_t>(2 * B * S);
+  unsigned* fcensus = f.take<unsigned>(kXChains * kXWG);
   const size_t fsync_bytes = f.off - (size_t)(fsync - scratch);
   char* bsync = g.take<char>(256);
   granule_t* gZ = g.take<granule_t>(2 * B * S);
@@ -128,6 +198,13 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
   granule_t* gDC = g.take<granule_t>(2 * B * A);
   granule_t* gPDWS = g.take<granule_t>(2 * B * NCH * Sc);
   granule_t* gDWS = g.take<granule_t>(2 * B * Sc);
+  granule_t* xgDGZ = g.take<granule_t>(2 * B * S);
+  granule_t* xgDGR = g.take<granule_t>(2 * B * S);
+  granule_t* xgDGH = g.take<granule_t>(2 * B * S);
+  granule_t* xgDC = g.take<granule_t>(2 * B * A);
+  granule_t* xgPDWS = g.take<granule_t>(2 * B * NX * Sc);
+  granule_t* xgDWS = g.take<granule_t>(2 * B * Sc);
+  unsigned* bcensus = g.take<unsigned>(kXChains * kXWG);
   const size_t bsync_bytes = g.off - (size_t)(bsync - scratch);
   if (k) {
     k->gS = gS; k->gWS = gWS; k->gPM = gPM; k->gPL = gPL; k->gPC = gPC; k->gC = gC; k->gCY = gCY; k->gD = gD;
@@ -143,6 +220,13 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch) {
     k->DO = DO; k->DU = DU; k->DV = DV; k->DGA = DGA; k->DS = DS; k->DSP = DSP; k->DSPF = DSPF; k->DD = DD;
     k->DCY = DCY; k->DC = DC; k->DVH = DVH; k->PDWS = PDWS; k->DWS = DWS; k->DWEACC = DWEACC; k->YP = YP;
     k->WhT = WhT; k->GT = GT; k->WdT = WdT; k->WcT = WcT; k->WsT = WsT;
+  }
+  if (x) {
+    x->WX = WX; x->WXT = WXT; x->WXD = WXD; x->WDC = WDC; x->KX = KX; x->KD = KD; x->BKD = BKD; x->DE = DE;
+    x->DCS = DC; x->VBAR = VBAR;
+    x->gS = xgS; x->gWS = xgWS; x->gPM = xgPM; x->gPL = xgPL; x->gPC = xgPC; x->gC = xgC; x->gQ = xgQ;
+    x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
+    x->fcensus = fcensus; x->bcensus = bcensus;
   }
   return Layout{sv.off + 256, f.off + 256, g.off + 256};
 }
@@ -652,6 +736,7 @@ __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const in
 }
 
 #include "attn_persist.inc"
+#include "dec_xcd.inc"
 
 }  // namespace
 
@@ -749,12 +834,61 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
   return 0;
 }
 
+static int g_dec_allow_local = 1;
+
+template <int S, int A, int SC>
+static int launch_xcd_t(bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
+  const size_t lds = xdec_lds<S, A, SC>(x.XLC);
+  const void* fn = fwd ? (const void*)dec_xcd_fwd<S, A, SC> : (const void*)dec_xcd_bwd<S, A, SC>;
+  S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* args[] = {&k, &x};
+  S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
+  return 0;
+}
+static int launch_xcd(int var, bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
+  if (var == 1) return launch_xcd_t<256, 512, 512>(fwd, st, k, x);
+  return launch_xcd_t<64, 128, 128>(fwd, st, k, x);
+}
+
+// Weight folds and teacher-forced constants of the XCD-local decoder (params and labels only, so
+// the model step runs it on the side stream beside the encoder).
+static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const GemmWs& gws) {
+  const int S = d.S, A = d.A, rows = d.B * d.T;
+  S2S_TRY(copy2d_f32(st, k.P.Wz + S, 2L * S, x.WXD, S, S, S, false));
+  S2S_TRY(copy2d_f32(st, k.P.Wr + S, 2L * S, x.WXD + (long)S * S, S, S, S, false));
+  S2S_TRY(copy2d_f32(st, k.P.Wh + S, 2L * S, x.WXD + 2L * S * S, S, S, S, false));
+  // WDC = Wd_c Wc (S x A); WX = WXD WDC (3S x A); WXT = WX^T
+  S2S_TRY(gemm1(st, false, false, S, A, S, 1.f, k.P.Wd, 2L * S, k.P.Wc, A, 0.f, x.WDC, A, nullptr, gws));
+  S2S_TRY(gemm1(st, false, false, 3 * S, A, S, 1.f, x.WXD, S, x.WDC, A, 0.f, x.WX, A, nullptr, gws));
+  S2S_TRY(transpose_f32(st, x.WX, A, 3 * S, A, x.WXT, 3L * S));
+  // y_in -> CY[:, S:]; BKD = Wd_c bc + bd; KD = y_in Wd_y^T + BKD; KX = KD WXD^T
+  hipLaunchKernelGGL(dec_xcd_yin, dim3(256), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);
+  S2S_CHECK_HIP(hipGetLastError());
+  S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
+  S2S_TRY(gemm1(st, false, true, rows, 3 * S, S, 1.f, x.KD, S, x.WXD, S, 0.f, x.KX, 3L * S, nullptr, gws));
+  return 0;
+}
+
+int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, const AttnParams& P, void* saved,
+                      void* scratch) {
+  const XPlan xp = dec_xcd_plan(d);
+  if (!xp.var) return 0;
+  AttnK k{};
+  XArgs x{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x);
+  k.P = P;
+  k.labels = labels;
+  return dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch));
+}
+
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
-             void* saved, void* scratch, size_t scratch_bytes) {
+             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done) {
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
-  carve(d, &k, (char*)saved, (char*)scratch);
+  XArgs x{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x);
   k.P = P;
   k.h = h;
   k.labels = labels;
@@ -766,10 +900,25 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
   hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  const XPlan xp = dec_xcd_plan(d);
   const int pgrid = kDecWG * ((B + 15) / 16);
-  const int pvar = dec_persist_variant(d);
+  const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pf = pvar ? pick_dec_fwd(pvar, d, pgrid) : PersistLaunch{};
-  if (pf.fn) {
+  if (xp.var) {
+    if (!prologue_done) S2S_TRY(dec_xcd_prologue(st, d, k, x, gws));
+    x.U = xp.U;
+    x.nchains = xp.nchains;
+    x.XLC = xp.XLC;
+    x.NCH = xp.NCH;
+    x.allow_local = g_dec_allow_local;
+    S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
+    {
+      ProfScope ps(st, "dec_fwd_xcd", 0.0, 0.0);
+      S2S_TRY(launch_xcd(xp.var, true, st, k, x));
+    }
+    hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, st, k);
+    S2S_CHECK_HIP(hipGetLastError());
+  } else if (pf.fn) {
     S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
     {
       ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
@@ -806,7 +955,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
-  carve(d, &k, (char*)saved, (char*)scratch);
+  XArgs x{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x);
   k.P = P;
   k.h = h;
   k.labels = labels;
@@ -816,9 +966,12 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   k.lddh = d.A;
   const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
   const int rows = B * T, bt = (B + 15) / 16;
+  const XPlan xp = dec_xcd_plan(d);
   if (!accumulate_dh) S2S_CHECK_HIP(hipMemsetAsync(dh, 0, sizeof(float) * (size_t)B * L * A, st));
-  S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
-  S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
+  if (!xp.var) {  // the XCD-local path writes DVH / DWEACC whole after its loop
+    S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
+    S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
+  }
   // packed transposes for the backward products
   S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
   S2S_TRY(transpose_f32(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
@@ -836,9 +989,34 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A, nullptr, gws));
   const int pgrid = kDecWG * ((B + 15) / 16);
-  const int pvar = dec_persist_variant(d);
+  const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pb = pvar ? pick_dec_bwd(pvar, d, pgrid) : PersistLaunch{};
-  if (pb.fn) {
+  if (xp.var) {
+    x.U = xp.U;
+    x.nchains = xp.nchains;
+    x.XLC = xp.XLC;
+    x.NCH = xp.NCH;
+    x.allow_local = g_dec_allow_local;
+    S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
+    hipLaunchKernelGGL(dec_xcd_vbar, dim3(B), dim3(256), 0, st, k, x);
+    {
+      ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
+      S2S_TRY(launch_xcd(xp.var, false, st, k, x));
+    }
+    // dh_l += sum_t alpha_{t,l} dc_t  (one GEMM per utterance: alpha_b^T (L x T) . dc_b (T x A))
+    for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
+      GemmProblem pr[kMaxGemmBatch];
+      const int nb = std::min(kMaxGemmBatch, B - b0);
+      for (int i = 0; i < nb; ++i) {
+        const long b = b0 + i;
+        pr[i] = GemmProblem{k.ALPHA + b * T * L, x.DCS + b * T * A, dh + b * L * A, nullptr, L, A, A, L, A, T,
+                            1.f, 1.f};
+      }
+      S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
+    }
+    hipLaunchKernelGGL(dec_xcd_dvh, dim3(k.NCH, B), dim3(256), 0, st, k, x);
+    S2S_CHECK_HIP(hipGetLastError());
+  } else if (pb.fn) {
     S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
     S2S_TRY(launch_persist(pb, pgrid, st, k));
@@ -866,15 +1044,26 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
 // Weight gradients: one GEMM per parameter over all B*T rows (accumulate, alpha = scale), then
 // the bias column sums.  Reads only the saved buffer and attn_bwd_core's scratch, so the model
 // step runs it on a side stream beside the encoder BPTT.
-int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const void* saved,
-                   const AttnGrads& G, float scale, void* scratch) {
+int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
+                   const void* saved, const AttnGrads& G, float scale, void* scratch) {
   AttnK k{};
-  carve(d, &k, (char*)saved, (char*)scratch);
+  XArgs x{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x);
   k.labels = labels;
   const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
   const int rows = B * T;
   hipLaunchKernelGGL(dec_onehot_prev, dim3(256), dim3(256), 0, st, k);
   S2S_CHECK_HIP(hipGetLastError());
+  if (dec_xcd_plan(d).var) {
+    // the XCD-local loop folded c -> c_in -> d away: recompute them (and dd, [dc_in | dy_in]) for
+    // the weight gradients, all B*T rows at once
+    const GemmWs gws = attn_gemm_ws(d, scratch);
+    S2S_TRY(gemm1(st, false, true, rows, S, A, 1.f, k.C, A, P.Wc, A, 0.f, k.CY, 2L * S, P.bc, gws));
+    S2S_TRY(gemm1(st, false, true, rows, S, 2 * S, 1.f, k.CY, 2L * S, P.Wd, 2L * S, 0.f, k.HX + S, 2L * S, P.bd, gws));
+    S2S_TRY(copy2d_f32(st, k.HX + S, 2L * S, k.RHX + S, 2L * S, rows, S, false));
+    S2S_TRY(gemm1(st, false, false, rows, S, 3 * S, 1.f, k.DGA, 3L * S, x.WXD, S, 0.f, k.DD, S, nullptr, gws));
+    S2S_TRY(gemm1(st, false, false, rows, 2 * S, S, 1.f, k.DD, S, P.Wd, 2L * S, 0.f, k.DCY, 2L * S, nullptr, gws));
+  }
   {
     GemmProblem pr[16];
     int n = 0;
@@ -904,7 +1093,7 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
              const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
              void* scratch, size_t scratch_bytes) {
   S2S_TRY(attn_bwd_core(st, d, h, labels, P, saved, dlogp, dh, accumulate_dh, scratch, scratch_bytes));
-  return attn_bwd_wgrad(st, d, h, labels, saved, G, scale, scratch);
+  return attn_bwd_wgrad(st, d, h, labels, P, saved, G, scale, scratch);
 }
 
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
@@ -918,6 +1107,8 @@ int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* 
 
 // Diagnostic (not part of the C ABI header): device buffers of (grid * T * 8) uint64 that the
 // persistent decoder kernels fill with s_memrealtime stamps at phase ends; nullptr turns it off.
+// diagnostic: 0 forces write-through (sc1) hand-offs in every XCD-local decoder chain
+extern "C" void s2s_debug_dec_local(int allow) { s2s::g_dec_allow_local = allow; }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);

@@ -221,6 +221,21 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
   if (flags & S2S_ZERO_GRADS) S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, st));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
+  const AttnDims ad = model_attn(d);
+  AttnParams ap;
+  AttnGrads ag;
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  float** gp = reinterpret_cast<float**>(&ag);
+  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+    pp[i] = P[6 * nl + i];
+    gp[i] = G[6 * nl + i];
+  }
+  // the decoder's parameter folds need only params and labels: beside the encoder when split
+  if (split) {
+    S2S_TRY(fork_to(st, side, ev[13]));
+    S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+    S2S_CHECK_HIP(hipEventRecord(ev[14], side));
+  }
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   // layer-1 input padded to a multiple of 32 columns: its GEMMs then run on aligned full tiles
   const float* x0 = x;
@@ -250,17 +265,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
     ldin = 2L * H;
   }
   // ---- attention decoder forward
-  const AttnDims ad = model_attn(d);
-  AttnParams ap;
-  AttnGrads ag;
-  const float** pp = reinterpret_cast<const float**>(&ap);
-  float** gp = reinterpret_cast<float**>(&ag);
-  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
-    pp[i] = P[6 * nl + i];
-    gp[i] = G[6 * nl + i];
-  }
+  if (split) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
-  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes));
+  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, split));
   // ---- loss seed: dlogp = -labelmask
   S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
   // ---- decoder backward -> dh
@@ -269,7 +276,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
                         w.attn_scratch_bytes));
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
-  S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, w.attn_saved, ag, scale, w.attn_scratch));
+  S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
   // ---- encoder backward
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;

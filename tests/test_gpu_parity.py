@@ -137,6 +137,36 @@ ATT_CASES = [
 
 @pytest.mark.parametrize("B,L,T,A,Sc,S,O,M,K,pen", ATT_CASES)
 def test_attention_decoder_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen):
+    _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen)
+
+
+# shapes served by the XCD-local decoder kernels (dec_xcd.inc): chains of U utterances on one XCD;
+# U = 8 (4 chunks of 32 frames), ragged last chain, U = 4 (7 chunks), penalty on
+XCD_CASES = [
+    (32, 128, 12, 512, 512, 256, 62, 8, 7, 0.0),
+    (21, 50, 9, 128, 128, 64, 29, 4, 7, 0.2),
+    (5, 200, 7, 128, 128, 64, 29, 4, 7, 0.0),
+    (3, 20, 5, 128, 128, 64, 11, 4, 3, 0.0),
+]
+
+
+@pytest.mark.parametrize("local", [1, 0])
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O,M,K,pen", XCD_CASES)
+def test_xcd_decoder_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen, local):
+    """XCD-local decoder (folded Wx' = W_d Wd_c Wc, L2-resident granule hand-offs when local=1 and
+    the census finds each chain on one XCD; write-through sc1 hand-offs when local=0)."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_dec_local
+    fn.argtypes = [ctypes.c_int]
+    fn(local)
+    try:
+        _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen)
+    finally:
+        fn(1)
+
+
+def _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen):
     rng = np.random.default_rng(L * 7 + T)
     cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
                           outputDepth=O, mlpDepth=M, maxoutWindow=K, penalty=pen, numLayers=1)
@@ -312,7 +342,7 @@ def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B
     labels = cu(rng.integers(0, O, (B, T)), torch.int32)
     dlogp = cu(rng.standard_normal((B, T, O)))
     outs = {}
-    for mode in ("step", "persistent"):
+    for mode in ("step", "persist"):
         monkeypatch.setenv("S2S_DEC_MODE", mode)
         res = []
         for _ in range(2):
@@ -325,5 +355,5 @@ def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B
         outs[mode] = res
     names = ["logp", "alpha", "dh"] + ["d" + n for n in s2s.Attention.PARAM_NAMES]
     for rep in range(2):
-        for name, a, b in zip(names, outs["step"][rep], outs["persistent"][rep]):
+        for name, a, b in zip(names, outs["step"][rep], outs["persist"][rep]):
             assert torch.equal(a, b), f"{name} differs (rep {rep}): max |d| = {(a - b).abs().max().item():.3e}"
