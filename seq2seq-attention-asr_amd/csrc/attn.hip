@@ -76,6 +76,9 @@ struct XArgs {
   float* DE;    // (B*T, L)  de_{t,l}                                 (bwd scratch)
   float* DCS;   // (B*T, A)  dc_t (= AttnK::DC)                       (bwd scratch)
   float* VBAR;  // (B, Sc)   mean Vh row per utterance                 (bwd scratch)
+  float* XWHT;  // (S, S)    Wh[:, :S]^T                               (saved)
+  float* XZRT;  // (S, 2S)   [Wz[:, :S]; Wr[:, :S]]^T                   (saved)
+  float* XWST;  // (S, Sc)   Ws^T                                      (saved)
   // granule buffers, [2 slots][...]
   granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gQ;     // forward (inside fsync)
   granule_t *gDGZ, *gDGR, *gDGH, *gDC, *gPDWS, *gDWS;  // backward (inside bsync)
@@ -105,7 +108,7 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   if (U > 16) return p;
   const int nmax = std::min(kXMaxCh, kXWG / U);
   const int xlc = ((d.L + nmax - 1) / nmax + 3) / 4 * 4;
-  if (xlc > kXLC) return p;
+  if (xlc > kXLC || d.T > 256) return p;  // (dec_xcd_dvh stages up to 256 steps)
   p.var = var;
   p.U = U;
   p.nchains = (d.B + U - 1) / U;
@@ -136,6 +139,9 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* WX = sv.take<float>(3 * S * A);
   float* WXT = sv.take<float>(3 * S * A);
   float* WXD = sv.take<float>(3 * S * S);
+  float* XWHT = sv.take<float>(S * S);
+  float* XZRT = sv.take<float>(2 * S * S);
+  float* XWST = sv.take<float>(S * Sc);
   const long NX = std::max(1, dec_xcd_plan(d).NCH);
   Bump f{scratch, 0, 0};
   float* PM = f.take<float>(B * NCH);
@@ -223,7 +229,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   }
   if (x) {
     x->WX = WX; x->WXT = WXT; x->WXD = WXD; x->WDC = WDC; x->KX = KX; x->KD = KD; x->BKD = BKD; x->DE = DE;
-    x->DCS = DC; x->VBAR = VBAR;
+    x->DCS = DC; x->VBAR = VBAR; x->XWHT = XWHT; x->XZRT = XZRT; x->XWST = XWST;
     x->gS = xgS; x->gWS = xgWS; x->gPM = xgPM; x->gPL = xgPL; x->gPC = xgPC; x->gC = xgC; x->gQ = xgQ;
     x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
     x->fcensus = fcensus; x->bcensus = bcensus;
@@ -867,6 +873,11 @@ static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const X
   S2S_CHECK_HIP(hipGetLastError());
   S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
   S2S_TRY(gemm1(st, false, true, rows, 3 * S, S, 1.f, x.KD, S, x.WXD, S, 0.f, x.KX, 3L * S, nullptr, gws));
+  // backward operand layouts (rows = output units, K contiguous)
+  S2S_TRY(transpose_f32(st, k.P.Wh, 2L * S, S, S, x.XWHT, S));
+  S2S_TRY(transpose_f32(st, k.P.Wz, 2L * S, S, S, x.XZRT, 2L * S));
+  S2S_TRY(transpose_f32(st, k.P.Wr, 2L * S, S, S, x.XZRT + S, 2L * S));
+  S2S_TRY(transpose_f32(st, k.P.Ws, S, d.Sc, S, x.XWST, d.Sc));
   return 0;
 }
 
@@ -973,6 +984,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
   }
   // packed transposes for the backward products
+  if (!xp.var) {  // (the XCD-local path's operand layouts come from its prologue)
   S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
   S2S_TRY(transpose_f32(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
   S2S_TRY(transpose_f32(st, P.Wr, 2L * S, S, 2 * S, k.GT + S, 3L * S));
@@ -982,6 +994,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_TRY(transpose_f32(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
   S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
   S2S_TRY(transpose_f32(st, P.Ws, S, Sc, S, k.WsT, Sc));
+  }
   // MLP backward for all rows (not on the recurrence)
   hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
@@ -998,7 +1011,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
     S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
-    hipLaunchKernelGGL(dec_xcd_vbar, dim3(B), dim3(256), 0, st, k, x);
+    hipLaunchKernelGGL(dec_xcd_vbar, dim3((Sc + 63) / 64, B), dim3(256), 0, st, k, x);
     {
       ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
       S2S_TRY(launch_xcd(xp.var, false, st, k, x));
@@ -1014,7 +1027,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       }
       S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
     }
-    hipLaunchKernelGGL(dec_xcd_dvh, dim3(k.NCH, B), dim3(256), 0, st, k, x);
+    hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 255) / 256, k.NCH, B), dim3(256), 0, st, k, x);
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pb.fn) {
     S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));

@@ -142,6 +142,7 @@ struct ModelWs {
   std::vector<float*> saved;  // 2 per layer
   std::vector<float*> Y;      // per layer output (B, L, 2H)
   std::vector<float*> dA;     // per layer gate gradients (B, L, 6H), read by the side-stream dW GEMMs
+  std::vector<float*> pack;   // per layer packed weight layouts (gru_layer_pack)
   void* attn_saved;
   void* attn_scratch;
   size_t attn_scratch_bytes;
@@ -164,6 +165,7 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
     w.saved.push_back(bp.take<float>(B * L * 5 * ld.H));
     w.Y.push_back(bp.take<float>(B * L * 2 * ld.H));
     w.dA.push_back(bp.take<float>(B * L * 6 * ld.H));
+    w.pack.push_back(bp.take<float>(gru_layer_pack_bytes(2, ld.D, ld.H) / sizeof(float)));
     size_t s = gru_layer_scratch_bytes(2, d->B, d->L, ld.D, ld.H);
     scr = s > scr ? s : scr;
     hmax = ld.H > hmax ? ld.H : hmax;
@@ -230,28 +232,20 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
     pp[i] = P[6 * nl + i];
     gp[i] = G[6 * nl + i];
   }
-  // the decoder's parameter folds need only params and labels: beside the encoder when split
-  if (split) {
-    S2S_TRY(fork_to(st, side, ev[13]));
-    S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
-    S2S_CHECK_HIP(hipEventRecord(ev[14], side));
-  }
-  // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   // layer-1 input padded to a multiple of 32 columns: its GEMMs then run on aligned full tiles
   const float* x0 = x;
   long ldx0 = d->inputFrameSize;
   if (w.xpad) {
-    S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
     x0 = w.xpad;
     ldx0 = w.Dp;
   }
-  const float* inp = x0;
-  long ldin = ldx0;
-  for (int l = 0; l < nl; ++l) {
+  // encoder layer l's operands (fwd: io.x is the layer input; bwd adds the grads)
+  auto layer_io = [&](int l) {
     const int H = layers[l].H;
     GruLayerIO io{};
     io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
-    io.x = inp; io.ldx = ldin;
+    io.x = l == 0 ? x0 : w.Y[l - 1];
+    io.ldx = l == 0 ? ldx0 : 2L * layers[l - 1].H;
     io.Dx = (l == 0 && w.xpad) ? w.Dp : 0;
     for (int dd = 0; dd < 2; ++dd) {
       for (int g = 0; g < 3; ++g) io.W[dd][g] = P[6 * l + 3 * dd + g];
@@ -260,14 +254,32 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
       io.saved[dd] = w.saved[2 * l + dd];
     }
     io.ldy = 2L * H;
-    S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
-    inp = w.Y[l];
-    ldin = 2L * H;
+    io.packed = w.pack[l];
+    return io;
+  };
+  if (w.xpad) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
+  // weight packing for every layer (both passes) and the decoder's parameter folds need only params
+  // and labels: layer 1 on the critical path, the rest beside layer 1's recurrence when split
+  // weight packing for every layer and both passes: one launch on the critical path (~10 us); the
+  // decoder's parameter folds (params and labels only) beside the encoder when split
+  {
+    std::vector<GruLayerIO> ios;
+    for (int l = 0; l < nl; ++l) ios.push_back(layer_io(l));
+    S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl));
   }
+  if (split) {
+    S2S_TRY(fork_to(st, side, ev[13]));
+    S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+    S2S_CHECK_HIP(hipEventRecord(ev[14], side));
+  } else {
+    S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
+  }
+  // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
+  for (int l = 0; l < nl; ++l) S2S_TRY(gru_layer_fwd(st, layer_io(l), w.scratch, w.scratch_bytes));
   // ---- attention decoder forward
   if (split) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
-  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, split));
+  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, true));
   // ---- loss seed: dlogp = -labelmask
   S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
   // ---- decoder backward -> dh
@@ -280,21 +292,10 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
   // ---- encoder backward
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
-    GruLayerIO io{};
-    io.ndir = 2; io.B = B; io.L = L; io.D = layers[l].D; io.H = H;
-    io.x = l == 0 ? x0 : w.Y[l - 1];
-    io.ldx = l == 0 ? ldx0 : 2L * layers[l - 1].H;
-    io.Dx = (l == 0 && w.xpad) ? w.Dp : 0;
-    io.ldy = 2L * H;
+    const GruLayerIO io = layer_io(l);
     GruLayerGrad gr{};
     for (int dd = 0; dd < 2; ++dd) {
-      for (int g = 0; g < 3; ++g) {
-        io.W[dd][g] = P[6 * l + 3 * dd + g];
-        gr.dW[dd][g] = G[6 * l + 3 * dd + g];
-      }
-      io.reverse[dd] = dd;
-      io.y[dd] = w.Y[l] + dd * H;
-      io.saved[dd] = w.saved[2 * l + dd];
+      for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
       gr.dy[dd] = dYcur + dd * H;
     }
     gr.lddy = 2L * H;

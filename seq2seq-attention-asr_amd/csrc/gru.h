@@ -16,6 +16,7 @@ struct GruLayerIO {
   float* saved[2];  // per direction (B, L, 5H)
   int Dx = 0;       // x columns [D, Dx) are readable zeros (0 = D; Dx <= round_up(D, 32)):
                     // the input GEMMs then run over K = Dx on aligned, unguarded tiles
+  const float* packed = nullptr;  // gru_layer_pack output for these weights (null: pack per call)
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]
@@ -28,6 +29,11 @@ struct GruLayerGrad {
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
+// Every kernel layout of one layer's weights (recurrent Uzr/Uh and their transposes, the padded
+// x-projection rows), packed once per step so the forward and backward launches skip it.
+size_t gru_layer_pack_bytes(int ndir, int D, int H);
+int gru_layer_pack(hipStream_t st, const GruLayerIO& io, float* packed);
+int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers);  // one launch
 int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes);
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes);
 // split form used by the model step: core = weight packing + BPTT + dx (critical path), writing the

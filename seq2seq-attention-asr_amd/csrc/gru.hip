@@ -16,6 +16,7 @@
 // Saved activations per direction: sv (B, L, 5H) = z | r | hh | h_{t-1} | q.
 #include "gru.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -182,7 +183,7 @@ struct PackArgs {
   float *Uzr, *Uh, *UhT, *UzrT, *Wx;
   int H, D, Kx;  // Wx rows have stride Kx >= D, columns [D, Kx) zero
 };
-__global__ void gru_pack(PackArgs p) {
+__device__ __forceinline__ void pack_body(const PackArgs& p) {
   const int H = p.H, D = p.D, HD = H + D, Kx = p.Kx;
   const long nU = 3L * H * H, nX = 3L * H * Kx;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nU + nX; i += (long)gridDim.x * blockDim.x) {
@@ -207,6 +208,13 @@ __global__ void gru_pack(PackArgs p) {
     }
   }
 }
+__global__ void gru_pack(PackArgs p) { pack_body(p); }
+// several layer-directions in one launch (blockIdx.y = which)
+constexpr int kMaxPack = 8;
+struct PackBatch {
+  PackArgs p[kMaxPack];
+};
+__global__ void gru_pack_multi(PackBatch b) { pack_body(b.p[blockIdx.y]); }
 
 int launch_pack(hipStream_t st, const float* Wz, const float* Wr, const float* Wh, int H, int D, int Kx, float* Uzr,
                 float* Uh, float* UhT, float* UzrT, float* Wx) {
@@ -246,6 +254,68 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   return bp.off + 256;
 }
 
+// packed layout: per direction Uzr (2H,H) | Uh (H,H) | UhT (H,H) | UzrT (H,2H), then Wx (3*ndir*H, Kp)
+size_t gru_layer_pack_bytes(int ndir, int D, int H) {
+  return sizeof(float) * ((size_t)ndir * 6 * H * H + 3ull * ndir * H * ((D + 31) / 32 * 32));
+}
+struct PackView {
+  const float *Uzr[2], *Uh[2], *UhT[2], *UzrT[2], *Wx;
+};
+static PackView pack_view(const float* pk, int nd, int H) {
+  PackView v{};
+  for (int d = 0; d < nd; ++d) {
+    v.Uzr[d] = pk;
+    v.Uh[d] = pk + 2L * H * H;
+    v.UhT[d] = pk + 3L * H * H;
+    v.UzrT[d] = pk + 4L * H * H;
+    pk += 6L * H * H;
+  }
+  v.Wx = pk;
+  return v;
+}
+int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers) {
+  PackBatch b{};
+  int n = 0;
+  long most = 0;
+  auto flush = [&]() -> int {
+    if (n == 0) return 0;
+    int blocks = (int)((most + 255) / 256);
+    if (blocks > 512) blocks = 512;
+    hipLaunchKernelGGL(gru_pack_multi, dim3(blocks, n), dim3(256), 0, st, b);
+    S2S_CHECK_HIP(hipGetLastError());
+    n = 0;
+    most = 0;
+    return 0;
+  };
+  for (int l = 0; l < nlayers; ++l) {
+    const GruLayerIO& io = ios[l];
+    const int nd = io.ndir, D = io.D, H = io.H;
+    const int Kx = io.Dx > D ? io.Dx : D;
+    S2S_REQUIRE(Kx <= (D + 31) / 32 * 32, "gru: Dx must be <= round_up(D, 32)");
+    const PackView v = pack_view(packed[l], nd, H);
+    for (int d = 0; d < nd; ++d) {
+      if (n == kMaxPack) S2S_TRY(flush());
+      b.p[n++] = PackArgs{{io.W[d][0], io.W[d][1], io.W[d][2]}, const_cast<float*>(v.Uzr[d]),
+                          const_cast<float*>(v.Uh[d]), const_cast<float*>(v.UhT[d]), const_cast<float*>(v.UzrT[d]),
+                          const_cast<float*>(v.Wx) + 3L * d * H * Kx, H, D, Kx};
+      most = std::max(most, 3L * H * (H + Kx));
+    }
+  }
+  return flush();
+}
+
+int gru_layer_pack(hipStream_t st, const GruLayerIO& io, float* packed) {
+  const int nd = io.ndir, D = io.D, H = io.H;
+  const int Kx = io.Dx > D ? io.Dx : D;
+  S2S_REQUIRE(Kx <= (D + 31) / 32 * 32, "gru: Dx must be <= round_up(D, 32)");
+  const PackView v = pack_view(packed, nd, H);
+  for (int d = 0; d < nd; ++d)
+    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, const_cast<float*>(v.Uzr[d]),
+                        const_cast<float*>(v.Uh[d]), const_cast<float*>(v.UhT[d]), const_cast<float*>(v.UzrT[d]),
+                        const_cast<float*>(v.Wx) + 3L * d * H * Kx));
+  return 0;
+}
+
 // the split-K region at the tail of a layer scratch (gru_layer_scratch_bytes)
 static GemmWs layer_gemm_ws(void* scratch, int ndir, int B, int L, int D, int H) {
   const size_t tail = gru_layer_scratch_bytes(ndir, B, L, D, H) - 256 - sizeof(float) * kGemmWsFloats;
@@ -274,9 +344,18 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* xp = bp.take<float>((long)B * L * 3 * nd * H);
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
-  for (int d = 0; d < nd; ++d)
-    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, Uzr[d], Uh[d], nullptr, nullptr,
-                        Wx + 3L * d * H * Kx));
+  if (io.packed) {
+    const PackView v = pack_view(io.packed, nd, H);
+    for (int d = 0; d < nd; ++d) {
+      Uzr[d] = const_cast<float*>(v.Uzr[d]);
+      Uh[d] = const_cast<float*>(v.Uh[d]);
+    }
+    Wx = const_cast<float*>(v.Wx);
+  } else {
+    for (int d = 0; d < nd; ++d)
+      S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, Uzr[d], Uh[d], nullptr, nullptr,
+                          Wx + 3L * d * H * Kx));
+  }
   // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, Kx) . Wx^T
   S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, Kx, 1.f, io.x, io.ldx, Wx, Kx, 0.f, xp, 3L * nd * H, nullptr,
                 layer_gemm_ws(scratch, nd, B, L, D, H)));
@@ -329,9 +408,18 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   float* dA = dA_ext ? dA_ext : dA_int;
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
   const long ldA = 3L * nd * H;
-  for (int d = 0; d < nd; ++d)
-    S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, nullptr, nullptr, UhT[d], UzrT[d],
-                        Wx + 3L * d * H * Kx));
+  if (io.packed) {
+    const PackView v = pack_view(io.packed, nd, H);
+    for (int d = 0; d < nd; ++d) {
+      UhT[d] = const_cast<float*>(v.UhT[d]);
+      UzrT[d] = const_cast<float*>(v.UzrT[d]);
+    }
+    Wx = const_cast<float*>(v.Wx);
+  } else {
+    for (int d = 0; d < nd; ++d)
+      S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, nullptr, nullptr, UhT[d], UzrT[d],
+                          Wx + 3L * d * H * Kx));
+  }
   GruBwdArgs a{};
   for (int d = 0; d < nd; ++d)
     a.d[d] = GruBwdDir{gr.dy[d], gr.lddy, io.saved[d], UhT[d], UzrT[d], dA + 3L * d * H, ldA, dhc[d], dhp[d],
