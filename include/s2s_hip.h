@@ -112,6 +112,9 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
                  float* const* grads, float scale, void* scratch, size_t scratch_bytes);
 /* decoder:alpha() (Attention.lua:241-243): device pointer to alpha (B, T, L) inside `saved` */
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
+/* (B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward (MonotonicAlignment.lua:
+ * 27-39): the discrete decision behind the penalty gradient (MonotonicAlignment.lua:44-77). */
+const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);

@@ -47,6 +47,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
+const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
 
 // -log p of the labels and the reference's seed dlogp = -labelmask (timit/timit.lua:262-282).
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,

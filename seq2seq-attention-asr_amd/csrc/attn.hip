@@ -769,6 +769,11 @@ const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
   carve(d, &k, (char*)saved, nullptr);
   return k.ALPHA;
 }
+const float* attn_saved_mono_ind(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.IND;
+}
 
 // S2S_DEC_MODE=step forces the per-step launch path (A/B and fallback); default: the persistent
 // decoder kernels whenever the shape has an instantiation.
@@ -922,7 +927,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       ProfScope ps(st, "dec_fwd_xcd", 0.0, 0.0);
       S2S_TRY(launch_xcd(xp.var, true, st, k, x));
@@ -930,7 +935,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, st, k);
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pf.fn) {
-    S2S_CHECK_HIP(hipMemsetAsync(k.fsync, 0, k.fsync_bytes, st));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
       S2S_TRY(launch_persist(pf, pgrid, st, k));
@@ -1010,7 +1015,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     hipLaunchKernelGGL(dec_xcd_vbar, dim3((Sc + 63) / 64, B), dim3(256), 0, st, k, x);
     {
       ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
@@ -1030,7 +1035,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 255) / 256, k.NCH, B), dim3(256), 0, st, k, x);
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pb.fn) {
-    S2S_CHECK_HIP(hipMemsetAsync(k.bsync, 0, k.bsync_bytes, st));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
     S2S_TRY(launch_persist(pb, pgrid, st, k));
     S2S_CHECK_HIP(hipGetLastError());

@@ -527,6 +527,9 @@ size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d) { return d ? attn_scratch_
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_alpha(to_attn(d), saved) : nullptr;
 }
+const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_mono_ind(to_attn(d), saved) : nullptr;
+}
 
 int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
                  const float* const* params, float* logp, void* saved, void* scratch, size_t scratch_bytes) {

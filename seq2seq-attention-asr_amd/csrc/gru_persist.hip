@@ -81,6 +81,7 @@ template <int NC>  // NC = H / 64
 __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
+  __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
@@ -94,7 +95,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
-  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds);
+  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 w1[NC], w2[NC];
   load_wfrag(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
@@ -120,7 +122,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(0);
     if (s > 0) {
       float4 av[NC];
-      ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), (unsigned)s, wave, lane, a.abort_word);
+      ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
       GRU_STAMP(1);
       acc = mfma_chunks<NC>(av, w1);
       // r tiles: the swept operand already holds h_{t-1} of this tile's 16 units (chunk it of
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
         const int j = on - H;
         const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
         const float q = gate * hp;
-        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, (unsigned)(s + 1), live, loc);  // critical first
+        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live, loc);  // critical first
         if (live) {
           sv[H + j] = gate;
           sv[3 * H + j] = hp;
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(3);
     if (s > 0) {
       float4 av[NC];
-      ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), (unsigned)(s + 1), wave, lane, a.abort_word);
+      ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
       GRU_STAMP(4);
       acc = mfma_chunks<NC>(av, w2);
     }
@@ -170,7 +172,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
       const float hh = tanhf(sum + xph);
       const float hp = hreg;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
-      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, (unsigned)(s + 1), live, loc);  // first
+      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live, loc);  // first
       if (live) {
         g.sv[row * 5 * H + 2 * H + on] = hh;
         g.y[row * g.ldy + on] = hreg;
@@ -186,6 +188,7 @@ template <int NC>
 __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
+  __shared__ unsigned tb_lds;
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
   if (cs.chain >= a.nchains) return;  // idle slot of the placement grid
@@ -197,7 +200,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
-  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds);
+  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 wh[NC], wzr[2 * NC];
   load_wfrag(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
@@ -231,13 +235,13 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   };
 
   const int tl = g.reverse ? 0 : L - 1;
-  gate(tl, live ? g.dy[((long)ob * L + tl) * g.lddy + ok_] : 0.f, 1u, 0, live);
+  gate(tl, live ? g.dy[((long)ob * L + tl) * g.lddy + ok_] : 0.f, tb + 1u, 0, live);
 
   for (int p = 0; p < L; ++p) {
     const int s = L - 1 - p;
     const int t = g.reverse ? L - 1 - s : s;
     const long row = (long)ob * L + t;
-    const unsigned tag = (unsigned)(p + 1);
+    const unsigned tag = tb + p + 1;
     const int sl = p & 1;
     // ---- p1: dq = Uh^T da_h -> da_r, partial dh_{t-1}
     float z = 0.f, r = 0.f, hp = 0.f, dyv = 0.f;
@@ -366,7 +370,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
-  S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(f.B, f.H), st));
+  S2S_TRY(launch_sync_prep(st, sync, gru_persist_sync_bytes(f.B, f.H)));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
   return launch(st, a, f.ndir, true);
@@ -383,7 +387,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
-  S2S_CHECK_HIP(hipMemsetAsync(sync, 0, gru_persist_sync_bytes(b.B, b.H), st));
+  S2S_TRY(launch_sync_prep(st, sync, gru_persist_sync_bytes(b.B, b.H)));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);

@@ -7,6 +7,8 @@
 #pragma once
 #include "s2s_common.h"
 
+#include <algorithm>
+
 namespace s2s {
 
 constexpr unsigned kSpinLimit = 1u << 21;
@@ -78,6 +80,49 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
   return false;
 }
 
+// ---- launch epochs
+// Granule tags are (epoch << 16) + step, with a fresh epoch per launch: granules a previous launch
+// left at the same addresses (same steps, so the same step tags) can never satisfy a wait, even if
+// a cache still holds them (measured: without epochs a repeated decoder launch with new weights
+// consumed the previous launch's values).  sync_prep (one launch replacing the memset) zeroes the
+// granule region past the 256-byte header and, in block 0, draws the epoch from a device counter
+// and resets the abort word -- both with memory-side atomics; every workgroup reads the epoch with
+// a memory-side atomic too (launch_tagbase).
+constexpr int kEpochWord = 16;  // u32 index of the epoch in the sync header (byte 64; abort word at 0)
+static __device__ unsigned g_s2s_epoch_ctr;
+static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    unsigned* hdr = reinterpret_cast<unsigned*>(sync);
+    const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const size_t n16 = (bytes - 256) / 16;
+  uint4* p = reinterpret_cast<uint4*>(sync + 256);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+}
+inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes) {
+  // bytes - 256 is a multiple of 8 (granules) and of 4 (census words); round the tail up is not
+  // allowed, so clear the last partial 16-byte piece with the memset only when present
+  const size_t n16 = (bytes - 256) / 16;
+  int blocks = (int)std::min<size_t>(1024, (n16 + 255) / 256);
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes);
+  if ((bytes - 256) % 16)
+    S2S_CHECK_HIP(hipMemsetAsync(static_cast<char*>(sync) + 256 + n16 * 16, 0, (bytes - 256) % 16, st));
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// tag base of this launch (all threads call; one barrier)
+__device__ __forceinline__ unsigned launch_tagbase(const unsigned* sync_hdr, unsigned* lds) {
+  if (threadIdx.x == 0)
+    *lds = __hip_atomic_fetch_add(const_cast<unsigned*>(sync_hdr) + kEpochWord, 0u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return (*lds & 0xffffu) << 16;
+}
+
 // ---- XCD-local chains
 // A chain = the workgroups that hand data to each other (independent of other chains).  Launches
 // place chain c's members at blockIdx = 8 * (member + nmem * (c / 8)) + c % 8, which the MI355X
@@ -95,8 +140,8 @@ __device__ __forceinline__ ChainSlot chain_slot(int nmem) {
 __host__ __device__ constexpr int chain_grid(int nchains, int nmem) { return 8 * nmem * ((nchains + 7) / 8); }
 // census: zeroed u32 per (chain, member); flag: a __shared__ int; all 256 threads call it
 __device__ __forceinline__ bool chain_is_local(unsigned* census, int chain, int nmem, int member, bool allow,
-                                               unsigned* abort_word, int* flag) {
-  const unsigned me = 0x100u | (__builtin_amdgcn_s_getreg(kXccIdHwreg) & 15u);
+                                               unsigned* abort_word, int* flag, unsigned tb) {
+  const unsigned me = tb | 0x100u | (__builtin_amdgcn_s_getreg(kXccIdHwreg) & 15u);
   unsigned* row = census + (long)chain * nmem;
   if (threadIdx.x == 0) {
     *flag = allow ? 1 : 0;
@@ -105,7 +150,8 @@ __device__ __forceinline__ bool chain_is_local(unsigned* census, int chain, int 
   __syncthreads();
   if ((int)threadIdx.x < nmem) {
     unsigned spins = 0, v;
-    while (((v = __hip_atomic_load(row + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0x100u) == 0u)
+    while (((v = __hip_atomic_load(row + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) & 0xffff0100u) !=
+           (tb | 0x100u))
       if (spin_give_up(spins, abort_word)) break;
     if (v != me) *flag = 0;
   }

@@ -29,6 +29,7 @@ int s2s_attn_bwd(s2s_ctx*, void* stream, const s2s_attn_dims* d, const float* h,
                  const float* const* params, const void* saved, const float* dlogp, float* dh, int dh_accumulate,
                  float* const* grads, float scale, void* scratch, size_t scratch_bytes);
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
+const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 int s2s_nll_seed(s2s_ctx*, void* stream, int B, int T, int O, const float* logp, const int* labels, int normalize,
                  float* nll, float* dlogp);
 int s2s_comm_unique_id(void* out_bytes);

@@ -55,6 +55,7 @@ SIGNATURES = [
     ("s2s_attn_bwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,
                              c_void_p, c_void_p, c_int, P(c_void_p), c_float, c_void_p, c_size_t]),
     ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_mono_ind", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                              c_void_p]),
     ("s2s_model_param_count", c_size_t, [P(s2s_model_dims)]),

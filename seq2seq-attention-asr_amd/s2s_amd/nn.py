@@ -392,6 +392,15 @@ class Attention(Module):
     def accGradParameters(self, input, gradOutput, scale=1.0):
         pass
 
+    def mono_ind(self):
+        """(B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward
+        (MonotonicAlignment.lua:27-39): the discrete decision its backward (:44-77) depends on."""
+        d = self._d
+        p = lib.s2s_attn_mono_ind(ctypes.byref(d), dptr(self._saved))
+        off = p - self._saved.data_ptr()
+        n = d.B * d.T
+        return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T)
+
     def alpha(self):
         """Attention:alpha() (Attention.lua:241-243): (B, T, L) attention weights of the last forward."""
         d = self._d
