@@ -22,7 +22,9 @@ def profile_step(model, x, labels, stream, reps=3):
     """Eager (un-captured) training steps with event timing on; returns per-family aggregates
     averaged over `reps` steps."""
     graph_ctx = model.ctx
-    model.ctx = Context(model.device.index, graph=False)
+    # same stream layout as the timed steps (weight-gradient GEMMs on the side stream), eager so the
+    # library can bracket every launch with events
+    model.ctx = Context(model.device.index, graph=False, overlap=True)
     try:
         model.step(x, labels, stream=stream)  # warm
         stream.synchronize()
