@@ -214,17 +214,27 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   float dhc = 0.f, dhp = 0.f;
   bool aborted = false;
 
+  // saved activations of one step for this thread's (utterance, unit): loaded one step ahead, while
+  // the previous hand-off is in flight, so no dependent global load sits on the recurrence
+  struct Row {
+    float z, r, hh, hp, dy;
+  };
+  auto load_row = [&](int t) {
+    Row v{0.f, 0.f, 0.f, 0.f, 0.f};
+    if (live) {
+      const long row = (long)ob * L + t;
+      const float* sv = g.sv + row * 5 * H;
+      v.z = sv[ok_]; v.r = sv[H + ok_]; v.hh = sv[2 * H + ok_]; v.hp = sv[3 * H + ok_];
+      v.dy = g.dy[row * g.lddy + ok_];
+    }
+    return v;
+  };
   // gate gradients of dh = dy_t + carry at time t (rows that are live), published with epoch `tag`
   // into slot `sl` when `pub`; every lane of the workgroup calls it (pair stores)
-  auto gate = [&](int t, float dh, unsigned tag, int sl, bool pub) {
+  auto gate = [&](int t, const Row& v, float dh, unsigned tag, int sl, bool pub) {
     const long row = (long)ob * L + t;
-    float z = 0.f, hh = 0.f, hp = 0.f;
-    if (pub) {
-      const float* sv = g.sv + row * 5 * H;
-      z = sv[ok_]; hh = sv[2 * H + ok_]; hp = sv[3 * H + ok_];
-    }
-    const float daz = dh * (hh - hp) * (z * (1.0f - z));
-    const float dah = (dh * z) * (1.0f - hh * hh);
+    const float daz = dh * (v.hh - v.hp) * (v.z * (1.0f - v.z));
+    const float dah = (dh * v.z) * (1.0f - v.hh * v.hh);
     const long off = sl * slot + (long)ob * H + ok_;
     put_granule_pair(g.g2, off, dah, tag, pub, loc);  // da_h gates the next p1: first
     put_granule_pair(g.g0, off, daz, tag, pub, loc);
@@ -235,7 +245,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   };
 
   const int tl = g.reverse ? 0 : L - 1;
-  gate(tl, live ? g.dy[((long)ob * L + tl) * g.lddy + ok_] : 0.f, tb + 1u, 0, live);
+  Row cur = load_row(tl);
+  gate(tl, cur, cur.dy, tb + 1u, 0, live);
 
   for (int p = 0; p < L; ++p) {
     const int s = L - 1 - p;
@@ -244,12 +255,6 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     const unsigned tag = tb + p + 1;
     const int sl = p & 1;
     // ---- p1: dq = Uh^T da_h -> da_r, partial dh_{t-1}
-    float z = 0.f, r = 0.f, hp = 0.f, dyv = 0.f;
-    if (live) {
-      const float* sv = g.sv + row * 5 * H;
-      z = sv[ok_]; r = sv[H + ok_]; hp = sv[3 * H + ok_];
-      dyv = g.dy[row * g.lddy + ok_];
-    }
     float4 av[NC];
     GRU_STAMP(0);
     bool ok = sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
@@ -257,17 +262,17 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * hp) * (r * (1.0f - r)), tag, live, loc);
+    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)), tag, live, loc);
     if (live) {
-      const float dar = (dq * hp) * (r * (1.0f - r));
+      const float dar = (dq * cur.hp) * (cur.r * (1.0f - cur.r));
       g.dA[row * g.ldA + H + ok_] = dar;
-      const float dh = dyv + dhc;
-      dhp = dh * (-z + 1.0f) + dq * r;
+      const float dh = cur.dy + dhc;
+      dhp = dh * (-cur.z + 1.0f) + dq * cur.r;
     }
     GRU_STAMP(2);
     // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
     const int tn = g.reverse ? t + 1 : t - 1;
-    const float dyn = (live && s > 0) ? g.dy[((long)ob * L + tn) * g.lddy + ok_] : 0.f;
+    const Row nxt = s > 0 ? load_row(tn) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     float4 azr[2 * NC];
     GRU_STAMP(3);
     {
@@ -285,7 +290,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
     if (live && s > 0) dhc = dhp + sm;
-    if (s > 0) gate(tn, dyn + dhc, tag + 1, sl ^ 1, live);
+    if (s > 0) gate(tn, nxt, nxt.dy + dhc, tag + 1, sl ^ 1, live);
+    cur = nxt;
     GRU_STAMP(5);
   }
 }
