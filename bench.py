@@ -26,6 +26,8 @@ CONFIGS = {
     # name: (model kwargs, B per GPU, L, T)
     "timit_chorowski_b32": (dict(), 32, 128, 40),
     "librispeech_chorowski_b32": (dict(inputFrameSize=80, outputDepth=29), 32, 400, 200),
+    # BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64 (fp32 here)
+    "timit_chorowski_dropout_b64": (dict(dropout=0.5), 64, 128, 40),
 }
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec

@@ -96,10 +96,18 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
  *   8 Wd (S, 2S) 9 bd (S)     10 Wz (S, 2S) 11 Wr (S, 2S) 12 Wh (S, 2S)   [decoder GRU]
  *  13 Wm (M*K, S+A) 14 bm (M*K)   15 Wo (O, M) 16 bo (O)                                     */
 #define S2S_ATTN_NPARAMS 17
+/* dropout: nn.Dropout(p) in front of the Maxout of the decoder MLP (timit/model_chorowski_baseline_
+ * dropout.lua:56), Torch7 semantics in training mode: [s_t; c_t] * mask, mask = Bernoulli(1-p)/(1-p).
+ * p = 0: no dropout.  dropout_mask: optional (B, T, S+A) multipliers (scaling included) used as given
+ * (parity with an external RNG); NULL: drawn in-kernel from dropout_seed (counter-based, so a seed
+ * reproduces the masks for any launch geometry).  The masks stay in `saved` for the backward. */
 typedef struct {
   int B, L, T;
   int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
   float penalty;
+  float dropout;
+  unsigned long long dropout_seed;
+  const float* dropout_mask;
 } s2s_attn_dims;
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
@@ -115,6 +123,8 @@ const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
 /* (B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward (MonotonicAlignment.lua:
  * 27-39): the discrete decision behind the penalty gradient (MonotonicAlignment.lua:44-77). */
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
+/* (B, T, S+A) dropout multipliers of the last forward inside `saved` (NULL when dropout == 0) */
+const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
 
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
@@ -132,6 +142,9 @@ typedef struct {
   int inputFrameSize, hiddenFrameSize, outputFrameSize, numLayers;
   int scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
   float penalty;
+  float dropout;                   /* as in s2s_attn_dims (model_chorowski_baseline_dropout.lua) */
+  unsigned long long dropout_seed;
+  const float* dropout_mask;
 } s2s_model_dims;
 #define S2S_ZERO_GRADS 1
 #define S2S_NORMALIZE_NLL 2

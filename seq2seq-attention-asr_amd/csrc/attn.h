@@ -17,6 +17,9 @@ struct AttnDims {
   int M;   // mlpDepth
   int K;   // maxout window
   float penalty;
+  float dropout = 0.f;                    // nn.Dropout(p) before the Maxout (0 = none)
+  unsigned long long dropout_seed = 0;
+  const float* dropout_mask = nullptr;    // injected (B, T, S+A) multipliers, or null
 };
 struct AttnParams {
   const float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
@@ -48,6 +51,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
+const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved);
 
 // -log p of the labels and the reference's seed dlogp = -labelmask (timit/timit.lua:262-282).
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,

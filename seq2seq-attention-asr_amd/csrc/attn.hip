@@ -40,7 +40,7 @@ struct AttnK {
   const float* h;
   const int* labels;
   // saved
-  float *Vh, *WS, *E, *ALPHA, *LSE, *IND, *C, *HX, *RHX, *CY, *GSV, *VV, *MM, *LOGP;
+  float *Vh, *WS, *E, *ALPHA, *LSE, *IND, *C, *HX, *RHX, *CY, *GSV, *VV, *MM, *LOGP, *MASK;
   int* AM;
   // fwd scratch
   float *PM, *PL, *PC, *U;
@@ -136,6 +136,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* MM = sv.take<float>(BT * M);
   int* AM = sv.take<int>(BT * M);
   float* LOGP = sv.take<float>(BT * O);
+  float* MASK = d.dropout > 0.f ? sv.take<float>(BT * (S + A)) : nullptr;
   float* WX = sv.take<float>(3 * S * A);
   float* WXT = sv.take<float>(3 * S * A);
   float* WXD = sv.take<float>(3 * S * S);
@@ -220,6 +221,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   if (k) {
     k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
     k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
+    k->MASK = MASK;
     k->Vh = Vh; k->WS = WS; k->E = E; k->ALPHA = ALPHA; k->LSE = LSE; k->IND = IND; k->C = C; k->HX = HX;
     k->RHX = RHX; k->CY = CY; k->GSV = GSV; k->VV = VV; k->MM = MM; k->AM = AM; k->LOGP = LOGP;
     k->PM = PM; k->PL = PL; k->PC = PC; k->U = U;
@@ -741,6 +743,37 @@ __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const in
   }
 }
 
+// nn.Dropout(p) (Torch7, training mode) on the decoder MLP input [s_t; c_t]
+// (timit/model_chorowski_baseline_dropout.lua:56): MASK = injected multipliers, or Bernoulli(1-p)/(1-p)
+// from a counter-based hash of (seed, element) -- any launch geometry draws the same mask -- and
+// VV *= MASK.  The backward multiplies dVV by the same MASK (dec_dropout_bwd).
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ void dec_dropout_fwd(AttnK k, float p, unsigned long long seed, const float* inj) {
+  const long n = (long)k.B * k.T * (k.S + k.A);
+  const float keep = 1.0f / (1.0f - p);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    float m;
+    if (inj) {
+      m = inj[i];
+    } else {
+      const unsigned long long h = mix64(seed * 0x9e3779b97f4a7c15ull + (unsigned long long)i);
+      const float u = (float)(h >> 40) * (1.0f / 16777216.0f);  // [0, 1)
+      m = u >= p ? keep : 0.f;
+    }
+    k.MASK[i] = m;
+    k.VV[i] = k.VV[i] * m;
+  }
+}
+__global__ void dec_dropout_bwd(AttnK k) {
+  const long n = (long)k.B * k.T * (k.S + k.A);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x)
+    k.DV[i] = k.DV[i] * k.MASK[i];
+}
+
 #include "attn_persist.inc"
 #include "dec_xcd.inc"
 
@@ -751,6 +784,7 @@ int attn_check_dims(const AttnDims& d) {
   S2S_REQUIRE(d.S % 16 == 0 && d.A % 16 == 0 && d.Sc % 16 == 0, "attn: S, A, scoreDepth must be multiples of 16");
   S2S_REQUIRE(d.Sc <= 1024, "attn: scoreDepth > 1024 not supported");
   S2S_REQUIRE(d.O > 0 && d.M > 0 && d.K > 0, "attn: bad output/mlp dims");
+  S2S_REQUIRE(d.dropout >= 0.f && d.dropout < 1.f, "attn: dropout must be in [0, 1)");
   return 0;
 }
 
@@ -773,6 +807,11 @@ const float* attn_saved_mono_ind(const AttnDims& d, const void* saved) {
   AttnK k{};
   carve(d, &k, (char*)saved, nullptr);
   return k.IND;
+}
+const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.MASK;
 }
 
 // S2S_DEC_MODE=step forces the per-step launch path (A/B and fallback); default: the persistent
@@ -958,6 +997,10 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   }
   // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
   const int rows = B * T;
+  if (d.dropout > 0.f) {
+    hipLaunchKernelGGL(dec_dropout_fwd, dim3(512), dim3(256), 0, st, k, d.dropout, d.dropout_seed, d.dropout_mask);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
   S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
                 (long)d.M * d.K, P.bm, gws));
   hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
@@ -1006,6 +1049,10 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A, nullptr, gws));
+  if (d.dropout > 0.f) {
+    hipLaunchKernelGGL(dec_dropout_bwd, dim3(512), dim3(256), 0, st, k);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
   const int pgrid = kDecWG * ((B + 15) / 16);
   const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pb = pvar ? pick_dec_bwd(pvar, d, pgrid) : PersistLaunch{};

@@ -105,7 +105,7 @@ int set_device(s2s_ctx* ctx) {
 
 AttnDims to_attn(const s2s_attn_dims* d) {
   return AttnDims{d->B, d->L, d->T, d->annotationDepth, d->scoreDepth, d->stateDepth, d->outputDepth, d->mlpDepth,
-                  d->maxoutWindow, d->penalty};
+                  d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
 }
 
 // ------------------------------------------------------------ model layout
@@ -124,7 +124,7 @@ std::vector<LayerDims> enc_layers(const s2s_model_dims* d) {
 }
 AttnDims model_attn(const s2s_model_dims* d) {
   return AttnDims{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
-                  d->mlpDepth, d->maxoutWindow, d->penalty};
+                  d->mlpDepth, d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
 }
 std::vector<long> param_sizes(const s2s_model_dims* d) {
   std::vector<long> s;
@@ -529,6 +529,9 @@ const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved) {
 }
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_mono_ind(to_attn(d), saved) : nullptr;
+}
+const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_dropout_mask(to_attn(d), saved) : nullptr;
 }
 
 int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,

@@ -18,13 +18,15 @@ P = ctypes.POINTER
 class s2s_attn_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("annotationDepth", c_int), ("scoreDepth", c_int),
                 ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
-                ("penalty", c_float)]
+                ("penalty", c_float), ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong),
+                ("dropout_mask", c_void_p)]
 
 
 class s2s_model_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("inputFrameSize", c_int), ("hiddenFrameSize", c_int),
                 ("outputFrameSize", c_int), ("numLayers", c_int), ("scoreDepth", c_int), ("stateDepth", c_int),
-                ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int), ("penalty", c_float)]
+                ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int), ("penalty", c_float),
+                ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong), ("dropout_mask", c_void_p)]
 
 
 # every symbol include/s2s_hip.h declares: (name, restype, argtypes)
@@ -56,6 +58,7 @@ SIGNATURES = [
                              c_void_p, c_void_p, c_int, P(c_void_p), c_float, c_void_p, c_size_t]),
     ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mono_ind", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_dropout_mask", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                              c_void_p]),
     ("s2s_model_param_count", c_size_t, [P(s2s_model_dims)]),

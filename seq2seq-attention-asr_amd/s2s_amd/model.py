@@ -27,6 +27,7 @@ class ModelConfig:
     maxoutWindow: int = 7
     penalty: float = 0.0
     numLayers: int = 3
+    dropout: float = 0.0         # opt.dropout of model_chorowski_baseline_dropout.lua (0: the baseline model)
 
     @property
     def annotationDepth(self):
@@ -39,7 +40,8 @@ class ModelConfig:
                    outputFrameSize=opt.get("outputFrameSize", 256), scoreDepth=opt.get("scoreDepth", 512),
                    stateDepth=opt.get("stateDepth", 256),
                    outputDepth=opt.get("numPhonemes", opt.get("outputDepth", 62)),
-                   mlpDepth=opt.get("mlpDepth", 64), penalty=opt.get("penalty", 0.0))
+                   mlpDepth=opt.get("mlpDepth", 64), penalty=opt.get("penalty", 0.0),
+                   dropout=opt.get("dropout", 0.0))
 
 
 def param_shapes(cfg: ModelConfig):
@@ -95,12 +97,22 @@ class ChorowskiBaseline:
         else:
             self.ctx = get_context(self.device.index)
         self._ws = {}
+        self.train = True
+        self._steps = 0
         self._check_layout()
 
     def dims(self, B, L, T):
         c = self.cfg
+        p = c.dropout if self.train else 0.0
         return _lib.s2s_model_dims(B, L, T, c.inputFrameSize, c.hiddenFrameSize, c.outputFrameSize, c.numLayers,
-                                   c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty)
+                                   c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty, p)
+
+    def training(self):
+        self.train = True
+
+    def evaluate(self):
+        """nn.Dropout's evaluate() mode: the decoder MLP input passes unscaled."""
+        self.train = False
 
     def _check_layout(self):
         d = self.dims(1, 1, 1)
@@ -125,7 +137,7 @@ class ChorowskiBaseline:
         return out
 
     def workspace(self, B, L, T):
-        key = (B, L, T)
+        key = (B, L, T, self.cfg.dropout > 0 and self.train)
         if key not in self._ws:
             d = self.dims(B, L, T)
             nbytes = lib.s2s_model_workspace_bytes(ctypes.byref(d))
@@ -134,9 +146,13 @@ class ChorowskiBaseline:
             self._ws[key] = _bytes(nbytes, self.device)
         return self._ws[key]
 
-    def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None):
+    def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None,
+             dropout_seed=None, dropout_mask=None):
         """One training-step gradient (timit/timit.lua:240-295): grads (+)= scale * d(sum_b nll_b)/dparams,
-        scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O))."""
+        scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O)).
+        With cfg.dropout > 0 (training mode) the decoder MLP input is dropped out with masks drawn
+        in-kernel from dropout_seed (default: a per-step counter) or given as dropout_mask
+        (B, T, S+A) multipliers."""
         if x.dim() == 2:
             x = x[None]
         if labels.dim() == 1:
@@ -156,6 +172,15 @@ class ChorowskiBaseline:
             nll = torch.empty(B, device=self.device, dtype=torch.float32)
         ws = self.workspace(B, L, T)
         d = self.dims(B, L, T)
+        self._steps += 1
+        if d.dropout > 0:
+            d.dropout_seed = self._steps if dropout_seed is None else int(dropout_seed)
+            if dropout_mask is not None:
+                S, A = self.cfg.stateDepth, self.cfg.annotationDepth
+                if dropout_mask.shape != (B, T, S + A) or dropout_mask.dtype != torch.float32:
+                    raise ValueError("dropout_mask must be float32 (B, T, stateDepth + annotationDepth)")
+                self._mask_keep = dropout_mask.contiguous()
+                d.dropout_mask = self._mask_keep.data_ptr()
         flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
         check(lib.s2s_model_step(self.ctx.handle, st, ctypes.byref(d), dptr(self.params), dptr(self.grads), dptr(x),
@@ -166,7 +191,7 @@ class ChorowskiBaseline:
     def encoder_output(self):
         B, L, T = self._last
         d = self.dims(B, L, T)
-        ws = self._ws[(B, L, T)]
+        ws = self._ws[(B, L, T, self.cfg.dropout > 0 and self.train)]
         p = lib.s2s_model_encoder_output(ctypes.byref(d), dptr(ws))
         off = p - ws.data_ptr()
         n = B * L * self.cfg.annotationDepth

@@ -272,13 +272,17 @@ class BiRNN(_GruSeq):
 
 class MaxoutMLP(Module):
     """decoder_mlp of timit/model_chorowski_baseline.lua:53-59:
-    Maxout(inDim, mlpDepth, window) -> Linear(mlpDepth, outputDepth) -> LogSoftMax.
+    [Dropout(p) ->] Maxout(inDim, mlpDepth, window) -> Linear(mlpDepth, outputDepth) -> LogSoftMax.
     Maxout = Linear(in, out*window) + TemporalMaxPooling(window, window) over consecutive groups
-    (Maxout.lua:14-18)."""
+    (Maxout.lua:14-18); dropout > 0 is timit/model_chorowski_baseline_dropout.lua:56 (Torch7
+    nn.Dropout: training mode scales kept inputs by 1/(1-p), evaluate() is the identity)."""
 
-    def __init__(self, inputDimension, mlpDepth, window, outputDepth, generator=None):
+    def __init__(self, inputDimension, mlpDepth, window, outputDepth, generator=None, dropout=0.0):
         super().__init__()
         self.inputDim, self.mlpDepth, self.window, self.outputDepth = inputDimension, mlpDepth, window, outputDepth
+        if not 0.0 <= dropout < 1.0:
+            raise S2SArgumentError("dropout must be in [0, 1)")
+        self.dropout = float(dropout)
         s1 = 1.0 / math.sqrt(inputDimension)
         s2 = 1.0 / math.sqrt(mlpDepth)
         self.weight = [_uniform((mlpDepth * window, inputDimension), s1, generator),
@@ -337,11 +341,37 @@ class Attention(Module):
     def parameters(self):
         return self._tensors(False), self._tensors(True)
 
+    # dropout: injected (B, T, S+A) multipliers for the next forward (parity with an external RNG),
+    # else drawn in-kernel from dropout_seed + the forward count
+    dropout_mask = None
+    dropout_seed = 0x5eed
+
     def _dims(self, h, T):
         B, L = (1, h.shape[0]) if h.dim() == 2 else (h.shape[0], h.shape[1])
         m = self.decoder_mlp
-        return _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
-                                  m.mlpDepth, m.window, self.penalty)
+        p = m.dropout if (m.dropout > 0 and self.train) else 0.0
+        d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
+                               m.mlpDepth, m.window, self.penalty, p)
+        if p > 0:
+            self._fwd_count = getattr(self, "_fwd_count", 0) + 1
+            d.dropout_seed = (self.dropout_seed * 1000003 + self._fwd_count) & ((1 << 64) - 1)
+            if self.dropout_mask is not None:
+                msk = self.dropout_mask
+                if msk.shape != (B, T, self.stateDepth + self.annotationDepth) or msk.dtype != torch.float32:
+                    raise S2SArgumentError("dropout_mask must be float32 (B, T, stateDepth + annotationDepth)")
+                self._mask_keep = msk.contiguous()
+                d.dropout_mask = self._mask_keep.data_ptr()
+        return d
+
+    def dropout_mask_used(self):
+        """(B, T, S+A) dropout multipliers of the last forward (inside the saved buffer)."""
+        d = self._d
+        if d.dropout <= 0:
+            return None
+        p = lib.s2s_attn_dropout_mask(ctypes.byref(d), dptr(self._saved))
+        off = p - self._saved.data_ptr()
+        n = d.B * d.T * (self.stateDepth + self.annotationDepth)
+        return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T, -1)
 
     @staticmethod
     def labels_from(y, O):

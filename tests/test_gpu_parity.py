@@ -212,6 +212,72 @@ def _adopt_mono_decisions(att, cache, L, margin=1e-4):
     cache["mono_ind"] = gi
 
 
+@pytest.mark.parametrize("injected", [True, False])
+def test_attention_dropout_matches_oracle(s2s, injected):
+    """Decoder MLP with nn.Dropout(p) in front (timit/model_chorowski_baseline_dropout.lua:56):
+    injected masks, or masks drawn in-kernel (Bernoulli(1-p)/(1-p) statistics checked, then the
+    oracle run with the mask the GPU used)."""
+    B, L, T, A, Sc, S, O, M, K, p = 32, 128, 12, 512, 512, 256, 62, 8, 7, 0.5
+    rng = np.random.default_rng(17)
+    torch.manual_seed(17)
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=K, numLayers=1)
+    att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, M, K, O, dropout=p), Sc, 10, 0, S, A, O, True,
+                        0.0).cuda()
+    P = {n: t.cpu().double().numpy() for n, t in zip(
+        ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "dec.Wz", "dec.Wr", "dec.Wh", "Wm", "bm", "Wo",
+         "bo"), att.parameters()[0])}
+    h = rng.standard_normal((B, L, A)) * 0.5
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    if injected:
+        mask = (rng.random((B, T, S + A)) >= p) / (1.0 - p)
+        att.dropout_mask = cu(mask)
+    logp = att.forward([cu(h), cu(labels, torch.int32)]).cpu().numpy()
+    used = att.dropout_mask_used().cpu().double().numpy()
+    if injected:
+        assert np.array_equal(used, mask.astype(np.float32).astype(np.float64))
+    else:
+        vals = np.unique(used)
+        assert set(vals.tolist()) <= {0.0, float(np.float32(1.0 / (1.0 - p)))}, vals[:5]
+        assert abs((used == 0).mean() - p) < 0.01
+        mask = used
+    lref, cache = orc.attention_fwd(h, labels, P, cfg, mask)
+    assert_rel(logp, lref, "logp")
+    dlogp = rng.standard_normal(logp.shape)
+    att.zeroGradParameters()
+    dh = att.backward([cu(h), None], cu(dlogp), 1.0)[0].cpu().numpy()
+    G = orc.zeros_like_params(P)
+    dhr = orc.attention_bwd(P, cfg, cache, dlogp, G, 1.0, mask)
+    assert_rel(dh, dhr, "dh")
+    for name, g in zip(P.keys(), att.parameters()[1]):
+        assert_rel(g.cpu().numpy(), G[name], "d" + name)
+    # evaluate(): nn.Dropout is the identity
+    att.evaluate()
+    logp_eval = att.forward([cu(h), cu(labels, torch.int32)]).cpu().numpy()
+    lref0, _ = orc.attention_fwd(h, labels, P, cfg)
+    assert_rel(logp_eval, lref0, "logp (evaluate)")
+
+
+def test_model_step_dropout_config3(s2s):
+    """BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64, injected
+    masks (L, T reduced so the float64 oracle stays in seconds)."""
+    kw = dict(dropout=0.5)
+    B, L, T = 64, 48, 16
+    cfg_o = orc.ModelConfig()
+    model = s2s.ChorowskiBaseline(s2s.ModelConfig(**kw))
+    P = orc.unflatten(model.params.cpu().double().numpy(), cfg_o)
+    x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=3, pad=10, eos=23)
+    rng = np.random.default_rng(4)
+    mask = (rng.random((B, T, cfg_o.stateDepth + 2 * cfg_o.outputFrameSize)) >= 0.5) / 0.5
+    nll, logp = model.step(cu(x), cu(labels, torch.int32), dropout_mask=cu(mask))
+    torch.cuda.synchronize()
+    nll_ref, G, lref, enc = orc.training_step(x, labels, P, cfg_o, dropout_mask=mask)
+    assert_rel(logp.cpu().numpy(), lref, "logp")
+    Gg = orc.unflatten(model.grads.cpu().double().numpy(), cfg_o)
+    for k in G:
+        assert_rel(Gg[k], G[k], "grad " + k)
+
+
 def test_labelmask_input_equals_int_labels(s2s):
     rng = np.random.default_rng(5)
     B, L, T, A, Sc, S, O = 2, 12, 4, 32, 32, 16, 9
