@@ -29,6 +29,11 @@ CONFIGS = {
     # BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64 (fp32 here)
     "timit_chorowski_dropout_b64": (dict(dropout=0.5), 64, 128, 40),
 }
+CONFIG_DESC = {
+    "timit_chorowski_b32": ("BASELINE config 2", "timit/model_chorowski_baseline.lua"),
+    "librispeech_chorowski_b32": ("BASELINE config 4 shape (1 GPU)", "librispeech/model_chorowski_baseline.lua"),
+    "timit_chorowski_dropout_b64": ("BASELINE config 3 (fp32)", "timit/model_chorowski_baseline_dropout.lua"),
+}
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -220,7 +225,7 @@ def main():
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp32", "data": "synthetic (N(0,1) log-mel-shaped features, uniform labels, random-init weights)",
-        "config": {"workload": f"BASELINE config 2: {args.config}", "model": "timit/model_chorowski_baseline.lua",
+        "config": {"workload": f"{CONFIG_DESC[args.config][0]}: {args.config}", "model": CONFIG_DESC[args.config][1],
                    "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
                    "feat_dim": cfg.inputFrameSize, "parallelism": f"dp{world}",
                    "launch": "eager" if args.no_graph else "hipGraph replay",
