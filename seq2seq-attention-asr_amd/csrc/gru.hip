@@ -249,7 +249,7 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   }
   bp.take<float>(3L * ndir * H * ((D + 31) / 32 * 32));  // Wx (both dirs, rows padded)
   bp.take<float>((long)B * L * 3 * ndir * H);    // xp or dA (both dirs)
-  bp.take<char>(gru_persist_sync_bytes(B, H));   // persistent-kernel granule buffers
+  bp.take<char>(gru_persist_sync_bytes(B, L, H));   // persistent-kernel granule buffers
   bp.take<float>(kGemmWsFloats);                 // split-K slabs of this layer's GEMMs
   return bp.off + 256;
 }
@@ -343,7 +343,7 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   S2S_REQUIRE(Kx <= (D + 31) / 32 * 32 && io.ldx >= Kx, "gru: Dx must be <= round_up(D, 32) and <= ldx");
   float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* xp = bp.take<float>((long)B * L * 3 * nd * H);
-  char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
+  char* sync = bp.take<char>(gru_persist_sync_bytes(B, L, H));
   if (io.packed) {
     const PackView v = pack_view(io.packed, nd, H);
     for (int d = 0; d < nd; ++d) {
@@ -406,7 +406,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* dA_int = bp.take<float>((long)B * L * 3 * nd * H);
   float* dA = dA_ext ? dA_ext : dA_int;
-  char* sync = bp.take<char>(gru_persist_sync_bytes(B, H));
+  char* sync = bp.take<char>(gru_persist_sync_bytes(B, L, H));
   const long ldA = 3L * nd * H;
   if (io.packed) {
     const PackView v = pack_view(io.packed, nd, H);

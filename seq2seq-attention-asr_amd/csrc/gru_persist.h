@@ -30,7 +30,7 @@ bool gru_persist_supported(int ndir, int B, int H);
 // 1 = persistent GRU launches reserve their CU (see kExclLds); set around a step whose weight-gradient
 // GEMMs run on a side stream
 void gru_persist_set_exclusive(int on);
-size_t gru_persist_sync_bytes(int B, int H);
+size_t gru_persist_sync_bytes(int B, int L, int H);
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync);
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync);
 

@@ -45,6 +45,10 @@ struct PDir {
   granule_t* g0;  // fwd: h      bwd: da_z
   granule_t* g1;  // fwd: q      bwd: da_r
   granule_t* g2;  //             bwd: da_h
+  // sentinel rows (XCD-local chains), each [L slots][B][H] floats, same roles as g0..g2
+  float* s0;
+  float* s1;
+  float* s2;
 };
 struct PArgs {
   PDir d[2];
@@ -96,13 +100,17 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  {
+    float* mine = isz ? g.s0 : g.s1;  // z tiles publish h, r tiles q
+    rearm_sent(&mine, 1, (long)B * H, L, B, H, mt * 16, isz ? c1 * 16 : c1 * 16 - H);
+  }
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 w1[NC], w2[NC];
   load_wfrag(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
   if (isz) load_wfrag(w2, g.Wb + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
 
-  const __amdgpu_buffer_rsrc_t hg = rsrc_of(g.g0), qg = rsrc_of(g.g1);
+  const __amdgpu_buffer_rsrc_t hg = rsrc_of(g.g0), qg = rsrc_of(g.g1), hs = rsrc_of(g.s0), qs = rsrc_of(g.s1);
   const long slot = (long)B * H;  // granules per slot
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), on = c1 * 16 + (tid & 15);  // this thread's output
@@ -122,7 +130,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(0);
     if (s > 0) {
       float4 av[NC];
-      ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
+      if (loc) ok = sweep_sent<NC>(av, hs, 4 * ((s - 1) * slot + (long)br * H), wave, lane, a.abort_word);
+      else ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
       GRU_STAMP(1);
       acc = mfma_chunks<NC>(av, w1);
       // r tiles: the swept operand already holds h_{t-1} of this tile's 16 units (chunk it of
@@ -145,7 +154,11 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
         const int j = on - H;
         const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
         const float q = gate * hp;
-        put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live, loc);  // critical first
+        if (loc) {  // critical first
+          if (live) put_sent(g.s1 + s * slot + (long)ob * H + j, q);
+        } else {
+          put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live);
+        }
         if (live) {
           sv[H + j] = gate;
           sv[3 * H + j] = hp;
@@ -162,7 +175,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(3);
     if (s > 0) {
       float4 av[NC];
-      ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
+      if (loc) ok = sweep_sent<NC>(av, qs, 4 * (s * slot + (long)br * H), wave, lane, a.abort_word);
+      else ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
       GRU_STAMP(4);
       acc = mfma_chunks<NC>(av, w2);
     }
@@ -172,7 +186,11 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
       const float hh = tanhf(sum + xph);
       const float hp = hreg;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
-      put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live, loc);  // first
+      if (loc) {  // first
+        if (live) put_sent(g.s0 + s * slot + (long)ob * H + on, hreg);
+      } else {
+        put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live);
+      }
       if (live) {
         g.sv[row * 5 * H + 2 * H + on] = hh;
         g.y[row * g.ldy + on] = hreg;
@@ -201,12 +219,17 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  {
+    float* const mine[3] = {g.s0, g.s1, g.s2};
+    rearm_sent(mine, 3, (long)B * H, L, B, H, mt * 16, c * 16);
+  }
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 wh[NC], wzr[2 * NC];
   load_wfrag(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
   load_wfrag(wzr, g.Wb + (long)(c * 16 + (lane & 15)) * 2 * H, wave, lane);
   const __amdgpu_buffer_rsrc_t zg = rsrc_of(g.g0), rg = rsrc_of(g.g1), hg = rsrc_of(g.g2);
+  const __amdgpu_buffer_rsrc_t zs = rsrc_of(g.s0), rs_ = rsrc_of(g.s1), hs = rsrc_of(g.s2);
   const long slot = (long)B * H;
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), ok_ = c * 16 + (tid & 15);
@@ -229,15 +252,23 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     }
     return v;
   };
-  // gate gradients of dh = dy_t + carry at time t (rows that are live), published with epoch `tag`
-  // into slot `sl` when `pub`; every lane of the workgroup calls it (pair stores)
-  auto gate = [&](int t, const Row& v, float dh, unsigned tag, int sl, bool pub) {
+  // gate gradients of dh = dy_t + carry at time t (rows that are live), published as hand-off
+  // step pn (tag tb + pn + 1, slot pn & 1; sentinel slot pn) when `pub`; every lane calls it
+  auto gate = [&](int t, const Row& v, float dh, int pn, bool pub) {
     const long row = (long)ob * L + t;
     const float daz = dh * (v.hh - v.hp) * (v.z * (1.0f - v.z));
     const float dah = (dh * v.z) * (1.0f - v.hh * v.hh);
-    const long off = sl * slot + (long)ob * H + ok_;
-    put_granule_pair(g.g2, off, dah, tag, pub, loc);  // da_h gates the next p1: first
-    put_granule_pair(g.g0, off, daz, tag, pub, loc);
+    if (loc) {
+      const long off = pn * slot + (long)ob * H + ok_;
+      if (pub) {
+        put_sent(g.s2 + off, dah);  // da_h gates the next p1: first
+        put_sent(g.s0 + off, daz);
+      }
+    } else {
+      const long off = (pn & 1) * slot + (long)ob * H + ok_;
+      put_granule_pair(g.g2, off, dah, tb + pn + 1, pub);
+      put_granule_pair(g.g0, off, daz, tb + pn + 1, pub);
+    }
     if (pub) {
       g.dA[row * g.ldA + ok_] = daz;
       g.dA[row * g.ldA + 2 * H + ok_] = dah;
@@ -246,7 +277,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
 
   const int tl = g.reverse ? 0 : L - 1;
   Row cur = load_row(tl);
-  gate(tl, cur, cur.dy, tb + 1u, 0, live);
+  gate(tl, cur, cur.dy, 0, live);
 
   for (int p = 0; p < L; ++p) {
     const int s = L - 1 - p;
@@ -257,12 +288,17 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     // ---- p1: dq = Uh^T da_h -> da_r, partial dh_{t-1}
     float4 av[NC];
     GRU_STAMP(0);
-    bool ok = sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+    bool ok = loc ? sweep_sent<NC>(av, hs, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word)
+                  : sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
     GRU_STAMP(1);
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)), tag, live, loc);
+    if (loc) {
+      if (live) put_sent(g.s1 + p * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
+    } else {
+      put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)), tag, live);
+    }
     if (live) {
       const float dar = (dq * cur.hp) * (cur.r * (1.0f - cur.r));
       g.dA[row * g.ldA + H + ok_] = dar;
@@ -279,8 +315,13 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
       // da_z (ready since the previous step) first, then poll da_r (this step's p1) alone: a
       // merged poll of both rows re-reads da_z while waiting for da_r (measured slower)
       float4 az[NC], ar[NC];
-      ok = sweep_skinny<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
-      ok = ok && sweep_skinny<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      if (loc) {
+        ok = sweep_sent<NC>(az, zs, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word);
+        ok = ok && sweep_sent<NC>(ar, rs_, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word);
+      } else {
+        ok = sweep_skinny<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+        ok = ok && sweep_skinny<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+      }
       GRU_STAMP(4);
       // chunk i of the K = 2H product: i < NC reads da_z, i >= NC reads da_r (H % 64 == 0)
 #pragma unroll
@@ -290,7 +331,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
     if (live && s > 0) dhc = dhp + sm;
-    if (s > 0) gate(tn, nxt, nxt.dy + dhc, tag + 1, sl ^ 1, live);
+    if (s > 0) gate(tn, nxt, nxt.dy + dhc, p + 1, live);
     cur = nxt;
     GRU_STAMP(5);
   }
@@ -349,12 +390,18 @@ bool gru_persist_supported(int ndir, int B, int H) {
 
 static size_t census_bytes(int B, int H) { return 4 * (size_t)(2 * ((B + 15) / 16)) * (2 * H / 16); }
 
-size_t gru_persist_sync_bytes(int B, int H) {
+// header | tagged granules | census (zeroed by sync_prep every launch) | sentinel rows (re-armed in-kernel)
+static size_t prep_bytes(int B, int H) {
   return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H);
 }
+static size_t sent_offset(int B, int H) { return (prep_bytes(B, H) + 255) / 256 * 256; }
 
-static void carve_granules(char* sync, int B, int H, unsigned** abort_word, granule_t* (&g)[2][3],
-                           unsigned** census) {
+size_t gru_persist_sync_bytes(int B, int L, int H) {
+  return sent_offset(B, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H;
+}
+
+static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_word, granule_t* (&g)[2][3],
+                           float* (&sv)[2][3], unsigned** census) {
   *abort_word = reinterpret_cast<unsigned*>(sync);
   granule_t* p = reinterpret_cast<granule_t*>(sync + 256);
   for (int d = 0; d < 2; ++d)
@@ -363,20 +410,27 @@ static void carve_granules(char* sync, int B, int H, unsigned** abort_word, gran
       p += 2L * B * H;
     }
   *census = reinterpret_cast<unsigned*>(p);
+  float* q = reinterpret_cast<float*>(sync + sent_offset(B, H));
+  for (int d = 0; d < 2; ++d)
+    for (int k = 0; k < 3; ++k) {
+      sv[d][k] = q;
+      q += (long)L * B * H;
+    }
 }
 
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   PArgs a{};
   const int MT = (f.B + 15) / 16;
   granule_t* gr[2][3];
-  carve_granules(static_cast<char*>(sync), f.B, f.H, &a.abort_word, gr, &a.census);
+  float* sr[2][3];
+  carve_granules(static_cast<char*>(sync), f.B, f.L, f.H, &a.abort_word, gr, sr, &a.census);
   for (int d = 0; d < f.ndir; ++d)
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
-                  gr[d][0], gr[d][1], gr[d][2]};
+                  gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
-  S2S_TRY(launch_sync_prep(st, sync, gru_persist_sync_bytes(f.B, f.H)));
+  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.H)));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
   return launch(st, a, f.ndir, true);
@@ -386,14 +440,15 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   PArgs a{};
   const int MT = (b.B + 15) / 16;
   granule_t* gr[2][3];
-  carve_granules(static_cast<char*>(sync), b.B, b.H, &a.abort_word, gr, &a.census);
+  float* sr[2][3];
+  carve_granules(static_cast<char*>(sync), b.B, b.L, b.H, &a.abort_word, gr, sr, &a.census);
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
-                  b.reverse[d], gr[d][0], gr[d][1], gr[d][2]};
+                  b.reverse[d], gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
-  S2S_TRY(launch_sync_prep(st, sync, gru_persist_sync_bytes(b.B, b.H)));
+  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.H)));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);

@@ -159,6 +159,59 @@ __device__ __forceinline__ bool chain_is_local(unsigned* census, int chain, int 
   return *flag != 0;
 }
 
+// ---- sentinel hand-offs (XCD-local chains)
+// A granule is 8 bytes to carry 4 bytes of payload; a sweep reads every handed-off value of its
+// rows (16 rows x K per workgroup and phase), so the tag halves the useful rate of the per-CU L2
+// path that bounds a recurrence step (measured: half the swept bytes took a GRU layer from 1.55
+// to 1.15 ms).  Where every slot is written once per launch, the plain fp32 value can be its own
+// flag: the slot is re-armed to kSent (an all-ones NaN pattern no finite computation produces)
+// before the launch's first publication, and a consumer polls until no word equals kSent.
+// Re-arming is done by the slot's own producer at launch start with plain stores into its XCD's
+// L2 -- the L2 every consumer of a local chain reads -- drained (vmcnt(0)) before the producer's
+// census word (chain_is_local), which every member waits for before its first poll; a chain that
+// turns out not to be XCD-local uses tagged granules instead (stale lines of an earlier launch in
+// another XCD's L2 could otherwise pass for fresh values).
+constexpr unsigned kSent = 0xffffffffu;
+__device__ __forceinline__ void put_sent(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store: stays in this XCD's L2
+}
+// rows [b0, min(b0 + 16, B)) x units [u0, u0 + 16) of slots 0..L-1 (slot stride `slot` floats,
+// row stride H) of nk sentinel buffers; all 256 threads call it; ends drained and barriered
+__device__ __forceinline__ void rearm_sent(float* const* kinds, int nk, long slot, int L, int B, int H, int b0,
+                                           int u0) {
+  const int tid = threadIdx.x, c4 = tid & 3, r = (tid >> 2) & 15, sg = tid >> 6;
+  const int b = b0 + r;
+  if (b < B) {
+    const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
+                                  __uint_as_float(kSent));
+    for (int k = 0; k < nk; ++k)
+      for (int t = sg; t < L; t += 4)
+        *reinterpret_cast<float4*>(kinds[k] + t * slot + (long)b * H + u0 + 4 * c4) = sv;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+// sweep_skinny's operand layout over a sentinel row (row_off in bytes): one 16-byte load per chunk
+template <int NC>
+__device__ __forceinline__ bool sweep_sent(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, int wave,
+                                           int lane, unsigned* abort_word) {
+  const long kq = 4 * (lane >> 4);
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const long off = row_off + 4 * (wave * 16 + 64 * i + kq);
+      const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+      ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+      a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
 // one thread waits for one granule
 __device__ __forceinline__ float wait_granule(const granule_t* g, unsigned tag, unsigned* abort_word, bool& ok) {
   unsigned spins = 0;
