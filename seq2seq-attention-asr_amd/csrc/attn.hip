@@ -83,6 +83,8 @@ struct XArgs {
   granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gQ;     // forward (inside fsync)
   granule_t *gDGZ, *gDGR, *gDGH, *gDC, *gPDWS, *gDWS;  // backward (inside bsync)
   unsigned *fcensus, *bcensus;
+  // sentinel rows of XCD-local chains (handoff.h), [T slots][B][...] floats, outside the zeroed regions
+  float *sS, *sQ, *sC;  // forward: s_t, q_t (S), c_t (A)
 };
 constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder
 constexpr int kXMaxCh = 16;  // chunks per utterance
@@ -196,6 +198,9 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   granule_t* xgQ = f.take<granule_t>(2 * B * S);
   unsigned* fcensus = f.take<unsigned>(kXChains * kXWG);
   const size_t fsync_bytes = f.off - (size_t)(fsync - scratch);
+  float* xsS = f.take<float>(BT * S);
+  float* xsQ = f.take<float>(BT * S);
+  float* xsC = f.take<float>(BT * A);
   char* bsync = g.take<char>(256);
   granule_t* gZ = g.take<granule_t>(2 * B * S);
   granule_t* gR = g.take<granule_t>(2 * B * S);
@@ -235,6 +240,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     x->gS = xgS; x->gWS = xgWS; x->gPM = xgPM; x->gPL = xgPL; x->gPC = xgPC; x->gC = xgC; x->gQ = xgQ;
     x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
     x->fcensus = fcensus; x->bcensus = bcensus;
+    x->sS = xsS; x->sQ = xsQ; x->sC = xsC;
   }
   return Layout{sv.off + 256, f.off + 256, g.off + 256};
 }

@@ -100,10 +100,9 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
-  {
-    float* mine = isz ? g.s0 : g.s1;  // z tiles publish h, r tiles q
-    rearm_sent(&mine, 1, (long)B * H, L, B, H, mt * 16, isz ? c1 * 16 : c1 * 16 - H);
-  }
+  // z tiles publish h, r tiles q
+  rearm_rect(isz ? g.s0 : g.s1, (long)B * H, L, H, b0, min(16, B - b0), isz ? c1 * 16 : c1 * 16 - H, 16);
+  rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 w1[NC], w2[NC];
@@ -219,10 +218,10 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
-  {
-    float* const mine[3] = {g.s0, g.s1, g.s2};
-    rearm_sent(mine, 3, (long)B * H, L, B, H, mt * 16, c * 16);
-  }
+  rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  rearm_rect(g.s1, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  rearm_rect(g.s2, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
   float4 wh[NC], wzr[2 * NC];

@@ -176,19 +176,27 @@ __device__ __forceinline__ void put_sent(float* p, float v) {
   __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_WORKGROUP);  // plain store: stays in this XCD's L2
 }
-// rows [b0, min(b0 + 16, B)) x units [u0, u0 + 16) of slots 0..L-1 (slot stride `slot` floats,
-// row stride H) of nk sentinel buffers; all 256 threads call it; ends drained and barriered
-__device__ __forceinline__ void rearm_sent(float* const* kinds, int nk, long slot, int L, int B, int H, int b0,
-                                           int u0) {
-  const int tid = threadIdx.x, c4 = tid & 3, r = (tid >> 2) & 15, sg = tid >> 6;
-  const int b = b0 + r;
-  if (b < B) {
-    const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
-                                  __uint_as_float(kSent));
-    for (int k = 0; k < nk; ++k)
-      for (int t = sg; t < L; t += 4)
-        *reinterpret_cast<float4*>(kinds[k] + t * slot + (long)b * H + u0 + 4 * c4) = sv;
+// re-arm rows [r0, r0 + nr) x columns [c0, c0 + nc) (nc % 4 == 0, 16-byte aligned) of slots
+// 0..nslots-1 (slot stride `slot`, row stride ld floats); all 256 threads call it; the producer's
+// re-arms end with rearm_done() before its census word
+__device__ __forceinline__ void rearm_rect(float* base, long slot, int nslots, long ld, int r0, int nr, int c0,
+                                           int nc) {
+  const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
+                                __uint_as_float(kSent));
+  const int n4 = nc / 4, per = nr * n4;
+  if (per <= 0) return;
+  if (256 % per == 0) {  // every thread keeps one (row, column) and strides over the slots
+    const int spp = 256 / per, s0 = threadIdx.x / per, rem = threadIdx.x - s0 * per, r = rem / n4, c = rem - r * n4;
+    float* p = base + (long)(r0 + r) * ld + c0 + 4 * c;
+    for (int s = s0; s < nslots; s += spp) *reinterpret_cast<float4*>(p + s * slot) = sv;
+    return;
   }
+  for (int i = threadIdx.x; i < nslots * per; i += 256) {
+    const int s = i / per, rem = i - s * per, r = rem / n4, c = rem - r * n4;
+    *reinterpret_cast<float4*>(base + s * slot + (long)(r0 + r) * ld + c0 + 4 * c) = sv;
+  }
+}
+__device__ __forceinline__ void rearm_done() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 }
