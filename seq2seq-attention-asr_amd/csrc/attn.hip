@@ -85,6 +85,7 @@ struct XArgs {
   unsigned *fcensus, *bcensus;
   // sentinel rows of XCD-local chains (handoff.h), [T slots][B][...] floats, outside the zeroed regions
   float *sS, *sQ, *sC;  // forward: s_t, q_t (S), c_t (A)
+  float *sDGZ, *sDGR, *sDGH, *sDC, *sDWS;  // backward: da_z, da_r, da_h (S), dc (A), dws (Sc)
 };
 constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder
 constexpr int kXMaxCh = 16;  // chunks per utterance
@@ -218,6 +219,11 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   granule_t* xgDWS = g.take<granule_t>(2 * B * Sc);
   unsigned* bcensus = g.take<unsigned>(kXChains * kXWG);
   const size_t bsync_bytes = g.off - (size_t)(bsync - scratch);
+  float* xsDGZ = g.take<float>(BT * S);
+  float* xsDGR = g.take<float>(BT * S);
+  float* xsDGH = g.take<float>(BT * S);
+  float* xsDC = g.take<float>(BT * A);
+  float* xsDWS = g.take<float>(BT * Sc);
   if (k) {
     k->gS = gS; k->gWS = gWS; k->gPM = gPM; k->gPL = gPL; k->gPC = gPC; k->gC = gC; k->gCY = gCY; k->gD = gD;
     k->gQ = gQ; k->gZ = gZ; k->gR = gR; k->gH = gH; k->gDD = gDD; k->gDCY = gDCY; k->gDC = gDC; k->gPDWS = gPDWS;
@@ -241,6 +247,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
     x->fcensus = fcensus; x->bcensus = bcensus;
     x->sS = xsS; x->sQ = xsQ; x->sC = xsC;
+    x->sDGZ = xsDGZ; x->sDGR = xsDGR; x->sDGH = xsDGH; x->sDC = xsDC; x->sDWS = xsDWS;
   }
   return Layout{sv.off + 256, f.off + 256, g.off + 256};
 }

@@ -220,6 +220,49 @@ __device__ __forceinline__ bool sweep_sent(float4 (&a)[NC], __amdgpu_buffer_rsrc
   }
 }
 
+// sweep_skinny_rows over sentinel rows: all R * NC loads of a pass issued before any check
+template <int NC, int R>
+__device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],
+                                                const long (&row_off)[R], int wave, int lane, unsigned* abort_word) {
+  const long kq = 4 * (lane >> 4);
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const long off = row_off[r] + 4 * (wave * 16 + 64 * i + kq);
+        const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[r], (int)off, 0, 16));
+        ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+        a[r][i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+      }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+// sweep_vec over a sentinel row (row_off in bytes): float4 c4 = lane + 64 i, lanes with c4 >= n4 idle
+template <int NV>
+__device__ __forceinline__ bool sweep_vec_sent(float4 (&a)[NV], __amdgpu_buffer_rsrc_t rs, long row_off, int n4,
+                                               int lane, unsigned* abort_word) {
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      const int c4 = lane + 64 * i;
+      if (c4 < n4) {
+        const uint4 p =
+            __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(row_off + 16L * c4), 0, 16));
+        ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+        a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+      }
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
 // one thread waits for one granule
 __device__ __forceinline__ float wait_granule(const granule_t* g, unsigned tag, unsigned* abort_word, bool& ok) {
   unsigned spins = 0;
