@@ -154,6 +154,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--flat-allreduce", action="store_true",
+                    help="N>1: one all-reduce of the whole gradient after the step instead of the bucketed, "
+                         "overlapped one")
     args = ap.parse_args()
 
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
@@ -191,9 +194,17 @@ def main():
     stream = torch.cuda.Stream()
     scale = s2s_dist.step_scale(B)
 
+    comm = torch.cuda.Stream()
+    buckets = model.grad_buckets()
+    bucketed = world > 1 and not args.flat_allreduce
+
     def step():
-        model.step(x, labels, scale=scale, stream=stream)
-        if world > 1:
+        model.step(x, labels, scale=scale, stream=stream, bucket_events=bucketed)
+        if bucketed:
+            # per-bucket RCCL all-reduce issued as each bucket's gradients become final (decoder,
+            # then encoder layers top-down), overlapping the BPTT of the layers below
+            s2s_dist.allreduce_buckets(model.grads, buckets, wait=model.wait_bucket, comm_stream=comm)
+        elif world > 1:
             s2s_dist.allreduce_gradients(model.grads)
 
     with torch.cuda.stream(stream):
@@ -228,6 +239,8 @@ def main():
         "config": {"workload": f"{CONFIG_DESC[args.config][0]}: {args.config}", "model": CONFIG_DESC[args.config][1],
                    "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
                    "feat_dim": cfg.inputFrameSize, "parallelism": f"dp{world}",
+                   "allreduce": ("none" if world == 1 else "flat RCCL after the step" if not bucketed
+                                 else f"{len(buckets)} RCCL buckets overlapped with encoder BPTT"),
                    "launch": "eager" if args.no_graph else "hipGraph replay",
                    "flop_per_step_per_gpu": flop_step},
         "step_tflops_per_gpu": round(flop_step / (ms / 1000.0) / 1e12, 3),

@@ -148,6 +148,16 @@ typedef struct {
 } s2s_model_dims;
 #define S2S_ZERO_GRADS 1
 #define S2S_NORMALIZE_NLL 2
+/* S2S_BUCKET_EVENTS: the step records one ctx-owned event per gradient bucket at the point where
+ * that bucket's gradients are final (also inside a captured hipGraph, as external event nodes), so
+ * a data-parallel caller can start each bucket's all-reduce while the encoder BPTT of the layers
+ * below is still running: s2s_stream_wait_bucket(ctx, comm_stream, i) then the
+ * collective on comm_stream.  Buckets in completion order: 0 = the decoder's parameters, then
+ * encoder layers numLayers .. 1 (s2s_model_bucket gives each one's slice of the flat buffer). */
+#define S2S_BUCKET_EVENTS 4
+int s2s_model_bucket_count(const s2s_model_dims* d);
+int s2s_model_bucket(const s2s_model_dims* d, int i, size_t* offset, size_t* count);
+int s2s_stream_wait_bucket(s2s_ctx* ctx, s2s_stream_t stream, int i);
 size_t s2s_model_param_count(const s2s_model_dims* d);
 /* offset (in floats) of parameter #i of the flat layout and its element count; -1 past the end */
 long s2s_model_param_offset(const s2s_model_dims* d, int i, long* numel);

@@ -83,11 +83,14 @@ struct GraphKey {
   bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
 };
 
+constexpr int kMaxBuckets = 17;  // decoder + up to 16 encoder layers
+
 struct s2s_ctx {
   int device = 0;
   int flags = 0;
   hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
   hipEvent_t ev[16] = {};
+  hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
   bool have_graph = false;
   GraphKey key{};
   hipGraph_t graph = nullptr;
@@ -204,9 +207,30 @@ int fork_to(hipStream_t st, hipStream_t side, hipEvent_t ev) {
   return 0;
 }
 
-int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_model_dims* d, const float* params,
-                    float* grads, const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
-                    void* workspace) {
+// bucket i's gradients are final on stream s (S2S_BUCKET_EVENTS); an external event node when captured
+int mark_bucket(hipEvent_t* bev, int i, hipStream_t s) {
+  if (!bev) return 0;
+  if (!capturing(s)) {
+    S2S_CHECK_HIP(hipEventRecord(bev[i], s));
+    return 0;
+  }
+  // an event-record node appended to the capture (hipEventRecordWithFlags(..., hipEventRecordExternal)
+  // is refused by this runtime): it fires on every replay, after everything captured on s so far
+  hipStreamCaptureStatus cs;
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t nd = 0;
+  S2S_CHECK_HIP(hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &nd));
+  hipGraphNode_t node;
+  S2S_CHECK_HIP(hipGraphAddEventRecordNode(&node, g, deps, nd, bev[i]));
+  S2S_CHECK_HIP(hipStreamUpdateCaptureDependencies(s, &node, 1, hipStreamSetCaptureDependencies));
+  return 0;
+}
+
+int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
+                    const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
+                    float* logp, float* nll, void* workspace) {
   const bool split = side != nullptr;
   gru_persist_set_exclusive(split ? 1 : 0);
   ModelWs w = model_ws(d, workspace);
@@ -289,6 +313,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
                         w.attn_scratch_bytes));
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
   S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
+  S2S_TRY(mark_bucket(bev, 0, split ? side : st));
   // ---- encoder backward
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
@@ -306,6 +331,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, const s2s_
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
     if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
     S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
+    S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
     float* tmp = dYcur;
     dYcur = dYnext;
     dYnext = tmp;
@@ -397,6 +423,8 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
+    if (e) (void)hipEventDestroy(e);
+  for (auto& e : ctx->bev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   delete ctx;
@@ -609,9 +637,16 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   S2S_REQUIRE(params && grads && x && labels && workspace, "model: null argument");
   S2S_REQUIRE(workspace_bytes >= model_ws(d, nullptr).total, "model: workspace too small");
   hipStream_t st = static_cast<hipStream_t>(stream);
+  hipEvent_t* bev = nullptr;
+  if (flags & S2S_BUCKET_EVENTS) {
+    S2S_REQUIRE(d->numLayers + 1 <= kMaxBuckets, "model: too many layers for S2S_BUCKET_EVENTS");
+    for (auto& e : ctx->bev)
+      if (!e) S2S_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    bev = ctx->bev;
+  }
   if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
-    return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, d, params,
-                           grads, x, labels, scale, flags, logp, nll, workspace);
+    return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, bev, d,
+                           params, grads, x, labels, scale, flags, logp, nll, workspace);
   GraphKey key;
   std::memset(&key, 0, sizeof(key));
   key.d = *d;
@@ -627,8 +662,8 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     ctx->graph = nullptr;
     ctx->have_graph = false;
     S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, d, params,
-                                   grads, x, labels, scale, flags, logp, nll, workspace);
+    const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, bev, d,
+                                   params, grads, x, labels, scale, flags, logp, nll, workspace);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(st, &g);
     if (rc != 0) {
@@ -642,6 +677,35 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     ctx->have_graph = true;
   }
   S2S_CHECK_HIP(hipGraphLaunch(ctx->exec, st));
+  return 0;
+}
+
+int s2s_model_bucket_count(const s2s_model_dims* d) {
+  if (check_model_dims(d) != 0) return -1;
+  return d->numLayers + 1;
+}
+
+int s2s_model_bucket(const s2s_model_dims* d, int i, size_t* offset, size_t* count) {
+  S2S_TRY(check_model_dims(d));
+  const int nl = d->numLayers;
+  S2S_REQUIRE(offset && count && i >= 0 && i <= nl, "bucket: bad index");
+  const std::vector<long> sizes = param_sizes(d);
+  // bucket 0: the decoder (params 6 nl ..); bucket j >= 1: encoder layer nl - j (params 6 l .. 6 l + 5)
+  const int p0 = i == 0 ? 6 * nl : 6 * (nl - i), p1 = i == 0 ? (int)sizes.size() : p0 + 6;
+  size_t off = 0, n = 0;
+  for (int p = 0; p < (int)sizes.size(); ++p) {
+    if (p < p0) off += sizes[p];
+    else if (p < p1) n += sizes[p];
+  }
+  *offset = off;
+  *count = n;
+  return 0;
+}
+
+int s2s_stream_wait_bucket(s2s_ctx* ctx, s2s_stream_t stream, int i) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(i >= 0 && i < kMaxBuckets && ctx->bev[i], "bucket: no event (step without S2S_BUCKET_EVENTS?)");
+  S2S_CHECK_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(stream), ctx->bev[i], 0));
   return 0;
 }
 

@@ -36,6 +36,7 @@ int s2s_nll_seed(s2s_ctx*, void* stream, int B, int T, int O, const float* logp,
 int s2s_comm_unique_id(void* out_bytes);
 int s2s_comm_init(s2s_ctx* ctx, const void* id_bytes, int nranks, int rank);
 int s2s_allreduce_sum(s2s_ctx* ctx, void* stream, float* buf, size_t count);
+int s2s_stream_wait_bucket(s2s_ctx* ctx, void* stream, int i);
 ]]
 
 local C = ffi.load('s2s_hip')

@@ -69,6 +69,9 @@ SIGNATURES = [
     ("s2s_model_encoder_output", c_void_p, [P(s2s_model_dims), c_void_p]),
     ("s2s_prof_enable", c_int, [c_int]),
     ("s2s_prof_collect", c_int, [ctypes.c_char_p, c_size_t]),
+    ("s2s_model_bucket_count", c_int, [P(s2s_model_dims)]),
+    ("s2s_model_bucket", c_int, [P(s2s_model_dims), c_int, P(c_size_t), P(c_size_t)]),
+    ("s2s_stream_wait_bucket", c_int, [c_void_p, c_void_p, c_int]),
     ("s2s_comm_unique_id", c_int, [c_void_p]),
     ("s2s_comm_init", c_int, [c_void_p, c_void_p, c_int, c_int]),
     ("s2s_allreduce_sum", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
@@ -78,6 +81,7 @@ S2S_CTX_GRAPH = 1
 S2S_CTX_OVERLAP = 2
 S2S_ZERO_GRADS = 1
 S2S_NORMALIZE_NLL = 2
+S2S_BUCKET_EVENTS = 4
 S2S_ATTN_NPARAMS = 17
 S2S_UNIQUE_ID_BYTES = 128
 

@@ -32,6 +32,36 @@ def allreduce_gradients(flat_grads: torch.Tensor, bucket_elems: int = 0):
     return flat_grads
 
 
+def allreduce_buckets(grads: torch.Tensor, buckets, wait=None, comm_stream=None):
+    """Bucketed gradient sum over ranks, overlapped with the rest of the step.
+
+    buckets: [(offset, count)] in the order the step finalises them (ChorowskiBaseline.grad_buckets:
+    the decoder, then the encoder layers top-down).  On GPUs, wait(i, comm_stream) makes comm_stream
+    wait for bucket i's "final" event (ChorowskiBaseline.wait_bucket, recorded inside the step, also
+    under hipGraph replay), and bucket i's all-reduce is issued from comm_stream -- so it runs on
+    RCCL while the BPTT of the encoder layers below is still in flight.  The caller's current stream
+    then waits for every bucket (the optimizer reads the summed gradient).  Sums are elementwise,
+    so the result equals one all-reduce of the flat buffer."""
+    if world() == 1:
+        return grads
+    works = []
+    cur = torch.cuda.current_stream() if grads.is_cuda else None
+    for i, (off, n) in enumerate(buckets):
+        view = grads[off:off + n]
+        if grads.is_cuda:
+            if wait is not None:
+                wait(i, comm_stream)
+            else:
+                comm_stream.wait_stream(cur)
+            with torch.cuda.stream(comm_stream):
+                works.append(dist.all_reduce(view, async_op=True))
+        else:
+            works.append(dist.all_reduce(view, async_op=True))
+    for w in works:
+        w.wait()
+    return grads
+
+
 def allreduce_mean_scalar(x: float, device=None) -> float:
     if world() == 1:
         return x

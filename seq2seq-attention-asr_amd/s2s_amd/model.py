@@ -71,6 +71,30 @@ def _fan_in(name, shape, cfg):
     return table.get(name, shape[1] if len(shape) > 1 else shape[0])
 
 
+def buckets_of_shapes(shapes, num_layers):
+    """grad_buckets from a param_shapes list (pure Python; pins s2s_model_bucket in the ABI tests)."""
+    sizes = [math.prod(s) for _, s in shapes]
+    starts = [sum(sizes[:i]) for i in range(len(sizes) + 1)]
+    out = [(starts[6 * num_layers], starts[-1] - starts[6 * num_layers])]
+    for l in range(num_layers - 1, -1, -1):
+        out.append((starts[6 * l], starts[6 * l + 6] - starts[6 * l]))
+    return out
+
+
+def grad_buckets(cfg: ModelConfig):
+    """[(offset, count)] slices of the flat gradient in the order the step finalises them: the
+    decoder, then encoder layers numLayers .. 1 (s2s_model_bucket; host-only, no GPU call)."""
+    c = cfg
+    d = _lib.s2s_model_dims(1, 1, 1, c.inputFrameSize, c.hiddenFrameSize, c.outputFrameSize, c.numLayers,
+                            c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty, 0.0)
+    out = []
+    for i in range(lib.s2s_model_bucket_count(ctypes.byref(d))):
+        off, n = ctypes.c_size_t(), ctypes.c_size_t()
+        check(lib.s2s_model_bucket(ctypes.byref(d), i, ctypes.byref(off), ctypes.byref(n)))
+        out.append((off.value, n.value))
+    return out
+
+
 class ChorowskiBaseline:
     """autoencoder = decoder({encoder(x), labelmask}) with flat params/grads on one device."""
 
@@ -146,13 +170,21 @@ class ChorowskiBaseline:
             self._ws[key] = _bytes(nbytes, self.device)
         return self._ws[key]
 
+    def grad_buckets(self):
+        return grad_buckets(self.cfg)
+
+    def wait_bucket(self, i, stream):
+        """`stream` waits until gradient bucket i of the last step(bucket_events=True) is final."""
+        check(lib.s2s_stream_wait_bucket(self.ctx.handle, ctypes.c_void_p(stream.cuda_stream), i))
+
     def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None,
-             dropout_seed=None, dropout_mask=None):
+             dropout_seed=None, dropout_mask=None, bucket_events=False):
         """One training-step gradient (timit/timit.lua:240-295): grads (+)= scale * d(sum_b nll_b)/dparams,
         scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O)).
         With cfg.dropout > 0 (training mode) the decoder MLP input is dropped out with masks drawn
         in-kernel from dropout_seed (default: a per-step counter) or given as dropout_mask
-        (B, T, S+A) multipliers."""
+        (B, T, S+A) multipliers.  bucket_events=True records the per-bucket "gradients final" events
+        that dist.allreduce_buckets waits on."""
         if x.dim() == 2:
             x = x[None]
         if labels.dim() == 1:
@@ -182,6 +214,8 @@ class ChorowskiBaseline:
                 self._mask_keep = dropout_mask.contiguous()
                 d.dropout_mask = self._mask_keep.data_ptr()
         flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
+        if bucket_events:
+            flags |= _lib.S2S_BUCKET_EVENTS
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
         check(lib.s2s_model_step(self.ctx.handle, st, ctypes.byref(d), dptr(self.params), dptr(self.grads), dptr(x),
                                  dptr(lab), float(scale), flags, dptr(logp), dptr(nll), dptr(ws), ws.numel()))

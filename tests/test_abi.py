@@ -44,6 +44,21 @@ def test_param_layout_matches_oracle():
         assert _lib.lib.s2s_model_param_offset(ctypes.byref(d), 10 ** 6, None) == -1
 
 
+def test_grad_buckets_cover_the_flat_layout():
+    """s2s_model_bucket (S2S_BUCKET_EVENTS order: decoder, then encoder layers top-down) agrees with
+    the Python layout and tiles the flat gradient exactly once."""
+    from s2s_amd import model
+    for kw in ({}, dict(numLayers=2, hiddenFrameSize=128), dict(numLayers=4)):
+        cfg = model.ModelConfig(**kw)
+        shapes = model.param_shapes(cfg)
+        got = model.grad_buckets(cfg)
+        assert got == model.buckets_of_shapes(shapes, cfg.numLayers)
+        assert len(got) == cfg.numLayers + 1
+        cover = sorted(got)
+        assert cover[0][0] == 0 and cover[-1][0] + cover[-1][1] == sum(math.prod(s) for _, s in shapes)
+        assert all(o + n == o2 for (o, n), (o2, _) in zip(cover, cover[1:]))
+
+
 def test_chorowski_param_count():
     """4,356,735 incl. the two zero TCZB biases (512 + 1) the flat layout omits."""
     from s2s_amd import model

@@ -51,14 +51,26 @@ def _worker(rank, world, port, B, out_path, buckets):
         for k in G:
             G[k] += g1[k]
     flat = torch.tensor(orc.flatten(G, cfg)) * (sd.step_scale(B) * 1.0)
-    sd.allreduce_gradients(flat, bucket_elems=buckets)
+    if buckets == "model":
+        # the step's bucket order (decoder, then encoder layers top-down) over the flat layout
+        import s2s_amd
+        mcfg = s2s_amd.ModelConfig(**{f: getattr(cfg, f) for f in (
+            "inputFrameSize", "hiddenFrameSize", "outputFrameSize", "scoreDepth", "stateDepth", "outputDepth",
+            "mlpDepth", "maxoutWindow", "numLayers")})
+        mb = s2s_amd.model.buckets_of_shapes(s2s_amd.param_shapes(mcfg), cfg.numLayers)
+        cover = sorted(mb)
+        assert cover[0][0] == 0 and sum(n for _, n in mb) == flat.numel()
+        assert all(o + n == o2 for (o, n), (o2, _) in zip(cover, cover[1:]))
+        sd.allreduce_buckets(flat, mb)
+    else:
+        sd.allreduce_gradients(flat, bucket_elems=buckets)
     if rank == 0:
         np.save(out_path, flat.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("buckets", [0, 37])
+@pytest.mark.parametrize("buckets", [0, 37, "model"])
 def test_dp_allreduce_equals_global_batch(tmp_path, buckets):
     from oracle import s2s_oracle as orc
     world, B = 2, 2

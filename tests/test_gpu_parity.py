@@ -378,6 +378,35 @@ def test_model_step_overlap_bitwise(s2s, graph):
     assert torch.equal(ovl.grads, ref.grads)
 
 
+@pytest.mark.parametrize("graph", [False, True])
+def test_bucket_events_mark_final_gradients(s2s, graph):
+    """S2S_BUCKET_EVENTS: a stream that waits on bucket i's event sees that bucket's
+    final gradients -- eager and under hipGraph replay (external event nodes).  A copy taken on a
+    second stream right after each wait must equal the gradient after the whole step; a wait that
+    did not hold would copy zeroed or half-accumulated values (the step zeroes grads first)."""
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=graph, overlap=True)
+    buckets = model.grad_buckets()
+    assert len(buckets) == cfg.numLayers + 1
+    st, comm = torch.cuda.Stream(), torch.cuda.Stream()
+    snaps = [torch.empty(n, device="cuda") for _, n in buckets]
+    g = torch.Generator().manual_seed(11)
+    for rep in range(3):
+        x = torch.randn(32, 128, cfg.inputFrameSize, generator=g).cuda()
+        lab = torch.randint(0, cfg.outputDepth, (32, 40), generator=g).to(torch.int32).cuda()
+        st.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(st):
+            model.step(x, lab, stream=st, bucket_events=True)
+            for i, (off, n) in enumerate(buckets):
+                model.wait_bucket(i, comm)
+                with torch.cuda.stream(comm):
+                    snaps[i].copy_(model.grads[off:off + n])
+        torch.cuda.synchronize()
+        for i, (off, n) in enumerate(buckets):
+            assert torch.equal(snaps[i], model.grads[off:off + n]), (rep, i)
+        assert model.grads.abs().sum() > 0
+
+
 @pytest.mark.parametrize("local", [1, 0])
 @pytest.mark.parametrize("B,H", [(32, 256), (45, 128)])
 def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, B, H):
