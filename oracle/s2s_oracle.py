@@ -320,6 +320,27 @@ def encoder_bwd(P: Dict[str, Array], caches, dout: Array, G: Dict[str, Array], s
 # Attention decoder (Attention.lua + RNNAttention.lua + MonotonicAlignment.lua)
 # ----------------------------------------------------------------------------
 
+def hybrid_pads(kW: int):
+    """Attention.lua:77-86: odd kW pads (kW-1)/2 on both sides; even kW pads kW/2 on the left
+    (nn.Padding(1, -pad_left, 2)) and kW/2 - 1 on the right, so the conv returns L frames."""
+    if kW % 2 == 1:
+        return (kW - 1) // 2, (kW - 1) // 2
+    return kW // 2, kW // 2 - 1
+
+
+def hybrid_features(alpha_prev: Array, P: Dict[str, Array], kW: int):
+    """Location features of the hybrid attention (Attention.lua:75-97): alpha_{t-1} (B, L) as an
+    (L, 1) sequence, zero-padded (hybrid_pads), -> F = TemporalConvolution(1, nF, kW) with bias
+    (:90) -> UF = TCZB(nF, Sc, 1) (:91, zero bias).  Returns (UF (B, L, Sc), F (B, L, nF), the
+    padded sequence (B, L + kW - 1))."""
+    pl, pr = hybrid_pads(kW)
+    B, L = alpha_prev.shape
+    apad = np.concatenate([np.zeros((B, pl), alpha_prev.dtype), alpha_prev, np.zeros((B, pr), alpha_prev.dtype)], 1)
+    Fm = temporal_conv(P["hybW"], P["hybb"], apad[..., None], kW)   # (B, L, nF)
+    UF = temporal_conv(P["hybU"], None, Fm, 1)                       # (B, L, Sc)
+    return UF, Fm, apad
+
+
 def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfig",
                   dropout_mask: Optional[Array] = None):
     """nn.Attention:updateOutput (Attention.lua:305-322) = decoder gModule
@@ -332,7 +353,8 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
 
     Per step (decoder_base_, Attention.lua:51-184):
       ws = Ws s + bs            TemporalConvolution(1,Sc,S) on View(S,1) (:65-66)
-      Z = expand_L(ws) + Vh      ExpandAs + CAddTable (:67,98)  [hybrid off]
+      Z = expand_L(ws) + Vh [+ UF] ExpandAs + CAddTable (:67,95-98); UF = hybrid_features(alpha_prev)
+                                 when cfg.hybridAttendFeatureMaps > 0 (:75-94)
       e = we . tanh(Z)           TCZB(Sc,1,1) (:104-110)
       alpha = softmax_L(e)       (:117)
       alpha = MonoAlign(alpha, alpha_prev) identity fwd (:122-125, MonotonicAlignment.lua:19-42)
@@ -352,12 +374,15 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
                                  "z", "r", "hh", "u", "argmax", "m", "logp", "v", "alpha_prev")}
     logp_all = np.zeros((B, T, O), dt)
     Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    hyb = cfg.hybridAttendFeatureMaps > 0
     for t in range(T):
         yprev = np.zeros((B, O), dt)
         if t > 0:
             yprev[np.arange(B), labels[:, t - 1]] = 1.0
         ws = s @ P["Ws"].T + P["bs"]                               # (B, Sc)
         Z = ws[:, None, :] + Vh
+        if hyb:
+            Z = Z + hybrid_features(alpha_prev, P, cfg.hybridAttendFilterSize)[0]
         th = np.tanh(Z)
         e = (th @ P["we"].T)[..., 0]                               # (B, L)
         alpha = softmax(e, axis=1)
@@ -414,6 +439,8 @@ def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, 
     dalpha_carry = np.zeros((B, L), dt)
     jw = (L + 1 - np.arange(1, L + 1)).astype(dt)               # (L+1-j), j 1-based
     Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    hyb = cfg.hybridAttendFeatureMaps > 0
+    kW = cfg.hybridAttendFilterSize
     for t in range(T - 1, -1, -1):
         g_ = lambda key: cache[key][:, t]
         logp = g_("logp")
@@ -479,10 +506,28 @@ def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, 
         # softmax backward (3p)
         de = alpha * (dalpha - np.sum(alpha * dalpha, 1, keepdims=True))
         ws = g_("ws")
-        th = np.tanh(ws[:, None, :] + Vh)
+        Z = ws[:, None, :] + Vh
+        if hyb:
+            UF, Fm, apad = hybrid_features(g_("alpha_prev"), P, kW)
+            Z = Z + UF
+        th = np.tanh(Z)
         G["we"] += scale * np.einsum("bl,blk->k", de, th)[None, :]
         dZ = de[:, :, None] * P["we"][0][None, None, :] * (1 - th * th)
         dVh += dZ
+        if hyb:
+            # UF = TCZB(F -> Sc) of F = conv(alpha_{t-1}): grads of U, the conv, and d alpha_{t-1}
+            # (alpha is part of the carried hidden state, RNNAttention.lua:233-250)
+            G["hybU"] += scale * np.einsum("bls,blf->sf", dZ, Fm)
+            dF = dZ @ P["hybU"]                                      # (B, L, nF)
+            G["hybb"] += scale * dF.sum((0, 1))
+            win = np.stack([apad[:, i:i + L] for i in range(kW)], 2)  # (B, L, kW)
+            G["hybW"] += scale * np.einsum("blf,bli->fi", dF, win)
+            dq = dF @ P["hybW"]                                      # (B, L, kW): d apad[l + i]
+            dapad = np.zeros_like(apad)
+            for i in range(kW):
+                dapad[:, i:i + L] += dq[:, :, i]
+            pl, _ = hybrid_pads(kW)
+            dalpha_carry = dalpha_carry + dapad[:, pl:pl + L]
         dws = dZ.sum(1)
         G["Ws"] += scale * (dws.T @ sp)
         G["bs"] += scale * dws.sum(0)
@@ -510,6 +555,8 @@ class ModelConfig:
     maxoutWindow: int = 7          # Maxout(..., 7) (model_chorowski_baseline.lua:56)
     penalty: float = 0.0           # MonotonicAlignment lambda
     numLayers: int = 3
+    hybridAttendFilterSize: int = 0    # Attention(..., hybridAttendFilterSize, hybridAttendFeatureMaps, ...):
+    hybridAttendFeatureMaps: int = 0   # 0 maps = content-only attention (model_chorowski_baseline.lua:39-40)
 
     @property
     def annotationDepth(self) -> int:
@@ -532,6 +579,9 @@ def param_shapes(cfg: ModelConfig):
                ("Wd", (S, 2 * S)), ("bd", (S,)),
                ("dec.Wz", (S, 2 * S)), ("dec.Wr", (S, 2 * S)), ("dec.Wh", (S, 2 * S)),
                ("Wm", (M * k, S + A)), ("bm", (M * k,)), ("Wo", (O, M)), ("bo", (O,))]
+    if cfg.hybridAttendFeatureMaps > 0:  # Attention.lua:90-91: conv (nF, kW) + bias, UF TCZB (Sc, nF)
+        nF, kW = cfg.hybridAttendFeatureMaps, cfg.hybridAttendFilterSize
+        shapes += [("hybW", (nF, kW)), ("hybb", (nF,)), ("hybU", (Sc, nF))]
     return shapes
 
 
@@ -540,7 +590,8 @@ def fan_in(name: str, shape, cfg: ModelConfig) -> int:
     TemporalConvolutionZeroBias.lua:21-35 (kW*inFrame), nn.Linear / nn.TemporalConvolution (3p)."""
     S, Sc, A, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.annotationDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
     table = {"V": A, "Ws": S, "bs": S, "we": Sc, "Wy": O, "by": O, "Wc": A, "bc": A, "Wd": 2 * S, "bd": 2 * S,
-             "Wm": S + A, "bm": S + A, "Wo": M, "bo": M}
+             "Wm": S + A, "bm": S + A, "Wo": M, "bo": M, "hybW": cfg.hybridAttendFilterSize,
+             "hybb": cfg.hybridAttendFilterSize, "hybU": cfg.hybridAttendFeatureMaps}
     if name in table:
         return table[name]
     return shape[1]

@@ -88,9 +88,12 @@ def _torch_loss(x, labels, TP, cfg, B):
     return loss / (B if B > 1 else 1), logp
 
 
-@pytest.mark.parametrize("penalty", [0.0, 0.3])
-def test_oracle_matches_torch_autograd(penalty):
-    cfg = tiny_cfg(penalty=penalty)
+@pytest.mark.parametrize("penalty,kW,nF", [(0.0, 0, 0), (0.3, 0, 0), (0.0, 3, 2), (0.3, 4, 3)])
+def test_oracle_matches_torch_autograd(penalty, kW, nF):
+    """kW/nF > 0: hybrid location-aware attention (Attention.lua:75-98), odd and even filters;
+    torch's conv1d + autograd is an independent statement of the conv, its padding and the
+    d alpha_{t-1} path through the carried hidden state."""
+    cfg = tiny_cfg(penalty=penalty, hybridAttendFilterSize=kW, hybridAttendFeatureMaps=nF)
     B, L, T = 3, 6, 5
     P = orc.init_params(cfg, seed=7)
     x, labels = orc.synthetic_batch(cfg, B, L, T, seed=3, pad=1, eos=2)
@@ -103,8 +106,9 @@ def test_oracle_matches_torch_autograd(penalty):
         np.testing.assert_allclose(G[k], TP[k].grad.numpy(), rtol=1e-9, atol=1e-11, err_msg=k)
 
 
-def test_oracle_finite_differences():
-    cfg = tiny_cfg()
+@pytest.mark.parametrize("kW,nF", [(0, 0), (5, 2)])
+def test_oracle_finite_differences(kW, nF):
+    cfg = tiny_cfg(hybridAttendFilterSize=kW, hybridAttendFeatureMaps=nF)
     B, L, T = 2, 5, 4
     P = orc.init_params(cfg, seed=11)
     x, labels = orc.synthetic_batch(cfg, B, L, T, seed=5, pad=1, eos=1)

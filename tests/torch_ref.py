@@ -78,7 +78,17 @@ def model_forward(x, labels, P, cfg, dropout_mask=None):
         if t > 0:
             y = torch.nn.functional.one_hot(torch.as_tensor(labels[:, t - 1]).long(), O).to(h.dtype)
         ws = s @ P["Ws"].t() + P["bs"]
-        e = (torch.tanh(ws[:, None, :] + Vh) @ P["we"].t())[..., 0]
+        Z = ws[:, None, :] + Vh
+        nF = getattr(cfg, "hybridAttendFeatureMaps", 0)
+        if nF > 0:  # Attention.lua:75-98 via torch's conv1d (cross-correlation = TemporalConvolution)
+            kW = cfg.hybridAttendFilterSize
+            pl, pr = (kW - 1) // 2, (kW - 1) // 2 if kW % 2 else None
+            if kW % 2 == 0:
+                pl, pr = kW // 2, kW // 2 - 1
+            apad = torch.nn.functional.pad(aprev, (pl, pr))
+            Fm = torch.nn.functional.conv1d(apad[:, None, :], P["hybW"][:, None, :], P["hybb"])  # (B, nF, L)
+            Z = Z + Fm.transpose(1, 2) @ P["hybU"].t()
+        e = (torch.tanh(Z) @ P["we"].t())[..., 0]
         a = torch.softmax(e, 1)
         # MonotonicAlignment as a loss-free regulariser: its backward equals the
         # gradient of lambda * (sum_j (L+1-j)(a_j - aprev_j)) where the indicator is on.
