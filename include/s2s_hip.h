@@ -87,15 +87,19 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
 
 /* ---------------------------------------------------------------- attention decoder
  * nn.Attention(decoder_recurrent = GRU(S,S), decoder_mlp = Maxout(S+A, M, K) -> Linear(M, O)
- * -> LogSoftMax, scoreDepth Sc, hybrid off, stateDepth S, annotationDepth A, outputDepth O,
+ * -> LogSoftMax, scoreDepth Sc, hybrid features (optional), stateDepth S, annotationDepth A, outputDepth O,
  * monoAlignPenalty true, penaltyLambda) -- Attention.lua:15-211, RNNAttention.lua:144-253,
  * MonotonicAlignment.lua, Maxout.lua, timit/model_chorowski_baseline.lua:37-70.
  * Parameter pointers, in this order (W = (out, in)):
  *   0 V (Sc, A)  [Vh TCZB]     1 Ws (Sc, S)  2 bs (Sc)   [TemporalConvolution(1, Sc, S)]
  *   3 we (1, Sc) [e TCZB]      4 Wy (S, O)   5 by (S)    6 Wc (S, A)   7 bc (S)
  *   8 Wd (S, 2S) 9 bd (S)     10 Wz (S, 2S) 11 Wr (S, 2S) 12 Wh (S, 2S)   [decoder GRU]
- *  13 Wm (M*K, S+A) 14 bm (M*K)   15 Wo (O, M) 16 bo (O)                                     */
+ *  13 Wm (M*K, S+A) 14 bm (M*K)   15 Wo (O, M) 16 bo (O)
+ * and with hybrid attention (hybridAttendFeatureMaps nF > 0, Attention.lua:75-98):
+ *  17 hybW (nF, kW) 18 hybb (nF)  [TemporalConvolution(1, nF, kW) on the padded alpha_{t-1}]
+ *  19 hybU (Sc, nF)               [UF = TCZB(nF, Sc, 1)]                                        */
 #define S2S_ATTN_NPARAMS 17
+#define S2S_ATTN_NPARAMS_HYBRID 20
 /* dropout: nn.Dropout(p) in front of the Maxout of the decoder MLP (timit/model_chorowski_baseline_
  * dropout.lua:56), Torch7 semantics in training mode: [s_t; c_t] * mask, mask = Bernoulli(1-p)/(1-p).
  * p = 0: no dropout.  dropout_mask: optional (B, T, S+A) multipliers (scaling included) used as given
@@ -108,6 +112,10 @@ typedef struct {
   float dropout;
   unsigned long long dropout_seed;
   const float* dropout_mask;
+  /* hybrid location-aware attention: Attention(..., hybridAttendFilterSize kW, hybridAttendFeatureMaps
+   * nF, ...); nF = 0 is the content-only baseline (model_chorowski_baseline.lua:39-40); nF > 0 needs
+   * 1 <= kW <= 8 and runs the per-step decoder kernels */
+  int hybridAttendFilterSize, hybridAttendFeatureMaps;
 } s2s_attn_dims;
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);

@@ -20,12 +20,18 @@ struct AttnDims {
   float dropout = 0.f;                    // nn.Dropout(p) before the Maxout (0 = none)
   unsigned long long dropout_seed = 0;
   const float* dropout_mask = nullptr;    // injected (B, T, S+A) multipliers, or null
+  // hybrid location-aware attention (Attention.lua:75-98): hybridAttendFilterSize kW and
+  // hybridAttendFeatureMaps nF; nF = 0: content-only (the Chorowski baseline)
+  int hk = 0, hf = 0;
 };
+constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
 struct AttnParams {
   const float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
+  const float *hybW = nullptr, *hybb = nullptr, *hybU = nullptr;  // (nF, kW), (nF), (Sc, nF) when hf > 0
 };
 struct AttnGrads {
   float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
+  float *hybW = nullptr, *hybb = nullptr, *hybU = nullptr;
 };
 
 int attn_check_dims(const AttnDims& d);

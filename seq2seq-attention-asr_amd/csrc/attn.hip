@@ -35,6 +35,7 @@ struct AttnK {
   // dims
   int B, L, T, A, Sc, S, O, M, K, NCH, t;
   float penalty;
+  int hk, hf;  // hybrid attention filter size / feature maps (hf = 0: off)
   // params
   AttnParams P;
   const float* h;
@@ -46,6 +47,9 @@ struct AttnK {
   float *PM, *PL, *PC, *U;
   // bwd scratch
   float *DO, *DU, *DV, *DGA, *DS, *DSP, *DSPF, *DD, *DCY, *DC, *DVH, *PDWS, *DWS, *DWEACC, *YP;
+  // hybrid attention: HGT (kW, Sc) = (U W)^T and HCU (Sc) = U b (saved); QA [2][B][L][kW] the
+  // d alpha_{t-1} partials q_{l,i} of the step after; PDG [B*NCH][kW][Sc] dG partials; DGT, DCU (bwd)
+  float *HGT, *HCU, *QA, *PDG, *DGT, *DCU;
   float *WhT, *GT, *WdT, *WcT, *WsT;
   // persistent-kernel granule buffers ([2 slots][...]) and abort word; one zeroed region each
   granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gCY, *gD, *gQ;           // forward
@@ -103,6 +107,7 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   XPlan p;
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && (std::strcmp(m, "step") == 0 || std::strcmp(m, "persist") == 0)) return p;
+  if (d.hf > 0) return p;  // hybrid attention: per-step kernels only
   int var = 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
   else if (d.S == 64 && d.A == 128 && d.Sc == 128) var = 2;
@@ -146,6 +151,9 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* XWHT = sv.take<float>(S * S);
   float* XZRT = sv.take<float>(2 * S * S);
   float* XWST = sv.take<float>(S * Sc);
+  const long HK = d.hf > 0 ? d.hk : 0;
+  float* HGT = HK ? sv.take<float>(HK * Sc) : nullptr;
+  float* HCU = HK ? sv.take<float>(Sc) : nullptr;
   const long NX = std::max(1, dec_xcd_plan(d).NCH);
   Bump f{scratch, 0, 0};
   float* PM = f.take<float>(B * NCH);
@@ -179,6 +187,10 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* WsT = g.take<float>(S * Sc);
   float* DE = g.take<float>(BT * L);
   float* VBAR = g.take<float>(B * Sc);
+  float* QA = HK ? g.take<float>(2 * B * L * HK) : nullptr;
+  float* PDG = HK ? g.take<float>(B * NCH * HK * Sc) : nullptr;
+  float* DGT = HK ? g.take<float>(HK * Sc) : nullptr;
+  float* DCU = HK ? g.take<float>(Sc) : nullptr;
   // granule regions (256-byte header = abort word), zeroed by one memset before each persistent launch
   char* fsync = f.take<char>(256);
   granule_t* gS = f.take<granule_t>(2 * B * S);
@@ -232,6 +244,8 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   if (k) {
     k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
     k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
+    k->hk = (int)HK; k->hf = d.hf;
+    k->HGT = HGT; k->HCU = HCU; k->QA = QA; k->PDG = PDG; k->DGT = DGT; k->DCU = DCU;
     k->MASK = MASK;
     k->Vh = Vh; k->WS = WS; k->E = E; k->ALPHA = ALPHA; k->LSE = LSE; k->IND = IND; k->C = C; k->HX = HX;
     k->RHX = RHX; k->CY = CY; k->GSV = GSV; k->VV = VV; k->MM = MM; k->AM = AM; k->LOGP = LOGP;
@@ -256,6 +270,80 @@ __device__ __forceinline__ int brow(int b0, int lane, int B) { return min(b0 + (
 
 // ------------------------------------------------------------------ forward step kernels
 
+// ---- hybrid location-aware attention (Attention.lua:75-98), per-step path only
+// F = TemporalConvolution(1, nF, kW)(pad(alpha_{t-1})) with bias, UF = TCZB(nF, Sc, 1)(F): both are
+// linear in alpha_{t-1}, so UF_{l,j} = HCU_j + sum_i HG_{j,i} alpha_{t-1}[l + i - pad_left] with
+// HG = U W (Sc x kW) and HCU = U b, folded once per call (dec_hyb_fold).
+__device__ __forceinline__ int hyb_pad_left(int kw) { return kw % 2 ? (kw - 1) / 2 : kw / 2; }
+
+__global__ void dec_hyb_fold(AttnK k) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= k.Sc) return;
+  const int nf = k.hf, kw = k.hk;
+  const float* u = k.P.hybU + (long)j * nf;
+  for (int i = 0; i < kw; ++i) {
+    float s = 0.f;
+    for (int f = 0; f < nf; ++f) s += u[f] * k.P.hybW[f * kw + i];
+    k.HGT[(long)i * k.Sc + j] = s;
+  }
+  float c = 0.f;
+  for (int f = 0; f < nf; ++f) c += u[f] * k.P.hybb[f];
+  k.HCU[j] = c;
+}
+
+// UF of frame l for the 4 score columns of float4 c4; ap = alpha_{t-1} of the utterance (nullptr at t = 0)
+__device__ __forceinline__ float4 hyb_uf4(const AttnK& k, int c4, const float* ap, int l) {
+  float4 u = reinterpret_cast<const float4*>(k.HCU)[c4];
+  if (ap) {
+    const int pl = hyb_pad_left(k.hk);
+    for (int i = 0; i < k.hk; ++i) {
+      const int m = l + i - pl;
+      if (m < 0 || m >= k.L) continue;
+      const float a = ap[m];
+      const float4 g = reinterpret_cast<const float4*>(k.HGT + (long)i * k.Sc)[c4];
+      u.x += g.x * a; u.y += g.y * a; u.z += g.z * a; u.w += g.w * a;
+    }
+  }
+  return u;
+}
+
+// d alpha_t[l] from the hybrid features of step t + 1: sum_i q_{t+1}[l - i + pad_left][i]
+__device__ __forceinline__ float hyb_carry(const AttnK& k, int b, int l) {
+  if (k.t + 1 >= k.T) return 0.f;
+  const int kw = k.hk, pl = hyb_pad_left(kw);
+  const float* q = k.QA + ((long)((k.t + 1) & 1) * k.B + b) * k.L * kw;
+  float s = 0.f;
+  for (int i = 0; i < kw; ++i) {
+    const int lp = l - i + pl;
+    if (lp >= 0 && lp < k.L) s += q[(long)lp * kw + i];
+  }
+  return s;
+}
+
+// weight gradients of the hybrid features from DGT = sum dG^T (kW x Sc) and DCU = sum dws (Sc):
+// G = U W, cu = U b  ->  dU = dG W^T + dcu b^T, dW = U^T dG, db = U^T dcu
+__global__ void dec_hyb_wgrad(AttnK k, AttnGrads G, float scale) {
+  const int nf = k.hf, kw = k.hk, Sc = k.Sc;
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < Sc * nf) {
+    const int j = idx / nf, f = idx % nf;
+    float v = 0.f;
+    for (int i = 0; i < kw; ++i) v += k.DGT[(long)i * Sc + j] * k.P.hybW[f * kw + i];
+    v += k.DCU[j] * k.P.hybb[f];
+    G.hybU[idx] += scale * v;
+  } else if (idx < Sc * nf + nf * kw) {
+    const int r = idx - Sc * nf, f = r / kw, i = r % kw;
+    float v = 0.f;
+    for (int j = 0; j < Sc; ++j) v += k.P.hybU[(long)j * nf + f] * k.DGT[(long)i * Sc + j];
+    G.hybW[r] += scale * v;
+  } else if (idx < Sc * nf + nf * kw + nf) {
+    const int f = idx - Sc * nf - nf * kw;
+    float v = 0.f;
+    for (int j = 0; j < Sc; ++j) v += k.P.hybU[(long)j * nf + f] * k.DCU[j];
+    G.hybb[f] += scale * v;
+  }
+}
+
 // F1: ws[b] = Ws s_{t-1}[b] + bs  (N = Sc, K = S)
 __global__ __launch_bounds__(256) void dec_f1_ws(AttnK k) {
   __shared__ SkinnyRed red;
@@ -279,16 +367,22 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
   const int L = k.L, Sc = k.Sc, A = k.A;
   const float* ws = k.WS + ((long)b * k.T + t) * Sc;
   const float* we = k.P.we;
+  const float* ap = (k.hf > 0 && t > 0) ? k.ALPHA + ((long)b * k.T + t - 1) * L : nullptr;  // alpha_{t-1}
   for (int i = 0; i < 4; ++i) {
     const int li = wave * 4 + i, l = ch * LC + li;
     float part = 0.f;
     if (l < L) {
       const float* vh = k.Vh + ((long)b * L + l) * Sc;
       for (int c4 = lane; c4 < Sc / 4; c4 += 64) {
-        const float4 v = reinterpret_cast<const float4*>(vh)[c4];
+        float4 v = reinterpret_cast<const float4*>(vh)[c4];
         const float4 w = reinterpret_cast<const float4*>(ws)[c4];
         const float4 e = reinterpret_cast<const float4*>(we)[c4];
-        part += e.x * tanhf(w.x + v.x) + e.y * tanhf(w.y + v.y) + e.z * tanhf(w.z + v.z) + e.w * tanhf(w.w + v.w);
+        float4 z = make_float4(w.x + v.x, w.y + v.y, w.z + v.z, w.w + v.w);
+        if (k.hf > 0) {  // Z = Ws + Vh + UF (Attention.lua:95)
+          const float4 u = hyb_uf4(k, c4, ap, l);
+          z.x += u.x; z.y += u.y; z.z += u.z; z.w += u.w;
+        }
+        part += e.x * tanhf(z.x) + e.y * tanhf(z.y) + e.z * tanhf(z.z) + e.w * tanhf(z.w);
       }
     }
     part = wave_sum(part);
@@ -608,6 +702,9 @@ __global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
 //   d alpha_l = dc . h_l + carry_l + gdiff_l      (MM bwd + MonotonicAlignment.lua:44-77)
 //   de_l = alpha_l (d alpha_l - sum_j alpha_j d alpha_j)   with sum = dc . c + sum alpha (carry + gdiff)
 //   dh_l += alpha_l dc;  dZ = de_l we (1 - tanh^2);  dVh_l += dZ;  partial dws, dwe
+//   HYB (hybrid attention): Z includes UF; d alpha_l also gets the carry from step t+1's location
+//   features (hyb_carry); q_{l,i} = sum_j dZ_lj HG_ji -> QA for step t-1; dG partials -> PDG
+template <bool HYB>
 __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   __shared__ float redv[4];
   __shared__ float pws[4][1024];
@@ -623,7 +720,9 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   // sum_j alpha_j d alpha_j
   float part = 0.f;
   for (int a = tid; a < A; a += 256) part += dc[a] * c[a];
-  for (int l = tid; l < L; l += 256) part += alpha[l] * (lam * (float)(L - l) * (ind - indn));
+  for (int l = tid; l < L; l += 256)
+    part += alpha[l] * (HYB ? lam * (float)(L - l) * (ind - indn) + hyb_carry(k, b, l)
+                            : lam * (float)(L - l) * (ind - indn));
   part = wave_sum(part);
   if (lane == 0) redv[wave] = part;
   __syncthreads();
@@ -634,6 +733,16 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   float dwsp[16], dwep[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dwsp[i] = 0.f; dwep[i] = 0.f; }
+  constexpr int HK = HYB ? kMaxHybK : 1;
+  float dgp[HK][16];  // dG partials: [tap i][column 4 c4 + e of this lane]
+  if (HYB) {
+#pragma unroll
+    for (int i = 0; i < HK; ++i)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) dgp[i][e] = 0.f;
+  }
+  const float* ap = (HYB && t > 0) ? k.ALPHA + (row - 1) * L : nullptr;  // alpha_{t-1}
+  const int pl = HYB ? hyb_pad_left(k.hk) : 0;
   for (int i4 = 0; i4 < 4; ++i4) {
     const int l = ch * LC + wave * 4 + i4;
     if (l >= L) break;
@@ -646,8 +755,14 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     }
     dd = wave_sum(dd);
     const float al = alpha[l];
-    const float dal = dd + lam * (float)(L - l) * (ind - indn);
+    const float dal = HYB ? dd + (lam * (float)(L - l) * (ind - indn) + hyb_carry(k, b, l))
+                          : dd + lam * (float)(L - l) * (ind - indn);
     const float de = al * (dal - ssum);
+    float qv[HK];
+    if (HYB) {
+#pragma unroll
+      for (int i = 0; i < HK; ++i) qv[i] = 0.f;
+    }
     float* dhl = k.dh + ((long)b * L + l) * k.lddh;
     for (int a = lane; a < A; a += 64) dhl[a] += al * dc[a];
     const float* vh = k.Vh + ((long)b * L + l) * Sc;
@@ -660,13 +775,39 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
         const float4 w = reinterpret_cast<const float4*>(ws)[c4];
         const float4 e = reinterpret_cast<const float4*>(we)[c4];
         float4 o = reinterpret_cast<float4*>(dvh)[c4];
-        const float th0 = tanhf(w.x + v.x), th1 = tanhf(w.y + v.y), th2 = tanhf(w.z + v.z), th3 = tanhf(w.w + v.w);
+        float4 zz = make_float4(w.x + v.x, w.y + v.y, w.z + v.z, w.w + v.w);
+        if (HYB) {
+          const float4 u = hyb_uf4(k, c4, ap, l);
+          zz.x += u.x; zz.y += u.y; zz.z += u.z; zz.w += u.w;
+        }
+        const float th0 = tanhf(zz.x), th1 = tanhf(zz.y), th2 = tanhf(zz.z), th3 = tanhf(zz.w);
         const float z0 = de * e.x * (1.f - th0 * th0), z1 = de * e.y * (1.f - th1 * th1);
         const float z2 = de * e.z * (1.f - th2 * th2), z3 = de * e.w * (1.f - th3 * th3);
+        if (HYB) {
+#pragma unroll
+          for (int ii = 0; ii < HK; ++ii) {
+            if (ii >= k.hk) break;
+            const float4 g = reinterpret_cast<const float4*>(k.HGT + (long)ii * Sc)[c4];
+            qv[ii] += ((z0 * g.x + z1 * g.y) + z2 * g.z) + z3 * g.w;
+            const int m = l + ii - pl;
+            const float a = (ap && m >= 0 && m < L) ? ap[m] : 0.f;
+            dgp[ii][4 * i] += z0 * a; dgp[ii][4 * i + 1] += z1 * a;
+            dgp[ii][4 * i + 2] += z2 * a; dgp[ii][4 * i + 3] += z3 * a;
+          }
+        }
         o.x += z0; o.y += z1; o.z += z2; o.w += z3;
         reinterpret_cast<float4*>(dvh)[c4] = o;
         dwsp[4 * i] += z0; dwsp[4 * i + 1] += z1; dwsp[4 * i + 2] += z2; dwsp[4 * i + 3] += z3;
         dwep[4 * i] += de * th0; dwep[4 * i + 1] += de * th1; dwep[4 * i + 2] += de * th2; dwep[4 * i + 3] += de * th3;
+      }
+    }
+    if (HYB) {  // q_{l,i} for d alpha_{t-1} (read by step t-1's kernel through hyb_carry)
+      float* qa = k.QA + ((long)(t & 1) * k.B + b) * L * k.hk + (long)l * k.hk;
+#pragma unroll
+      for (int ii = 0; ii < HK; ++ii) {
+        if (ii >= k.hk) break;
+        const float s = wave_sum(qv[ii]);
+        if (lane == 0) qa[ii] = s;
       }
     }
   }
@@ -689,6 +830,22 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     for (int kk = tid; kk < Sc; kk += 256) {
       const float v = ((pws[0][kk] + pws[1][kk]) + pws[2][kk]) + pws[3][kk];
       if (pass == 0) pd[kk] = v; else pe[kk] += v;
+    }
+  }
+  if (HYB) {  // dG partials of this chunk, accumulated over the steps (PDG zeroed before the loop)
+    for (int ii = 0; ii < k.hk && ii < HK; ++ii) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c4 = lane + 64 * i;
+        if (c4 < Sc / 4) {
+          float* dst = &pws[wave][4 * c4];
+          dst[0] = dgp[ii][4 * i]; dst[1] = dgp[ii][4 * i + 1]; dst[2] = dgp[ii][4 * i + 2]; dst[3] = dgp[ii][4 * i + 3];
+        }
+      }
+      __syncthreads();
+      float* pg = k.PDG + (((long)b * k.NCH + ch) * k.hk + ii) * Sc;
+      for (int kk = tid; kk < Sc; kk += 256) pg[kk] += ((pws[0][kk] + pws[1][kk]) + pws[2][kk]) + pws[3][kk];
     }
   }
 }
@@ -798,6 +955,8 @@ int attn_check_dims(const AttnDims& d) {
   S2S_REQUIRE(d.Sc <= 1024, "attn: scoreDepth > 1024 not supported");
   S2S_REQUIRE(d.O > 0 && d.M > 0 && d.K > 0, "attn: bad output/mlp dims");
   S2S_REQUIRE(d.dropout >= 0.f && d.dropout < 1.f, "attn: dropout must be in [0, 1)");
+  S2S_REQUIRE(d.hf >= 0 && (d.hf == 0 || (d.hk >= 1 && d.hk <= kMaxHybK)),
+              "attn: hybridAttendFilterSize must be in [1, 8] when hybridAttendFeatureMaps > 0");
   return 0;
 }
 
@@ -834,6 +993,7 @@ static unsigned long long* g_dec_stamps[2] = {nullptr, nullptr};
 static int dec_persist_variant(const AttnDims& d) {
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && std::strcmp(m, "step") == 0) return 0;
+  if (d.hf > 0) return 0;
   if ((d.L + LC - 1) / LC > 256) return 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) return 1;
   if (d.S == 64 && d.A == 128 && d.Sc == 128) return 2;
@@ -996,6 +1156,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     S2S_CHECK_HIP(hipGetLastError());
   } else {
   ProfScope ps(st, "dec_fwd_steps", 0.0, 0.0);
+  if (d.hf > 0) hipLaunchKernelGGL(dec_hyb_fold, dim3((d.Sc + 255) / 256), dim3(256), 0, st, k);
   for (int t = 0; t < T; ++t) {
     k.t = t;
     hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
@@ -1101,6 +1262,10 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_CHECK_HIP(hipGetLastError());
   } else {
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  if (d.hf > 0) {
+    S2S_CHECK_HIP(hipMemsetAsync(k.QA, 0, sizeof(float) * 2 * (size_t)B * L * d.hk, st));
+    S2S_CHECK_HIP(hipMemsetAsync(k.PDG, 0, sizeof(float) * (size_t)B * k.NCH * d.hk * Sc, st));
+  }
   ProfScope ps(st, "dec_bwd_steps", 0.0, 0.0);
   for (int t = T - 1; t >= 0; --t) {
     k.t = t;
@@ -1108,7 +1273,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_b6_attn, dim3(k.NCH, B), dim3(256), 0, st, k);
+    if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), 0, st, k);
+    else hipLaunchKernelGGL(dec_b6_attn<false>, dim3(k.NCH, B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b7_dws, dim3(B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
@@ -1164,6 +1330,14 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
   S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));
   S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs));
   S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we));
+  if (d.hf > 0) {  // hybrid features: dG (sum over utterances, chunks; steps summed in the loop), dcu = sum dws
+    k.P = P;
+    S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT));
+    S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, 1.f, 0.f, k.DCU));
+    const int n = Sc * d.hf + d.hf * d.hk + d.hf;
+    hipLaunchKernelGGL(dec_hyb_wgrad, dim3((n + 255) / 256), dim3(256), 0, st, k, G, scale);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
   return 0;
 }
 

@@ -107,8 +107,14 @@ int set_device(s2s_ctx* ctx) {
 }
 
 AttnDims to_attn(const s2s_attn_dims* d) {
-  return AttnDims{d->B, d->L, d->T, d->annotationDepth, d->scoreDepth, d->stateDepth, d->outputDepth, d->mlpDepth,
-                  d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
+  AttnDims a{d->B, d->L, d->T, d->annotationDepth, d->scoreDepth, d->stateDepth, d->outputDepth, d->mlpDepth,
+             d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
+  a.hk = d->hybridAttendFilterSize;
+  a.hf = d->hybridAttendFeatureMaps;
+  return a;
+}
+int attn_nparams(const s2s_attn_dims* d) {
+  return d->hybridAttendFeatureMaps > 0 ? S2S_ATTN_NPARAMS_HYBRID : S2S_ATTN_NPARAMS;
 }
 
 // ------------------------------------------------------------ model layout
@@ -568,7 +574,7 @@ int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
   S2S_REQUIRE(d && h && labels && params && logp && saved, "attn: null argument");
   AttnParams ap;
   const float** pp = reinterpret_cast<const float**>(&ap);
-  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+  for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
     S2S_REQUIRE(pp[i] != nullptr, "attn: null parameter");
   }
@@ -584,7 +590,7 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
   float** gp = reinterpret_cast<float**>(&ag);
-  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i) {
+  for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
     gp[i] = grads[i];
     S2S_REQUIRE(pp[i] != nullptr && gp[i] != nullptr, "attn: null parameter/grad");

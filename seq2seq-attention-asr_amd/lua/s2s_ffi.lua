@@ -20,7 +20,8 @@ int s2s_gru_bwd(s2s_ctx*, void* stream, int ndir, int B, int L, int D, int H, co
                 const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate,
                 float* const* dW, float scale, void* scratch, size_t scratch_bytes);
 typedef struct { int B, L, T; int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
-                 float penalty; float dropout; unsigned long long dropout_seed; const float* dropout_mask; } s2s_attn_dims;
+                 float penalty; float dropout; unsigned long long dropout_seed; const float* dropout_mask;
+                 int hybridAttendFilterSize, hybridAttendFeatureMaps; } s2s_attn_dims;
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
 int s2s_attn_fwd(s2s_ctx*, void* stream, const s2s_attn_dims* d, const float* h, const int* labels,

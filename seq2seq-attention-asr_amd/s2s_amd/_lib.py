@@ -19,7 +19,7 @@ class s2s_attn_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("annotationDepth", c_int), ("scoreDepth", c_int),
                 ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
                 ("penalty", c_float), ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong),
-                ("dropout_mask", c_void_p)]
+                ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int)]
 
 
 class s2s_model_dims(ctypes.Structure):
@@ -83,6 +83,7 @@ S2S_ZERO_GRADS = 1
 S2S_NORMALIZE_NLL = 2
 S2S_BUCKET_EVENTS = 4
 S2S_ATTN_NPARAMS = 17
+S2S_ATTN_NPARAMS_HYBRID = 20
 S2S_UNIQUE_ID_BYTES = 128
 
 

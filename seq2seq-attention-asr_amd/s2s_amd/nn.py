@@ -307,8 +307,9 @@ class Attention(Module):
                  stateDepth, annotationDepth, outputDepth, monoAlignPenalty=False, penaltyLambda=0.0,
                  generator=None):
         super().__init__()
-        if hybridAttendFeatureMaps and hybridAttendFeatureMaps > 0:
-            raise NotImplementedError("hybrid (location-aware) attention is a 'next' row (SURVEY.md §8f.4)")
+        nF = int(hybridAttendFeatureMaps or 0)
+        if nF > 0 and not 1 <= int(hybridAttendFilterSize or 0) <= 8:
+            raise S2SArgumentError("hybridAttendFilterSize must be in [1, 8] with hybrid attention")
         if not isinstance(decoder_recurrent, GRU) or decoder_recurrent.dimoutput != stateDepth:
             raise S2SArgumentError("decoder_recurrent must be GRU(stateDepth, stateDepth)")
         if not isinstance(decoder_mlp, MaxoutMLP) or decoder_mlp.inputDim != stateDepth + annotationDepth:
@@ -328,6 +329,10 @@ class Attention(Module):
                "Wy": _uniform((S, O), 1 / math.sqrt(O), g), "by": _uniform((S,), 1 / math.sqrt(O), g),
                "Wc": _uniform((S, A), 1 / math.sqrt(A), g), "bc": _uniform((S,), 1 / math.sqrt(A), g),
                "Wd": _uniform((S, 2 * S), 1 / math.sqrt(2 * S), g), "bd": _uniform((S,), 1 / math.sqrt(2 * S), g)}
+        if nF > 0:  # Attention.lua:90-91: TemporalConvolution(1, nF, kW) + TCZB(nF, Sc, 1)
+            kW = int(hybridAttendFilterSize)
+            own.update({"hybW": _uniform((nF, kW), 1 / math.sqrt(kW), g), "hybb": _uniform((nF,), 1 / math.sqrt(kW), g),
+                        "hybU": _uniform((Sc, nF), 1 / math.sqrt(nF), g)})
         self.own = own
         self.own_grad = {k: torch.zeros_like(v) for k, v in own.items()}
 
@@ -335,8 +340,11 @@ class Attention(Module):
         o = self.own_grad if grads else self.own
         r = self.decoder_recurrent.gradWeight if grads else self.decoder_recurrent.weight
         m = self.decoder_mlp.gradWeight if grads else self.decoder_mlp.weight
-        return [o["V"], o["Ws"], o["bs"], o["we"], o["Wy"], o["by"], o["Wc"], o["bc"], o["Wd"], o["bd"],
-                r[0], r[1], r[2], m[0], m[1], m[2], m[3]]
+        out = [o["V"], o["Ws"], o["bs"], o["we"], o["Wy"], o["by"], o["Wc"], o["bc"], o["Wd"], o["bd"],
+               r[0], r[1], r[2], m[0], m[1], m[2], m[3]]
+        if "hybW" in o:
+            out += [o["hybW"], o["hybb"], o["hybU"]]
+        return out
 
     def parameters(self):
         return self._tensors(False), self._tensors(True)
@@ -352,6 +360,9 @@ class Attention(Module):
         p = m.dropout if (m.dropout > 0 and self.train) else 0.0
         d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
                                m.mlpDepth, m.window, self.penalty, p)
+        if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
+            d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
+            d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
         if p > 0:
             self._fwd_count = getattr(self, "_fwd_count", 0) + 1
             d.dropout_seed = (self.dropout_seed * 1000003 + self._fwd_count) & ((1 << 64) - 1)

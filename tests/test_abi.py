@@ -77,7 +77,12 @@ def test_errors_are_reported_not_aborted():
 
 def test_unsupported_configs_raise():
     import s2s_amd
-    with pytest.raises(NotImplementedError):
-        s2s_amd.Attention(s2s_amd.GRU(16, 16), s2s_amd.MaxoutMLP(48, 4, 7, 10), 32, 5, 16, 16, 32, 10, True, 0)
+    # hybrid attention needs a filter of 1..8 taps (kMaxHybK); the baseline (0 maps) any value
+    with pytest.raises(s2s_amd.nn.S2SArgumentError):
+        s2s_amd.Attention(s2s_amd.GRU(16, 16), s2s_amd.MaxoutMLP(48, 4, 7, 10), 32, 0, 16, 16, 32, 10, True, 0)
+    with pytest.raises(s2s_amd.nn.S2SArgumentError):
+        s2s_amd.Attention(s2s_amd.GRU(16, 16), s2s_amd.MaxoutMLP(48, 4, 7, 10), 32, 9, 16, 16, 32, 10, True, 0)
+    att = s2s_amd.Attention(s2s_amd.GRU(16, 16), s2s_amd.MaxoutMLP(48, 4, 7, 10), 32, 5, 16, 16, 32, 10, True, 0)
+    assert [tuple(t.shape) for t in att.parameters()[0][17:]] == [(16, 5), (16,), (32, 16)]
     with pytest.raises(s2s_amd.nn.S2SArgumentError):
         s2s_amd.RNN(s2s_amd.GRU(5, 10))

@@ -166,17 +166,18 @@ def test_xcd_decoder_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen, local)
         fn(1)
 
 
-def _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen):
+def _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen, kW=10, nF=0):
     rng = np.random.default_rng(L * 7 + T)
     torch.manual_seed(L * 7 + T)  # module init draws from torch's generator
     cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
-                          outputDepth=O, mlpDepth=M, maxoutWindow=K, penalty=pen, numLayers=1)
+                          outputDepth=O, mlpDepth=M, maxoutWindow=K, penalty=pen, numLayers=1,
+                          hybridAttendFilterSize=kW if nF else 0, hybridAttendFeatureMaps=nF)
     dec_gru = s2s.GRU(S, S)
     mlp = s2s.MaxoutMLP(S + A, M, K, O)
-    att = s2s.Attention(dec_gru, mlp, Sc, 10, 0, S, A, O, True, pen).cuda()
+    att = s2s.Attention(dec_gru, mlp, Sc, kW, nF, S, A, O, True, pen).cuda()
     P = {n: t.cpu().double().numpy() for n, t in zip(
         ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "dec.Wz", "dec.Wr", "dec.Wh", "Wm", "bm", "Wo",
-         "bo"), att.parameters()[0])}
+         "bo", "hybW", "hybb", "hybU"), att.parameters()[0])}
     h = rng.standard_normal((B, L, A)) * 0.5
     labels = rng.integers(0, O, (B, T)).astype(np.int32)
     hs = cu(h)
@@ -194,6 +195,19 @@ def _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen):
     assert_rel(dh, dhr, "dh")
     for name, g in zip(P.keys(), att.parameters()[1]):
         assert_rel(g.cpu().numpy(), G[name], "d" + name)
+
+
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O,M,K,pen,kW,nF", [
+    (3, 37, 7, 32, 48, 32, 11, 4, 3, 0.0, 5, 6),      # the reference's fallback filter (timit.lua:129-130), ragged chunk
+    (2, 20, 6, 32, 32, 16, 9, 3, 2, 0.3, 4, 3),       # even filter (pads kW/2 left, kW/2-1 right), penalty on
+    (4, 128, 12, 512, 512, 256, 62, 8, 7, 0.0, 5, 16),  # Chorowski sizes with hybrid features on
+])
+def test_hybrid_attention_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen, kW, nF):
+    """Hybrid location-aware attention (Attention.lua:75-98): UF = TCZB(nF, Sc, 1)(
+    TemporalConvolution(1, nF, kW)(pad(alpha_{t-1}))) added to the scores; the backward carries
+    d alpha_{t-1} into the previous step's softmax.  Per-step kernels vs the oracle (itself pinned by
+    torch autograd and finite differences), forward, dh and every gradient incl. the conv's."""
+    _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen, kW, nF)
 
 
 def _adopt_mono_decisions(att, cache, L, margin=1e-4):
