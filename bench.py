@@ -227,6 +227,19 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     ms = 1000.0 * elapsed / args.steps
+    # the optimizer (timit.lua:292-347: clip, adadelta, column-norm constraint) is outside t_step
+    #  and reported on its own: device step on the flat buffers, HBM-bound
+    opt = s2s_amd.optim.Adadelta(model, rho=0.95, eps=1e-8, colnormconstr=True)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            opt.step(stream)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            opt.step(stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    opt_us = 1000.0 * e0.elapsed_time(e1) / 20
     frames_per_step = world * B * L
     value = frames_per_step / (ms / 1000.0)
 
@@ -244,6 +257,8 @@ def main():
                    "launch": "eager" if args.no_graph else "hipGraph replay",
                    "flop_per_step_per_gpu": flop_step},
         "step_tflops_per_gpu": round(flop_step / (ms / 1000.0) / 1e12, 3),
+        "optimizer": {"us_per_step": round(opt_us, 2), "what": "adadelta (rho .95, eps 1e-8) + global-norm clip + "
+                      "column-norm constraint on the flat buffers (s2s_optim_adadelta_step), not in ms_per_step"},
     }
     if rank == 0 and not args.no_kernel_timing:
         with torch.cuda.stream(stream):

@@ -178,6 +178,27 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
  * (encoder.output, timit/timit.lua:397). */
 const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace);
 
+/* ---------------------------------------------------------------- optimizer step
+ * After the (all-reduced) backward, timit/timit.lua:292-347 on the flat buffers, fused on the device:
+ * clip the global gradient norm to maxnorm (:297-302), g += weightDecay * x (:305-308), optim.adadelta
+ * (rho, eps; timit.lua:179, exp_logmel7_chorowski_normNLL_colnorm.lua:32-33), then -- colnorm_max > 0 --
+ * TrainUtils.columnNormConstraint(colnorm_max) on every weight matrix (TrainUtils.lua:52-104, applied
+ * to the graph at timit.lua:344-346): rows with ||W_r|| + 1e-8 >= max are divided by that / max.
+ * `gradients` is left clipped / decayed in place as the reference leaves it.  state: the optimizer's
+ * paramVariance / accDelta (s2s_optim_state_bytes, zero it with s2s_optim_reset).  mats: n_mats
+ * (offset, rows, cols) weight matrices of the flat buffer (s2s_model_weight_matrices for the model).
+ * gradnorm (device float, may be NULL) receives ||g|| before clipping (timit.lua:297 gradnorms). */
+typedef struct {
+  float rho, eps, maxnorm, weightDecay, colnorm_max;
+} s2s_optim_config;
+size_t s2s_optim_state_bytes(size_t n);
+int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);
+int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                            float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+/* the model's weight matrices (every module weight: encoder W_z/W_r/W_h, V, Ws, we, Wy, Wc, Wd, decoder
+ * W_z/W_r/W_h, Wm, Wo) as (offset, rows, cols) triples; returns their count (mats may be NULL) */
+int s2s_model_weight_matrices(const s2s_model_dims* d, long* mats);
+
 /* ---------------------------------------------------------------- live kernel timing
  * s2s_prof_enable(1): every subsequent eager (non-captured) launch is bracketed by two
  * hipEvents on its stream and tagged with its kernel family's algorithmic flops/bytes.

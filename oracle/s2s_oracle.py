@@ -663,3 +663,42 @@ def synthetic_batch(cfg: ModelConfig, B: int, L: int, T: int, seed: int = 1234, 
     labels = choices[rng.integers(0, len(choices), size=(B, T))]
     labels[:, -1] = eos
     return x, labels.astype(np.int32)
+
+
+# ----------------------------------------------------------------------------
+# Optimizer step (timit/timit.lua:292-347; optim.adadelta (3p); TrainUtils.lua:52-104)
+# ----------------------------------------------------------------------------
+
+def column_norm_constraint(W: Array, maxval: float = 1.0) -> Array:
+    """TrainUtils.columnNormConstraint (TrainUtils.lua:52-104): norm = W:norm(2,2) + 1e-8 (per
+    output row of W (out, in)); rows with norm >= maxval are divided by norm / maxval (:64-79)."""
+    norm = np.sqrt((W * W).sum(1, keepdims=True)) + 1e-8
+    div = np.where(norm >= maxval, norm / maxval, 1.0)
+    return W / div
+
+
+def optimizer_step(x: Array, g: Array, state: Dict[str, Array], rho: float = 0.95, eps: float = 1e-8,
+                   maxnorm: float = 1e20, weightDecay: float = 0.0, colnorm_max: float = 0.0, mats=()):
+    """One optimizer step on the flat buffers after the (1/B-scaled) backward:
+    clip on the global norm (timit.lua:297-302), L2 (:305-308), optim.adadelta (3p) -- v = rho v +
+    (1-rho) g^2; delta = sqrt(u + eps) / sqrt(v + eps) * g; x -= delta; u = rho u + (1-rho) delta^2 --
+    and the column-norm constraint on every weight matrix (:344-346).  mats: (offset, rows, cols).
+    Updates x, g, state in place; returns ||g|| before clipping."""
+    gn = float(np.sqrt((g * g).sum()))
+    if gn > maxnorm:
+        g *= maxnorm / gn
+    if weightDecay > 0:
+        g += weightDecay * x
+    v = state.setdefault("paramVariance", np.zeros_like(x))
+    u = state.setdefault("accDelta", np.zeros_like(x))
+    v *= rho
+    v += (1 - rho) * g * g
+    delta = np.sqrt(u + eps) / np.sqrt(v + eps) * g
+    x -= delta
+    u *= rho
+    u += (1 - rho) * delta * delta
+    if colnorm_max > 0:
+        for off, r, c in mats:
+            W = x[off:off + r * c].reshape(r, c)
+            W[...] = column_norm_constraint(W, colnorm_max)
+    return gn

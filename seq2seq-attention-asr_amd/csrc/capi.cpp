@@ -686,6 +686,48 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   return 0;
 }
 
+int s2s_model_weight_matrices(const s2s_model_dims* d, long* mats) {
+  if (check_model_dims(d) != 0) return -1;
+  const std::vector<long> sizes = param_sizes(d);
+  std::vector<long> t;
+  long off = 0;
+  int p = 0;
+  for (auto& ld : enc_layers(d))
+    for (int i = 0; i < 6; ++i, ++p) {
+      t.insert(t.end(), {off, (long)ld.H, (long)ld.H + ld.D});
+      off += sizes[p];
+    }
+  const long A = 2L * d->outputFrameSize, Sc = d->scoreDepth, S = d->stateDepth, O = d->outputDepth,
+             M = d->mlpDepth, Mk = (long)d->mlpDepth * d->maxoutWindow;
+  // decoder parameters in s2s_attn order; rows x cols of the weights, 0 for the biases
+  const long shp[S2S_ATTN_NPARAMS][2] = {{Sc, A}, {Sc, S}, {0, 0}, {1, Sc}, {S, O}, {0, 0}, {S, A}, {0, 0},
+                                         {S, 2 * S}, {0, 0}, {S, 2 * S}, {S, 2 * S}, {S, 2 * S}, {Mk, S + A},
+                                         {0, 0}, {O, M}, {0, 0}};
+  for (int i = 0; i < S2S_ATTN_NPARAMS; ++i, ++p) {
+    if (shp[i][0] > 0) t.insert(t.end(), {off, shp[i][0], shp[i][1]});
+    off += sizes[p];
+  }
+  if (mats) std::copy(t.begin(), t.end(), mats);
+  return (int)(t.size() / 3);
+}
+
+size_t s2s_optim_state_bytes(size_t n) { return optim_state_bytes(n); }
+
+int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(state && n > 0, "optim: null state");
+  return optim_state_reset(static_cast<hipStream_t>(stream), state, n);
+}
+
+int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                            float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(cfg != nullptr, "optim: null config");
+  S2S_REQUIRE(cfg->rho >= 0.f && cfg->rho < 1.f && cfg->eps > 0.f && cfg->maxnorm > 0.f, "optim: bad config");
+  return optim_adadelta_step(static_cast<hipStream_t>(stream), cfg->rho, cfg->eps, cfg->maxnorm, cfg->weightDecay,
+                             cfg->colnorm_max, params, grads, n, state, mats, n_mats, gradnorm);
+}
+
 int s2s_model_bucket_count(const s2s_model_dims* d) {
   if (check_model_dims(d) != 0) return -1;
   return d->numLayers + 1;

@@ -1,0 +1,156 @@
+// Optimizer step on the flat parameter / gradient buffers, fused on the device:
+// what timit/timit.lua:292-347 does after the backward, minus the host round trips --
+//   gradient clipping on the global norm       (timit.lua:297-302: if ||g|| > maxnorm: g *= maxnorm/||g||)
+//   L2 regularisation                          (timit.lua:305-308: g += weightDecay * x)
+//   optim.adadelta (3p, rho / eps config)      (timit.lua:179, exp_logmel7_chorowski_normNLL_colnorm.lua:32-33)
+//   TrainUtils.columnNormConstraint(maxval)    (timit.lua:344-346, TrainUtils.lua:52-104) on every weight matrix
+// The 1/B normalisation (timit.lua:292-295) is the model step's `scale`.
+//
+// HBM-bound elementwise work: the norm is a two-pass deterministic reduction (fixed per-block
+// order, then one block over the partials), the update one pass reading x, g, v, u and writing
+// x, g, v, u (32 B per parameter), the constraint one wave per weight row.  No host sync: the clip
+// factor stays on the device.
+#include "s2s_common.h"
+
+#include <algorithm>
+
+namespace s2s {
+
+namespace {
+
+constexpr int kNormBlocks = 512;
+constexpr int kMaxMats = 64;
+
+struct OptState {
+  float* v;        // optim.adadelta paramVariance
+  float* u;        // optim.adadelta accDelta
+  float* partial;  // [kNormBlocks] sums of squares
+  float* scal;     // [0] ||g||, [1] clip factor
+};
+
+OptState carve_state(void* state, size_t n) {
+  char* p = static_cast<char*>(state);
+  const size_t nn = (n + 63) / 64 * 64;
+  OptState s;
+  s.v = reinterpret_cast<float*>(p);
+  s.u = s.v + nn;
+  s.partial = s.u + nn;
+  s.scal = s.partial + kNormBlocks;
+  return s;
+}
+
+__global__ __launch_bounds__(256) void opt_sumsq(const float* __restrict__ g, size_t n, float* partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x) s += g[i] * g[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+__global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb, float maxnorm, float* scal,
+                                                    float* gradnorm_out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float gn = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+    scal[0] = gn;
+    scal[1] = gn > maxnorm ? maxnorm / gn : 1.f;
+    if (gradnorm_out) *gradnorm_out = gn;
+  }
+}
+
+// optim.adadelta (3p):  v = rho v + (1-rho) g^2;  std = sqrt(v + eps);
+//   delta = sqrt(u + eps) / std * g;  x -= delta;  u = rho u + (1-rho) delta^2
+__global__ __launch_bounds__(256) void opt_adadelta(float* __restrict__ x, float* __restrict__ g,
+                                                    float* __restrict__ v, float* __restrict__ u, size_t n,
+                                                    const float* scal, float rho, float eps, float wd) {
+  const float clip = scal[1];
+  for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x) {
+    float gi = g[i];
+    if (clip != 1.f) gi = gi * clip;
+    const float xi = x[i];
+    if (wd != 0.f) gi = gi + wd * xi;
+    const float vi = v[i] * rho + (1.f - rho) * (gi * gi);
+    const float sd = sqrtf(vi + eps);
+    const float ui = u[i];
+    const float delta = sqrtf(ui + eps) / sd * gi;
+    x[i] = xi - delta;
+    v[i] = vi;
+    u[i] = ui * rho + (1.f - rho) * (delta * delta);
+    g[i] = gi;  // the reference clips / decays `gradients` in place
+  }
+}
+
+struct MatTable {
+  long off[kMaxMats];
+  int rows[kMaxMats], cols[kMaxMats], first[kMaxMats + 1];  // first[m] = global index of matrix m's row 0
+  int n;
+};
+
+// TrainUtils.columnNormConstraint: norm_r = ||W_r||_2 + 1e-8 over each output row (W:norm(2,2));
+// rows with norm >= maxval are divided by norm / maxval, the others kept.  One wave per row.
+__global__ __launch_bounds__(256) void opt_colnorm(float* __restrict__ x, MatTable t, float maxval) {
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (row >= t.first[t.n]) return;
+  int m = 0;
+  while (row >= t.first[m + 1]) ++m;
+  const int r = row - t.first[m], cols = t.cols[m];
+  float* w = x + t.off[m] + (long)r * cols;
+  float s = 0.f;
+  for (int c = lane; c < cols; c += 64) s += w[c] * w[c];
+  s = wave_sum(s);
+  const float norm = sqrtf(s) + 1e-8f;
+  if (norm < maxval) return;
+  const float div = norm / maxval;
+  for (int c = lane; c < cols; c += 64) w[c] = w[c] / div;
+}
+
+}  // namespace
+
+size_t optim_state_bytes(size_t n) {
+  const size_t nn = (n + 63) / 64 * 64;
+  return sizeof(float) * (2 * nn + kNormBlocks + 64);
+}
+
+int optim_adadelta_step(hipStream_t st, float rho, float eps, float maxnorm, float wd, float colnorm_max,
+                        float* x, float* g, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
+  S2S_REQUIRE(x && g && state && n > 0, "optim: null argument");
+  S2S_REQUIRE(colnorm_max <= 0.f || (mats && n_mats > 0 && n_mats <= kMaxMats), "optim: bad weight-matrix table");
+  const OptState s = carve_state(state, n);
+  const int nb = (int)std::min<size_t>(kNormBlocks, (n + 255) / 256);
+  hipLaunchKernelGGL(opt_sumsq, dim3(nb), dim3(256), 0, st, g, n, s.partial);
+  hipLaunchKernelGGL(opt_finalize, dim3(1), dim3(256), 0, st, s.partial, nb, maxnorm, s.scal, gradnorm);
+  const int ne = (int)std::min<size_t>(2048, (n + 255) / 256);
+  hipLaunchKernelGGL(opt_adadelta, dim3(ne), dim3(256), 0, st, x, g, s.v, s.u, n, s.scal, rho, eps, wd);
+  if (colnorm_max > 0.f) {
+    MatTable t{};
+    t.n = n_mats;
+    t.first[0] = 0;
+    for (int m = 0; m < n_mats; ++m) {
+      t.off[m] = mats[3 * m];
+      t.rows[m] = (int)mats[3 * m + 1];
+      t.cols[m] = (int)mats[3 * m + 2];
+      S2S_REQUIRE(t.off[m] >= 0 && t.rows[m] > 0 && t.cols[m] > 0 &&
+                      (size_t)t.off[m] + (size_t)t.rows[m] * t.cols[m] <= n,
+                  "optim: weight matrix outside the flat buffer");
+      t.first[m + 1] = t.first[m] + t.rows[m];
+    }
+    hipLaunchKernelGGL(opt_colnorm, dim3((t.first[n_mats] + 3) / 4), dim3(256), 0, st, x, t, colnorm_max);
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// zero paramVariance / accDelta (optim.adadelta's lazily created state)
+int optim_state_reset(hipStream_t st, void* state, size_t n) {
+  S2S_CHECK_HIP(hipMemsetAsync(state, 0, optim_state_bytes(n), st));
+  return 0;
+}
+
+}  // namespace s2s

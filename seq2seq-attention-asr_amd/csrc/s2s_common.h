@@ -132,4 +132,10 @@ struct Bump {
   }
 };
 
+// ---------------------------------------------------------------- optimizer (optim.hip)
+size_t optim_state_bytes(size_t n);
+int optim_state_reset(hipStream_t st, void* state, size_t n);
+int optim_adadelta_step(hipStream_t st, float rho, float eps, float maxnorm, float wd, float colnorm_max,
+                        float* x, float* g, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+
 }  // namespace s2s

@@ -38,6 +38,11 @@ int s2s_comm_unique_id(void* out_bytes);
 int s2s_comm_init(s2s_ctx* ctx, const void* id_bytes, int nranks, int rank);
 int s2s_allreduce_sum(s2s_ctx* ctx, void* stream, float* buf, size_t count);
 int s2s_stream_wait_bucket(s2s_ctx* ctx, void* stream, int i);
+typedef struct { float rho, eps, maxnorm, weightDecay, colnorm_max; } s2s_optim_config;
+size_t s2s_optim_state_bytes(size_t n);
+int s2s_optim_reset(s2s_ctx* ctx, void* stream, void* state, size_t n);
+int s2s_optim_adadelta_step(s2s_ctx* ctx, void* stream, const s2s_optim_config* cfg, float* params,
+                            float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
 ]]
 
 local C = ffi.load('s2s_hip')

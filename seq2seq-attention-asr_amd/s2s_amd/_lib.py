@@ -22,6 +22,11 @@ class s2s_attn_dims(ctypes.Structure):
                 ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int)]
 
 
+class s2s_optim_config(ctypes.Structure):
+    _fields_ = [("rho", c_float), ("eps", c_float), ("maxnorm", c_float), ("weightDecay", c_float),
+                ("colnorm_max", c_float)]
+
+
 class s2s_model_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("inputFrameSize", c_int), ("hiddenFrameSize", c_int),
                 ("outputFrameSize", c_int), ("numLayers", c_int), ("scoreDepth", c_int), ("stateDepth", c_int),
@@ -69,6 +74,11 @@ SIGNATURES = [
     ("s2s_model_encoder_output", c_void_p, [P(s2s_model_dims), c_void_p]),
     ("s2s_prof_enable", c_int, [c_int]),
     ("s2s_prof_collect", c_int, [ctypes.c_char_p, c_size_t]),
+    ("s2s_optim_state_bytes", c_size_t, [c_size_t]),
+    ("s2s_optim_reset", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
+    ("s2s_optim_adadelta_step", c_int, [c_void_p, c_void_p, P(s2s_optim_config), c_void_p, c_void_p, c_size_t,
+                                        c_void_p, c_void_p, c_int, c_void_p]),
+    ("s2s_model_weight_matrices", c_int, [P(s2s_model_dims), c_void_p]),
     ("s2s_model_bucket_count", c_int, [P(s2s_model_dims)]),
     ("s2s_model_bucket", c_int, [P(s2s_model_dims), c_int, P(c_size_t), P(c_size_t)]),
     ("s2s_stream_wait_bucket", c_int, [c_void_p, c_void_p, c_int]),

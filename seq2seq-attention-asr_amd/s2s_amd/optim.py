@@ -1,0 +1,61 @@
+"""Device optimizer step: timit/timit.lua:292-347 on the flat buffers --
+global-norm clip, L2, optim.adadelta and TrainUtils.columnNormConstraint -- in one stream-ordered
+sequence of kernels (libs2s_hip.so: s2s_optim_adadelta_step), no host round trip.
+
+    opt = Adadelta(model, rho=0.95, eps=1e-8, colnormconstr=True)   # exp_logmel7_..._colnorm.lua
+    model.step(x, labels)                                           # grads = mean over the batch
+    opt.step()                                                      # x updated in place
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import check, lib
+from .nn import dptr, get_context, stream_ptr
+
+
+def weight_matrices(cfg):
+    """(offset, rows, cols) of every module weight of the flat layout (s2s_model_weight_matrices)."""
+    from .model import ModelConfig  # noqa: F401
+    c = cfg
+    d = _lib.s2s_model_dims(1, 1, 1, c.inputFrameSize, c.hiddenFrameSize, c.outputFrameSize, c.numLayers,
+                            c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty, 0.0)
+    n = lib.s2s_model_weight_matrices(ctypes.byref(d), None)
+    if n < 0:
+        check(1)
+    buf = (ctypes.c_long * (3 * n))()
+    lib.s2s_model_weight_matrices(ctypes.byref(d), buf)
+    return [tuple(buf[3 * i:3 * i + 3]) for i in range(n)]
+
+
+class Adadelta:
+    """optim.adadelta with the reference trainer's surroundings (timit/timit.lua:292-347):
+    opt.maxnorm (gradient clip), opt.weightDecay (L2), opt.colnormconstr (max row norm 1).
+    params / grads: flat float32 CUDA tensors (ChorowskiBaseline.getParameters()), or pass the model."""
+
+    def __init__(self, model=None, params=None, grads=None, mats=None, rho=0.95, eps=1e-8, maxnorm=1e20,
+                 weightDecay=0.0, colnormconstr=False, colnorm_max=1.0):
+        if model is not None:
+            params, grads = model.getParameters()
+            if mats is None:
+                mats = weight_matrices(model.cfg)
+        if not (params.is_cuda and params.dtype == torch.float32 and params.is_contiguous()
+                and grads.shape == params.shape):
+            raise ValueError("params / grads must be flat contiguous float32 CUDA tensors of one size")
+        self.params, self.grads = params, grads
+        self.n = params.numel()
+        self.cfg = _lib.s2s_optim_config(rho, eps, maxnorm, weightDecay, colnorm_max if colnormconstr else 0.0)
+        mats = list(mats or [])
+        self._mats = (ctypes.c_long * max(1, 3 * len(mats)))(*[v for m in mats for v in m])
+        self._nmats = len(mats)
+        self.state = torch.zeros(lib.s2s_optim_state_bytes(self.n), dtype=torch.uint8, device=params.device)
+        self.gradnorm = torch.zeros(1, dtype=torch.float32, device=params.device)
+        self.ctx = get_context(params.device.index)
+
+    def step(self, stream=None):
+        """One update; self.gradnorm holds ||g|| before clipping (timit.lua:297 gradnorms)."""
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        check(lib.s2s_optim_adadelta_step(self.ctx.handle, st, ctypes.byref(self.cfg), dptr(self.params),
+                                          dptr(self.grads), self.n, dptr(self.state), self._mats, self._nmats,
+                                          dptr(self.gradnorm)))

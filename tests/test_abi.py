@@ -59,6 +59,20 @@ def test_grad_buckets_cover_the_flat_layout():
         assert all(o + n == o2 for (o, n), (o2, _) in zip(cover, cover[1:]))
 
 
+def test_weight_matrices_are_the_2d_params():
+    """s2s_model_weight_matrices (the column-norm constraint's targets) = every 2-D parameter of the
+    flat layout, at its offset, rows x cols = its (out, in) shape."""
+    from s2s_amd import model, optim
+    for kw in ({}, dict(numLayers=2, hiddenFrameSize=128)):
+        cfg = model.ModelConfig(**kw)
+        want, off = [], 0
+        for _, shp in model.param_shapes(cfg):
+            if len(shp) == 2:
+                want.append((off, shp[0], shp[1]))
+            off += math.prod(shp)
+        assert optim.weight_matrices(cfg) == want
+
+
 def test_chorowski_param_count():
     """4,356,735 incl. the two zero TCZB biases (512 + 1) the flat layout omits."""
     from s2s_amd import model

@@ -485,3 +485,35 @@ def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B
     for rep in range(2):
         for name, a, b in zip(names, outs["step"][rep], outs["persist"][rep]):
             assert torch.equal(a, b), f"{name} differs (rep {rep}): max |d| = {(a - b).abs().max().item():.3e}"
+
+
+@pytest.mark.parametrize("maxnorm,wd,colnorm", [(1e20, 0.0, False), (0.5, 0.0, True), (1e20, 1e-3, True)])
+def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm):
+    """Device optimizer step (s2s_optim_adadelta_step) vs the oracle's restatement of
+    timit.lua:292-347: global-norm clip, L2, optim.adadelta (rho .95, eps 1e-8,
+    exp_logmel7_chorowski_normNLL_colnorm.lua:32-33), column-norm constraint -- three steps on the
+    Chorowski flat layout, fp32 on the GPU vs float64."""
+    cfg = s2s.ModelConfig()
+    mats = s2s.optim.weight_matrices(cfg)
+    n = sum(int(np.prod(s)) for _, s in s2s.param_shapes(cfg))
+    rng = np.random.default_rng(21)
+    x = (rng.standard_normal(n) * 0.08).astype(np.float32)   # many rows above norm 1
+    xg = cu(x)
+    gg = torch.empty_like(xg)
+    opt = s2s.optim.Adadelta(params=xg, grads=gg, mats=mats, rho=0.95, eps=1e-8, maxnorm=maxnorm, weightDecay=wd,
+                             colnormconstr=colnorm)
+    xr, st = x.astype(np.float64), {}
+    for it in range(3):
+        g = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+        gg.copy_(cu(g))
+        opt.step()
+        gr = g.astype(np.float64)
+        gn = orc.optimizer_step(xr, gr, st, 0.95, 1e-8, maxnorm, wd, 1.0 if colnorm else 0.0, mats)
+        torch.cuda.synchronize()
+        assert abs(opt.gradnorm.item() - gn) <= 1e-5 * gn
+        assert_rel(gg.cpu().numpy(), gr, f"g[{it}]", 1e-5)
+        assert_rel(xg.cpu().numpy(), xr, f"x[{it}]", 1e-5)
+    if colnorm:
+        xs = xg.cpu().numpy()
+        for off, r, c in mats:
+            assert np.linalg.norm(xs[off:off + r * c].reshape(r, c), axis=1).max() <= 1.0 + 1e-5

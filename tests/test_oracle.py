@@ -213,3 +213,31 @@ def test_oracle_reproduces_chorowski_fixture():
     flatG = orc.flatten(G, cfg)
     np.testing.assert_allclose(flatG[g["grad_idx"]], g["grad_vals"], rtol=1e-9, atol=1e-14)
     assert flatG.size == 4356735 - 512 - 1  # SURVEY §8d count includes the zero TCZB biases (V: 512, we: 1)
+
+
+def test_column_norm_constraint_semantics():
+    """TrainUtils.lua:52-104: rows (W:norm(2,2)) with norm + 1e-8 >= maxval are scaled to maxval
+    (up to the 1e-8), the others untouched; applied after the update (timit.lua:344-346)."""
+    rng = np.random.default_rng(4)
+    W = rng.standard_normal((6, 9))
+    W[:3] *= 0.05                       # rows well inside the unit ball
+    out = orc.column_norm_constraint(W, 1.0)
+    np.testing.assert_array_equal(out[:3], W[:3])
+    np.testing.assert_allclose(np.linalg.norm(out[3:], axis=1), 1.0, rtol=1e-7)
+    out2 = orc.column_norm_constraint(W, 0.5)
+    assert np.all(np.linalg.norm(out2, axis=1) <= 0.5 + 1e-7)
+
+
+def test_optimizer_step_matches_adadelta_definition():
+    """optim.adadelta (3p) with the trainer's clip and L2 (timit.lua:292-308), two steps by hand."""
+    rng = np.random.default_rng(8)
+    x0 = rng.standard_normal(50)
+    g0 = rng.standard_normal(50)
+    x, g, st = x0.copy(), g0.copy(), {}
+    gn = orc.optimizer_step(x, g, st, rho=0.9, eps=1e-6, maxnorm=2.0, weightDecay=0.01)
+    assert abs(gn - np.linalg.norm(g0)) < 1e-12
+    gc = g0 * (2.0 / np.linalg.norm(g0)) + 0.01 * x0
+    v = 0.1 * gc * gc
+    d = np.sqrt(1e-6) / np.sqrt(v + 1e-6) * gc
+    np.testing.assert_allclose(x, x0 - d, rtol=1e-13)
+    np.testing.assert_allclose(st["accDelta"], 0.1 * d * d, rtol=1e-13)
