@@ -134,6 +134,20 @@ const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 /* (B, T, S+A) dropout multipliers of the last forward inside `saved` (NULL when dropout == 0) */
 const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
 
+/* decoder:BeamSearch(annotations, eos, K, maxseqlength) (Attention.lua:332-438; timit/timit.lua:401) for
+ * B utterances at once, in evaluate() mode: h (B, L, A); eos and the output tokens 0-based; out (B, ldo),
+ * ldo >= maxseqlength + 1, the best finished hypothesis of each utterance padded with -1; out_len (B);
+ * out_score (B, may be NULL) its summed log-probability.  Hypotheses finish on eos or at maxseqlength;
+ * K in [1, 16].  Blocks until done (it polls for the end of the search).  Content-only attention. */
+size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength);
+int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
+                         const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len,
+                         float* out_score, void* workspace, size_t workspace_bytes);
+/* WagnerFischer(a, b) (utils.lua:3-27) for n pairs on the device: a (n, lda) with lengths alen, b (n, ldb)
+ * with blen, out (n) the edit distances (PER/CER numerators, timit/timit.lua:396-410). */
+int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b,
+                      const int* blen, int ldb, int* out);
+
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
  * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).       */

@@ -702,3 +702,96 @@ def optimizer_step(x: Array, g: Array, state: Dict[str, Array], rho: float = 0.9
             W = x[off:off + r * c].reshape(r, c)
             W[...] = column_norm_constraint(W, colnorm_max)
     return gn
+
+
+# ----------------------------------------------------------------------------
+# Decode path: Attention:BeamSearch (Attention.lua:332-438) and WagnerFischer (utils.lua:3-27)
+# ----------------------------------------------------------------------------
+
+def decoder_step(h: Array, Vh: Array, s: Array, yprev: int, alpha_prev: Array, P: Dict[str, Array],
+                 cfg: "ModelConfig"):
+    """One decoder_base forward for one utterance (Attention.lua:51-184) in evaluate() mode:
+    h (L, A), Vh (L, Sc), s (S), yprev the previous label (-1 = zeros_y), alpha_prev (L).
+    Returns (logp (O), s_new (S), alpha (L))."""
+    O, M, k = cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
+    ws = P["Ws"] @ s + P["bs"]
+    Z = ws[None, :] + Vh
+    if cfg.hybridAttendFeatureMaps > 0:
+        Z = Z + hybrid_features(alpha_prev[None], P, cfg.hybridAttendFilterSize)[0][0]
+    e = np.tanh(Z) @ P["we"][0]
+    alpha = softmax(e, axis=0)
+    c = alpha @ h
+    y = np.zeros(O, h.dtype)
+    if yprev >= 0:
+        y[yprev] = 1.0
+    yin = P["Wy"] @ y + P["by"]
+    cin = P["Wc"] @ c + P["bc"]
+    d = P["Wd"] @ np.concatenate([cin, yin]) + P["bd"]
+    hx = np.concatenate([s, d])
+    z = sigmoid(P["dec.Wz"] @ hx)
+    r = sigmoid(P["dec.Wr"] @ hx)
+    hh = np.tanh(P["dec.Wh"] @ np.concatenate([r * s, d]))
+    s_new = (1.0 - z) * s + z * hh
+    u = P["Wm"] @ np.concatenate([s_new, c]) + P["bm"]
+    m = u.reshape(M, k).max(1)
+    logp = log_softmax(P["Wo"] @ m + P["bo"], 0)
+    return logp, s_new, alpha
+
+
+def beam_search(h: Array, P: Dict[str, Array], cfg: "ModelConfig", eos: int, K: int = 5,
+                maxseqlength: Optional[int] = None):
+    """Attention:BeamSearch (Attention.lua:332-438) for one utterance h (L, A), 0-based labels.
+    Step 0 from zeros_y / zero hidden (:356-367), torch.topk(K) sorted (:369); then while fewer
+    than K hypotheses finished and count < maxseqlength (:384): every active hypothesis k is
+    extended (p_next[k] = logp + p_beam[k], :386-399), topk(K) over the flattened candidates
+    (:400-402), of which the first K - finished are taken (:408): eos or count == maxseqlength
+    finishes (:413-417), else it survives with its parent's hidden state.  Returns
+    (prediction = the finished hypothesis of highest score (first maximum, :432-434), score)."""
+    L = h.shape[0]
+    maxlen = maxseqlength or L
+    Vh = h @ P["V"].T
+    S = cfg.stateDepth
+    logp, s, a = decoder_step(h, Vh, np.zeros(S, h.dtype), -1, np.zeros(L, h.dtype), P, cfg)
+    order = np.argsort(-logp, kind="stable")[:K]
+    beams, fin = [], []
+    for j in order:
+        if j == eos:
+            fin.append(([int(j)], float(logp[j])))
+        else:
+            beams.append(([int(j)], (s, a), float(logp[j])))
+    count = 0
+    while len(fin) < K and count < maxlen:
+        count += 1
+        nexts = []
+        for seq, (sp, ap), pb in beams:
+            lp, sn, an = decoder_step(h, Vh, sp, seq[-1], ap, P, cfg)
+            nexts.append((lp + pb, (sn, an)))
+        flat = np.concatenate([n[0] for n in nexts])
+        O = nexts[0][0].size
+        top = np.argsort(-flat, kind="stable")[:K]
+        new_beams = []
+        for idx in top[:len(beams)]:
+            i, j = divmod(int(idx), O)
+            seq = beams[i][0] + [j]
+            if j == eos or count == maxlen:
+                fin.append((seq, float(flat[idx])))
+            else:
+                new_beams.append((seq, nexts[i][1], float(flat[idx])))
+        beams = new_beams
+    best = int(np.argmax([f[1] for f in fin]))
+    return fin[best][0], fin[best][1]
+
+
+def wagner_fischer(a, b) -> int:
+    """utils.lua:3-27: Levenshtein distance (substitution, insertion, deletion cost 1)."""
+    m, n = len(a) + 1, len(b) + 1
+    d = np.zeros((m, n), np.int64)
+    d[:, 0] = np.arange(m)
+    d[0, :] = np.arange(n)
+    for j in range(1, n):
+        for i in range(1, m):
+            if a[i - 1] == b[j - 1]:
+                d[i, j] = d[i - 1, j - 1]
+            else:
+                d[i, j] = min(d[i - 1, j] + 1, d[i, j - 1] + 1, d[i - 1, j - 1] + 1)
+    return int(d[m - 1, n - 1])

@@ -59,6 +59,16 @@ const float* attn_saved_alpha(const AttnDims& d, const void* saved);
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
 const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved);
 
+// Attention:BeamSearch (Attention.lua:332-438) for B utterances: h (B, L, A); labels 0-based; out
+// (B, ldo >= maxlen + 1) best hypothesis per utterance (tokens, -1 padded), out_len, out_score (its
+// summed log-probability).  Synchronises the stream (stops when every utterance has K finished).
+size_t attn_beam_workspace_bytes(const AttnDims& d, int K, int maxlen);
+int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K,
+                     int maxlen, int* out, int ldo, int* out_len, float* out_score, void* ws, size_t ws_bytes);
+// WagnerFischer (utils.lua:3-27) over n sequence pairs (row-major, lengths alen / blen)
+int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda, const int* b, const int* blen,
+                  int ldb, int* out);
+
 // -log p of the labels and the reference's seed dlogp = -labelmask (timit/timit.lua:262-282).
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
              float* dlogp);

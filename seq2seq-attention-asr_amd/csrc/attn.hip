@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "handoff.h"
 #include "skinny.h"
@@ -483,7 +484,9 @@ __global__ __launch_bounds__(256) void dec_f4_cin(AttnK k) {
   const long row = (long)b * k.T + t;
   k.CY[row * 2 * S + n] = s + k.P.bc[n];
   float yin = k.P.by[n];
-  if (t > 0) yin += k.P.Wy[(long)n * k.O + k.labels[(long)b * k.T + t - 1]];
+  // y_{t-1} one-hot (teacher forcing, RNNAttention.lua:172-176); a negative label = zeros_y (beam search's
+  // first step, Attention.lua:359)
+  if (t > 0 && k.labels[(long)b * k.T + t - 1] >= 0) yin += k.P.Wy[(long)n * k.O + k.labels[(long)b * k.T + t - 1]];
   k.CY[row * 2 * S + S + n] = yin;
 }
 
@@ -1346,6 +1349,307 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
              void* scratch, size_t scratch_bytes) {
   S2S_TRY(attn_bwd_core(st, d, h, labels, P, saved, dlogp, dh, accumulate_dh, scratch, scratch_bytes));
   return attn_bwd_wgrad(st, d, h, labels, P, saved, G, scale, scratch);
+}
+
+// ================================================================== beam search
+// Attention:BeamSearch (Attention.lua:332-438) for B utterances at once, all on the device.  The
+// K hypotheses of every utterance are R = B*K rows of the per-step decoder kernels run as a T = 2
+// problem: row t = 1 of each is the decode step, its s_{t-1} and y_{t-1} written by beam_prep into
+// the t = 1 slots (HX[:, :S], labels[:, 0]; label -1 = zeros_y at the first step).  beam_update then
+// does the reference's bookkeeping per utterance: p_next = logp + p_beam over the active hypotheses,
+// torch.topk(K) of the flattened candidates (sorted; ties -> lower index), the first K - finished of
+// them extend their parent (finished on eos or at maxseqlength), states gathered from the parents.
+namespace {
+
+struct BeamK {
+  int B, K, maxlen, eos, S, O;
+  int *nact, *nfin, *done;
+  int *yprev, *hist, *hlen, *fseq, *flen, *lab2;
+  float *pbeam, *s, *fscore;
+};
+
+// hypothesis row r = b*K + k gets utterance b's annotations (grid.y = utterance)
+__global__ void beam_rep_h(const float* h, float* hr, int K, long per) {
+  const int b = blockIdx.y;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (long)K * per; i += (long)gridDim.x * blockDim.x)
+    hr[(long)b * K * per + i] = h[(long)b * per + i % per];
+}
+
+__global__ void beam_init(BeamK q) {
+  const int R = q.B * q.K;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * q.S; i += gridDim.x * blockDim.x) q.s[i] = 0.f;
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
+    q.pbeam[r] = 0.f;
+    q.yprev[r] = -1;
+    q.hlen[r] = 0;
+    q.flen[r] = 0;
+    if (r < q.B) {
+      q.nact[r] = 1;
+      q.nfin[r] = 0;
+      q.done[r] = 0;
+    }
+  }
+}
+
+// s_{t-1} and y_{t-1} of every hypothesis row into the t = 1 slots of the T = 2 problem
+__global__ void beam_prep(AttnK k, BeamK q, int par) {
+  const int R = q.B * q.K, S = q.S;
+  const float* s = q.s + (long)par * R * S;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * S; i += gridDim.x * blockDim.x) {
+    const int r = i / S, n = i - r * S;
+    k.HX[((long)r * 2 + 1) * 2 * S + n] = s[i];
+  }
+  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
+    q.lab2[2 * r] = q.yprev[r];
+    q.lab2[2 * r + 1] = 0;
+  }
+}
+
+constexpr int kBeamMaxK = 16;
+
+__global__ __launch_bounds__(256) void beam_update(AttnK k, BeamK q, int count) {
+  __shared__ float bv[256];
+  __shared__ int bi[256];
+  __shared__ int sel[kBeamMaxK];
+  __shared__ float selv[kBeamMaxK];
+  __shared__ int fpar[kBeamMaxK], ftok[kBeamMaxK], fdst[kBeamMaxK], npar[kBeamMaxK], ntok[kBeamMaxK];
+  __shared__ float fsc[kBeamMaxK], np_[kBeamMaxK];
+  __shared__ int nf_new, nn_new;
+  const int b = blockIdx.x, tid = threadIdx.x, K = q.K, O = q.O, S = q.S, R = q.B * K;
+  if (q.done[b]) return;
+  const int nact = q.nact[b], ncand = nact * O;
+  const int par = count & 1, nxt = par ^ 1;
+  auto cval = [&](int c) {
+    const int i = c / O, j = c - i * O;
+    return k.LOGP[((long)(b * K + i) * 2 + 1) * O + j] + q.pbeam[b * K + i];
+  };
+  // torch.topk(p_next, K, 1, true): K rounds of a block arg-max over the unselected candidates
+  const int nsel = min(K, ncand);
+  for (int m = 0; m < nsel; ++m) {
+    float best = -INFINITY;
+    int bidx = 0x7fffffff;
+    for (int c = tid; c < ncand; c += 256) {
+      bool taken = false;
+      for (int p = 0; p < m; ++p) taken = taken || sel[p] == c;
+      if (taken) continue;
+      const float v = cval(c);
+      if (v > best || (v == best && c < bidx)) { best = v; bidx = c; }
+    }
+    bv[tid] = best;
+    bi[tid] = bidx;
+    __syncthreads();
+    if (tid == 0) {
+      float bb = bv[0];
+      int ii = bi[0];
+      for (int x = 1; x < 256; ++x)
+        if (bv[x] > bb || (bv[x] == bb && bi[x] < ii)) { bb = bv[x]; ii = bi[x]; }
+      sel[m] = ii;
+      selv[m] = bb;
+    }
+    __syncthreads();
+  }
+  // the first K - finished of the sorted candidates extend their parents (Attention.lua:413-430)
+  if (tid == 0) {
+    int nf = 0, nn = 0;
+    const int fin = q.nfin[b];
+    for (int m = 0; m < nact && m < nsel; ++m) {
+      const int i = sel[m] / O, j = sel[m] - i * O;
+      if (j == q.eos || (count > 0 && count == q.maxlen)) {
+        fpar[nf] = i; ftok[nf] = j; fsc[nf] = selv[m]; fdst[nf] = fin + nf; ++nf;
+      } else {
+        npar[nn] = i; ntok[nn] = j; np_[nn] = selv[m]; ++nn;
+      }
+    }
+    nf_new = nf;
+    nn_new = nn;
+  }
+  __syncthreads();
+  const int nf = nf_new, nn = nn_new, L1 = q.maxlen + 1;
+  const int* hcur = q.hist + (long)par * R * L1;
+  int* hnew = q.hist + (long)nxt * R * L1;
+  const int* lcur = q.hlen + par * R;
+  int* lnew = q.hlen + nxt * R;
+  for (int f = 0; f < nf; ++f) {  // finished hypotheses: parent's tokens + the final token
+    const int src = b * K + fpar[f], dst = b * K + fdst[f], len = lcur[src];
+    for (int x = tid; x < len; x += 256) q.fseq[(long)dst * L1 + x] = hcur[(long)src * L1 + x];
+    if (tid == 0) {
+      q.fseq[(long)dst * L1 + len] = ftok[f];
+      q.flen[dst] = len + 1;
+      q.fscore[dst] = fsc[f];
+    }
+  }
+  float* snew = q.s + (long)nxt * R * S;
+  for (int e = 0; e < nn; ++e) {  // surviving hypotheses: gather tokens and the decoder state of the parent
+    const int src = b * K + npar[e], dst = b * K + e, len = lcur[src];
+    for (int x = tid; x < len; x += 256) hnew[(long)dst * L1 + x] = hcur[(long)src * L1 + x];
+    const float* sv = k.VV + ((long)src * 2 + 1) * (S + k.A);
+    for (int n = tid; n < S; n += 256) snew[(long)dst * S + n] = sv[n];
+    if (tid == 0) {
+      hnew[(long)dst * L1 + len] = ntok[e];
+      lnew[dst] = len + 1;
+      q.pbeam[dst] = np_[e];
+      q.yprev[dst] = ntok[e];
+    }
+  }
+  if (tid == 0) {
+    q.nfin[b] += nf;
+    q.nact[b] = nn;
+    q.done[b] = (q.nfin[b] >= K || count >= q.maxlen) ? 1 : 0;
+  }
+}
+
+// prediction = y_finished[argmax p_finished] (first maximum)
+__global__ void beam_final(BeamK q, int* out, int ldo, int* out_len, float* out_score) {
+  const int b = blockIdx.x, K = q.K, L1 = q.maxlen + 1;
+  __shared__ int best;
+  if (threadIdx.x == 0) {
+    int bi = 0;
+    float bs = -INFINITY;
+    for (int f = 0; f < q.nfin[b]; ++f)
+      if (q.fscore[b * K + f] > bs) { bs = q.fscore[b * K + f]; bi = f; }
+    best = bi;
+    out_len[b] = q.nfin[b] > 0 ? q.flen[b * K + bi] : 0;
+    if (out_score) out_score[b] = bs;
+  }
+  __syncthreads();
+  const int len = q.nfin[b] > 0 ? q.flen[b * K + best] : 0;
+  for (int x = threadIdx.x; x < ldo; x += blockDim.x)
+    out[(long)b * ldo + x] = x < len ? q.fseq[((long)b * K + best) * L1 + x] : -1;
+}
+
+// WagnerFischer (utils.lua:3-27): Levenshtein distance of one sequence pair per block
+__global__ void edit_distance_kernel(int n, const int* a, const int* alen, int lda, const int* b, const int* blen,
+                                     int ldb, int* out) {
+  extern __shared__ int row[];
+  const int p = blockIdx.x;
+  if (p >= n || threadIdx.x != 0) return;
+  const int m = alen[p], nb = blen[p];
+  const int* x = a + (long)p * lda;
+  const int* y = b + (long)p * ldb;
+  for (int i = 0; i <= m; ++i) row[i] = i;  // column j = 0: d[i][0] = i
+  for (int j = 1; j <= nb; ++j) {
+    int diag = row[0];
+    row[0] = j;
+    for (int i = 1; i <= m; ++i) {
+      const int up = row[i];
+      row[i] = x[i - 1] == y[j - 1] ? diag : min(min(up + 1, row[i - 1] + 1), diag + 1);
+      diag = up;
+    }
+  }
+  out[p] = row[m];
+}
+
+AttnDims beam_dims(const AttnDims& d, int K) {
+  AttnDims d2 = d;
+  d2.B = d.B * K;
+  d2.T = 2;
+  d2.dropout = 0.f;  // evaluate() mode
+  d2.dropout_mask = nullptr;
+  return d2;
+}
+
+struct BeamLayout {
+  size_t hrep, saved, scratch, state, fstate, total;
+};
+BeamLayout beam_layout(const AttnDims& d, int K, int maxlen) {
+  const AttnDims d2 = beam_dims(d, K);
+  const size_t R = (size_t)d.B * K, L1 = (size_t)maxlen + 1;
+  auto up = [](size_t x) { return (x + 255) / 256 * 256; };
+  BeamLayout l;
+  l.hrep = 0;
+  l.saved = up(sizeof(float) * R * d.L * d.A);
+  l.scratch = l.saved + up(attn_saved_bytes(d2));
+  l.state = l.scratch + up(attn_scratch_bytes(d2));
+  const size_t ints = 3 * (size_t)d.B + R /*yprev*/ + 2 * R * L1 /*hist*/ + 2 * R /*hlen*/ + R * L1 /*fseq*/ +
+                      R /*flen*/ + 2 * R /*lab2*/;
+  const size_t floats = R /*pbeam*/ + 2 * R * d.S /*s*/ + R /*fscore*/;
+  l.fstate = l.state + up(4 * ints);
+  l.total = l.fstate + up(4 * floats);
+  return l;
+}
+
+}  // namespace
+
+size_t attn_beam_workspace_bytes(const AttnDims& d, int K, int maxlen) { return beam_layout(d, K, maxlen).total; }
+
+int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K,
+                     int maxlen, int* out, int ldo, int* out_len, float* out_score, void* ws, size_t ws_bytes) {
+  S2S_TRY(attn_check_dims(d));
+  S2S_REQUIRE(d.hf == 0, "beam search: hybrid attention not supported");
+  S2S_REQUIRE(K >= 1 && K <= kBeamMaxK && K <= d.O, "beam search: K must be in [1, 16] and <= outputDepth");
+  S2S_REQUIRE(maxlen >= 1 && eos >= 0 && eos < d.O && ldo >= maxlen + 1, "beam search: bad eos / maxlen / ldo");
+  const BeamLayout bl = beam_layout(d, K, maxlen);
+  S2S_REQUIRE(ws && ws_bytes >= bl.total, "beam search: workspace too small");
+  const AttnDims d2 = beam_dims(d, K);
+  char* base = static_cast<char*>(ws);
+  float* hrep = reinterpret_cast<float*>(base + bl.hrep);
+  AttnK k{};
+  carve(d2, &k, base + bl.saved, base + bl.scratch);
+  const int B = d.B, R = B * K, S = d.S, L = d.L, L1 = maxlen + 1;
+  BeamK q{};
+  q.B = B; q.K = K; q.maxlen = maxlen; q.eos = eos; q.S = S; q.O = d.O;
+  int* ip = reinterpret_cast<int*>(base + bl.state);
+  q.nact = ip; ip += B;
+  q.nfin = ip; ip += B;
+  q.done = ip; ip += B;
+  q.yprev = ip; ip += R;
+  q.hist = ip; ip += 2L * R * L1;
+  q.hlen = ip; ip += 2 * R;
+  q.fseq = ip; ip += (long)R * L1;
+  q.flen = ip; ip += R;
+  q.lab2 = ip;
+  float* fp = reinterpret_cast<float*>(base + bl.fstate);
+  q.pbeam = fp; fp += R;
+  q.s = fp; fp += 2L * R * S;
+  q.fscore = fp;
+  k.P = P;
+  k.h = hrep;
+  k.labels = q.lab2;
+  k.logp = nullptr;
+  // annotations and Vh once per hypothesis row (Attention.lua:356-357: vh = Vh:forward(annotations))
+  hipLaunchKernelGGL(beam_rep_h, dim3(64, B), dim3(256), 0, st, h, hrep, K, (long)L * d.A);
+  const GemmWs gws = attn_gemm_ws(d2, base + bl.scratch);
+  S2S_TRY(gemm1(st, false, true, R * L, d.Sc, d.A, 1.f, hrep, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
+  hipLaunchKernelGGL(beam_init, dim3(64), dim3(256), 0, st, q);
+  S2S_CHECK_HIP(hipGetLastError());
+  const int bt = (R + 15) / 16, rows = 2 * R;
+  std::vector<int> done(B);
+  k.t = 1;
+  for (int count = 0; count <= maxlen; ++count) {
+    hipLaunchKernelGGL(beam_prep, dim3(64), dim3(256), 0, st, k, q, count & 1);
+    hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, R), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f3_combine, dim3(R), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
+    S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
+                  (long)d.M * d.K, P.bm, gws));
+    hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
+    hipLaunchKernelGGL(beam_update, dim3(B), dim3(256), 0, st, k, q, count);
+    S2S_CHECK_HIP(hipGetLastError());
+    if ((count & 3) == 3 || count == maxlen) {  // stop once every utterance has K finished hypotheses
+      S2S_CHECK_HIP(hipMemcpyAsync(done.data(), q.done, sizeof(int) * B, hipMemcpyDeviceToHost, st));
+      S2S_CHECK_HIP(hipStreamSynchronize(st));
+      bool all = true;
+      for (int v : done) all = all && v;
+      if (all) break;
+    }
+  }
+  hipLaunchKernelGGL(beam_final, dim3(B), dim3(256), 0, st, q, out, ldo, out_len, out_score);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda, const int* b, const int* blen,
+                  int ldb, int* out) {
+  S2S_REQUIRE(n >= 0 && lda >= 0 && ldb >= 0 && lda < 16384, "edit distance: bad sizes");
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(edit_distance_kernel, dim3(n), dim3(64), sizeof(int) * (lda + 1), st, n, a, alen, lda, b, blen,
+                     ldb, out);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
 }
 
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,

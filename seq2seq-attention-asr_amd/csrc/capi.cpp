@@ -599,6 +599,33 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
                   scale, scratch, scratch_bytes);
 }
 
+size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength) {
+  if (!d || K < 1 || maxseqlength < 1) return 0;
+  return attn_beam_workspace_bytes(to_attn(d), K, maxseqlength);
+}
+
+int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
+                         const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len,
+                         float* out_score, void* workspace, size_t workspace_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && h && params && out && out_len && workspace, "beam search: null argument");
+  AttnParams ap;
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  for (int i = 0; i < attn_nparams(d); ++i) {
+    pp[i] = params[i];
+    S2S_REQUIRE(pp[i] != nullptr, "beam search: null parameter");
+  }
+  return attn_beam_search(static_cast<hipStream_t>(stream), to_attn(d), h, ap, eos, K, maxseqlength, out, ldo,
+                          out_len, out_score, workspace, workspace_bytes);
+}
+
+int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b,
+                      const int* blen, int ldb, int* out) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(n == 0 || (a && alen && b && blen && out), "edit distance: null argument");
+  return edit_distance(static_cast<hipStream_t>(stream), n, a, alen, lda, b, blen, ldb, out);
+}
+
 int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,
                  int normalize, float* nll, float* dlogp) {
   S2S_TRY(set_device(ctx));

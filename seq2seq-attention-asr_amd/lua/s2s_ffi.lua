@@ -38,6 +38,12 @@ int s2s_comm_unique_id(void* out_bytes);
 int s2s_comm_init(s2s_ctx* ctx, const void* id_bytes, int nranks, int rank);
 int s2s_allreduce_sum(s2s_ctx* ctx, void* stream, float* buf, size_t count);
 int s2s_stream_wait_bucket(s2s_ctx* ctx, void* stream, int i);
+size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength);
+int s2s_attn_beam_search(s2s_ctx* ctx, void* stream, const s2s_attn_dims* d, const float* h,
+                         const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len,
+                         float* out_score, void* workspace, size_t workspace_bytes);
+int s2s_edit_distance(s2s_ctx* ctx, void* stream, int n, const int* a, const int* alen, int lda, const int* b,
+                      const int* blen, int ldb, int* out);
 typedef struct { float rho, eps, maxnorm, weightDecay, colnorm_max; } s2s_optim_config;
 size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, void* stream, void* state, size_t n);

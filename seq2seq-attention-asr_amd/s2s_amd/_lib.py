@@ -74,6 +74,11 @@ SIGNATURES = [
     ("s2s_model_encoder_output", c_void_p, [P(s2s_model_dims), c_void_p]),
     ("s2s_prof_enable", c_int, [c_int]),
     ("s2s_prof_collect", c_int, [ctypes.c_char_p, c_size_t]),
+    ("s2s_attn_beam_workspace_bytes", c_size_t, [P(s2s_attn_dims), c_int, c_int]),
+    ("s2s_attn_beam_search", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, c_int, c_int, c_int,
+                                     c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_size_t]),
+    ("s2s_edit_distance", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
+                                  c_void_p]),
     ("s2s_optim_state_bytes", c_size_t, [c_size_t]),
     ("s2s_optim_reset", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),
     ("s2s_optim_adadelta_step", c_int, [c_void_p, c_void_p, P(s2s_optim_config), c_void_p, c_void_p, c_size_t,

@@ -433,6 +433,36 @@ class Attention(Module):
     def accGradParameters(self, input, gradOutput, scale=1.0):
         pass
 
+    def BeamSearch(self, annotations, eos, K=5, maxseqlength=None):
+        """decoder:BeamSearch(annotations, eos, K, maxseqlength) (Attention.lua:332-438) in evaluate()
+        mode.  annotations (L, A) -> 1-D int tensor (the prediction, 0-based tokens, eos last when it
+        finished on eos); (B, L, A) -> (tokens (B, maxseqlength + 1) padded with -1, lengths (B),
+        scores (B)).  maxseqlength defaults to L (:337)."""
+        h = annotations
+        if h.dim() not in (2, 3):
+            raise S2SArgumentError("annotations must be 2d or 3d")
+        _require_cuda_f32(h, "annotations")
+        single = h.dim() == 2
+        if single:
+            h = h[None]
+        B, L = h.shape[0], h.shape[1]
+        maxlen = int(maxseqlength or L)
+        was_train, self.train = self.train, False
+        d = self._dims(h, 1)
+        self.train = was_train
+        dev = h.device
+        ws = _bytes(lib.s2s_attn_beam_workspace_bytes(ctypes.byref(d), K, maxlen), dev)
+        out = torch.empty((B, maxlen + 1), dtype=torch.int32, device=dev)
+        olen = torch.empty(B, dtype=torch.int32, device=dev)
+        osc = torch.empty(B, dtype=torch.float32, device=dev)
+        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
+        check(lib.s2s_attn_beam_search(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h), params,
+                                       int(eos), int(K), maxlen, dptr(out), maxlen + 1, dptr(olen), dptr(osc),
+                                       dptr(ws), ws.numel()))
+        if single:
+            return out[0, :int(olen[0].item())]
+        return out, olen, osc
+
     def mono_ind(self):
         """(B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward
         (MonotonicAlignment.lua:27-39): the discrete decision its backward (:44-77) depends on."""
@@ -460,3 +490,16 @@ def nll_seed(logp, labels, normalize=False):
     check(lib.s2s_nll_seed(get_context(logp.device.index).handle, stream_ptr(), B, T, O, dptr(logp), dptr(lab),
                            int(normalize), dptr(nll), dptr(dlogp)))
     return nll, dlogp
+
+
+def edit_distance(a, alen, b, blen):
+    """WagnerFischer (utils.lua:3-27) for n sequence pairs on the device: a (n, la), b (n, lb) int32
+    CUDA tensors with per-row lengths -> (n,) int32 distances (PER/CER numerators, timit.lua:396-410)."""
+    a = a.to(torch.int32).contiguous()
+    b = b.to(torch.int32).contiguous()
+    alen = alen.to(torch.int32).contiguous()
+    blen = blen.to(torch.int32).contiguous()
+    out = torch.empty(a.shape[0], dtype=torch.int32, device=a.device)
+    check(lib.s2s_edit_distance(get_context(a.device.index).handle, stream_ptr(), a.shape[0], dptr(a), dptr(alen),
+                                a.shape[1], dptr(b), dptr(blen), b.shape[1], dptr(out)))
+    return out

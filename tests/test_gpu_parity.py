@@ -517,3 +517,54 @@ def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm):
         xs = xg.cpu().numpy()
         for off, r, c in mats:
             assert np.linalg.norm(xs[off:off + r * c].reshape(r, c), axis=1).max() <= 1.0 + 1e-5
+
+
+@pytest.mark.parametrize("K,maxlen", [(1, 8), (5, 12)])
+def test_beam_search_matches_oracle(s2s, K, maxlen):
+    """decoder:BeamSearch (Attention.lua:332-438) on the device for a batch of
+    utterances vs the oracle's per-utterance restatement.  A hypothesis choice may legitimately flip
+    only at an fp32-vs-fp64 near tie, so a differing prediction must score (teacher-forced, oracle)
+    within 1e-4 of the oracle's best; the reported score must equal the oracle's rescoring of the
+    GPU's own prediction."""
+    B, L, A, Sc, S, O, M, Kw, eos = 6, 30, 64, 64, 32, 11, 4, 3, 2
+    rng = np.random.default_rng(K * 100 + maxlen)
+    torch.manual_seed(K)
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=Kw, numLayers=1)
+    att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, M, Kw, O), Sc, 10, 0, S, A, O, True, 0.0).cuda()
+    P = {n: t.cpu().double().numpy() for n, t in zip(
+        ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "dec.Wz", "dec.Wr", "dec.Wh", "Wm", "bm", "Wo",
+         "bo"), att.parameters()[0])}
+    h = rng.standard_normal((B, L, A)) * 1.5
+    toks, lens, scores = att.BeamSearch(cu(h), eos, K, maxlen)
+    toks, lens, scores = toks.cpu().numpy(), lens.cpu().numpy(), scores.cpu().numpy()
+    agree = 0
+    for b in range(B):
+        seq = list(toks[b, :lens[b]])
+        assert all(t == -1 for t in toks[b, lens[b]:])
+        assert seq[-1] == eos or len(seq) == maxlen + 1
+        ref_seq, ref_score = orc.beam_search(h[b], P, cfg, eos, K, maxlen)
+        lp, _ = orc.attention_fwd(h[b][None], np.array([seq]), P, cfg)
+        mine = float(lp[0, np.arange(len(seq)), seq].sum())
+        assert abs(mine - scores[b]) <= 1e-4 * max(1.0, abs(mine)), (b, mine, scores[b])
+        if seq == list(ref_seq):
+            agree += 1
+        else:
+            assert mine >= ref_score - 1e-4 * max(1.0, abs(ref_score)), (b, seq, ref_seq, mine, ref_score)
+    assert agree >= B - 1
+    one = att.BeamSearch(cu(h[0]), eos, K, maxlen).cpu().numpy()
+    assert list(one) == list(toks[0, :lens[0]])
+
+
+def test_edit_distance_matches_oracle(s2s):
+    """WagnerFischer (utils.lua:3-27) on the device vs the oracle, ragged lengths incl. empty."""
+    rng = np.random.default_rng(5)
+    n, la, lb = 40, 25, 31
+    a = rng.integers(0, 5, (n, la)).astype(np.int32)
+    b = rng.integers(0, 5, (n, lb)).astype(np.int32)
+    alen = rng.integers(0, la + 1, n).astype(np.int32)
+    blen = rng.integers(0, lb + 1, n).astype(np.int32)
+    got = s2s.nn.edit_distance(cu(a, torch.int32), cu(alen, torch.int32), cu(b, torch.int32),
+                               cu(blen, torch.int32)).cpu().numpy()
+    want = [orc.wagner_fischer(list(a[i, :alen[i]]), list(b[i, :blen[i]])) for i in range(n)]
+    assert list(got) == want

@@ -241,3 +241,37 @@ def test_optimizer_step_matches_adadelta_definition():
     d = np.sqrt(1e-6) / np.sqrt(v + 1e-6) * gc
     np.testing.assert_allclose(x, x0 - d, rtol=1e-13)
     np.testing.assert_allclose(st["accDelta"], 0.1 * d * d, rtol=1e-13)
+
+
+def test_wagner_fischer_known_answers():
+    """utils.lua:3-27 on textbook pairs (kitten/sitting = 3, flaw/lawn = 2) and the empty cases."""
+    enc = lambda w: [ord(c) for c in w]
+    assert orc.wagner_fischer(enc("kitten"), enc("sitting")) == 3
+    assert orc.wagner_fischer(enc("flaw"), enc("lawn")) == 2
+    assert orc.wagner_fischer([], [1, 2, 3]) == 3
+    assert orc.wagner_fischer([4, 5], []) == 2
+    assert orc.wagner_fischer([1, 2, 3], [1, 2, 3]) == 0
+
+
+def test_beam_search_step_matches_teacher_forced_forward():
+    """decoder_step restates the training forward's step: the beam search's score of its best
+    hypothesis equals the teacher-forced log-likelihood of that sequence (attention_fwd with the
+    hypothesis as labels), and K = 1 is greedy decoding."""
+    cfg = tiny_cfg()
+    P = orc.init_params(cfg, seed=13)
+    rng = np.random.default_rng(3)
+    h = rng.standard_normal((9, cfg.annotationDepth))
+    for K in (1, 3):
+        seq, score = orc.beam_search(h, P, cfg, eos=2, K=K, maxseqlength=6)
+        logp, _ = orc.attention_fwd(h[None], np.array([seq]), P, cfg)
+        assert abs(logp[0, np.arange(len(seq)), seq].sum() - score) < 1e-10
+        assert seq[-1] == 2 or len(seq) == 7
+    greedy, y, s, a = [], -1, np.zeros(cfg.stateDepth), np.zeros(9)
+    Vh = h @ P["V"].T
+    for _ in range(7):
+        lp, s, a = orc.decoder_step(h, Vh, s, y, a, P, cfg)
+        y = int(np.argmax(lp))
+        greedy.append(y)
+        if y == 2:
+            break
+    assert orc.beam_search(h, P, cfg, eos=2, K=1, maxseqlength=6)[0] == greedy
