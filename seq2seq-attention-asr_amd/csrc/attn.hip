@@ -1256,7 +1256,13 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       }
       S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
     }
-    hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 255) / 256, k.NCH, B), dim3(256), 0, st, k, x);
+    {
+      const size_t lds = dec_xcd_dvh_lds(T);
+      if (lds > 64 * 1024)
+        S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_xcd_dvh),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 63) / 64, k.NCH, B), dim3(256), lds, st, k, x);
+    }
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pb.fn) {
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
