@@ -38,8 +38,11 @@ int attn_check_dims(const AttnDims& d);
 size_t attn_saved_bytes(const AttnDims& d);
 size_t attn_scratch_bytes(const AttnDims& d);
 // h (B, L, A) contiguous; labels (B, T) int32 0-based; logp (B, T, O) out.
+// side / ev (optional, both or neither): a second stream and 5 events for work off the critical
+// path (the model step's split mode); attn_fwd and attn_bwd_core must then use the same ones.
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
-             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done = false);
+             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done = false, hipStream_t side = nullptr,
+             hipEvent_t* ev = nullptr);
 // The decoder's parameter folds / teacher-forced constants (needs only P and labels): the model
 // step issues it beside the encoder and then calls attn_fwd(..., prologue_done = true).
 int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, const AttnParams& P, void* saved,
@@ -51,7 +54,7 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
 // split form used by the model step (wgrad may run on a side stream after core)
 int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                   const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
-                  size_t scratch_bytes);
+                  size_t scratch_bytes, hipStream_t side = nullptr, hipEvent_t* ev = nullptr);
 int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)

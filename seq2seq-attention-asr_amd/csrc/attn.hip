@@ -152,6 +152,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* XWHT = sv.take<float>(S * S);
   float* XZRT = sv.take<float>(2 * S * S);
   float* XWST = sv.take<float>(S * Sc);
+  float* VBAR = sv.take<float>(B * Sc);  // mean Vh row per utterance (computed by the forward)
   const long HK = d.hf > 0 ? d.hk : 0;
   float* HGT = HK ? sv.take<float>(HK * Sc) : nullptr;
   float* HCU = HK ? sv.take<float>(Sc) : nullptr;
@@ -187,7 +188,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* WcT = g.take<float>(A * S);
   float* WsT = g.take<float>(S * Sc);
   float* DE = g.take<float>(BT * L);
-  float* VBAR = g.take<float>(B * Sc);
+
   float* QA = HK ? g.take<float>(2 * B * L * HK) : nullptr;
   float* PDG = HK ? g.take<float>(B * NCH * HK * Sc) : nullptr;
   float* DGT = HK ? g.take<float>(HK * Sc) : nullptr;
@@ -904,13 +905,13 @@ __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const in
   for (int i = threadIdx.x; i < T * O; i += blockDim.x) {
     const int t = i / O, o = i - t * O;
     const bool hit = labels[b * T + t] == o;
-    if (hit) s += logp[((long)b * T + t) * O + o];
+    if (hit && logp) s += logp[((long)b * T + t) * O + o];
     if (dlogp) dlogp[((long)b * T + t) * O + o] = hit ? -1.f : 0.f;
   }
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && nll) {
     float v = -(((red[0] + red[1]) + red[2]) + red[3]);
     nll[b] = normalize ? v / (float)T : v;
   }
@@ -1114,7 +1115,7 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
 }
 
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
-             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done) {
+             void* saved, void* scratch, size_t scratch_bytes, bool prologue_done, hipStream_t side, hipEvent_t* ev) {
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
@@ -1142,12 +1143,26 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
+    // VBAR (the backward's dws reference point) needs only Vh: beside the decoder loop when a side
+    // stream is given (joined by attn_bwd_core through ev[2])
+    if (side) {
+      S2S_CHECK_HIP(hipEventRecord(ev[0], st));
+      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
+    }
+    hipLaunchKernelGGL(dec_xcd_vbar, dim3((d.Sc + 63) / 64, B), dim3(256), 0, side ? side : st, k, x);
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       ProfScope ps(st, "dec_fwd_xcd", 0.0, 0.0);
       S2S_TRY(launch_xcd(xp.var, true, st, k, x));
     }
-    hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, st, k);
+    // alpha / MonotonicAlignment indicators from the saved scores: only the backward (and alpha())
+    // read them, so beside the MLP head when split
+    if (side) {
+      S2S_CHECK_HIP(hipEventRecord(ev[1], st));
+      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1], 0));
+    }
+    hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, side ? side : st, k);
+    if (side) S2S_CHECK_HIP(hipEventRecord(ev[2], side));
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pf.fn) {
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
@@ -1187,7 +1202,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
 
 int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                   const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
-                  size_t scratch_bytes) {
+                  size_t scratch_bytes, hipStream_t side, hipEvent_t* ev) {
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
@@ -1203,7 +1218,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
   const int rows = B * T, bt = (B + 15) / 16;
   const XPlan xp = dec_xcd_plan(d);
-  if (!accumulate_dh) S2S_CHECK_HIP(hipMemsetAsync(dh, 0, sizeof(float) * (size_t)B * L * A, st));
+  // the XCD-local path's first dh writer is the alpha^T dc GEMM (beta 0 when not accumulating)
+  if (!accumulate_dh && !xp.var) S2S_CHECK_HIP(hipMemsetAsync(dh, 0, sizeof(float) * (size_t)B * L * A, st));
   if (!xp.var) {  // the XCD-local path writes DVH / DWEACC whole after its loop
     S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
     S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
@@ -1240,30 +1256,37 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
-    hipLaunchKernelGGL(dec_xcd_vbar, dim3((Sc + 63) / 64, B), dim3(256), 0, st, k, x);
+    if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
       ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
       S2S_TRY(launch_xcd(xp.var, false, st, k, x));
     }
-    // dh_l += sum_t alpha_{t,l} dc_t  (one GEMM per utterance: alpha_b^T (L x T) . dc_b (T x A))
-    for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
-      GemmProblem pr[kMaxGemmBatch];
-      const int nb = std::min(kMaxGemmBatch, B - b0);
-      for (int i = 0; i < nb; ++i) {
-        const long b = b0 + i;
-        pr[i] = GemmProblem{k.ALPHA + b * T * L, x.DCS + b * T * A, dh + b * L * A, nullptr, L, A, A, L, A, T,
-                            1.f, 1.f};
-      }
-      S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
+    // dVh / dwe (dec_xcd_dvh) beside the alpha^T dc GEMMs when split; both feed dh
+    if (side) {
+      S2S_CHECK_HIP(hipEventRecord(ev[3], st));
+      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[3], 0));
     }
     {
       const size_t lds = dec_xcd_dvh_lds(T);
       if (lds > 64 * 1024)
         S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_xcd_dvh),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 63) / 64, k.NCH, B), dim3(256), lds, st, k, x);
+      hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 63) / 64, k.NCH, B), dim3(256), lds, side ? side : st, k, x);
+      S2S_CHECK_HIP(hipGetLastError());
     }
-    S2S_CHECK_HIP(hipGetLastError());
+    if (side) S2S_CHECK_HIP(hipEventRecord(ev[4], side));
+    // dh_l (+)= sum_t alpha_{t,l} dc_t  (one GEMM per utterance: alpha_b^T (L x T) . dc_b (T x A))
+    for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
+      GemmProblem pr[kMaxGemmBatch];
+      const int nb = std::min(kMaxGemmBatch, B - b0);
+      for (int i = 0; i < nb; ++i) {
+        const long b = b0 + i;
+        pr[i] = GemmProblem{k.ALPHA + b * T * L, x.DCS + b * T * A, dh + b * L * A, nullptr, L, A, A, L, A, T,
+                            1.f, accumulate_dh ? 1.f : 0.f};
+      }
+      S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
+    }
+    if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[4], 0));
   } else if (pb.fn) {
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);

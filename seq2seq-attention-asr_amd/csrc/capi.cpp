@@ -89,7 +89,7 @@ struct s2s_ctx {
   int device = 0;
   int flags = 0;
   hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
-  hipEvent_t ev[16] = {};
+  hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
   hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
   bool have_graph = false;
   GraphKey key{};
@@ -234,6 +234,7 @@ int mark_bucket(hipEvent_t* bev, int i, hipStream_t s) {
   return 0;
 }
 
+int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
                     const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
                     float* logp, float* nll, void* workspace) {
@@ -300,6 +301,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   if (split) {
     S2S_TRY(fork_to(st, side, ev[13]));
     S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+    S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));  // dlogp = -labelmask
     S2S_CHECK_HIP(hipEventRecord(ev[14], side));
   } else {
     S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
@@ -309,14 +311,18 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // ---- attention decoder forward
   if (split) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
-  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, true));
-  // ---- loss seed: dlogp = -labelmask
-  S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
+  hipStream_t dside = (split && g_dec_side) ? side : nullptr;
+  S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, true,
+                   dside, dside ? ev + 16 : nullptr));
+  // ---- loss seed: dlogp = -labelmask needs only the labels (computed beside the encoder when split);
+  // the reported nll (timit.lua:268-272) is computed on the side stream at the end of the step
+  if (!split)
+    S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
   // ---- decoder backward -> dh
   float* dYcur = w.dY0;
   float* dYnext = w.dY1;
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
-                        w.attn_scratch_bytes));
+                        w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr));
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
   S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
   S2S_TRY(mark_bucket(bev, 0, split ? side : st));
@@ -343,6 +349,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     dYnext = tmp;
   }
   if (split) {  // join: the step ends when the side stream's gradient GEMMs are done
+    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr));
     S2S_CHECK_HIP(hipEventRecord(ev[15], side));
     S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[15], 0));
   }
@@ -815,3 +822,6 @@ int s2s_allreduce_sum(s2s_ctx* ctx, s2s_stream_t stream, float* buf, size_t coun
 }
 
 }  // extern "C"
+
+// diagnostic: 1 runs the decoder's off-path kernels (vbar, alpha/indicators, dVh) on the side stream
+extern "C" void s2s_debug_dec_side(int on) { g_dec_side = on; }
