@@ -356,9 +356,13 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
       S2S_TRY(launch_pack(st, io.W[d][0], io.W[d][1], io.W[d][2], H, D, Kx, Uzr[d], Uh[d], nullptr, nullptr,
                           Wx + 3L * d * H * Kx));
   }
-  // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, Kx) . Wx^T
-  S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, Kx, 1.f, io.x, io.ldx, Wx, Kx, 0.f, xp, 3L * nd * H, nullptr,
-                layer_gemm_ws(scratch, nd, B, L, D, H)));
+  // hoisted x-projections for both directions: xp (B*L, 3*nd*H) = x (B*L, Kx) . Wx^T -- one GEMM, or
+  // computed inside the persistent launch by its spare workgroups (gru_persist_fused_xproj)
+  const bool fuse = use_persistent(nd, B, H) && gru_persist_fused_xproj(nd, B, H, Kx) && io.ldx % 4 == 0 &&
+                    (reinterpret_cast<uintptr_t>(io.x) & 15) == 0;
+  if (!fuse)
+    S2S_TRY(gemm1(st, false, true, B * L, 3 * nd * H, Kx, 1.f, io.x, io.ldx, Wx, Kx, 0.f, xp, 3L * nd * H, nullptr,
+                  layer_gemm_ws(scratch, nd, B, L, D, H)));
   GruFwdArgs a{};
   for (int d = 0; d < nd; ++d)
     a.d[d] = GruFwdDir{xp + 3L * d * H, 3L * nd * H, Uzr[d], Uh[d], io.y[d], io.ldy, io.saved[d], io.reverse[d]};
@@ -368,6 +372,9 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   if (use_persistent(nd, B, H)) {
     GruPersistFwd f{};
     f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 3L * nd * H; f.ldy = io.ldy;
+    if (fuse) {
+      f.x = io.x; f.ldx = io.ldx; f.Kx = Kx; f.Wx = Wx;
+    }
     for (int d = 0; d < nd; ++d) {
       f.xp[d] = xp + 3L * d * H; f.Uzr[d] = Uzr[d]; f.Uh[d] = Uh[d]; f.y[d] = io.y[d]; f.sv[d] = io.saved[d];
       f.reverse[d] = io.reverse[d];

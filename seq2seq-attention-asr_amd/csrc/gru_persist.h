@@ -5,6 +5,13 @@ namespace s2s {
 
 struct GruPersistFwd {
   int ndir, B, L, H;
+  // fused x-projection (gru_persist_fused_xproj): x (B*L, ldx) with Kx readable columns and the
+  // packed x-weights Wx (ndir*3H, Kx); xp[0] is then the (B*L, ldxp) output base.  x = nullptr: xp
+  // precomputed by the caller
+  const float* x = nullptr;
+  long ldx = 0;
+  int Kx = 0;
+  const float* Wx = nullptr;
   const float* xp[2];
   long ldxp;
   const float* Uzr[2];
@@ -27,6 +34,7 @@ struct GruPersistBwd {
 };
 
 bool gru_persist_supported(int ndir, int B, int H);
+bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx);
 // 1 = persistent GRU launches reserve their CU (see kExclLds); set around a step whose weight-gradient
 // GEMMs run on a side stream
 void gru_persist_set_exclusive(int on);

@@ -50,7 +50,30 @@ struct PDir {
   float* s1;
   float* s2;
 };
+// Fused x-projection (forward): the placement grid's spare XCDs (slots past the chains) compute
+// xp = x Wx^T themselves, time slice by time slice in the order the recurrence consumes them, instead
+// of a GEMM launch in front of the layer.  Work item = (slice, direction, 64-column tile) of a
+// 64-row tile whose rows are (utterance b, step j of the slice); the MFMA schedule and k order are
+// gemm_f32's 64x64 NT kernel (bitwise-equal xp; work items dealt round-robin to the producers, so
+// every loop bound is uniform).  Hand-off (cross-XCD): write-through stores, every
+// wave drains, one agent-scope add per tile to the slice's counter; a consumer polls the counter
+// (sc1) and then reads xp with sc1 loads (MI355X guide, visibility table row 1).
+struct XProj {
+  const float* x;
+  long ldx;
+  int K;            // padded input width (% 32 == 0): x and W hold K readable columns
+  const float* W;   // (nd*3H, K) x-weights, direction d's rows [3H d, 3H (d+1))
+  float* xp;
+  long ldxp;
+  int tpt;          // steps per slice (64 / B)
+  int nslices, ntn, nwork;
+  unsigned* done;   // [nd][nslices] finished column tiles
+};
+constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
+
 struct PArgs {
+  XProj xq;
+  int fused;
   PDir d[2];
   int B, L, H, MT, nwg;  // nwg = workgroups per direction
   int nmem, nchains;     // chains = (direction, 16-row tile); members = column tiles
@@ -78,6 +101,98 @@ __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds,
   return s;
 }
 
+// ------------------------------------------------------------------------------ fused x-projection
+// producer p of nprod takes work items p, p + nprod, ... (a static round-robin in consumption order:
+// uniform loop bounds, no shared work counter)
+__device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p, int nprod) {
+  const XProj& q = a.xq;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wy = wave >> 1, wx = wave & 1, li = lane & 31, lk = lane >> 5;
+  const int B = a.B, L = a.L, H3 = 3 * a.H, nd = q.nslices > 0 ? q.nwork / (q.nslices * q.ntn) : 1;
+  constexpr int LDK = 36;
+  float* As[2] = {lds, lds + 64 * LDK};
+  float* Bs[2] = {lds + 128 * LDK, lds + 192 * LDK};
+  for (int w = p; w < q.nwork; w += nprod) {
+    const int sl = w / (nd * q.ntn), rem = w - sl * nd * q.ntn, d = rem / q.ntn, ct = rem - d * q.ntn;
+    const int rev = a.d[d].reverse;
+    // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows
+    const float* arow[2];
+    bool aval[2];
+    const float* brow[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int r = (tid >> 3) + 32 * j, jt = r / B, b = r - jt * B, s = sl * q.tpt + jt;
+      aval[j] = jt < q.tpt && s < L;
+      const int t = rev ? L - 1 - s : s;
+      arow[j] = q.x + (aval[j] ? ((long)b * L + t) * q.ldx : 0);
+      brow[j] = q.W + (long)(d * H3 + ct * 64 + r) * q.K;
+    }
+    const int kq = 4 * (tid & 7);
+    floatx4 ra[2], rb[2];
+    auto gload = [&](int k0) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        ra[j] = aval[j] ? *reinterpret_cast<const floatx4*>(arow[j] + k0 + kq) : floatx4{0.f, 0.f, 0.f, 0.f};
+        rb[j] = *reinterpret_cast<const floatx4*>(brow[j] + k0 + kq);
+      }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int f = tid + 256 * j;
+        *reinterpret_cast<floatx4*>(As[buf] + (f >> 3) * LDK + 4 * (f & 7)) = ra[j];
+        *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = rb[j];
+      }
+    };
+    floatx16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.f;
+    const int nk = q.K / 32;
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {  // gemm_f32's double-buffered 64x64 main loop, same MFMA order
+      const int buf = kt & 1;
+      const bool more = kt + 1 < nk;
+      if (more) gload((kt + 1) * 32);
+      floatx4 av[4], bv[4];
+      const float* pa = As[buf] + (wy * 32 + li) * LDK + 16 * lk;
+      const float* pb = Bs[buf] + (wx * 32 + li) * LDK + 16 * lk;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        av[c] = *reinterpret_cast<const floatx4*>(pa + 4 * c);
+        bv[c] = *reinterpret_cast<const floatx4*>(pb + 4 * c);
+      }
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
+      if (more) lstore(buf ^ 1);
+      __syncthreads();
+    }
+    // epilogue: write-through stores of the valid rows, drain, one counter add per tile
+    const int col = d * H3 + ct * 64 + wx * 32 + li;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int tr = wy * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, jt = tr / B, b = tr - jt * B, s = sl * q.tpt + jt;
+      if (jt < q.tpt && s < L) {
+        const int t = rev ? L - 1 - s : s;
+        __hip_atomic_store(q.xp + ((long)b * L + t) * q.ldxp + col, 1.f * acc[r], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(q.done + d * q.nslices + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// consumer side: is slice `sl` of direction d complete?  (one sc1 load)
+__device__ __forceinline__ bool xproj_ready(const XProj& q, int d, int sl) {
+  return __hip_atomic_load(q.done + d * q.nslices + sl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >=
+         (unsigned)q.ntn;
+}
+
 // ------------------------------------------------------------------------------ forward
 // chain (dir, mt) has nmem = 2H/16 members c1 (chain_slot placement, handoff.h); z-column
 // workgroups (c1 < H/16) also own the candidate tile of the same units.
@@ -87,9 +202,17 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   __shared__ int abort_lds, local_lds;
   __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
+  __shared__ int xnext_lds[2];
+  extern __shared__ __attribute__((aligned(16))) float xlds[];  // producer tiles (fused x-projection)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
-  if (cs.chain >= a.nchains) return;  // idle slot of the placement grid
+  if (cs.chain >= a.nchains) {  // spare slot of the placement grid: x-projection producer (or idle)
+    if (a.fused) {
+      const int gch = 8 * ((a.nchains + 7) / 8);
+      xproj_produce(a, xlds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
+    }
+    return;
+  }
   const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
   const PDir& g = a.d[dir];
   const int ncol = 2 * H / 16;
@@ -119,11 +242,41 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   float zreg = 0.f, hreg = 0.f;
   bool aborted = false;
 
+  // x-projection operands of step s (this thread's gate column, and the candidate column for z tiles),
+  // loaded one step ahead; with the fused x-projection only after the slice's counter says ready
+  auto xp_load = [&](int s, float& xz, float& xh) {
+    const int t = g.reverse ? L - 1 - s : s;
+    const float* p = g.xp + ((long)ob * L + t) * g.ldxp;
+    xz = 0.f;
+    xh = 0.f;
+    if (!live) return;
+    if (a.fused) {
+      xz = __hip_atomic_load(p + on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (isz) xh = __hip_atomic_load(p + 2 * H + on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      xz = p[on];
+      if (isz) xh = p[2 * H + on];
+    }
+  };
+  auto xp_wait = [&](int s) {  // blocking: thread 0 polls, then a barrier
+    if (tid == 0) {
+      unsigned spins = 0;
+      while (!xproj_ready(a.xq, dir, s / a.xq.tpt))
+        if (spin_give_up(spins, a.abort_word)) break;
+    }
+    __syncthreads();
+  };
+  float xz_n = 0.f, xh_n = 0.f;
+  if (a.fused) xp_wait(0);
+  xp_load(0, xz_n, xh_n);
+
   for (int s = 0; s < L; ++s) {
     const int t = g.reverse ? L - 1 - s : s;
     const long row = (long)ob * L + t;
     // ---- p1: [z | r] = sig(Uzr h_{t-1} + xp)
-    const float xpv = live ? g.xp[row * g.ldxp + on] : 0.f;
+    const float xpv = xz_n, xph_s = xh_n;
+    if (a.fused && tid == 0)  // double-buffered: a lagging thread may still read the previous step's
+      xnext_lds[s & 1] = (s + 1 < L && xproj_ready(a.xq, dir, (s + 1) / a.xq.tpt)) ? 1 : 0;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     bool ok = true;
     GRU_STAMP(0);
@@ -143,6 +296,10 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     }
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
+    if (s + 1 < L) {  // next step's x-projection (xnext_lds was set before the reduce barrier)
+      if (a.fused && !__builtin_amdgcn_readfirstlane(xnext_lds[s & 1])) xp_wait(s + 1);
+      xp_load(s + 1, xz_n, xh_n);
+    }
     {
       const float gate = sigmoidf_(sum + xpv);
       float* sv = g.sv + row * 5 * H;
@@ -168,7 +325,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(2);
     if (!isz) continue;
     // ---- p2: hh = tanh(Uh q + xp_h); h = (1-z) h_{t-1} + z hh
-    const float xph = live ? g.xp[row * g.ldxp + 2 * H + on] : 0.f;
+    const float xph = xph_s;
     acc = floatx4{0.f, 0.f, 0.f, 0.f};
     ok = true;
     GRU_STAMP(3);
@@ -350,7 +507,7 @@ int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
   const dim3 grid(chain_grid(a.nchains, a.nmem));
   // exclusive only while one chain per XCD fits one workgroup per CU (32 CUs per XCD)
   const bool excl = g_excl && a.nchains <= 8 && a.nmem <= 32;
-  const unsigned shm = excl ? kExclLds : 0;
+  const unsigned shm = excl ? kExclLds : (a.fused ? kXpLds : 0);
   if (fwd) {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
@@ -379,6 +536,14 @@ int launch(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
 
 void gru_persist_set_exclusive(int on) { g_excl = on; }
 
+int g_fuse_xproj = 1;  // S2S_GRU_FUSED_XPROJ=0 (diagnostic) keeps the separate x-projection GEMM
+
+bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx) {
+  if (!g_fuse_xproj || B > 64 || Kx % 32 != 0 || H % 64 != 0) return false;
+  const int MT = (B + 15) / 16, nchains = ndir * MT, nmem = 2 * H / 16;
+  return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
+}
+
 bool gru_persist_supported(int ndir, int B, int H) {
   if (!(H == 64 || H == 128 || H == 256 || H == 512)) return false;
   const int MT = (B + 15) / 16;
@@ -389,18 +554,20 @@ bool gru_persist_supported(int ndir, int B, int H) {
 
 static size_t census_bytes(int B, int H) { return 4 * (size_t)(2 * ((B + 15) / 16)) * (2 * H / 16); }
 
-// header | tagged granules | census (zeroed by sync_prep every launch) | sentinel rows (re-armed in-kernel)
-static size_t prep_bytes(int B, int H) {
-  return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H);
+// header | tagged granules | census | x-projection counters (zeroed by sync_prep every launch) |
+// sentinel rows (re-armed in-kernel)
+static size_t xcount_words(int L) { return 2 * (size_t)L; }
+static size_t prep_bytes(int B, int L, int H) {
+  return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H) + 4 * xcount_words(L);
 }
-static size_t sent_offset(int B, int H) { return (prep_bytes(B, H) + 255) / 256 * 256; }
+static size_t sent_offset(int B, int L, int H) { return (prep_bytes(B, L, H) + 255) / 256 * 256; }
 
 size_t gru_persist_sync_bytes(int B, int L, int H) {
-  return sent_offset(B, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H;
+  return sent_offset(B, L, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H;
 }
 
 static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_word, granule_t* (&g)[2][3],
-                           float* (&sv)[2][3], unsigned** census) {
+                           float* (&sv)[2][3], unsigned** census, unsigned** xcount = nullptr) {
   *abort_word = reinterpret_cast<unsigned*>(sync);
   granule_t* p = reinterpret_cast<granule_t*>(sync + 256);
   for (int d = 0; d < 2; ++d)
@@ -409,7 +576,8 @@ static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_wor
       p += 2L * B * H;
     }
   *census = reinterpret_cast<unsigned*>(p);
-  float* q = reinterpret_cast<float*>(sync + sent_offset(B, H));
+  if (xcount) *xcount = *census + census_bytes(B, H) / 4;
+  float* q = reinterpret_cast<float*>(sync + sent_offset(B, L, H));
   for (int d = 0; d < 2; ++d)
     for (int k = 0; k < 3; ++k) {
       sv[d][k] = q;
@@ -422,14 +590,25 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   const int MT = (f.B + 15) / 16;
   granule_t* gr[2][3];
   float* sr[2][3];
-  carve_granules(static_cast<char*>(sync), f.B, f.L, f.H, &a.abort_word, gr, sr, &a.census);
+  unsigned* xcount = nullptr;
+  carve_granules(static_cast<char*>(sync), f.B, f.L, f.H, &a.abort_word, gr, sr, &a.census, &xcount);
   for (int d = 0; d < f.ndir; ++d)
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
                   gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
-  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.H)));
+  if (f.x) {  // fused x-projection by the grid's spare slots
+    XProj& q = a.xq;
+    q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.xp = const_cast<float*>(f.xp[0]); q.ldxp = f.ldxp;
+    q.tpt = 64 / f.B;
+    q.nslices = (f.L + q.tpt - 1) / q.tpt;
+    q.ntn = 3 * f.H / 64;
+    q.nwork = q.nslices * f.ndir * q.ntn;
+    q.done = xcount;
+    a.fused = 1;
+  }
+  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
   return launch(st, a, f.ndir, true);
@@ -447,7 +626,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
-  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.H)));
+  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);
@@ -459,6 +638,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
 // nullptr turns it off.  Not part of the C ABI header.
 // diagnostic: 0 forces write-through (sc1) hand-offs in every chain (tests cover both forms)
 extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
+extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);

@@ -20,6 +20,7 @@ struct GemmProblem {
   long lda, ldb, ldc;
   int M, N, K;
   float alpha, beta;
+  int Mread = 0, Nread = 0;  // (mirror of s2s_common.h)
 };
 struct GemmWs {
   float* p = nullptr;
