@@ -234,6 +234,14 @@ int mark_bucket(hipEvent_t* bev, int i, hipStream_t s) {
   return 0;
 }
 
+// S2S_PROLOGUE=0|1|2 (diagnostics; see model_step_impl), read once
+int prologue_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("S2S_PROLOGUE");
+    return e ? std::atoi(e) : 0;
+  }();
+  return m;
+}
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
                     const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
@@ -251,7 +259,12 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     G.push_back(grads + off);
     off += s;
   }
-  if (flags & S2S_ZERO_GRADS) S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, st));
+  // gradients are first written by the side stream's weight-gradient work when split: zero them
+  // there (the fork precedes every gradient writer), off the critical path
+  const int pmode = prologue_mode();
+  if (split) S2S_TRY(fork_to(st, side, ev[13]));
+  if (flags & S2S_ZERO_GRADS)
+    S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, split ? side : st));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   const AttnDims ad = model_attn(d);
@@ -263,6 +276,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     pp[i] = P[6 * nl + i];
     gp[i] = G[6 * nl + i];
   }
+  // prologue mode 1: beside pad + pack, joined before the first recurrence
+  if (split && pmode == 1) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
   // layer-1 input padded to a multiple of 32 columns: its GEMMs then run on aligned full tiles
   const float* x0 = x;
   long ldx0 = d->inputFrameSize;
@@ -298,18 +313,22 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     for (int l = 0; l < nl; ++l) ios.push_back(layer_io(l));
     S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl));
   }
-  if (split) {
-    S2S_TRY(fork_to(st, side, ev[13]));
-    S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+  // decoder parameter folds + dlogp = -labelmask (params and labels only). Mode 0: on the side
+  // stream, joined before the decoder (the persistent GRU launches hold every CU, so it runs in the
+  // gaps between layers); 1: beside pad + pack, joined before layer 1; 2: inline on the main stream
+  if (split && pmode != 2) {
+    if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
     S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));  // dlogp = -labelmask
     S2S_CHECK_HIP(hipEventRecord(ev[14], side));
+    if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   } else {
     S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
+    if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));
   }
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   for (int l = 0; l < nl; ++l) S2S_TRY(gru_layer_fwd(st, layer_io(l), w.scratch, w.scratch_bytes));
   // ---- attention decoder forward
-  if (split) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
+  if (split && pmode == 0) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
   hipStream_t dside = (split && g_dec_side) ? side : nullptr;
   S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, true,
@@ -326,6 +345,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
   S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
   S2S_TRY(mark_bucket(bev, 0, split ? side : st));
+  // the reported nll (timit.lua:268-272) beside the encoder BPTT
+  if (split)
+    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr));
   // ---- encoder backward
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
@@ -349,7 +371,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     dYnext = tmp;
   }
   if (split) {  // join: the step ends when the side stream's gradient GEMMs are done
-    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr));
     S2S_CHECK_HIP(hipEventRecord(ev[15], side));
     S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[15], 0));
   }
