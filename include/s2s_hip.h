@@ -148,6 +148,48 @@ int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims*
 int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b,
                       const int* blen, int ldb, int* out);
 
+/* ---------------------------------------------------------------- encoder front-ends
+ * The operators of the reference's two other encoders: the conv + BiLSTM encoder of timit/timit.lua:108-125
+ * (3 x [TemporalConvolution(D, 256, 3) -> ReLU -> TemporalMaxPooling(2, 2)] -> BiLSTM, s2s_lstm_*) and the VGG
+ * stack of librispeech/model_vgg.lua:23-51.  Torch7 semantics and layouts; `relu` = 1 fuses the nn.ReLU that
+ * follows the convolution in both encoders (its backward then needs the conv's output y).  Batches of
+ * equal-length utterances, batch axis leading.  Gradients accumulate (dW += scale * ...); dx is overwritten
+ * unless dx_accumulate; any gradient pointer may be NULL (not computed).
+ *
+ * nn.TemporalConvolution(Din, Dout, kW) (dW = 1): x (B, L, Din) -> y (B, L - kW + 1, Dout); weight (Dout, kW*Din),
+ * bias (Dout) or NULL (TemporalConvolutionZeroBias, TemporalConvolutionZeroBias.lua:37-54). */
+size_t s2s_tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW);
+int s2s_tconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* b, float* y);
+int s2s_tconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
+                  float scale, void* scratch, size_t scratch_bytes);
+/* nn.TemporalMaxPooling(kW, dW): x (B, L, D) -> y (B, (L - kW)/dW + 1, D); idx (same shape as y, int32) = argmax
+ * offset within the window, first maximum wins; the backward overwrites dx (B, L, D). */
+int s2s_tmaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const float* x, float* y,
+                     int* idx);
+int s2s_tmaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const int* idx,
+                     const float* dy, float* dx);
+/* nn.SpatialConvolutionMM(Cin, Cout, kW, kH) (stride 1, no padding): x (B, Cin, H, W) -> y (B, Cout, H-kH+1, W-kW+1);
+ * weight (Cout, Cin*kH*kW) in (c, i, j) order, bias (Cout) or NULL.  Scratch holds the im2col panel. */
+size_t s2s_sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW);
+int s2s_sconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* bias, float* y, void* scratch,
+                  size_t scratch_bytes);
+int s2s_sconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* y, const float* dy, float* dx, int dx_accumulate,
+                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes);
+/* nn.SpatialMaxPooling(kW, kH, dW, dH) (floor mode): x (B, C, H, W) -> y (B, C, (H-kH)/dH+1, (W-kW)/dW+1);
+ * idx = i*kW + j of the window's first maximum. */
+int s2s_smaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const float* x, float* y, int* idx);
+int s2s_smaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const int* idx, const float* dy, float* dx);
+/* nn.Transpose2({1,2},3) on a batch (Transpose2.lua:23-37): (B, D1, D2, D3) -> (B, D2, D1, D3); the
+ * backward is the same call with D1 and D2 exchanged.  nn.ReLU: y = max(x, 0), dx = dy * 1[x > 0]. */
+int s2s_swap12(s2s_ctx* ctx, s2s_stream_t stream, int B, int D1, int D2, int D3, const float* x, float* y);
+int s2s_relu_fwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, float* y);
+int s2s_relu_bwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, const float* dy, float* dx);
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
  * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).       */

@@ -1,0 +1,250 @@
+"""CPU oracle for the encoder front-ends.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/ as the checker; nothing in the product path
+(`seq2seq-attention-asr_amd/`, `libs2s_hip.so`) imports or calls it.
+
+NumPy restatement (float64) of the Torch7 `nn` operators (3p, no version pinned by the reference)
+that the reference's two other encoders call, with their published semantics:
+  * conv + BiLSTM encoder, timit/timit.lua:108-125: 3 x [TemporalConvolution(D, 256, 3) -> ReLU ->
+    TemporalMaxPooling(2, 2)] shared by both directions (the same `convlayer` module is applied twice
+    to the same input, :123-124, so its output is one tensor and its weight gradient the sum of both
+    directions' contributions), then RNN(LSTM(256, 128)) forward and reverse, JoinTable(2,2);
+  * VGG encoder, librispeech/model_vgg.lua:23-51: SpatialConvolutionMM(3,64,3,3) ReLU,
+    (64,64,3,3) ReLU, SpatialMaxPooling(2,1,2,1), (64,128,3,3) ReLU, (128,128,3,3) ReLU,
+    SpatialMaxPooling(2,2,2,2), Transpose2({1,2},3), View(-1, 128*H'), four TemporalConvolution(., ., 1)
+    each followed by ReLU.
+Operator semantics restated: TemporalConvolution y_t = W [x_t; ...; x_{t+kW-1}] + b, W (out, kW*in)
+frame-major (pinned by Attention.ipynb cells 4-6, see s2s_oracle.temporal_conv);
+TemporalMaxPooling / SpatialMaxPooling floor mode, first maximum wins (strict >), gradient to the
+argmax; SpatialConvolutionMM weight (out, in*kH*kW) in (c, i, j) order, no padding, stride 1, input
+(C, H, W) with H = time, W = frequency; ReLU dx = dy * 1[x > 0]; Transpose2 swaps dims 1 and 2 of
+(nFeat, L, H) (Transpose2.lua:23-37).  Independently checked against torch.nn.functional autograd in
+tests/test_frontend.py.
+"""
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import s2s_oracle as orc
+
+Array = np.ndarray
+
+
+# ---------------------------------------------------------------- TemporalConvolution (3p)
+
+def tconv_fwd(x: Array, W: Array, b: Optional[Array], kW: int) -> Array:
+    """x (B, L, Din) -> (B, L - kW + 1, Dout); timit/timit.lua:113, model_vgg.lua:43-50."""
+    return orc.temporal_conv(W, b, x, kW)
+
+
+def tconv_bwd(x: Array, W: Array, dy: Array, kW: int):
+    """Returns (dx, dW, db) of TemporalConvolution: dW = sum_t dy_t window_t^T, db = sum_t dy_t,
+    dx[t] = sum_i (W^T dy_{t-i})[i*Din:(i+1)*Din]."""
+    B, L, Din = x.shape
+    Lo = L - kW + 1
+    win = np.stack([x[:, j:j + Lo, :] for j in range(kW)], axis=-2).reshape(B, Lo, kW * Din)
+    dW = np.einsum("blo,blk->ok", dy, win)
+    db = dy.sum(axis=(0, 1))
+    dU = dy @ W  # (B, Lo, kW*Din)
+    dx = np.zeros_like(x)
+    for i in range(kW):
+        dx[:, i:i + Lo, :] += dU[:, :, i * Din:(i + 1) * Din]
+    return dx, dW, db
+
+
+# ---------------------------------------------------------------- TemporalMaxPooling (3p)
+
+def tmaxpool_fwd(x: Array, kW: int, dW: int):
+    """x (B, L, D) -> y (B, (L-kW)//dW + 1, D), idx = argmax offset (first maximum); timit/timit.lua:115."""
+    B, L, D = x.shape
+    Lo = (L - kW) // dW + 1
+    win = np.stack([x[:, i:i + (Lo - 1) * dW + 1:dW, :] for i in range(kW)], axis=0)  # (kW, B, Lo, D)
+    idx = np.argmax(win, axis=0)  # numpy argmax returns the first maximum
+    y = np.take_along_axis(win, idx[None], axis=0)[0]
+    return y, idx
+
+
+def tmaxpool_bwd(idx: Array, dy: Array, L: int, kW: int, dW: int) -> Array:
+    B, Lo, D = dy.shape
+    dx = np.zeros((B, L, D), dy.dtype)
+    bb, oo, cc = np.meshgrid(np.arange(B), np.arange(Lo), np.arange(D), indexing="ij")
+    np.add.at(dx, (bb, oo * dW + idx, cc), dy)
+    return dx
+
+
+# ---------------------------------------------------------------- ReLU (3p)
+
+def relu_fwd(x: Array) -> Array:
+    return np.maximum(x, 0.0)
+
+
+def relu_bwd(x: Array, dy: Array) -> Array:
+    return np.where(x > 0, dy, 0.0)
+
+
+# ---------------------------------------------------------------- SpatialConvolutionMM (3p)
+
+def _im2col(x: Array, kH: int, kW: int) -> Array:
+    """x (B, C, H, W) -> (B, C*kH*kW, Ho*Wo) in (c, i, j) row order."""
+    B, C, H, W = x.shape
+    Ho, Wo = H - kH + 1, W - kW + 1
+    cols = np.stack([x[:, :, i:i + Ho, j:j + Wo] for i in range(kH) for j in range(kW)], axis=2)  # (B,C,kHkW,Ho,Wo)
+    return cols.reshape(B, C * kH * kW, Ho * Wo)
+
+
+def sconv_fwd(x: Array, Wt: Array, b: Optional[Array], kH: int, kW: int) -> Array:
+    """model_vgg.lua:24-32: y[b, o] = Wt[o] . unfold(x[b]) + b[o]."""
+    B, C, H, W = x.shape
+    Ho, Wo = H - kH + 1, W - kW + 1
+    y = np.einsum("ok,bkn->bon", Wt, _im2col(x, kH, kW))
+    if b is not None:
+        y = y + b[None, :, None]
+    return y.reshape(B, Wt.shape[0], Ho, Wo)
+
+
+def sconv_bwd(x: Array, Wt: Array, dy: Array, kH: int, kW: int):
+    B, C, H, W = x.shape
+    Ho, Wo = H - kH + 1, W - kW + 1
+    O = Wt.shape[0]
+    d2 = dy.reshape(B, O, Ho * Wo)
+    dW = np.einsum("bon,bkn->ok", d2, _im2col(x, kH, kW))
+    db = d2.sum(axis=(0, 2))
+    dcol = np.einsum("ok,bon->bkn", Wt, d2).reshape(B, C, kH, kW, Ho, Wo)
+    dx = np.zeros_like(x)
+    for i in range(kH):
+        for j in range(kW):
+            dx[:, :, i:i + Ho, j:j + Wo] += dcol[:, :, i, j]
+    return dx, dW, db
+
+
+# ---------------------------------------------------------------- SpatialMaxPooling (3p)
+
+def smaxpool_fwd(x: Array, kW: int, kH: int, dW: int, dH: int):
+    """x (B, C, H, W) -> y (B, C, Ho, Wo); idx = i*kW + j of the window's first maximum (scan i then j)."""
+    B, C, H, W = x.shape
+    Ho, Wo = (H - kH) // dH + 1, (W - kW) // dW + 1
+    win = np.stack([x[:, :, i:i + (Ho - 1) * dH + 1:dH, j:j + (Wo - 1) * dW + 1:dW]
+                    for i in range(kH) for j in range(kW)], axis=0)
+    idx = np.argmax(win, axis=0)
+    y = np.take_along_axis(win, idx[None], axis=0)[0]
+    return y, idx
+
+
+def smaxpool_bwd(idx: Array, dy: Array, H: int, W: int, kW: int, kH: int, dW: int, dH: int) -> Array:
+    B, C, Ho, Wo = dy.shape
+    dx = np.zeros((B, C, H, W), dy.dtype)
+    bb, cc, oh, ow = np.meshgrid(np.arange(B), np.arange(C), np.arange(Ho), np.arange(Wo), indexing="ij")
+    np.add.at(dx, (bb, cc, oh * dH + idx // kW, ow * dW + idx % kW), dy)
+    return dx
+
+
+# ---------------------------------------------------------------- encoders
+
+def conv_stack_fwd(x: Array, P: Dict[str, Array], nconv: int = 3, kW: int = 3):
+    """The shared `convlayer` of timit/timit.lua:112-121 on x (B, L, D)."""
+    cache = []
+    h = x
+    for l in range(nconv):
+        u = tconv_fwd(h, P[f"conv{l}.W"], P[f"conv{l}.b"], kW)
+        r = relu_fwd(u)
+        p, idx = tmaxpool_fwd(r, 2, 2)
+        cache.append((h, u, idx, r.shape[1]))
+        h = p
+    return h, cache
+
+
+def conv_stack_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], kW: int = 3, scale: float = 1.0):
+    d = dout
+    for l in reversed(range(len(cache))):
+        h, u, idx, Lr = cache[l]
+        dr = tmaxpool_bwd(idx, d, Lr, 2, 2)
+        du = relu_bwd(u, dr)
+        dx, dW, db = tconv_bwd(h, P[f"conv{l}.W"], du, kW)
+        G[f"conv{l}.W"] += scale * dW
+        G[f"conv{l}.b"] += scale * db
+        d = dx
+    return d
+
+
+def _lstm_p(P, prefix):
+    return {k[len(prefix):]: v for k, v in P.items() if k.startswith(prefix)}
+
+
+def conv_bilstm_fwd(x: Array, P: Dict[str, Array]):
+    """timit/timit.lua:108-125: conv stack -> [RNN(LSTM) fwd | RNN(LSTM) reverse] (JoinTable(2,2))."""
+    c, ccache = conv_stack_fwd(x, P)
+    yf, sf = orc.lstm_seq_fwd(c, _lstm_p(P, "f."), reverse=False)
+    yb, sb = orc.lstm_seq_fwd(c, _lstm_p(P, "b."), reverse=True)
+    return np.concatenate([yf, yb], axis=-1), (c, ccache, sf, sb)
+
+
+def conv_bilstm_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], scale: float = 1.0):
+    c, ccache, sf, sb = cache
+    H = dout.shape[-1] // 2
+    gf, gb = {k: np.zeros_like(v) for k, v in _lstm_p(P, "f.").items()}, {k: np.zeros_like(v) for k, v in
+                                                                          _lstm_p(P, "b.").items()}
+    dcf = orc.lstm_seq_bwd(c, _lstm_p(P, "f."), sf, dout[..., :H], gf, reverse=False, scale=scale)
+    dcb = orc.lstm_seq_bwd(c, _lstm_p(P, "b."), sb, dout[..., H:], gb, reverse=True, scale=scale)
+    for k, v in gf.items():
+        G["f." + k] += v
+    for k, v in gb.items():
+        G["b." + k] += v
+    return conv_stack_bwd(P, ccache, dcf + dcb, G, scale=scale)
+
+
+VGG_CONVS = ((3, 64), (64, 64), (64, 128), (128, 128))
+VGG_POOLS = {1: (2, 1, 2, 1), 3: (2, 2, 2, 2)}  # after conv index: (kW, kH, dW, dH)
+
+
+def vgg_dims(F: int, hidden: int = 2048, out: int = 512):
+    Hf = ((F - 4) // 2 - 4) // 2
+    return [(128 * Hf, hidden), (hidden, hidden), (hidden, hidden), (hidden, out)]
+
+
+def vgg_fwd(x: Array, P: Dict[str, Array]):
+    """librispeech/model_vgg.lua:23-51 on x (B, 3, L, F) -> (B, (L-8)//2, out)."""
+    cache = {"conv": [], "pool": {}, "lin": []}
+    h = x
+    for l in range(4):
+        u = sconv_fwd(h, P[f"vgg{l}.W"], P[f"vgg{l}.b"], 3, 3)
+        r = relu_fwd(u)
+        cache["conv"].append((h, u))
+        h = r
+        if l in VGG_POOLS:
+            kW, kH, dW, dH = VGG_POOLS[l]
+            p, idx = smaxpool_fwd(h, kW, kH, dW, dH)
+            cache["pool"][l] = (idx, h.shape)
+            h = p
+    B, C, Lq, Hf = h.shape
+    cache["tshape"] = h.shape
+    h = h.transpose(0, 2, 1, 3).reshape(B, Lq, C * Hf)  # Transpose2({1,2},3) + View(-1, 128*H)
+    for l in range(4):
+        u = tconv_fwd(h, P[f"lin{l}.W"], P[f"lin{l}.b"], 1)
+        cache["lin"].append((h, u))
+        h = relu_fwd(u)
+    return h, cache
+
+
+def vgg_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], scale: float = 1.0):
+    d = dout
+    for l in reversed(range(4)):
+        h, u = cache["lin"][l]
+        du = relu_bwd(u, d)
+        dx, dW, db = tconv_bwd(h, P[f"lin{l}.W"], du, 1)
+        G[f"lin{l}.W"] += scale * dW
+        G[f"lin{l}.b"] += scale * db
+        d = dx
+    B, C, Lq, Hf = cache["tshape"]
+    d = d.reshape(B, Lq, C, Hf).transpose(0, 2, 1, 3)
+    for l in reversed(range(4)):
+        if l in VGG_POOLS:
+            kW, kH, dW, dH = VGG_POOLS[l]
+            idx, shp = cache["pool"][l]
+            d = smaxpool_bwd(idx, d, shp[2], shp[3], kW, kH, dW, dH)
+        h, u = cache["conv"][l]
+        du = relu_bwd(u, d)
+        dx, dW, db = sconv_bwd(h, P[f"vgg{l}.W"], du, 3, 3)
+        G[f"vgg{l}.W"] += scale * dW
+        G[f"vgg{l}.b"] += scale * db
+        d = dx
+    return d

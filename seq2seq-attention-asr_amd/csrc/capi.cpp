@@ -13,6 +13,7 @@
 #include <vector>
 
 #include "attn.h"
+#include "frontend.h"
 #include "gru_persist.h"
 #include "gru.h"
 #include "lstm.h"
@@ -652,6 +653,81 @@ int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, co
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(n == 0 || (a && alen && b && blen && out), "edit distance: null argument");
   return edit_distance(static_cast<hipStream_t>(stream), n, a, alen, lda, b, blen, ldb, out);
+}
+
+// ---------------------------------------------------------------- encoder front-ends (frontend.hip)
+size_t s2s_tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW) {
+  return tconv_scratch_bytes(B, L, Din, Dout, kW);
+}
+int s2s_tconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* b, float* y) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && W && y, "TemporalConvolution: null argument");
+  return tconv_fwd(static_cast<hipStream_t>(stream), B, L, Din, Dout, kW, relu, x, W, b, y);
+}
+int s2s_tconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
+                  float scale, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && W && dy && scratch, "TemporalConvolution: null argument");
+  return tconv_bwd(static_cast<hipStream_t>(stream), B, L, Din, Dout, kW, relu, x, W, y, dy, dx, dx_accumulate, dW, db,
+                   scale, scratch, scratch_bytes);
+}
+int s2s_tmaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const float* x, float* y,
+                     int* idx) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && y && idx, "TemporalMaxPooling: null argument");
+  return tmaxpool_fwd(static_cast<hipStream_t>(stream), B, L, D, kW, dW, x, y, idx);
+}
+int s2s_tmaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const int* idx,
+                     const float* dy, float* dx) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(idx && dy && dx, "TemporalMaxPooling: null argument");
+  return tmaxpool_bwd(static_cast<hipStream_t>(stream), B, L, D, kW, dW, idx, dy, dx);
+}
+size_t s2s_sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
+  return sconv_scratch_bytes(B, Cin, H, W, Cout, kH, kW);
+}
+int s2s_sconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* bias, float* y, void* scratch,
+                  size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && weight && y && scratch, "SpatialConvolutionMM: null argument");
+  return sconv_fwd(static_cast<hipStream_t>(stream), B, Cin, H, W, Cout, kH, kW, relu, x, weight, bias, y, scratch,
+                   scratch_bytes);
+}
+int s2s_sconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* y, const float* dy, float* dx, int dx_accumulate,
+                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && weight && dy && scratch, "SpatialConvolutionMM: null argument");
+  return sconv_bwd(static_cast<hipStream_t>(stream), B, Cin, H, W, Cout, kH, kW, relu, x, weight, y, dy, dx,
+                   dx_accumulate, dweight, dbias, scale, scratch, scratch_bytes);
+}
+int s2s_smaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const float* x, float* y, int* idx) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && y && idx, "SpatialMaxPooling: null argument");
+  return smaxpool_fwd(static_cast<hipStream_t>(stream), B, C, H, W, kW, kH, dW, dH, x, y, idx);
+}
+int s2s_smaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const int* idx, const float* dy, float* dx) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(idx && dy && dx, "SpatialMaxPooling: null argument");
+  return smaxpool_bwd(static_cast<hipStream_t>(stream), B, C, H, W, kW, kH, dW, dH, idx, dy, dx);
+}
+int s2s_swap12(s2s_ctx* ctx, s2s_stream_t stream, int B, int D1, int D2, int D3, const float* x, float* y) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && y && x != y, "Transpose2: null or in-place argument");
+  return swap12(static_cast<hipStream_t>(stream), B, D1, D2, D3, x, y);
+}
+int s2s_relu_fwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, float* y) {
+  S2S_TRY(set_device(ctx));
+  return relu_fwd(static_cast<hipStream_t>(stream), n, x, y);
+}
+int s2s_relu_bwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, const float* dy, float* dx) {
+  S2S_TRY(set_device(ctx));
+  return relu_bwd(static_cast<hipStream_t>(stream), n, x, dy, dx);
 }
 
 int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,

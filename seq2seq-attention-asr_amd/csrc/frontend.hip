@@ -1,0 +1,439 @@
+// Encoder front-ends: the operators of the two non-GRU encoders the reference
+// builds --
+//   * the conv + BiLSTM encoder of timit/timit.lua:108-125: 3 x [TemporalConvolution(D, 256, 3) ->
+//     ReLU -> TemporalMaxPooling(2, 2)], then a BiLSTM (csrc/lstm.hip);
+//   * the VGG stack of librispeech/model_vgg.lua:23-51: SpatialConvolutionMM(3x3) + ReLU pairs,
+//     SpatialMaxPooling(2,1,2,1) / (2,2,2,2), Transpose2({1,2},3) + View, four
+//     TemporalConvolution(., ., 1) + ReLU layers.
+// Torch7 layouts at the boundary: TemporalConvolution x (B, L, Din), W (Dout, kW*Din) with the
+// window's frames consecutive (row = [x_t | x_{t+1} | ...]); SpatialConvolutionMM x (B, C, H, W)
+// with H = time, W = frequency (model_vgg.lua:37-41), weight (Cout, Cin*kH*kW) in (c, i, j) order.
+//
+// MI355X mapping: every contraction is the fp32 MFMA GEMM of gemm_f32.hip.
+//   * TemporalConvolution needs no unfold: window t of utterance b is the CONTIGUOUS row segment
+//     x[b, t:t+kW, :], so the forward is one GEMM per utterance on A = x_b with lda = Din and
+//     K = kW*Din (overlapping rows), bias and ReLU in the epilogue.  The weight gradient runs as ONE
+//     GEMM over all B*L - kW + 1 window rows of the batch against dY zero-padded to L rows per
+//     utterance (the windows that straddle two utterances meet zero rows), and dx is dU = dY W
+//     followed by a gather dx[t] = sum_i dU[t - i, i*Din:(i+1)*Din].
+//   * SpatialConvolutionMM: im2col into a (K, B*N) panel (K = Cin*kH*kW, N = H'*W'), forward GEMMs
+//     write NCHW directly (one problem per utterance, channel bias per output row, ReLU in the
+//     epilogue); the backward permutes dY (masked by the ReLU) into (Cout, B*N) once, so dW is one
+//     NT GEMM over all B*N columns and the input gradient one TN GEMM (dcol) + a col2im gather.
+//   * Pooling, masks, permutes: one thread per output element, coalesced along the innermost dim.
+// Every reduction has a fixed order (deterministic, graph-replay safe).
+#include "s2s_common.h"
+
+#include <algorithm>
+
+namespace s2s {
+
+namespace {
+
+inline unsigned grid1d(long n, int per = 256) { return (unsigned)std::min<long>(4096, (n + per - 1) / per); }
+
+// dyp[b, t, :] = dy[b, t, :] * (relu ? 1[y > 0] : 1) for t < Lo; 0 for Lo <= t < L.
+__global__ void tconv_pad_dy(const float* __restrict__ dy, const float* __restrict__ y, int relu, int B, int L,
+                             int Lo, int D, float* __restrict__ dyp) {
+  const long n = (long)B * L * D;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % D);
+    const long bt = e / D;
+    const int t = (int)(bt % L), b = (int)(bt / L);
+    float v = 0.f;
+    if (t < Lo) {
+      const long src = ((long)b * Lo + t) * D + c;
+      v = dy[src];
+      if (relu && !(y[src] > 0.f)) v = 0.f;
+    }
+    dyp[e] = v;
+  }
+}
+
+// dx[b, t, c] (+)= sum_{i <= t, i < kW} dU[b*L + t - i, i*Din + c]  (window rows past Lo are zero in dU)
+__global__ void tconv_gather_dx(const float* __restrict__ dU, int B, int L, int Din, int kW, int acc,
+                                float* __restrict__ dx) {
+  const long n = (long)B * L * Din;
+  const long ldu = (long)kW * Din;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % Din);
+    const long bt = e / Din;
+    const int t = (int)(bt % L);
+    float s = 0.f;
+    for (int i = 0; i < kW && i <= t; ++i) s += dU[(bt - i) * ldu + (long)i * Din + c];
+    dx[e] = acc ? dx[e] + s : s;
+  }
+}
+
+// TemporalMaxPooling(kW, dW): y[b, o, c] = max_{i < kW} x[b, o*dW + i, c], first maximum wins (strict >)
+__global__ void tmaxpool_fwd_kernel(const float* __restrict__ x, int B, int L, int D, int kW, int dW, int Lo,
+                                    float* __restrict__ y, int* __restrict__ idx) {
+  const long n = (long)B * Lo * D;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % D);
+    const long bo = e / D;
+    const int o = (int)(bo % Lo), b = (int)(bo / Lo);
+    const float* xp = x + ((long)b * L + (long)o * dW) * D + c;
+    float m = xp[0];
+    int k = 0;
+    for (int i = 1; i < kW; ++i) {
+      const float v = xp[(long)i * D];
+      if (v > m) {
+        m = v;
+        k = i;
+      }
+    }
+    y[e] = m;
+    idx[e] = k;
+  }
+}
+
+// dx[b, t, c] = sum over windows o containing t whose argmax is t of dy[b, o, c]  (gather: no atomics)
+__global__ void tmaxpool_bwd_kernel(const int* __restrict__ idx, const float* __restrict__ dy, int B, int L, int D,
+                                    int kW, int dW, int Lo, float* __restrict__ dx) {
+  const long n = (long)B * L * D;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int c = (int)(e % D);
+    const long bt = e / D;
+    const int t = (int)(bt % L), b = (int)(bt / L);
+    float s = 0.f;
+    const int ohi = min(t / dW, Lo - 1);
+    for (int o = ohi; o >= 0 && o * dW + kW > t; --o) {
+      const long oe = ((long)b * Lo + o) * D + c;
+      if (o * dW + idx[oe] == t) s += dy[oe];
+    }
+    dx[e] = s;
+  }
+}
+
+// col[(c*kH + i)*kW + j][b*N + oh*Wo + ow] = x[b, c, oh + i, ow + j]   (col row stride B*N)
+__global__ void im2col_kernel(const float* __restrict__ x, int B, int C, int H, int W, int kH, int kW, int Ho,
+                              int Wo, float* __restrict__ col) {
+  const long N = (long)Ho * Wo, BN = B * N;
+  const long n = (long)C * kH * kW * BN;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long q = e % BN;
+    const int r = (int)(e / BN);
+    const int b = (int)(q / N);
+    const int p = (int)(q % N);
+    const int oh = p / Wo, ow = p % Wo;
+    const int j = r % kW, i = (r / kW) % kH, c = r / (kW * kH);
+    col[e] = x[(((long)b * C + c) * H + oh + i) * W + ow + j];
+  }
+}
+
+// dx[b, c, h, w] (+)= sum_{i, j valid} dcol[(c*kH + i)*kW + j][b*N + (h - i)*Wo + (w - j)]
+__global__ void col2im_kernel(const float* __restrict__ dcol, int B, int C, int H, int W, int kH, int kW, int Ho,
+                              int Wo, int acc, float* __restrict__ dx) {
+  const long N = (long)Ho * Wo, BN = B * N;
+  const long n = (long)B * C * H * W;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int w = (int)(e % W);
+    const int h = (int)((e / W) % H);
+    const int c = (int)((e / ((long)W * H)) % C);
+    const int b = (int)(e / ((long)W * H * C));
+    float s = 0.f;
+    for (int i = 0; i < kH; ++i) {
+      const int oh = h - i;
+      if (oh < 0 || oh >= Ho) continue;
+      for (int j = 0; j < kW; ++j) {
+        const int ow = w - j;
+        if (ow < 0 || ow >= Wo) continue;
+        s += dcol[((long)(c * kH + i) * kW + j) * BN + (long)b * N + (long)oh * Wo + ow];
+      }
+    }
+    dx[e] = acc ? dx[e] + s : s;
+  }
+}
+
+// dyt[c][b*N + p] = dy[b, c, p] * (relu ? 1[y > 0] : 1)
+__global__ void nchw_to_cbn_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu, int B, int C,
+                                   long N, float* __restrict__ dyt) {
+  const long n = (long)B * C * N;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const long p = e % N;
+    const int c = (int)((e / N) % C);
+    const int b = (int)(e / (N * C));
+    float v = dy[e];
+    if (relu && !(y[e] > 0.f)) v = 0.f;
+    dyt[(long)c * B * N + (long)b * N + p] = v;
+  }
+}
+
+// out[r] = beta*out[r] + alpha * sum_j X[r*ld + j]  (one workgroup per row, fixed order)
+__global__ void rowsum_kernel(const float* __restrict__ X, long ld, long ncols, float alpha, float beta,
+                              float* __restrict__ out) {
+  __shared__ float red[4];
+  const float* row = X + blockIdx.x * ld;
+  float s = 0.f;
+  for (long j = threadIdx.x; j < ncols; j += 256) s += row[j];
+  s = wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float t = (red[0] + red[1]) + (red[2] + red[3]);
+    out[blockIdx.x] = (beta == 0.f ? 0.f : beta * out[blockIdx.x]) + alpha * t;
+  }
+}
+
+// SpatialMaxPooling(kW, kH, dW, dH) on (B*C) planes, floor mode; first maximum in (i, j) scan order
+__global__ void smaxpool_fwd_kernel(const float* __restrict__ x, long planes, int H, int W, int kW, int kH, int dW,
+                                    int dH, int Ho, int Wo, float* __restrict__ y, int* __restrict__ idx) {
+  const long n = planes * Ho * Wo;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int ow = (int)(e % Wo);
+    const int oh = (int)((e / Wo) % Ho);
+    const long pl = e / ((long)Wo * Ho);
+    const float* xp = x + (pl * H + (long)oh * dH) * W + (long)ow * dW;
+    float m = xp[0];
+    int k = 0;
+    for (int i = 0; i < kH; ++i)
+      for (int j = 0; j < kW; ++j) {
+        const float v = xp[(long)i * W + j];
+        if (v > m) {
+          m = v;
+          k = i * kW + j;
+        }
+      }
+    y[e] = m;
+    idx[e] = k;
+  }
+}
+
+__global__ void smaxpool_bwd_kernel(const int* __restrict__ idx, const float* __restrict__ dy, long planes, int H,
+                                    int W, int kW, int kH, int dW, int dH, int Ho, int Wo, float* __restrict__ dx) {
+  const long n = planes * H * W;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int w = (int)(e % W);
+    const int h = (int)((e / W) % H);
+    const long pl = e / ((long)W * H);
+    float s = 0.f;
+    for (int oh = min(h / dH, Ho - 1); oh >= 0 && oh * dH + kH > h; --oh)
+      for (int ow = min(w / dW, Wo - 1); ow >= 0 && ow * dW + kW > w; --ow) {
+        const long oe = (pl * Ho + oh) * Wo + ow;
+        const int k = idx[oe];
+        if (oh * dH + k / kW == h && ow * dW + k % kW == w) s += dy[oe];
+      }
+    dx[e] = s;
+  }
+}
+
+// (B, D1, D2, D3) -> (B, D2, D1, D3)   (Transpose2({1,2},3) with the batch leading; its own inverse
+// with D1, D2 exchanged).  e enumerates the output, so the stores are coalesced.
+__global__ void swap12_kernel(const float* __restrict__ x, int B, int D1, int D2, int D3, float* __restrict__ y) {
+  const long n = (long)B * D1 * D2 * D3;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
+    const int k = (int)(e % D3);
+    const int j = (int)((e / D3) % D1);          // output dim 2 = input dim 1
+    const int i = (int)((e / ((long)D3 * D1)) % D2);  // output dim 1 = input dim 2
+    const int b = (int)(e / ((long)D3 * D1 * D2));
+    y[e] = x[(((long)b * D1 + j) * D2 + i) * D3 + k];
+  }
+}
+
+// y = relu(x) ; dx = dy * 1[x > 0]
+__global__ void relu_fwd_kernel(const float* __restrict__ x, long n, float* __restrict__ y) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) y[e] = fmaxf(x[e], 0.f);
+}
+__global__ void relu_bwd_kernel(const float* __restrict__ x, const float* __restrict__ dy, long n,
+                                float* __restrict__ dx) {
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) dx[e] = x[e] > 0.f ? dy[e] : 0.f;
+}
+
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+}  // namespace
+
+// ------------------------------------------------------------------ TemporalConvolution
+// scratch layout: [split-K slabs | ...]: the weight-gradient GEMMs have few output tiles and a very
+// long K (every window / pixel of the batch), so they run split-K
+constexpr size_t kWsBytes = sizeof(float) * kGemmWsFloats;
+inline GemmWs ws_of(void* scratch) { return GemmWs{static_cast<float*>(scratch), kGemmWsFloats}; }
+
+size_t tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW) {
+  return kWsBytes + align256(sizeof(float) * (size_t)B * L * Dout) + align256(sizeof(float) * (size_t)B * L * kW * Din);
+}
+
+int tconv_fwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W,
+              const float* b, float* y) {
+  S2S_REQUIRE(B > 0 && Din > 0 && Dout > 0 && kW > 0, "TemporalConvolution: bad sizes");
+  S2S_REQUIRE(L >= kW, "TemporalConvolution: input sequence smaller than kernel size");
+  const int Lo = L - kW + 1;
+  for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
+    GemmProblem pr[kMaxGemmBatch];
+    const int nb = std::min(kMaxGemmBatch, B - b0);
+    for (int i = 0; i < nb; ++i) {
+      const long u = b0 + i;
+      pr[i] = GemmProblem{x + u * L * Din, W, y + u * Lo * Dout, b, Din, (long)kW * Din, Dout, Lo, Dout, kW * Din,
+                          1.f, 0.f};
+      pr[i].relu = relu;
+    }
+    S2S_TRY(gemm_f32(st, pr, nb, false, true));
+  }
+  return 0;
+}
+
+int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W,
+              const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db, float scale,
+              void* scratch, size_t scratch_bytes) {
+  S2S_REQUIRE(L >= kW && B > 0, "TemporalConvolution: bad sizes");
+  S2S_REQUIRE(!relu || y, "TemporalConvolution: relu backward needs the forward output");
+  S2S_REQUIRE(scratch_bytes >= tconv_scratch_bytes(B, L, Din, Dout, kW), "TemporalConvolution: scratch too small");
+  const int Lo = L - kW + 1;
+  float* dyp = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes);
+  float* dU = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes +
+                                       align256(sizeof(float) * (size_t)B * L * Dout));
+  hipLaunchKernelGGL(tconv_pad_dy, dim3(grid1d((long)B * L * Dout)), dim3(256), 0, st, dy, y, relu, B, L, Lo, Dout,
+                     dyp);
+  S2S_CHECK_HIP(hipGetLastError());
+  const long rows = (long)B * L - kW + 1;  // every window start of the flattened batch
+  // gradBias += scale * sum_t dY_t ; gradWeight += scale * dY^T [x_t | ... | x_{t+kW-1}]
+  if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db));
+  if (dW) S2S_TRY(gemm1(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
+                        nullptr, ws_of(scratch)));
+  if (dx) {
+    S2S_TRY(gemm1(st, false, false, B * L, kW * Din, Dout, 1.f, dyp, Dout, W, (long)kW * Din, 0.f, dU,
+                  (long)kW * Din));
+    hipLaunchKernelGGL(tconv_gather_dx, dim3(grid1d((long)B * L * Din)), dim3(256), 0, st, dU, B, L, Din, kW,
+                       dx_accumulate, dx);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ TemporalMaxPooling
+int tmaxpool_fwd(hipStream_t st, int B, int L, int D, int kW, int dW, const float* x, float* y, int* idx) {
+  S2S_REQUIRE(kW > 0 && dW > 0 && L >= kW, "TemporalMaxPooling: input sequence smaller than kernel size");
+  const int Lo = (L - kW) / dW + 1;
+  hipLaunchKernelGGL(tmaxpool_fwd_kernel, dim3(grid1d((long)B * Lo * D)), dim3(256), 0, st, x, B, L, D, kW, dW, Lo,
+                     y, idx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int tmaxpool_bwd(hipStream_t st, int B, int L, int D, int kW, int dW, const int* idx, const float* dy, float* dx) {
+  S2S_REQUIRE(kW > 0 && dW > 0 && L >= kW, "TemporalMaxPooling: bad sizes");
+  const int Lo = (L - kW) / dW + 1;
+  hipLaunchKernelGGL(tmaxpool_bwd_kernel, dim3(grid1d((long)B * L * D)), dim3(256), 0, st, idx, dy, B, L, D, kW, dW,
+                     Lo, dx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// ------------------------------------------------------------------ SpatialConvolutionMM
+size_t sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
+  const size_t N = (size_t)(H - kH + 1) * (W - kW + 1);
+  const size_t K = (size_t)Cin * kH * kW;
+  return kWsBytes + 2 * align256(sizeof(float) * K * B * N) + align256(sizeof(float) * (size_t)Cout * B * N);
+}
+
+int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
+              const float* Wt, const float* bias, float* y, void* scratch, size_t scratch_bytes) {
+  S2S_REQUIRE(B > 0 && Cin > 0 && Cout > 0 && kH > 0 && kW > 0, "SpatialConvolutionMM: bad sizes");
+  S2S_REQUIRE(H >= kH && W >= kW, "SpatialConvolutionMM: input image smaller than kernel");
+  S2S_REQUIRE(scratch_bytes >= sconv_scratch_bytes(B, Cin, H, W, Cout, kH, kW), "SpatialConvolutionMM: scratch too small");
+  const int Ho = H - kH + 1, Wo = W - kW + 1;
+  const long N = (long)Ho * Wo;
+  const int K = Cin * kH * kW;
+  float* col = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes);
+  hipLaunchKernelGGL(im2col_kernel, dim3(grid1d((long)K * B * N)), dim3(256), 0, st, x, B, Cin, H, W, kH, kW, Ho, Wo,
+                     col);
+  S2S_CHECK_HIP(hipGetLastError());
+  // y_b (Cout, N) = W (Cout, K) col[:, b*N : (b+1)*N] + bias (per row), ReLU in the epilogue
+  for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
+    GemmProblem pr[kMaxGemmBatch];
+    const int nb = std::min(kMaxGemmBatch, B - b0);
+    for (int i = 0; i < nb; ++i) {
+      const long u = b0 + i;
+      pr[i] = GemmProblem{Wt, col + u * N, y + u * Cout * N, nullptr, K, (long)B * N, N, Cout, (int)N, K, 1.f, 0.f};
+      pr[i].rbias = bias;
+      pr[i].relu = relu;
+    }
+    S2S_TRY(gemm_f32(st, pr, nb, false, false));
+  }
+  return 0;
+}
+
+int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
+              const float* Wt, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
+              float scale, void* scratch, size_t scratch_bytes) {
+  S2S_REQUIRE(H >= kH && W >= kW && B > 0, "SpatialConvolutionMM: bad sizes");
+  S2S_REQUIRE(!relu || y, "SpatialConvolutionMM: relu backward needs the forward output");
+  S2S_REQUIRE(scratch_bytes >= sconv_scratch_bytes(B, Cin, H, W, Cout, kH, kW), "SpatialConvolutionMM: scratch too small");
+  const int Ho = H - kH + 1, Wo = W - kW + 1;
+  const long N = (long)Ho * Wo, BN = B * N;
+  const int K = Cin * kH * kW;
+  char* base = static_cast<char*>(scratch) + kWsBytes;
+  float* col = reinterpret_cast<float*>(base);
+  float* dcol = reinterpret_cast<float*>(base + align256(sizeof(float) * K * BN));
+  float* dyt = reinterpret_cast<float*>(base + 2 * align256(sizeof(float) * K * BN));
+  hipLaunchKernelGGL(nchw_to_cbn_kernel, dim3(grid1d((long)Cout * BN)), dim3(256), 0, st, dy, y, relu, B, Cout, N,
+                     dyt);
+  S2S_CHECK_HIP(hipGetLastError());
+  if (db) {
+    hipLaunchKernelGGL(rowsum_kernel, dim3(Cout), dim3(256), 0, st, dyt, BN, BN, scale, 1.f, db);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
+  if (dW) {
+    hipLaunchKernelGGL(im2col_kernel, dim3(grid1d((long)K * BN)), dim3(256), 0, st, x, B, Cin, H, W, kH, kW, Ho, Wo,
+                       col);
+    S2S_CHECK_HIP(hipGetLastError());
+    // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
+    S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
+  }
+  if (dx) {
+    // dcol (K, B*N) = W^T dyt ; dx = col2im(dcol)
+    S2S_TRY(gemm1(st, true, false, K, (int)BN, Cout, 1.f, Wt, K, dyt, BN, 0.f, dcol, BN));
+    hipLaunchKernelGGL(col2im_kernel, dim3(grid1d((long)B * Cin * H * W)), dim3(256), 0, st, dcol, B, Cin, H, W, kH,
+                       kW, Ho, Wo, dx_accumulate, dx);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
+  return 0;
+}
+
+// ------------------------------------------------------------------ SpatialMaxPooling, Transpose2, ReLU
+int smaxpool_fwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int dW, int dH, const float* x, float* y,
+                 int* idx) {
+  S2S_REQUIRE(kW > 0 && kH > 0 && dW > 0 && dH > 0 && H >= kH && W >= kW, "SpatialMaxPooling: bad sizes");
+  const int Ho = (H - kH) / dH + 1, Wo = (W - kW) / dW + 1;
+  const long planes = (long)B * C;
+  hipLaunchKernelGGL(smaxpool_fwd_kernel, dim3(grid1d(planes * Ho * Wo)), dim3(256), 0, st, x, planes, H, W, kW, kH,
+                     dW, dH, Ho, Wo, y, idx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int smaxpool_bwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int dW, int dH, const int* idx,
+                 const float* dy, float* dx) {
+  S2S_REQUIRE(kW > 0 && kH > 0 && dW > 0 && dH > 0 && H >= kH && W >= kW, "SpatialMaxPooling: bad sizes");
+  const int Ho = (H - kH) / dH + 1, Wo = (W - kW) / dW + 1;
+  const long planes = (long)B * C;
+  hipLaunchKernelGGL(smaxpool_bwd_kernel, dim3(grid1d(planes * H * W)), dim3(256), 0, st, idx, dy, planes, H, W, kW,
+                     kH, dW, dH, Ho, Wo, dx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int swap12(hipStream_t st, int B, int D1, int D2, int D3, const float* x, float* y) {
+  const long n = (long)B * D1 * D2 * D3;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(swap12_kernel, dim3(grid1d(n)), dim3(256), 0, st, x, B, D1, D2, D3, y);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int relu_fwd(hipStream_t st, long n, const float* x, float* y) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(relu_fwd_kernel, dim3(grid1d(n)), dim3(256), 0, st, x, n, y);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int relu_bwd(hipStream_t st, long n, const float* x, const float* dy, float* dx) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid1d(n)), dim3(256), 0, st, x, dy, n, dx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace s2s

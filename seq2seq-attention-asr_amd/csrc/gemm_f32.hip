@@ -229,8 +229,10 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
           } else {
             float v = alpha * acc[f][g][r];
             if (bias) v += bias[col];
+            if (q.p.rbias) v += q.p.rbias[row];
             float* c = C + (long)row * q.p.ldc + col;
             if (beta != 0.f) v += beta * *c;
+            if (q.p.relu) v = fmaxf(v, 0.f);
             *c = v;
           }
         }
@@ -256,8 +258,12 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
       const int row = (int)(e / N), col = (int)(e % N);
       floatx4 v = alpha * sum;
       if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
+      if (q.p.rbias) v += q.p.rbias[row];
       floatx4* c = reinterpret_cast<floatx4*>(q.p.C + (long)row * q.p.ldc + col);
       if (beta != 0.f) v += beta * *c;
+      if (q.p.relu)
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) v[e2] = fmaxf(v[e2], 0.f);
       *c = v;
     }
     return;
@@ -268,8 +274,10 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
     const int row = (int)(e / N), col = (int)(e % N);
     float v = alpha * sum;
     if (bias) v += bias[col];
+    if (q.p.rbias) v += q.p.rbias[row];
     float* c = q.p.C + (long)row * q.p.ldc + col;
     if (beta != 0.f) v += beta * *c;
+    if (q.p.relu) v = fmaxf(v, 0.f);
     *c = v;
   }
 }

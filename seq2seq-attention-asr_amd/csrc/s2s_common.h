@@ -71,6 +71,8 @@ struct GemmProblem {
   int M, N, K;
   float alpha, beta;
   int Mread = 0, Nread = 0;
+  const float* rbias = nullptr;  // + rbias[row] (per output row, e.g. conv channels in NCHW)
+  int relu = 0;                  // epilogue max(v, 0) after bias and beta (fused nn.ReLU)
 };
 constexpr int kMaxGemmBatch = 16;
 // Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs

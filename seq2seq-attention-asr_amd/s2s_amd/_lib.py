@@ -87,6 +87,28 @@ SIGNATURES = [
     ("s2s_model_bucket_count", c_int, [P(s2s_model_dims)]),
     ("s2s_model_bucket", c_int, [P(s2s_model_dims), c_int, P(c_size_t), P(c_size_t)]),
     ("s2s_stream_wait_bucket", c_int, [c_void_p, c_void_p, c_int]),
+    ("s2s_tconv_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+    ("s2s_tconv_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                              c_void_p, c_void_p]),
+    ("s2s_tconv_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p, c_size_t]),
+    ("s2s_tmaxpool_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
+    ("s2s_tmaxpool_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p]),
+    ("s2s_sconv_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int, c_int]),
+    ("s2s_sconv_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
+    ("s2s_sconv_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                              c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
+                              c_size_t]),
+    ("s2s_smaxpool_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_void_p, c_void_p, c_void_p]),
+    ("s2s_smaxpool_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
+                                 c_void_p, c_void_p, c_void_p]),
+    ("s2s_swap12", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    ("s2s_relu_fwd", c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
+    ("s2s_relu_bwd", c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
     ("s2s_comm_unique_id", c_int, [c_void_p]),
     ("s2s_comm_init", c_int, [c_void_p, c_void_p, c_int, c_int]),
     ("s2s_allreduce_sum", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),

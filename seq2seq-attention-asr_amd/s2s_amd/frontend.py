@@ -1,0 +1,345 @@
+"""nn.Module mirrors of the encoder front-ends over libs2s_hip.so.
+
+Operators (Torch7 nn semantics, include/s2s_hip.h "encoder front-ends"): TemporalConvolution,
+TemporalMaxPooling, ReLU, SpatialConvolutionMM, SpatialMaxPooling, Transpose2 and a Sequential
+container; and the two encoders the reference builds from them:
+  * ConvBiLSTMEncoder -- timit/timit.lua:108-125 (conv stack shared by both LSTM directions);
+  * VGGEncoder        -- librispeech/model_vgg.lua:23-51.
+A convolution built with relu=True is the reference's `conv -> nn.ReLU()` pair fused (the ReLU runs in
+the GEMM epilogue; its backward masks by the conv output).  Gradients accumulate; backward returns
+gradInput (None for a module built with need_gradInput=False: the encoder input needs none).
+"""
+import math
+
+import torch
+
+from ._lib import check, lib
+from .nn import (LSTM, BiRNN, Module, S2SArgumentError, _bytes, _require_cuda_f32, _uniform, dptr, get_context,
+                 stream_ptr)
+
+
+def _ctx(t):
+    return get_context(t.device.index).handle
+
+
+class TemporalConvolution(Module):
+    """nn.TemporalConvolution(inputFrameSize, outputFrameSize, kW) (dW = 1): weight (out, kW*in), bias (out);
+    reset U(+-1/sqrt(kW*in)).  bias=False gives TemporalConvolutionZeroBias (TemporalConvolutionZeroBias.lua)."""
+
+    def __init__(self, inputFrameSize, outputFrameSize, kW, relu=False, bias=True, need_gradInput=True,
+                 generator=None):
+        super().__init__()
+        self.inputFrameSize, self.outputFrameSize, self.kW = inputFrameSize, outputFrameSize, kW
+        self.relu, self.need_gradInput = bool(relu), need_gradInput
+        stdv = 1.0 / math.sqrt(kW * inputFrameSize)
+        self.weight = _uniform((outputFrameSize, kW * inputFrameSize), stdv, generator)
+        self.bias = _uniform((outputFrameSize,), stdv, generator) if bias else None
+        self.gradWeight = torch.zeros_like(self.weight)
+        self.gradBias = torch.zeros_like(self.bias) if bias else None
+
+    def parameters(self):
+        ws = [self.weight] + ([self.bias] if self.bias is not None else [])
+        gs = [self.gradWeight] + ([self.gradBias] if self.gradBias is not None else [])
+        return ws, gs
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        x = input if input.dim() == 3 else input.unsqueeze(0)
+        if x.dim() != 3 or x.shape[2] != self.inputFrameSize:
+            raise S2SArgumentError("TemporalConvolution: input must be (L, inputFrameSize) or (B, L, inputFrameSize)")
+        B, L, _ = x.shape
+        y = torch.empty((B, L - self.kW + 1, self.outputFrameSize), device=x.device, dtype=torch.float32)
+        check(lib.s2s_tconv_fwd(_ctx(x), stream_ptr(), B, L, self.inputFrameSize, self.outputFrameSize, self.kW,
+                                int(self.relu), dptr(x), dptr(self.weight), dptr(self.bias), dptr(y)))
+        self.output = y if input.dim() == 3 else y[0]
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        x = input if input.dim() == 3 else input.unsqueeze(0)
+        B, L, _ = x.shape
+        go = (gradOutput if gradOutput.dim() == 3 else gradOutput.unsqueeze(0)).contiguous()
+        y = self.output if self.output.dim() == 3 else self.output.unsqueeze(0)
+        dx = torch.empty_like(x) if self.need_gradInput else None
+        scr = _bytes(lib.s2s_tconv_scratch_bytes(B, L, self.inputFrameSize, self.outputFrameSize, self.kW), x.device)
+        check(lib.s2s_tconv_bwd(_ctx(x), stream_ptr(), B, L, self.inputFrameSize, self.outputFrameSize, self.kW,
+                                int(self.relu), dptr(x), dptr(self.weight), dptr(y), dptr(go), dptr(dx), 0,
+                                dptr(self.gradWeight), dptr(self.gradBias), float(scale), dptr(scr), scr.numel()))
+        self.gradInput = None if dx is None else (dx if input.dim() == 3 else dx[0])
+        return self.gradInput
+
+
+class TemporalMaxPooling(Module):
+    """nn.TemporalMaxPooling(kW, dW): floor mode, first maximum wins."""
+
+    def __init__(self, kW, dW=None):
+        super().__init__()
+        self.kW, self.dW = kW, dW or kW
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        x = input if input.dim() == 3 else input.unsqueeze(0)
+        B, L, D = x.shape
+        Lo = (L - self.kW) // self.dW + 1
+        y = torch.empty((B, Lo, D), device=x.device, dtype=torch.float32)
+        self.indices = torch.empty((B, Lo, D), device=x.device, dtype=torch.int32)
+        check(lib.s2s_tmaxpool_fwd(_ctx(x), stream_ptr(), B, L, D, self.kW, self.dW, dptr(x), dptr(y),
+                                   dptr(self.indices)))
+        self.output = y if input.dim() == 3 else y[0]
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        x = input if input.dim() == 3 else input.unsqueeze(0)
+        B, L, D = x.shape
+        go = (gradOutput if gradOutput.dim() == 3 else gradOutput.unsqueeze(0)).contiguous()
+        dx = torch.empty_like(x)
+        check(lib.s2s_tmaxpool_bwd(_ctx(x), stream_ptr(), B, L, D, self.kW, self.dW, dptr(self.indices), dptr(go),
+                                   dptr(dx)))
+        self.gradInput = dx if input.dim() == 3 else dx[0]
+        return self.gradInput
+
+
+class ReLU(Module):
+    """nn.ReLU: y = max(x, 0); dx = dy * 1[x > 0]."""
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        self.output = torch.empty_like(input)
+        check(lib.s2s_relu_fwd(_ctx(input), stream_ptr(), input.numel(), dptr(input), dptr(self.output)))
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        go = gradOutput.contiguous()
+        self.gradInput = torch.empty_like(input)
+        check(lib.s2s_relu_bwd(_ctx(input), stream_ptr(), input.numel(), dptr(input), dptr(go),
+                               dptr(self.gradInput)))
+        return self.gradInput
+
+
+class SpatialConvolutionMM(Module):
+    """nn.SpatialConvolutionMM(nInputPlane, nOutputPlane, kW, kH) (stride 1, no padding): weight
+    (out, in*kH*kW), bias (out); reset U(+-1/sqrt(kW*kH*in)).  Input (B, C, H, W) or (C, H, W)."""
+
+    def __init__(self, nInputPlane, nOutputPlane, kW, kH=None, relu=False, need_gradInput=True, generator=None):
+        super().__init__()
+        self.nInputPlane, self.nOutputPlane, self.kW, self.kH = nInputPlane, nOutputPlane, kW, kH or kW
+        self.relu, self.need_gradInput = bool(relu), need_gradInput
+        stdv = 1.0 / math.sqrt(self.kW * self.kH * nInputPlane)
+        self.weight = _uniform((nOutputPlane, nInputPlane * self.kH * self.kW), stdv, generator)
+        self.bias = _uniform((nOutputPlane,), stdv, generator)
+        self.gradWeight = torch.zeros_like(self.weight)
+        self.gradBias = torch.zeros_like(self.bias)
+
+    def parameters(self):
+        return [self.weight, self.bias], [self.gradWeight, self.gradBias]
+
+    def _dims(self, x):
+        if x.dim() != 4 or x.shape[1] != self.nInputPlane:
+            raise S2SArgumentError("SpatialConvolutionMM: input must be (C, H, W) or (B, C, H, W) with C = nInputPlane")
+        return x.shape
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, C, H, W = self._dims(x)
+        y = torch.empty((B, self.nOutputPlane, H - self.kH + 1, W - self.kW + 1), device=x.device,
+                        dtype=torch.float32)
+        scr = _bytes(lib.s2s_sconv_scratch_bytes(B, C, H, W, self.nOutputPlane, self.kH, self.kW), x.device)
+        check(lib.s2s_sconv_fwd(_ctx(x), stream_ptr(), B, C, H, W, self.nOutputPlane, self.kH, self.kW,
+                                int(self.relu), dptr(x), dptr(self.weight), dptr(self.bias), dptr(y), dptr(scr),
+                                scr.numel()))
+        self.output = y if input.dim() == 4 else y[0]
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, C, H, W = self._dims(x)
+        go = (gradOutput if gradOutput.dim() == 4 else gradOutput.unsqueeze(0)).contiguous()
+        y = self.output if self.output.dim() == 4 else self.output.unsqueeze(0)
+        dx = torch.empty_like(x) if self.need_gradInput else None
+        scr = _bytes(lib.s2s_sconv_scratch_bytes(B, C, H, W, self.nOutputPlane, self.kH, self.kW), x.device)
+        check(lib.s2s_sconv_bwd(_ctx(x), stream_ptr(), B, C, H, W, self.nOutputPlane, self.kH, self.kW,
+                                int(self.relu), dptr(x), dptr(self.weight), dptr(y), dptr(go), dptr(dx), 0,
+                                dptr(self.gradWeight), dptr(self.gradBias), float(scale), dptr(scr), scr.numel()))
+        self.gradInput = None if dx is None else (dx if input.dim() == 4 else dx[0])
+        return self.gradInput
+
+
+class SpatialMaxPooling(Module):
+    """nn.SpatialMaxPooling(kW, kH, dW, dH) (floor mode, first maximum wins)."""
+
+    def __init__(self, kW, kH, dW=None, dH=None):
+        super().__init__()
+        self.kW, self.kH, self.dW, self.dH = kW, kH, dW or kW, dH or kH
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, C, H, W = x.shape
+        Ho, Wo = (H - self.kH) // self.dH + 1, (W - self.kW) // self.dW + 1
+        y = torch.empty((B, C, Ho, Wo), device=x.device, dtype=torch.float32)
+        self.indices = torch.empty((B, C, Ho, Wo), device=x.device, dtype=torch.int32)
+        check(lib.s2s_smaxpool_fwd(_ctx(x), stream_ptr(), B, C, H, W, self.kW, self.kH, self.dW, self.dH, dptr(x),
+                                   dptr(y), dptr(self.indices)))
+        self.output = y if input.dim() == 4 else y[0]
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, C, H, W = x.shape
+        go = (gradOutput if gradOutput.dim() == 4 else gradOutput.unsqueeze(0)).contiguous()
+        dx = torch.empty_like(x)
+        check(lib.s2s_smaxpool_bwd(_ctx(x), stream_ptr(), B, C, H, W, self.kW, self.kH, self.dW, self.dH,
+                                   dptr(self.indices), dptr(go), dptr(dx)))
+        self.gradInput = dx if input.dim() == 4 else dx[0]
+        return self.gradInput
+
+
+class Transpose2(Module):
+    """nn.Transpose2({1,2},3) (Transpose2.lua): (nFeat, L, H) -> (L, nFeat, H), batched (B, nFeat, L, H) ->
+    (B, L, nFeat, H).  Only this permutation (the one model_vgg.lua:41 uses) runs on this path."""
+
+    def __init__(self, *perms):
+        super().__init__()
+        if perms not in (((1, 2), 3), ([1, 2], 3)):
+            raise S2SArgumentError("Transpose2: only ({1,2}, 3) is implemented")
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        if input.dim() not in (3, 4):
+            raise S2SArgumentError("inconsistent tensor size")  # Transpose2.lua:29
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, D1, D2, D3 = x.shape
+        y = torch.empty((B, D2, D1, D3), device=x.device, dtype=torch.float32)
+        check(lib.s2s_swap12(_ctx(x), stream_ptr(), B, D1, D2, D3, dptr(x), dptr(y)))
+        self.output = y if input.dim() == 4 else y[0]
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        x = input if input.dim() == 4 else input.unsqueeze(0)
+        B, D1, D2, D3 = x.shape
+        go = (gradOutput if gradOutput.dim() == 4 else gradOutput.unsqueeze(0)).contiguous()
+        dx = torch.empty_like(x)
+        check(lib.s2s_swap12(_ctx(x), stream_ptr(), B, D2, D1, D3, dptr(go), dptr(dx)))
+        self.gradInput = dx if input.dim() == 4 else dx[0]
+        return self.gradInput
+
+
+class View(Module):
+    """nn.View(-1, n):setNumInputDims(3) on a batch: (B, L, C, H) -> (B, L, C*H) (a free reshape)."""
+
+    def updateOutput(self, input):
+        self.output = input.reshape(input.shape[0], input.shape[1], -1)
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        self.gradInput = gradOutput.reshape(input.shape)
+        return self.gradInput
+
+
+class Sequential(Module):
+    """nn.Sequential: forward in order, backward in reverse (each module's backward = updateGradInput +
+    accGradParameters)."""
+
+    def __init__(self, *modules):
+        super().__init__()
+        self.modules = list(modules)
+
+    def add(self, m):
+        self.modules.append(m)
+        return self
+
+    def parameters(self):
+        ws, gs = [], []
+        for m in self.modules:
+            w, g = m.parameters()
+            ws += w
+            gs += g
+        return ws, gs
+
+    def updateOutput(self, input):
+        self._inputs = []
+        h = input
+        for m in self.modules:
+            self._inputs.append(h)
+            h = m.forward(h)
+        self.output = h
+        return h
+
+    def backward(self, input, gradOutput, scale=1.0):
+        d = gradOutput
+        for m, x in zip(reversed(self.modules), reversed(self._inputs)):
+            d = m.backward(x, d, scale)
+        self.gradInput = d
+        return d
+
+
+class ConvBiLSTMEncoder(Module):
+    """timit/timit.lua:108-125: convlayer = 3 x [TemporalConvolution(D, hidden, kW) -> ReLU ->
+    TemporalMaxPooling(2, 2)], applied once and read by both RNN(LSTM(hidden, out, peepholes=nil))
+    directions (the reference calls the same module on the same input twice, :123-124, so the
+    forward is one conv stack and its weight gradients sum both directions' contributions), then
+    JoinTable(2,2).  x (B, L, D) -> (B, L', 2*out), L' = three times (L - kW + 1) // 2."""
+
+    def __init__(self, inputFrameSize, hiddenFrameSize=256, outputFrameSize=128, kW=3, generator=None):
+        super().__init__()
+        convs = []
+        for l in range(3):
+            convs += [TemporalConvolution(inputFrameSize if l == 0 else hiddenFrameSize, hiddenFrameSize, kW, relu=True,
+                                          need_gradInput=l > 0, generator=generator),
+                      TemporalMaxPooling(2, 2)]
+        self.convlayer = Sequential(*convs)
+        self.rnn = BiRNN(LSTM(hiddenFrameSize, outputFrameSize, False, generator),
+                         LSTM(hiddenFrameSize, outputFrameSize, False, generator))
+
+    def parameters(self):
+        w1, g1 = self.convlayer.parameters()
+        w2, g2 = self.rnn.parameters()
+        return w1 + w2, g1 + g2
+
+    def updateOutput(self, input):
+        self._c = self.convlayer.forward(input)
+        self.output = self.rnn.forward(self._c)
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        dc = self.rnn.backward(self._c, gradOutput, scale)  # sum of both directions' dx
+        self.gradInput = self.convlayer.backward(input, dc, scale)
+        return self.gradInput
+
+
+class VGGEncoder(Module):
+    """librispeech/model_vgg.lua:23-51 on x (B, 3, L, F) (H = time, W = frequency) -> (B, (L-8)//2, out):
+    SpatialConvolutionMM(3,64,3,3)+ReLU, (64,64)+ReLU, SpatialMaxPooling(2,1,2,1), (64,128)+ReLU,
+    (128,128)+ReLU, SpatialMaxPooling(2,2,2,2), Transpose2({1,2},3), View(-1, 128*H'), then
+    TemporalConvolution(128*H', hidden, 1), (hidden, hidden, 1) x 2, (hidden, out, 1), each + ReLU."""
+
+    def __init__(self, inputFrameSize=40, outputFrameSize=512, hidden=2048, generator=None):
+        super().__init__()
+        Hf = ((inputFrameSize - 4) // 2 - 4) // 2
+        if Hf < 1:
+            raise S2SArgumentError("VGGEncoder: inputFrameSize too small for the conv stack")
+        g = generator
+        self.seq = Sequential(
+            SpatialConvolutionMM(3, 64, 3, 3, relu=True, need_gradInput=False, generator=g),
+            SpatialConvolutionMM(64, 64, 3, 3, relu=True, generator=g),
+            SpatialMaxPooling(2, 1, 2, 1),
+            SpatialConvolutionMM(64, 128, 3, 3, relu=True, generator=g),
+            SpatialConvolutionMM(128, 128, 3, 3, relu=True, generator=g),
+            SpatialMaxPooling(2, 2, 2, 2),
+            Transpose2((1, 2), 3),
+            View(),
+            TemporalConvolution(128 * Hf, hidden, 1, relu=True, generator=g),
+            TemporalConvolution(hidden, hidden, 1, relu=True, generator=g),
+            TemporalConvolution(hidden, hidden, 1, relu=True, generator=g),
+            TemporalConvolution(hidden, outputFrameSize, 1, relu=True, generator=g))
+
+    def parameters(self):
+        return self.seq.parameters()
+
+    def updateOutput(self, input):
+        self.output = self.seq.forward(input)
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        self.gradInput = self.seq.backward(input, gradOutput, scale)
+        return self.gradInput

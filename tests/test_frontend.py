@@ -1,0 +1,329 @@
+"""Encoder front-ends: the conv + BiLSTM encoder (timit/timit.lua:108-125) and the VGG
+stack (librispeech/model_vgg.lua:23-51).
+
+CPU: the oracle's operator restatements (oracle/frontend_oracle.py) against torch.nn.functional autograd
+(an independent formulation of the same Torch7 nn semantics), and the encoder-level backward against
+central finite differences.  GPU: libs2s_hip.so through the host mirror (s2s_amd.frontend) against the
+oracle, tolerance max|gpu - ref| <= 1e-4 * max|ref| per tensor (fp32 vs float64).
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import frontend_oracle as fo
+
+RTOL = 1e-4
+
+
+def rel_err(g, r):
+    g = np.asarray(g, dtype=np.float64)
+    r = np.asarray(r, dtype=np.float64)
+    assert g.shape == r.shape, (g.shape, r.shape)
+    return float(np.abs(g - r).max() / max(np.abs(r).max(), 1e-30))
+
+
+def assert_rel(g, r, name, rtol=RTOL):
+    e = rel_err(g, r)
+    assert np.isfinite(np.asarray(g, dtype=np.float64)).all(), f"{name}: non-finite values"
+    assert e <= rtol, f"{name}: max rel err {e:.3e} > {rtol:.0e}"
+
+
+def t64(a, grad=False):
+    return torch.tensor(a, dtype=torch.float64, requires_grad=grad)
+
+
+# --------------------------------------------------------------------------- oracle vs torch autograd (CPU)
+
+@pytest.mark.parametrize("B,L,Din,Dout,kW", [(2, 11, 5, 4, 3), (1, 7, 3, 6, 1), (3, 9, 4, 2, 4)])
+def test_oracle_tconv_matches_torch(B, L, Din, Dout, kW):
+    rng = np.random.default_rng(L)
+    x, W, b = rng.standard_normal((B, L, Din)), rng.standard_normal((Dout, kW * Din)), rng.standard_normal(Dout)
+    dy = rng.standard_normal((B, L - kW + 1, Dout))
+    xt, Wt, bt = t64(x, True), t64(W, True), t64(b, True)
+    # Torch7 weight (out, kW*in), frame-major -> conv1d weight (out, in, kW)
+    yt = F.conv1d(xt.transpose(1, 2), Wt.reshape(Dout, kW, Din).transpose(1, 2), bt).transpose(1, 2)
+    yt.backward(t64(dy))
+    y = fo.tconv_fwd(x, W, b, kW)
+    dx, dW, db = fo.tconv_bwd(x, W, dy, kW)
+    for g, r, n in ((y, yt, "y"), (dx, xt.grad, "dx"), (dW, Wt.grad, "dW"), (db, bt.grad, "db")):
+        assert_rel(g, r.detach().numpy(), n, 1e-12)
+
+
+def test_oracle_tmaxpool_matches_torch():
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((2, 13, 5))
+    y, idx = fo.tmaxpool_fwd(x, 2, 2)
+    xt = t64(x, True)
+    yt = F.max_pool1d(xt.transpose(1, 2), 2, 2).transpose(1, 2)
+    dy = rng.standard_normal(y.shape)
+    yt.backward(t64(dy))
+    assert_rel(y, yt.detach().numpy(), "y", 0)
+    assert_rel(fo.tmaxpool_bwd(idx, dy, 13, 2, 2), xt.grad.numpy(), "dx", 0)
+    # first maximum wins on ties (THNN `if (val > maxval)`)
+    y2, idx2 = fo.tmaxpool_fwd(np.zeros((1, 4, 1)), 2, 2)
+    assert (idx2 == 0).all()
+
+
+@pytest.mark.parametrize("B,C,H,W,O,k", [(2, 3, 9, 8, 4, 3), (1, 2, 5, 7, 3, 2)])
+def test_oracle_sconv_matches_torch(B, C, H, W, O, k):
+    rng = np.random.default_rng(H * W)
+    x, Wt_, b = rng.standard_normal((B, C, H, W)), rng.standard_normal((O, C * k * k)), rng.standard_normal(O)
+    xt, wt, bt = t64(x, True), t64(Wt_, True), t64(b, True)
+    yt = F.conv2d(xt, wt.reshape(O, C, k, k), bt)
+    dy = rng.standard_normal(yt.shape)
+    yt.backward(t64(dy))
+    y = fo.sconv_fwd(x, Wt_, b, k, k)
+    dx, dW, db = fo.sconv_bwd(x, Wt_, dy, k, k)
+    for g, r, n in ((y, yt, "y"), (dx, xt.grad, "dx"), (dW, wt.grad, "dW"), (db, bt.grad, "db")):
+        assert_rel(g, r.detach().numpy(), n, 1e-12)
+
+
+@pytest.mark.parametrize("kW,kH,dW,dH", [(2, 1, 2, 1), (2, 2, 2, 2), (3, 2, 2, 1)])
+def test_oracle_smaxpool_matches_torch(kW, kH, dW, dH):
+    rng = np.random.default_rng(kW * 10 + kH)
+    x = rng.standard_normal((2, 3, 9, 11))
+    y, idx = fo.smaxpool_fwd(x, kW, kH, dW, dH)
+    xt = t64(x, True)
+    yt = F.max_pool2d(xt, (kH, kW), (dH, dW))
+    dy = rng.standard_normal(y.shape)
+    yt.backward(t64(dy))
+    assert_rel(y, yt.detach().numpy(), "y", 0)
+    assert_rel(fo.smaxpool_bwd(idx, dy, 9, 11, kW, kH, dW, dH), xt.grad.numpy(), "dx", 1e-15)
+
+
+def _vgg_params(rng, hidden=16, out=8, F_=16):
+    P = {}
+    for l, (ci, co) in enumerate(fo.VGG_CONVS):
+        P[f"vgg{l}.W"] = rng.standard_normal((co, ci * 9)) / np.sqrt(ci * 9)
+        P[f"vgg{l}.b"] = rng.standard_normal(co) * 0.1
+    for l, (di, do) in enumerate(fo.vgg_dims(F_, hidden, out)):
+        P[f"lin{l}.W"] = rng.standard_normal((do, di)) / np.sqrt(di)
+        P[f"lin{l}.b"] = rng.standard_normal(do) * 0.1
+    return P
+
+
+def _fd_check(fwd, bwd, P, x, keys, rng, n=3, eps=1e-6):
+    y, cache = fwd(x, P)
+    dy = rng.standard_normal(y.shape)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    bwd(P, cache, dy, G)
+    for k in keys:
+        for _ in range(n):
+            i = tuple(rng.integers(0, s) for s in P[k].shape)
+            old = P[k][i]
+            P[k][i] = old + eps
+            fp = (fwd(x, P)[0] * dy).sum()
+            P[k][i] = old - eps
+            fm = (fwd(x, P)[0] * dy).sum()
+            P[k][i] = old
+            fd = (fp - fm) / (2 * eps)
+            assert abs(fd - G[k][i]) <= 1e-6 * max(1.0, abs(fd)), (k, i, fd, G[k][i])
+
+
+def test_oracle_vgg_encoder_finite_differences():
+    rng = np.random.default_rng(7)
+    P = _vgg_params(rng)
+    x = rng.standard_normal((1, 3, 14, 16))
+    _fd_check(fo.vgg_fwd, fo.vgg_bwd, P, x, ["vgg0.W", "vgg3.b", "lin0.W", "lin3.b"], rng)
+
+
+def test_oracle_conv_bilstm_finite_differences():
+    rng = np.random.default_rng(8)
+    D, Hd, Ho = 5, 6, 4
+    P = {}
+    for l in range(3):
+        din = D if l == 0 else Hd
+        P[f"conv{l}.W"] = rng.standard_normal((Hd, 3 * din)) / np.sqrt(3 * din)
+        P[f"conv{l}.b"] = rng.standard_normal(Hd) * 0.1
+    for d in ("f.", "b."):
+        for q in "ifgo":
+            P[f"{d}W{q}x"] = rng.standard_normal((Ho, Hd)) * 0.4
+            P[f"{d}b{q}x"] = rng.standard_normal(Ho) * 0.1
+            P[f"{d}W{q}h"] = rng.standard_normal((Ho, Ho)) * 0.4
+            P[f"{d}b{q}h"] = rng.standard_normal(Ho) * 0.1
+    x = rng.standard_normal((2, 40, D))
+    _fd_check(fo.conv_bilstm_fwd, fo.conv_bilstm_bwd, P, x, ["conv0.W", "conv2.b", "f.Wix", "b.bfh"], rng)
+
+
+# --------------------------------------------------------------------------- GPU parity
+
+@pytest.fixture(scope="module")
+def fe():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from s2s_amd import frontend
+    return frontend
+
+
+def cu(a, dtype=torch.float32):
+    return torch.tensor(np.ascontiguousarray(a), dtype=dtype, device="cuda")
+
+
+def _np(t):
+    return t.double().cpu().numpy()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,Din,Dout,kW,relu", [(4, 64, 123, 256, 3, True), (3, 17, 256, 256, 3, True),
+                                                  (2, 9, 896, 2048, 1, True), (5, 12, 7, 5, 4, False),
+                                                  (1, 3, 40, 16, 3, False)])
+def test_tconv_matches_oracle(fe, B, L, Din, Dout, kW, relu):
+    rng = np.random.default_rng(B * 100 + L)
+    m = fe.TemporalConvolution(Din, Dout, kW, relu=relu).cuda()
+    x = rng.standard_normal((B, L, Din))
+    W, b = _np(m.weight), _np(m.bias)
+    y = m.forward(cu(x))
+    u = fo.tconv_fwd(x, W, b, kW)
+    yr = fo.relu_fwd(u) if relu else u
+    assert_rel(_np(y), yr, "y")
+    dy = rng.standard_normal(yr.shape)
+    m.gradWeight.fill_(0.5)
+    m.gradBias.fill_(-0.25)
+    dx = m.backward(cu(x), cu(dy), 0.5)
+    du = fo.relu_bwd(u, dy) if relu else dy
+    dxr, dWr, dbr = fo.tconv_bwd(x, W, du, kW)
+    torch.cuda.synchronize()
+    assert_rel(_np(dx), dxr, "dx")
+    assert_rel(_np(m.gradWeight), 0.5 + 0.5 * dWr, "dW")
+    assert_rel(_np(m.gradBias), -0.25 + 0.5 * dbr, "db")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,D,kW,dW", [(4, 62, 256, 2, 2), (3, 13, 5, 2, 2), (2, 10, 7, 3, 2), (2, 9, 3, 2, 1)])
+def test_tmaxpool_matches_oracle(fe, B, L, D, kW, dW):
+    rng = np.random.default_rng(L)
+    x = rng.standard_normal((B, L, D)).astype(np.float32).astype(np.float64)  # exact ops: compare on fp32 inputs
+    x[0, :2, 0] = 1.0  # a tie: the first maximum wins
+    m = fe.TemporalMaxPooling(kW, dW)
+    y = m.forward(cu(x))
+    yr, idx = fo.tmaxpool_fwd(x, kW, dW)
+    assert_rel(_np(y), yr, "y", 0)
+    assert (m.indices.cpu().numpy() == idx).all()
+    dy = rng.standard_normal(yr.shape)
+    dx = m.backward(cu(x), cu(dy))
+    assert_rel(_np(dx), fo.tmaxpool_bwd(idx, dy, L, kW, dW), "dx", 1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,C,H,W,O,k,relu", [(2, 3, 40, 40, 64, 3, True), (2, 64, 20, 18, 128, 3, True),
+                                              (3, 5, 9, 11, 7, 2, False), (1, 1, 3, 3, 1, 3, False)])
+def test_sconv_matches_oracle(fe, B, C, H, W, O, k, relu):
+    rng = np.random.default_rng(H * W + C)
+    m = fe.SpatialConvolutionMM(C, O, k, k, relu=relu).cuda()
+    x = rng.standard_normal((B, C, H, W))
+    Wt, b = _np(m.weight), _np(m.bias)
+    y = m.forward(cu(x))
+    u = fo.sconv_fwd(x, Wt, b, k, k)
+    yr = fo.relu_fwd(u) if relu else u
+    assert_rel(_np(y), yr, "y")
+    dy = rng.standard_normal(yr.shape)
+    m.gradWeight.fill_(0.5)
+    dx = m.backward(cu(x), cu(dy), 2.0)
+    du = fo.relu_bwd(u, dy) if relu else dy
+    dxr, dWr, dbr = fo.sconv_bwd(x, Wt, du, k, k)
+    torch.cuda.synchronize()
+    assert_rel(_np(dx), dxr, "dx")
+    assert_rel(_np(m.gradWeight), 0.5 + 2.0 * dWr, "dW")
+    assert_rel(_np(m.gradBias), 2.0 * dbr, "db")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kW,kH,dW,dH,H,W", [(2, 1, 2, 1, 36, 36), (2, 2, 2, 2, 33, 15), (3, 2, 2, 1, 9, 11)])
+def test_smaxpool_matches_oracle(fe, kW, kH, dW, dH, H, W):
+    rng = np.random.default_rng(H + W)
+    x = rng.standard_normal((2, 3, H, W)).astype(np.float32).astype(np.float64)
+    m = fe.SpatialMaxPooling(kW, kH, dW, dH)
+    y = m.forward(cu(x))
+    yr, idx = fo.smaxpool_fwd(x, kW, kH, dW, dH)
+    assert_rel(_np(y), yr, "y", 0)
+    assert (m.indices.cpu().numpy() == idx).all()
+    dy = rng.standard_normal(yr.shape)
+    assert_rel(_np(m.backward(cu(x), cu(dy))), fo.smaxpool_bwd(idx, dy, H, W, kW, kH, dW, dH), "dx", 1e-6)
+
+
+@pytest.mark.gpu
+def test_transpose2_relu(fe):
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((2, 4, 6, 3)).astype(np.float32).astype(np.float64)
+    m = fe.Transpose2((1, 2), 3)
+    y = m.forward(cu(x))
+    assert_rel(_np(y), x.transpose(0, 2, 1, 3), "y", 0)
+    dy = rng.standard_normal(y.shape).astype(np.float32).astype(np.float64)
+    assert_rel(_np(m.backward(cu(x), cu(dy))), dy.transpose(0, 2, 1, 3), "dx", 0)
+    r = fe.ReLU()
+    assert_rel(_np(r.forward(cu(x))), fo.relu_fwd(x), "relu", 0)
+    dy = rng.standard_normal(x.shape).astype(np.float32).astype(np.float64)
+    assert_rel(_np(r.backward(cu(x), cu(dy))), fo.relu_bwd(x, dy), "drelu", 0)
+
+
+def _assert_grads(pairs):
+    for name, g, r in pairs:
+        assert_rel(_np(g), r, name)
+
+
+@pytest.mark.gpu
+def test_conv_bilstm_encoder_matches_oracle(fe):
+    """timit/timit.lua:108-125 at its sizes (D=123, 256 conv maps, LSTM 128 per direction)."""
+    import s2s_amd
+    rng = np.random.default_rng(11)
+    B, L, D = 4, 64, 123
+    enc = s2s_amd.ConvBiLSTMEncoder(D).cuda()
+    P = {}
+    convs = [m for m in enc.convlayer.modules if isinstance(m, fe.TemporalConvolution)]
+    for l, m in enumerate(convs):
+        P[f"conv{l}.W"], P[f"conv{l}.b"] = _np(m.weight), _np(m.bias)
+    cells = enc.rnn.cells
+    for pre, c in zip(("f.", "b."), cells):
+        for k, v in c.named().items():
+            P[pre + k] = _np(v)
+    x = rng.standard_normal((B, L, D))
+    y = enc.forward(cu(x))
+    yr, cache = fo.conv_bilstm_fwd(x, P)
+    assert_rel(_np(y), yr, "y")
+    dy = rng.standard_normal(yr.shape)
+    enc.zeroGradParameters()
+    enc.backward(cu(x), cu(dy), 1.0)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    fo.conv_bilstm_bwd(P, cache, dy, G)
+    torch.cuda.synchronize()
+    pairs = []
+    for l, m in enumerate(convs):
+        pairs += [(f"dconv{l}.W", m.gradWeight, G[f"conv{l}.W"]), (f"dconv{l}.b", m.gradBias, G[f"conv{l}.b"])]
+    for pre, c in zip(("f.", "b."), cells):
+        pairs += [(f"d{pre}{k}", g, G[pre + k]) for k, g in c.named(grads=True).items()]
+    _assert_grads(pairs)
+
+
+@pytest.mark.gpu
+def test_vgg_encoder_matches_oracle(fe):
+    """librispeech/model_vgg.lua:23-51 with 40 mel bands (the 2048-wide 1x1 convs narrowed to 256)."""
+    import s2s_amd
+    rng = np.random.default_rng(12)
+    B, L, Fq = 2, 40, 40
+    enc = s2s_amd.VGGEncoder(Fq, outputFrameSize=128, hidden=256).cuda()
+    mods = enc.seq.modules
+    convs = [m for m in mods if isinstance(m, fe.SpatialConvolutionMM)]
+    lins = [m for m in mods if isinstance(m, fe.TemporalConvolution)]
+    P = {}
+    for l, m in enumerate(convs):
+        P[f"vgg{l}.W"], P[f"vgg{l}.b"] = _np(m.weight), _np(m.bias)
+    for l, m in enumerate(lins):
+        P[f"lin{l}.W"], P[f"lin{l}.b"] = _np(m.weight), _np(m.bias)
+    x = rng.standard_normal((B, 3, L, Fq))
+    y = enc.forward(cu(x))
+    yr, cache = fo.vgg_fwd(x, P)
+    assert y.shape == (B, (L - 8) // 2, 128)
+    assert_rel(_np(y), yr, "y")
+    dy = rng.standard_normal(yr.shape)
+    enc.zeroGradParameters()
+    enc.backward(cu(x), cu(dy), 1.0)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    fo.vgg_bwd(P, cache, dy, G)
+    torch.cuda.synchronize()
+    pairs = []
+    for l, m in enumerate(convs):
+        pairs += [(f"dvgg{l}.W", m.gradWeight, G[f"vgg{l}.W"]), (f"dvgg{l}.b", m.gradBias, G[f"vgg{l}.b"])]
+    for l, m in enumerate(lins):
+        pairs += [(f"dlin{l}.W", m.gradWeight, G[f"lin{l}.W"]), (f"dlin{l}.b", m.gradBias, G[f"lin{l}.b"])]
+    _assert_grads(pairs)

@@ -21,6 +21,8 @@ struct GemmProblem {
   int M, N, K;
   float alpha, beta;
   int Mread = 0, Nread = 0;  // (mirror of s2s_common.h)
+  const float* rbias = nullptr;
+  int relu = 0;
 };
 struct GemmWs {
   float* p = nullptr;
