@@ -1,0 +1,69 @@
+"""Checkpoints: the reference saves its whole model table with torch.save
+(model.t7, model_best_valid_*.t7; timit/timit.lua:551-562) -- the autoencoder's flat parameters
+(getParameters, timit.lua:172) plus optimState.  Here: one safetensors file (no code executed on
+load) holding every parameter of the flat layout under its module name, the optimizer state
+(optim.adadelta paramVariance / accDelta) when given, and the model config + trainer metadata as JSON.
+"""
+import dataclasses
+import json
+import math
+
+import torch
+from safetensors import safe_open
+from safetensors.torch import save_file
+
+from .model import ModelConfig, param_shapes
+
+
+def save_flat(path, cfg: ModelConfig, params, optim_state=None, meta=None):
+    """params: the flat (n,) float32 buffer; optim_state: the Adadelta state bytes (or None)."""
+    shapes = param_shapes(cfg)
+    n = sum(math.prod(s) for _, s in shapes)
+    if params.numel() != n:
+        raise ValueError(f"params has {params.numel()} elements, the layout {n}")
+    flat = params.detach().to("cpu", torch.float32).contiguous()
+    tensors, off = {}, 0
+    for name, shp in shapes:
+        sz = math.prod(shp)
+        tensors[f"param.{name}"] = flat[off:off + sz].view(shp).clone()
+        off += sz
+    if optim_state is not None:
+        tensors["optim.state"] = optim_state.detach().to("cpu").contiguous().view(torch.uint8).clone()
+    header = {"format": "s2s_amd-checkpoint-1", "config": json.dumps(dataclasses.asdict(cfg)),
+              "meta": json.dumps(meta or {})}
+    save_file(tensors, path, metadata=header)
+
+
+def load_flat(path):
+    """-> (cfg, params (n,) float32 CPU, optim_state uint8 CPU or None, meta dict)."""
+    with safe_open(path, framework="pt") as f:
+        md = f.metadata() or {}
+        if md.get("format") != "s2s_amd-checkpoint-1":
+            raise ValueError(f"{path}: not an s2s_amd checkpoint")
+        cfg = ModelConfig(**json.loads(md["config"]))
+        parts = [f.get_tensor(f"param.{name}").reshape(-1) for name, _ in param_shapes(cfg)]
+        state = f.get_tensor("optim.state") if "optim.state" in f.keys() else None
+        meta = json.loads(md.get("meta", "{}"))
+    return cfg, torch.cat(parts), state, meta
+
+
+def save(path, model, optimizer=None, meta=None):
+    """torch.save(paths.concat(savedir, 'model.t7'), model) for a ChorowskiBaseline (+ its Adadelta)."""
+    save_flat(path, model.cfg, model.params, optimizer.state if optimizer is not None else None, meta)
+
+
+def load(path, model=None, optimizer=None):
+    """Restore into an existing model (and optimizer) or build a new ChorowskiBaseline; returns
+    (model, meta)."""
+    cfg, params, state, meta = load_flat(path)
+    if model is None:
+        from .model import ChorowskiBaseline
+        model = ChorowskiBaseline(cfg)
+    elif dataclasses.asdict(model.cfg) != dataclasses.asdict(cfg):
+        raise ValueError("checkpoint config differs from the model's")
+    model.params.copy_(params.to(model.params.device))
+    if optimizer is not None:
+        if state is None or state.numel() != optimizer.state.numel():
+            raise ValueError("checkpoint holds no matching optimizer state")
+        optimizer.state.copy_(state.to(optimizer.state.device))
+    return model, meta

@@ -120,7 +120,7 @@ class ChorowskiBaseline:
             self.ctx = Context(self.device.index, graph=graph, overlap=overlap)
         else:
             self.ctx = get_context(self.device.index)
-        self._ws = {}
+        self._wsbuf = None
         self.train = True
         self._steps = 0
         self._check_layout()
@@ -161,14 +161,16 @@ class ChorowskiBaseline:
         return out
 
     def workspace(self, B, L, T):
-        key = (B, L, T, self.cfg.dropout > 0 and self.train)
-        if key not in self._ws:
-            d = self.dims(B, L, T)
-            nbytes = lib.s2s_model_workspace_bytes(ctypes.byref(d))
-            if nbytes == 0:
-                check(1)
-            self._ws[key] = _bytes(nbytes, self.device)
-        return self._ws[key]
+        """One workspace for every shape (grown on demand): ragged training (step_ragged) visits many
+        (B, L, T) and must not keep one ~100 MB buffer per shape."""
+        d = self.dims(B, L, T)
+        nbytes = lib.s2s_model_workspace_bytes(ctypes.byref(d))
+        if nbytes == 0:
+            check(1)
+        if self._wsbuf is None or self._wsbuf.numel() < nbytes:
+            self._wsbuf = None
+            self._wsbuf = _bytes(nbytes, self.device)
+        return self._wsbuf
 
     def grad_buckets(self):
         return grad_buckets(self.cfg)
@@ -222,10 +224,35 @@ class ChorowskiBaseline:
         self._last = (B, L, T)
         return nll, logp
 
+    def step_ragged(self, xs, labels, max_batch=None, normalizeNLL=True):
+        """The reference's minibatch over variable-length utterances (timit/timit.lua:240-295: one
+        forward/backward per utterance, gradients summed, then / B): utterances are grouped by equal
+        (L, T) (data.bucket_by_shape) and each group runs as one batched step accumulating into the same
+        gradient with scale 1/B (B = all utterances), so the result is the per-utterance sum exactly.
+        xs: list of (L_i, F) float32 CUDA tensors; labels: list of (T_i,) 0-based int tensors.
+        Returns nll (B,) in input order and the per-utterance logp list."""
+        from .data import bucket_by_shape
+        if len(xs) != len(labels) or not xs:
+            raise ValueError("step_ragged needs one label sequence per utterance")
+        B = len(xs)
+        scale = 1.0 / B if B > 1 else 1.0
+        nll = torch.empty(B, device=self.device, dtype=torch.float32)
+        logps = [None] * B
+        first = True
+        for idx in bucket_by_shape([(x.shape[0], y.shape[0]) for x, y in zip(xs, labels)], max_batch):
+            x = torch.stack([xs[i] for i in idx]).contiguous()
+            y = torch.stack([labels[i].to(torch.int32) for i in idx]).contiguous()
+            n, lp = self.step(x, y, scale=scale, zero_grads=first, normalizeNLL=normalizeNLL)
+            first = False
+            nll[torch.tensor(idx, device=self.device)] = n
+            for j, i in enumerate(idx):
+                logps[i] = lp[j]
+        return nll, logps
+
     def encoder_output(self):
         B, L, T = self._last
         d = self.dims(B, L, T)
-        ws = self._ws[(B, L, T, self.cfg.dropout > 0 and self.train)]
+        ws = self._wsbuf
         p = lib.s2s_model_encoder_output(ctypes.byref(d), dptr(ws))
         off = p - ws.data_ptr()
         n = B * L * self.cfg.annotationDepth
