@@ -171,14 +171,17 @@ int s2s_tmaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int
 int s2s_tmaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const int* idx,
                      const float* dy, float* dx);
 /* nn.SpatialConvolutionMM(Cin, Cout, kW, kH) (stride 1, no padding): x (B, Cin, H, W) -> y (B, Cout, H-kH+1, W-kW+1);
- * weight (Cout, Cin*kH*kW) in (c, i, j) order, bias (Cout) or NULL.  Scratch holds the im2col panel. */
+ * weight (Cout, Cin*kH*kW) in (c, i, j) order, bias (Cout) or NULL.  Scratch holds the im2col panel of x:
+ * col_from_fwd = 1 lets the backward reuse the panel the forward left in the SAME scratch (same x, scratch
+ * untouched in between) instead of rebuilding it. */
 size_t s2s_sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW);
 int s2s_sconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
                   const float* x, const float* weight, const float* bias, float* y, void* scratch,
                   size_t scratch_bytes);
 int s2s_sconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
                   const float* x, const float* weight, const float* y, const float* dy, float* dx, int dx_accumulate,
-                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes);
+                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes,
+                  int col_from_fwd);
 /* nn.SpatialMaxPooling(kW, kH, dW, dH) (floor mode): x (B, C, H, W) -> y (B, C, (H-kH)/dH+1, (W-kW)/dW+1);
  * idx = i*kW + j of the window's first maximum. */
 int s2s_smaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,

@@ -1081,6 +1081,13 @@ static int launch_xcd(int var, bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
 // the model step runs it on the side stream beside the encoder).
 static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const GemmWs& gws) {
   const int S = d.S, A = d.A, rows = d.B * d.T;
+  // backward operand layouts first (params only): on the side stream beside the encoder, kernels
+  // run only in the gaps the persistent GRU launches leave, so the independent ones go early and
+  // the dependent GEMM chain last
+  S2S_TRY(transpose_f32(st, k.P.Wh, 2L * S, S, S, x.XWHT, S));
+  S2S_TRY(transpose_f32(st, k.P.Wz, 2L * S, S, S, x.XZRT, 2L * S));
+  S2S_TRY(transpose_f32(st, k.P.Wr, 2L * S, S, S, x.XZRT + S, 2L * S));
+  S2S_TRY(transpose_f32(st, k.P.Ws, S, d.Sc, S, x.XWST, d.Sc));
   S2S_TRY(copy2d_f32(st, k.P.Wz + S, 2L * S, x.WXD, S, S, S, false));
   S2S_TRY(copy2d_f32(st, k.P.Wr + S, 2L * S, x.WXD + (long)S * S, S, S, S, false));
   S2S_TRY(copy2d_f32(st, k.P.Wh + S, 2L * S, x.WXD + 2L * S * S, S, S, S, false));
@@ -1094,11 +1101,6 @@ static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const X
   S2S_CHECK_HIP(hipGetLastError());
   S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
   S2S_TRY(gemm1(st, false, true, rows, 3 * S, S, 1.f, x.KD, S, x.WXD, S, 0.f, x.KX, 3L * S, nullptr, gws));
-  // backward operand layouts (rows = output units, K contiguous)
-  S2S_TRY(transpose_f32(st, k.P.Wh, 2L * S, S, S, x.XWHT, S));
-  S2S_TRY(transpose_f32(st, k.P.Wz, 2L * S, S, S, x.XZRT, 2L * S));
-  S2S_TRY(transpose_f32(st, k.P.Wr, 2L * S, S, S, x.XZRT + S, 2L * S));
-  S2S_TRY(transpose_f32(st, k.P.Ws, S, d.Sc, S, x.XWST, d.Sc));
   return 0;
 }
 

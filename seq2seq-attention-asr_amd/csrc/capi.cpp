@@ -318,8 +318,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // stream, joined before the decoder (the persistent GRU launches hold every CU, so it runs in the
   // gaps between layers); 1: beside pad + pack, joined before layer 1; 2: inline on the main stream
   if (split && pmode != 2) {
-    if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
     S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));  // dlogp = -labelmask
+    if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
     S2S_CHECK_HIP(hipEventRecord(ev[14], side));
     if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   } else {
@@ -698,11 +698,11 @@ int s2s_sconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int 
 }
 int s2s_sconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
                   const float* x, const float* weight, const float* y, const float* dy, float* dx, int dx_accumulate,
-                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes) {
+                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes, int col_from_fwd) {
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(x && weight && dy && scratch, "SpatialConvolutionMM: null argument");
   return sconv_bwd(static_cast<hipStream_t>(stream), B, Cin, H, W, Cout, kH, kW, relu, x, weight, y, dy, dx,
-                   dx_accumulate, dweight, dbias, scale, scratch, scratch_bytes);
+                   dx_accumulate, dweight, dbias, scale, scratch, scratch_bytes, col_from_fwd);
 }
 int s2s_smaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
                      const float* x, float* y, int* idx) {

@@ -17,7 +17,7 @@ int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
               const float* Wt, const float* bias, float* y, void* scratch, size_t scratch_bytes);
 int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
               const float* Wt, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
-              float scale, void* scratch, size_t scratch_bytes);
+              float scale, void* scratch, size_t scratch_bytes, int col_from_fwd);
 int smaxpool_fwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int dW, int dH, const float* x, float* y,
                  int* idx);
 int smaxpool_bwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int dW, int dH, const int* idx,

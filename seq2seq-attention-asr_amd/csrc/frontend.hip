@@ -107,73 +107,77 @@ __global__ void tmaxpool_bwd_kernel(const int* __restrict__ idx, const float* __
 }
 
 // col[(c*kH + i)*kW + j][b*N + oh*Wo + ow] = x[b, c, oh + i, ow + j]   (col row stride B*N)
-__global__ void im2col_kernel(const float* __restrict__ x, int B, int C, int H, int W, int kH, int kW, int Ho,
-                              int Wo, float* __restrict__ col) {
-  const long N = (long)Ho * Wo, BN = B * N;
-  const long n = (long)C * kH * kW * BN;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const long q = e % BN;
-    const int r = (int)(e / BN);
-    const int b = (int)(q / N);
-    const int p = (int)(q % N);
-    const int oh = p / Wo, ow = p % Wo;
-    const int j = r % kW, i = (r / kW) % kH, c = r / (kW * kH);
-    col[e] = x[(((long)b * C + c) * H + oh + i) * W + ow + j];
-  }
+// grid (ceil(N/256), K, B): one panel row r and utterance b per (y, z); 32-bit index math only
+__global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x, int B, int C, int H, int W, int kH,
+                                                     int kW, int Ho, int Wo, float* __restrict__ col) {
+  const int N = Ho * Wo;
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= N) return;
+  const int r = blockIdx.y, b = blockIdx.z;
+  const int j = r % kW, i = (r / kW) % kH, c = r / (kW * kH);
+  const int oh = p / Wo, ow = p - oh * Wo;
+  col[(long)r * B * N + (long)b * N + p] = x[(((long)b * C + c) * H + oh + i) * W + ow + j];
 }
 
 // dx[b, c, h, w] (+)= sum_{i, j valid} dcol[(c*kH + i)*kW + j][b*N + (h - i)*Wo + (w - j)]
-__global__ void col2im_kernel(const float* __restrict__ dcol, int B, int C, int H, int W, int kH, int kW, int Ho,
-                              int Wo, int acc, float* __restrict__ dx) {
+// grid (ceil(H*W/256), C, B)
+__global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcol, int B, int C, int H, int W,
+                                                     int kH, int kW, int Ho, int Wo, int acc, float* __restrict__ dx) {
+  const int hw = blockIdx.x * 256 + threadIdx.x;
+  if (hw >= H * W) return;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const int h = hw / W, w = hw - h * W;
   const long N = (long)Ho * Wo, BN = B * N;
-  const long n = (long)B * C * H * W;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const int w = (int)(e % W);
-    const int h = (int)((e / W) % H);
-    const int c = (int)((e / ((long)W * H)) % C);
-    const int b = (int)(e / ((long)W * H * C));
-    float s = 0.f;
-    for (int i = 0; i < kH; ++i) {
-      const int oh = h - i;
-      if (oh < 0 || oh >= Ho) continue;
-      for (int j = 0; j < kW; ++j) {
-        const int ow = w - j;
-        if (ow < 0 || ow >= Wo) continue;
-        s += dcol[((long)(c * kH + i) * kW + j) * BN + (long)b * N + (long)oh * Wo + ow];
-      }
-    }
-    dx[e] = acc ? dx[e] + s : s;
-  }
-}
-
-// dyt[c][b*N + p] = dy[b, c, p] * (relu ? 1[y > 0] : 1)
-__global__ void nchw_to_cbn_kernel(const float* __restrict__ dy, const float* __restrict__ y, int relu, int B, int C,
-                                   long N, float* __restrict__ dyt) {
-  const long n = (long)B * C * N;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const long p = e % N;
-    const int c = (int)((e / N) % C);
-    const int b = (int)(e / (N * C));
-    float v = dy[e];
-    if (relu && !(y[e] > 0.f)) v = 0.f;
-    dyt[(long)c * B * N + (long)b * N + p] = v;
-  }
-}
-
-// out[r] = beta*out[r] + alpha * sum_j X[r*ld + j]  (one workgroup per row, fixed order)
-__global__ void rowsum_kernel(const float* __restrict__ X, long ld, long ncols, float alpha, float beta,
-                              float* __restrict__ out) {
-  __shared__ float red[4];
-  const float* row = X + blockIdx.x * ld;
+  const float* base = dcol + (long)c * kH * kW * BN + (long)b * N;
   float s = 0.f;
-  for (long j = threadIdx.x; j < ncols; j += 256) s += row[j];
+  for (int i = 0; i < kH; ++i) {
+    const int oh = h - i;
+    if (oh < 0 || oh >= Ho) continue;
+    for (int j2 = 0; j2 < kW; ++j2) {
+      const int ow = w - j2;
+      if (ow < 0 || ow >= Wo) continue;
+      s += base[(long)(i * kW + j2) * BN + oh * Wo + ow];
+    }
+  }
+  const long e = ((long)b * C + c) * H * W + hw;
+  dx[e] = acc ? dx[e] + s : s;
+}
+
+// dyt[c][b*N + p] = dy[b, c, p] * (relu ? 1[y > 0] : 1); grid (ceil(N/256), C, B)
+__global__ __launch_bounds__(256) void nchw_to_cbn_kernel(const float* __restrict__ dy, const float* __restrict__ y,
+                                                          int relu, int B, int C, int N, float* __restrict__ dyt) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= N) return;
+  const int c = blockIdx.y, b = blockIdx.z;
+  const long e = ((long)b * C + c) * N + p;
+  float v = dy[e];
+  if (relu && !(y[e] > 0.f)) v = 0.f;
+  dyt[(long)c * B * N + (long)b * N + p] = v;
+}
+
+// Row sums in two fixed-order stages: part[r][q] = sum of chunk q of row r (grid (kRowParts, rows)),
+// then out[r] = beta*out[r] + alpha * sum_q part[r][q].
+constexpr int kRowParts = 64;
+__global__ __launch_bounds__(256) void rowsum_part_kernel(const float* __restrict__ X, long ld, long ncols,
+                                                          float* __restrict__ part) {
+  __shared__ float red[4];
+  const long chunk = (ncols + kRowParts - 1) / kRowParts;
+  const long j0 = blockIdx.x * chunk, j1 = min(ncols, j0 + chunk);
+  const float* row = X + blockIdx.y * ld;
+  float s = 0.f;
+  for (long j = j0 + threadIdx.x; j < j1; j += 256) s += row[j];
   s = wave_sum(s);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    const float t = (red[0] + red[1]) + (red[2] + red[3]);
-    out[blockIdx.x] = (beta == 0.f ? 0.f : beta * out[blockIdx.x]) + alpha * t;
-  }
+  if (threadIdx.x == 0) part[blockIdx.y * kRowParts + blockIdx.x] = (red[0] + red[1]) + (red[2] + red[3]);
+}
+__global__ void rowsum_final_kernel(const float* __restrict__ part, int rows, float alpha, float beta,
+                                    float* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= rows) return;
+  float t = 0.f;
+  for (int q = 0; q < kRowParts; ++q) t += part[r * kRowParts + q];
+  out[r] = (beta == 0.f ? 0.f : beta * out[r]) + alpha * t;
 }
 
 // SpatialMaxPooling(kW, kH, dW, dH) on (B*C) planes, floor mode; first maximum in (i, j) scan order
@@ -200,22 +204,24 @@ __global__ void smaxpool_fwd_kernel(const float* __restrict__ x, long planes, in
   }
 }
 
-__global__ void smaxpool_bwd_kernel(const int* __restrict__ idx, const float* __restrict__ dy, long planes, int H,
-                                    int W, int kW, int kH, int dW, int dH, int Ho, int Wo, float* __restrict__ dx) {
-  const long n = planes * H * W;
-  for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) {
-    const int w = (int)(e % W);
-    const int h = (int)((e / W) % H);
-    const long pl = e / ((long)W * H);
-    float s = 0.f;
-    for (int oh = min(h / dH, Ho - 1); oh >= 0 && oh * dH + kH > h; --oh)
-      for (int ow = min(w / dW, Wo - 1); ow >= 0 && ow * dW + kW > w; --ow) {
-        const long oe = (pl * Ho + oh) * Wo + ow;
-        const int k = idx[oe];
-        if (oh * dH + k / kW == h && ow * dW + k % kW == w) s += dy[oe];
-      }
-    dx[e] = s;
-  }
+// grid (ceil(H*W/256), B*C): 32-bit index math within a plane
+__global__ __launch_bounds__(256) void smaxpool_bwd_kernel(const int* __restrict__ idx, const float* __restrict__ dy,
+                                                           int H, int W, int kW, int kH, int dW, int dH, int Ho, int Wo,
+                                                           float* __restrict__ dx) {
+  const int hw = blockIdx.x * 256 + threadIdx.x;
+  if (hw >= H * W) return;
+  const long pl = blockIdx.y;
+  const int h = hw / W, w = hw - h * W;
+  const int* ip = idx + pl * Ho * Wo;
+  const float* dp = dy + pl * Ho * Wo;
+  float s = 0.f;
+  for (int oh = min(h / dH, Ho - 1); oh >= 0 && oh * dH + kH > h; --oh)
+    for (int ow = min(w / dW, Wo - 1); ow >= 0 && ow * dW + kW > w; --ow) {
+      const int oe = oh * Wo + ow;
+      const int k = ip[oe];
+      if (oh * dH + k / kW == h && ow * dW + k % kW == w) s += dp[oe];
+    }
+  dx[pl * H * W + hw] = s;
 }
 
 // (B, D1, D2, D3) -> (B, D2, D1, D3)   (Transpose2({1,2},3) with the batch leading; its own inverse
@@ -335,9 +341,10 @@ int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
   const int Ho = H - kH + 1, Wo = W - kW + 1;
   const long N = (long)Ho * Wo;
   const int K = Cin * kH * kW;
+  S2S_REQUIRE(K <= 65535 && B <= 65535 && (long)B * N < 2147483647L, "SpatialConvolutionMM: sizes exceed the grid");
   float* col = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes);
-  hipLaunchKernelGGL(im2col_kernel, dim3(grid1d((long)K * B * N)), dim3(256), 0, st, x, B, Cin, H, W, kH, kW, Ho, Wo,
-                     col);
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((N + 255) / 256), K, B), dim3(256), 0, st, x, B, Cin, H, W, kH, kW,
+                     Ho, Wo, col);
   S2S_CHECK_HIP(hipGetLastError());
   // y_b (Cout, N) = W (Cout, K) col[:, b*N : (b+1)*N] + bias (per row), ReLU in the epilogue
   for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
@@ -356,27 +363,33 @@ int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
 
 int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
               const float* Wt, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
-              float scale, void* scratch, size_t scratch_bytes) {
+              float scale, void* scratch, size_t scratch_bytes, int col_from_fwd) {
   S2S_REQUIRE(H >= kH && W >= kW && B > 0, "SpatialConvolutionMM: bad sizes");
   S2S_REQUIRE(!relu || y, "SpatialConvolutionMM: relu backward needs the forward output");
   S2S_REQUIRE(scratch_bytes >= sconv_scratch_bytes(B, Cin, H, W, Cout, kH, kW), "SpatialConvolutionMM: scratch too small");
   const int Ho = H - kH + 1, Wo = W - kW + 1;
   const long N = (long)Ho * Wo, BN = B * N;
   const int K = Cin * kH * kW;
+  S2S_REQUIRE(K <= 65535 && B <= 65535 && Cin <= 65535 && Cout <= 65535 && BN < 2147483647L,
+              "SpatialConvolutionMM: sizes exceed the grid");
   char* base = static_cast<char*>(scratch) + kWsBytes;
   float* col = reinterpret_cast<float*>(base);
   float* dcol = reinterpret_cast<float*>(base + align256(sizeof(float) * K * BN));
   float* dyt = reinterpret_cast<float*>(base + 2 * align256(sizeof(float) * K * BN));
-  hipLaunchKernelGGL(nchw_to_cbn_kernel, dim3(grid1d((long)Cout * BN)), dim3(256), 0, st, dy, y, relu, B, Cout, N,
-                     dyt);
+  hipLaunchKernelGGL(nchw_to_cbn_kernel, dim3((unsigned)((N + 255) / 256), Cout, B), dim3(256), 0, st, dy, y, relu, B,
+                     Cout, (int)N, dyt);
   S2S_CHECK_HIP(hipGetLastError());
   if (db) {
-    hipLaunchKernelGGL(rowsum_kernel, dim3(Cout), dim3(256), 0, st, dyt, BN, BN, scale, 1.f, db);
+    // the split-K slab region is free until the dW GEMM below (stream order)
+    float* part = static_cast<float*>(scratch);
+    hipLaunchKernelGGL(rowsum_part_kernel, dim3(kRowParts, Cout), dim3(256), 0, st, dyt, BN, BN, part);
+    hipLaunchKernelGGL(rowsum_final_kernel, dim3((Cout + 255) / 256), dim3(256), 0, st, part, Cout, scale, 1.f, db);
     S2S_CHECK_HIP(hipGetLastError());
   }
   if (dW) {
-    hipLaunchKernelGGL(im2col_kernel, dim3(grid1d((long)K * BN)), dim3(256), 0, st, x, B, Cin, H, W, kH, kW, Ho, Wo,
-                       col);
+    if (!col_from_fwd)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
+    hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((N + 255) / 256), K, B), dim3(256), 0, st, x, B, Cin, H, W, kH,
+                       kW, Ho, Wo, col);
     S2S_CHECK_HIP(hipGetLastError());
     // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
     S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
@@ -384,8 +397,8 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
   if (dx) {
     // dcol (K, B*N) = W^T dyt ; dx = col2im(dcol)
     S2S_TRY(gemm1(st, true, false, K, (int)BN, Cout, 1.f, Wt, K, dyt, BN, 0.f, dcol, BN));
-    hipLaunchKernelGGL(col2im_kernel, dim3(grid1d((long)B * Cin * H * W)), dim3(256), 0, st, dcol, B, Cin, H, W, kH,
-                       kW, Ho, Wo, dx_accumulate, dx);
+    hipLaunchKernelGGL(col2im_kernel, dim3((unsigned)((H * W + 255) / 256), Cin, B), dim3(256), 0, st, dcol, B, Cin, H,
+                       W, kH, kW, Ho, Wo, dx_accumulate, dx);
     S2S_CHECK_HIP(hipGetLastError());
   }
   return 0;
@@ -408,8 +421,9 @@ int smaxpool_bwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int
   S2S_REQUIRE(kW > 0 && kH > 0 && dW > 0 && dH > 0 && H >= kH && W >= kW, "SpatialMaxPooling: bad sizes");
   const int Ho = (H - kH) / dH + 1, Wo = (W - kW) / dW + 1;
   const long planes = (long)B * C;
-  hipLaunchKernelGGL(smaxpool_bwd_kernel, dim3(grid1d(planes * H * W)), dim3(256), 0, st, idx, dy, planes, H, W, kW,
-                     kH, dW, dH, Ho, Wo, dx);
+  S2S_REQUIRE(planes <= 65535, "SpatialMaxPooling: B*C above the grid's 65535 planes");
+  hipLaunchKernelGGL(smaxpool_bwd_kernel, dim3((unsigned)((H * W + 255) / 256), (unsigned)planes), dim3(256), 0, st, idx,
+                     dy, H, W, kW, kH, dW, dH, Ho, Wo, dx);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

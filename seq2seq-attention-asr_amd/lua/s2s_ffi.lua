@@ -49,6 +49,29 @@ size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, void* stream, void* state, size_t n);
 int s2s_optim_adadelta_step(s2s_ctx* ctx, void* stream, const s2s_optim_config* cfg, float* params,
                             float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+size_t s2s_tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW);
+int s2s_tconv_fwd(s2s_ctx*, void* stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* b, float* y);
+int s2s_tconv_bwd(s2s_ctx*, void* stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x,
+                  const float* W, const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db,
+                  float scale, void* scratch, size_t scratch_bytes);
+int s2s_tmaxpool_fwd(s2s_ctx*, void* stream, int B, int L, int D, int kW, int dW, const float* x, float* y, int* idx);
+int s2s_tmaxpool_bwd(s2s_ctx*, void* stream, int B, int L, int D, int kW, int dW, const int* idx, const float* dy,
+                     float* dx);
+size_t s2s_sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW);
+int s2s_sconv_fwd(s2s_ctx*, void* stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* bias, float* y, void* scratch, size_t scratch_bytes);
+int s2s_sconv_bwd(s2s_ctx*, void* stream, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu,
+                  const float* x, const float* weight, const float* y, const float* dy, float* dx, int dx_accumulate,
+                  float* dweight, float* dbias, float scale, void* scratch, size_t scratch_bytes,
+                  int col_from_fwd);
+int s2s_smaxpool_fwd(s2s_ctx*, void* stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const float* x, float* y, int* idx);
+int s2s_smaxpool_bwd(s2s_ctx*, void* stream, int B, int C, int H, int W, int kW, int kH, int dW, int dH,
+                     const int* idx, const float* dy, float* dx);
+int s2s_swap12(s2s_ctx*, void* stream, int B, int D1, int D2, int D3, const float* x, float* y);
+int s2s_relu_fwd(s2s_ctx*, void* stream, long n, const float* x, float* y);
+int s2s_relu_bwd(s2s_ctx*, void* stream, long n, const float* x, const float* dy, float* dx);
 ]]
 
 local C = ffi.load('s2s_hip')
@@ -83,6 +106,29 @@ function M.gru_forward(ctx, stream, x, W, H, reverse, output, saved, scratch)
    M.check(C.s2s_gru_fwd(ctx, stream, 1, B, L, D, H, ffi.new('int[1]', {reverse and 1 or 0}), dptr(x3), D, w, y, H,
                          sv, ffi.cast('void*', torch.data(scratch)), scratch:nElement()))
    return output
+end
+
+-- nn.TemporalConvolution(Din, Dout, kW) on a (L x Din) or (B x L x Din) CudaTensor, as the conv + BiLSTM
+-- encoder's convlayer uses it (timit/timit.lua:113-121); relu = true fuses the nn.ReLU that follows.
+function M.tconv_forward(ctx, stream, m, x, relu, output)
+   local x3 = x:nDimension() == 2 and x:view(1, x:size(1), x:size(2)) or x
+   local B, L, Din = x3:size(1), x3:size(2), x3:size(3)
+   output:resize(B, L - m.kW + 1, m.outputFrameSize)
+   M.check(C.s2s_tconv_fwd(ctx, stream, B, L, Din, m.outputFrameSize, m.kW, relu and 1 or 0, dptr(x3),
+                           dptr(m.weight), dptr(m.bias), dptr(output)))
+   return output
+end
+
+-- updateGradInput + accGradParameters(scale) of the same module (gradInput overwritten)
+function M.tconv_backward(ctx, stream, m, x, relu, output, gradOutput, gradInput, scale, scratch)
+   local x3 = x:nDimension() == 2 and x:view(1, x:size(1), x:size(2)) or x
+   local B, L, Din = x3:size(1), x3:size(2), x3:size(3)
+   gradInput:resizeAs(x3)
+   scratch:resize(tonumber(C.s2s_tconv_scratch_bytes(B, L, Din, m.outputFrameSize, m.kW)))
+   M.check(C.s2s_tconv_bwd(ctx, stream, B, L, Din, m.outputFrameSize, m.kW, relu and 1 or 0, dptr(x3), dptr(m.weight),
+                           dptr(output), dptr(gradOutput), dptr(gradInput), 0, dptr(m.gradWeight), dptr(m.gradBias),
+                           scale or 1, ffi.cast('void*', torch.data(scratch)), scratch:nElement()))
+   return gradInput
 end
 
 return M

@@ -101,7 +101,7 @@ SIGNATURES = [
                               c_void_p, c_void_p, c_void_p, c_void_p, c_size_t]),
     ("s2s_sconv_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p,
                               c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_float, c_void_p,
-                              c_size_t]),
+                              c_size_t, c_int]),
     ("s2s_smaxpool_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,
                                  c_void_p, c_void_p, c_void_p]),
     ("s2s_smaxpool_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_int,

@@ -144,6 +144,7 @@ class SpatialConvolutionMM(Module):
         y = torch.empty((B, self.nOutputPlane, H - self.kH + 1, W - self.kW + 1), device=x.device,
                         dtype=torch.float32)
         scr = _bytes(lib.s2s_sconv_scratch_bytes(B, C, H, W, self.nOutputPlane, self.kH, self.kW), x.device)
+        self._scr = (scr, x.data_ptr(), x.shape)  # the im2col panel, reused by the backward on the same input
         check(lib.s2s_sconv_fwd(_ctx(x), stream_ptr(), B, C, H, W, self.nOutputPlane, self.kH, self.kW,
                                 int(self.relu), dptr(x), dptr(self.weight), dptr(self.bias), dptr(y), dptr(scr),
                                 scr.numel()))
@@ -156,10 +157,15 @@ class SpatialConvolutionMM(Module):
         go = (gradOutput if gradOutput.dim() == 4 else gradOutput.unsqueeze(0)).contiguous()
         y = self.output if self.output.dim() == 4 else self.output.unsqueeze(0)
         dx = torch.empty_like(x) if self.need_gradInput else None
-        scr = _bytes(lib.s2s_sconv_scratch_bytes(B, C, H, W, self.nOutputPlane, self.kH, self.kW), x.device)
+        saved = getattr(self, "_scr", None)
+        reuse = saved is not None and saved[1] == x.data_ptr() and saved[2] == x.shape
+        scr = saved[0] if reuse else _bytes(lib.s2s_sconv_scratch_bytes(B, C, H, W, self.nOutputPlane, self.kH,
+                                                                         self.kW), x.device)
         check(lib.s2s_sconv_bwd(_ctx(x), stream_ptr(), B, C, H, W, self.nOutputPlane, self.kH, self.kW,
                                 int(self.relu), dptr(x), dptr(self.weight), dptr(y), dptr(go), dptr(dx), 0,
-                                dptr(self.gradWeight), dptr(self.gradBias), float(scale), dptr(scr), scr.numel()))
+                                dptr(self.gradWeight), dptr(self.gradBias), float(scale), dptr(scr), scr.numel(),
+                                int(reuse)))
+        self._scr = None
         self.gradInput = None if dx is None else (dx if input.dim() == 4 else dx[0])
         return self.gradInput
 
