@@ -92,7 +92,8 @@ struct XArgs {
   float *sS, *sQ, *sC;  // forward: s_t, q_t (S), c_t (A)
   float *sDGZ, *sDGR, *sDGH, *sDC, *sDWS;  // backward: da_z, da_r, da_h (S), dc (A), dws (Sc)
 };
-constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder
+constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder, LDS-resident
+constexpr int kXLCStream = 64;  // largest chunk when h / Vh rows are read from global memory each step
 constexpr int kXMaxCh = 16;  // chunks per utterance
 constexpr int kXChains = 8;  // chains per launch (one per XCD)
 constexpr int kXWG = 32;     // workgroups per chain
@@ -102,7 +103,7 @@ constexpr int kXWG = 32;     // workgroups per chain
 // into NCH chunks of XLC frames (U * NCH <= 32 workgroups).  var = 0: the shape is served by the
 // older kernels (S2S_DEC_MODE=persist / step force those).
 struct XPlan {
-  int var = 0, U = 0, nchains = 0, XLC = 0, NCH = 0;
+  int var = 0, U = 0, nchains = 0, XLC = 0, NCH = 0, res = 1;
 };
 XPlan dec_xcd_plan(const AttnDims& d) {
   XPlan p;
@@ -117,7 +118,14 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   if (U > 16) return p;
   const int nmax = std::min(kXMaxCh, kXWG / U);
   const int xlc = ((d.L + nmax - 1) / nmax + 3) / 4 * 4;
-  if (xlc > kXLC || d.T > 256) return p;  // (dec_xcd_dvh stages up to 256 steps)
+  if (xlc > kXLCStream || d.T > 256) return p;  // (dec_xcd_dvh stages up to 256 steps)
+  // resident chunks while they fit LDS (U utterances x L frames x (A + Sc) floats per XCD); longer
+  // utterances stream their h / Vh rows from global memory (L2 / MALL) every step
+  // (S2S_DEC_STREAM = 1 / 0: force Vh-only / no residency -- diagnostics and the bitwise tests)
+  const char* fs = std::getenv("S2S_DEC_STREAM");
+  p.res = xlc <= kXLC ? 2 : 1;
+  if (fs && std::strcmp(fs, "1") == 0) p.res = 1;
+  if (fs && std::strcmp(fs, "0") == 0) p.res = 0;
   p.var = var;
   p.U = U;
   p.nchains = (d.B + U - 1) / U;
@@ -1064,17 +1072,19 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
 static int g_dec_allow_local = 1;
 
 template <int S, int A, int SC>
-static int launch_xcd_t(bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
-  const size_t lds = xdec_lds<S, A, SC>(x.XLC);
-  const void* fn = fwd ? (const void*)dec_xcd_fwd<S, A, SC> : (const void*)dec_xcd_bwd<S, A, SC>;
-  S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+static int launch_xcd_t(bool fwd, int res, hipStream_t st, AttnK& k, XArgs& x) {
+  const size_t lds = xdec_lds<S, A, SC>(x.XLC, res);
+  const void* fn = res == 2 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 2> : (const void*)dec_xcd_bwd<S, A, SC, 2>)
+                 : res == 1 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 1> : (const void*)dec_xcd_bwd<S, A, SC, 1>)
+                            : (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 0> : (const void*)dec_xcd_bwd<S, A, SC, 0>);
+  if (lds) S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {&k, &x};
   S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
   return 0;
 }
-static int launch_xcd(int var, bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
-  if (var == 1) return launch_xcd_t<256, 512, 512>(fwd, st, k, x);
-  return launch_xcd_t<64, 128, 128>(fwd, st, k, x);
+static int launch_xcd(const XPlan& xp, bool fwd, hipStream_t st, AttnK& k, XArgs& x) {
+  if (xp.var == 1) return launch_xcd_t<256, 512, 512>(fwd, xp.res, st, k, x);
+  return launch_xcd_t<64, 128, 128>(fwd, xp.res, st, k, x);
 }
 
 // Weight folds and teacher-forced constants of the XCD-local decoder (params and labels only, so
@@ -1155,7 +1165,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       ProfScope ps(st, "dec_fwd_xcd", 0.0, 0.0);
-      S2S_TRY(launch_xcd(xp.var, true, st, k, x));
+      S2S_TRY(launch_xcd(xp, true, st, k, x));
     }
     // alpha / MonotonicAlignment indicators from the saved scores: only the backward (and alpha())
     // read them, so beside the MLP head when split
@@ -1261,7 +1271,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
       ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
-      S2S_TRY(launch_xcd(xp.var, false, st, k, x));
+      S2S_TRY(launch_xcd(xp, false, st, k, x));
     }
     // dVh / dwe (dec_xcd_dvh) beside the alpha^T dc GEMMs when split; both feed dh
     if (side) {

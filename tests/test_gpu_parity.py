@@ -166,6 +166,40 @@ def test_xcd_decoder_matches_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen, local)
         fn(1)
 
 
+# chunks too long for LDS residency (> 32 frames): h / Vh rows streamed from global memory each step
+XCD_STREAM_CASES = [
+    (32, 400, 6, 512, 512, 256, 29, 8, 7, 0.0),
+    (21, 500, 5, 128, 128, 64, 29, 4, 7, 0.2),
+]
+
+
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O,M,K,pen", XCD_STREAM_CASES)
+def test_xcd_decoder_streamed_chunks_match_oracle(s2s, B, L, T, A, Sc, S, O, M, K, pen):
+    """LibriSpeech-length utterances (config 4: L = 400) on the XCD-local decoder with streamed chunks."""
+    _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen)
+
+
+@pytest.mark.parametrize("B,L,T,A,Sc,S,O", [(32, 128, 12, 512, 512, 256, 62), (21, 50, 9, 128, 128, 64, 29)])
+def test_xcd_decoder_streamed_bitwise_equals_resident(s2s, monkeypatch, B, L, T, A, Sc, S, O):
+    """The streamed-chunk kernels do the resident kernels' arithmetic in the same order: bitwise equal."""
+    rng = np.random.default_rng(4)
+    att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, 8, 7, O), Sc, 10, 0, S, A, O, True, 0.2).cuda()
+    h = cu(rng.standard_normal((B, L, A)) * 0.5)
+    labels = cu(rng.integers(0, O, (B, T)), torch.int32)
+    dlogp = cu(rng.standard_normal((B, T, O)))
+    outs = {}
+    for stream in ("2", "0", "1"):  # resident (default at these shapes), no residency, Vh-only
+        monkeypatch.setenv("S2S_DEC_STREAM", stream)
+        logp = att.forward([h, labels]).clone()
+        att.zeroGradParameters()
+        dh = att.backward([h, None], dlogp)[0].clone()
+        outs[stream] = [logp, dh] + [g.clone() for g in att.parameters()[1]]
+    torch.cuda.synchronize()
+    for mode in ("0", "1"):
+        for i, (a, b) in enumerate(zip(outs["2"], outs[mode])):
+            assert torch.equal(a, b), f"mode {mode} tensor {i} differs: max |d| = {(a - b).abs().max().item():.3e}"
+
+
 def _check_attention(s2s, B, L, T, A, Sc, S, O, M, K, pen, kW=10, nF=0):
     rng = np.random.default_rng(L * 7 + T)
     torch.manual_seed(L * 7 + T)  # module init draws from torch's generator
