@@ -116,6 +116,11 @@ typedef struct {
    * nF, ...); nF = 0 is the content-only baseline (model_chorowski_baseline.lua:39-40); nF > 0 needs
    * 1 <= kW <= 8 and runs the per-step decoder kernels */
   int hybridAttendFilterSize, hybridAttendFeatureMaps;
+  /* external_mlp = 1: a decoder_mlp other than Maxout -> Linear -> LogSoftMax (e.g. the two-Maxout MLP of
+   * librispeech/model_vgg.lua:71-77) runs on the caller's side: s2s_attn_fwd stops at the MLP input
+   * [s_t; c_t] (s2s_attn_mlp_input; logp may be NULL), s2s_attn_bwd takes d[s_t; c_t] (B, T, S+A) in place of
+   * dlogp, and params / grads 13-16 (Wm, bm, Wo, bo) are unused (may be NULL).  Needs dropout == 0. */
+  int external_mlp;
 } s2s_attn_dims;
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
@@ -126,6 +131,8 @@ int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
 int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
                  const float* const* params, const void* saved, const float* dlogp, float* dh, int dh_accumulate,
                  float* const* grads, float scale, void* scratch, size_t scratch_bytes);
+/* the decoder_mlp input rows [s_t; c_t] (B, T, S+A) of the last forward inside `saved` (RNNAttention.lua:165) */
+const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved);
 /* decoder:alpha() (Attention.lua:241-243): device pointer to alpha (B, T, L) inside `saved` */
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
 /* (B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward (MonotonicAlignment.lua:
@@ -193,6 +200,11 @@ int s2s_smaxpool_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int C, int H, int
 int s2s_swap12(s2s_ctx* ctx, s2s_stream_t stream, int B, int D1, int D2, int D3, const float* x, float* y);
 int s2s_relu_fwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, float* y);
 int s2s_relu_bwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, const float* dy, float* dx);
+/* nn.LogSoftMax over `rows` rows of n (the output layer of an external decoder_mlp): forward and
+ * dx = dy - exp(y) * sum(dy). */
+int s2s_logsoftmax_fwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, const float* x, float* y);
+int s2s_logsoftmax_bwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, const float* y, const float* dy,
+                       float* dx);
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
  * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).       */

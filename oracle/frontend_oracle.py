@@ -248,3 +248,80 @@ def vgg_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], scale:
         G[f"vgg{l}.b"] += scale * db
         d = dx
     return d
+
+
+# ---------------------------------------------------------------- decoder_mlp stacks (3p nn + Maxout.lua)
+
+def mlp_fwd(v: Array, layers):
+    """A decoder_mlp Sequential on rows v (N, D): layers are ("maxout", W, b, window) (Maxout.lua:14-18:
+    Linear + TemporalMaxPooling(window, window) over consecutive groups), ("linear", W, b), ("logsoftmax",)."""
+    cache = []
+    h = v
+    for L in layers:
+        if L[0] == "maxout":
+            _, W, b, k = L
+            u = h @ W.T + b
+            g = u.reshape(u.shape[0], -1, k)
+            am = np.argmax(g, axis=2)
+            cache.append((h, am, u.shape))
+            h = np.take_along_axis(g, am[..., None], axis=2)[..., 0]
+        elif L[0] == "linear":
+            cache.append((h,))
+            h = h @ L[1].T + L[2]
+        else:
+            h = orc.log_softmax(h, 1)
+            cache.append((h,))
+    return h, cache
+
+
+def mlp_bwd(layers, cache, dout: Array, grads, scale: float = 1.0) -> Array:
+    """grads: list of (dW, db) per maxout / linear layer (None for logsoftmax), accumulated."""
+    d = dout
+    for L, c, gr in zip(reversed(layers), reversed(cache), reversed(grads)):
+        if L[0] == "maxout":
+            _, W, b, k = L
+            h, am, ushape = c
+            du = np.zeros(ushape, d.dtype).reshape(ushape[0], -1, k)
+            np.put_along_axis(du, am[..., None], d[..., None], axis=2)
+            du = du.reshape(ushape)
+            gr[0][...] += scale * (du.T @ h)
+            gr[1][...] += scale * du.sum(0)
+            d = du @ W
+        elif L[0] == "linear":
+            (h,) = c
+            gr[0][...] += scale * (d.T @ h)
+            gr[1][...] += scale * d.sum(0)
+            d = d @ L[1]
+        else:
+            (y,) = c
+            d = d - np.exp(y) * d.sum(1, keepdims=True)
+    return d
+
+
+def vgg_model_step(x: Array, labels: Array, P: Dict[str, Array], mlp_layers, cfg):
+    """librispeech/model_vgg.lua end to end + the trainer's loss seed (train.lua:139-165): VGG encoder,
+    attention decoder (GRU recurrence) with the external decoder_mlp stack, nll = -sum onehot * logp,
+    dlogp = -onehot, gradients summed over the batch then / B.  P holds the encoder (vgg*/lin*) and the
+    decoder's own parameters; cfg an s2s_oracle.ModelConfig for the decoder dims.
+    Returns (nll per utterance, logp, G encoder+decoder, mlp grads)."""
+    B = x.shape[0]
+    h, ecache = vgg_fwd(x, P)
+    Pd = dict(P)
+    S, A, M, k, O = cfg.stateDepth, cfg.annotationDepth, cfg.mlpDepth, cfg.maxoutWindow, cfg.outputDepth
+    for name, shp in (("Wm", (M * k, S + A)), ("bm", (M * k,)), ("Wo", (O, M)), ("bo", (O,))):
+        Pd.setdefault(name, np.zeros(shp))  # the fused MLP is not used (external decoder_mlp)
+    _, acache = orc.attention_fwd(h, labels, Pd, cfg)
+    T = labels.shape[1]
+    v = acache["v"].reshape(B * T, -1)
+    logp, mcache = mlp_fwd(v, mlp_layers)
+    logp = logp.reshape(B, T, O)
+    onehot = np.zeros_like(logp)
+    np.put_along_axis(onehot, labels[..., None].astype(np.int64), 1.0, axis=2)
+    nll = -(onehot * logp).sum(axis=(1, 2))
+    scale = 1.0 / B if B > 1 else 1.0
+    mgrads = [(np.zeros_like(L[1]), np.zeros_like(L[2])) if L[0] != "logsoftmax" else None for L in mlp_layers]
+    dv = mlp_bwd(mlp_layers, mcache, (-onehot).reshape(B * T, O), mgrads, scale)
+    G = {kk: np.zeros_like(vv) for kk, vv in Pd.items()}
+    dh = orc.attention_bwd(Pd, cfg, acache, None, G, scale, dmlp_in=dv.reshape(B, T, -1))
+    vgg_bwd(P, ecache, dh, G, scale)
+    return nll, logp, G, mgrads

@@ -423,14 +423,14 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
 
 
 def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, G: Dict[str, Array],
-                  scale: float = 1.0, dropout_mask: Optional[Array] = None):
+                  scale: float = 1.0, dropout_mask: Optional[Array] = None, dmlp_in: Optional[Array] = None):
     """nn.Attention:updateGradInput (Attention.lua:324-327): RNNAttention's reverse BPTT
     (RNNAttention.lua:203-253) accumulating d{Vh, h} over all t (:247); dy discarded
     (:248).  MonotonicAlignment.lua:44-77 adds lambda*(L+1-j)*ind to d alpha and its
     negation to d alpha_prev.  Returns dh (B, L, A)."""
     h, Vh, labels = cache["h"], cache["Vh"], cache["labels"]
     B, L, A = h.shape
-    T = dlogp.shape[1]
+    T = (dlogp if dmlp_in is None else dmlp_in).shape[1]
     S, Sc, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
     dt = h.dtype
     dh = np.zeros_like(h)
@@ -443,20 +443,23 @@ def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, 
     kW = cfg.hybridAttendFilterSize
     for t in range(T - 1, -1, -1):
         g_ = lambda key: cache[key][:, t]
-        logp = g_("logp")
-        # LogSoftMax backward (3p): do = dlogp - exp(logp) * sum(dlogp)
-        dl = dlogp[:, t]
-        do = dl - np.exp(logp) * dl.sum(1, keepdims=True)
-        G["Wo"] += scale * (do.T @ g_("m"))
-        G["bo"] += scale * do.sum(0)
-        dm = do @ P["Wo"]
-        du = np.zeros((B, M * k), dt)
-        idx = np.arange(M) * k + g_("argmax")
-        np.put_along_axis(du, idx, dm, axis=1)
-        v = g_("v")
-        G["Wm"] += scale * (du.T @ v)
-        G["bm"] += scale * du.sum(0)
-        dv = du @ P["Wm"]
+        if dmlp_in is not None:  # an external decoder_mlp's gradient w.r.t. its input [s_t; c_t]
+            dv = dmlp_in[:, t].copy()
+        else:
+            logp = g_("logp")
+            # LogSoftMax backward (3p): do = dlogp - exp(logp) * sum(dlogp)
+            dl = dlogp[:, t]
+            do = dl - np.exp(logp) * dl.sum(1, keepdims=True)
+            G["Wo"] += scale * (do.T @ g_("m"))
+            G["bo"] += scale * do.sum(0)
+            dm = do @ P["Wo"]
+            du = np.zeros((B, M * k), dt)
+            idx = np.arange(M) * k + g_("argmax")
+            np.put_along_axis(du, idx, dm, axis=1)
+            v = g_("v")
+            G["Wm"] += scale * (du.T @ v)
+            G["bm"] += scale * du.sum(0)
+            dv = du @ P["Wm"]
         if dropout_mask is not None:
             dv = dv * dropout_mask[:, t]
         ds = dv[:, :S] + ds_carry

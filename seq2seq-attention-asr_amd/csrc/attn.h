@@ -23,6 +23,9 @@ struct AttnDims {
   // hybrid location-aware attention (Attention.lua:75-98): hybridAttendFilterSize kW and
   // hybridAttendFeatureMaps nF; nF = 0: content-only (the Chorowski baseline)
   int hk = 0, hf = 0;
+  // external decoder_mlp: the forward stops at the MLP input [s_t; c_t] (saved VV rows) and the
+  // backward takes its gradient in place of dlogp; Wm / bm / Wo / bo are not used
+  int ext = 0;
 };
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
 struct AttnParams {
@@ -59,6 +62,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
+const float* attn_saved_mlp_input(const AttnDims& d, const void* saved);
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
 const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved);
 

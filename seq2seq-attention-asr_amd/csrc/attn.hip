@@ -966,6 +966,7 @@ int attn_check_dims(const AttnDims& d) {
   S2S_REQUIRE(d.S % 16 == 0 && d.A % 16 == 0 && d.Sc % 16 == 0, "attn: S, A, scoreDepth must be multiples of 16");
   S2S_REQUIRE(d.Sc <= 1024, "attn: scoreDepth > 1024 not supported");
   S2S_REQUIRE(d.O > 0 && d.M > 0 && d.K > 0, "attn: bad output/mlp dims");
+  S2S_REQUIRE(!d.ext || d.dropout == 0.f, "attn: dropout belongs to the external decoder_mlp");
   S2S_REQUIRE(d.dropout >= 0.f && d.dropout < 1.f, "attn: dropout must be in [0, 1)");
   S2S_REQUIRE(d.hf >= 0 && (d.hf == 0 || (d.hk >= 1 && d.hk <= kMaxHybK)),
               "attn: hybridAttendFilterSize must be in [1, 8] when hybridAttendFeatureMaps > 0");
@@ -981,6 +982,11 @@ static size_t attn_ws_offset(const AttnDims& d) {
 size_t attn_scratch_bytes(const AttnDims& d) { return attn_ws_offset(d) + sizeof(float) * kGemmWsFloats; }
 static GemmWs attn_gemm_ws(const AttnDims& d, void* scratch) {
   return GemmWs{reinterpret_cast<float*>(static_cast<char*>(scratch) + attn_ws_offset(d)), kGemmWsFloats};
+}
+const float* attn_saved_mlp_input(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.VV;
 }
 const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
   AttnK k{};
@@ -1200,6 +1206,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   S2S_CHECK_HIP(hipGetLastError());
   }
   // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
+  if (d.ext) return 0;  // external decoder_mlp: the caller runs it on the saved VV rows
   const int rows = B * T;
   if (d.dropout > 0.f) {
     hipLaunchKernelGGL(dec_dropout_fwd, dim3(512), dim3(256), 0, st, k, d.dropout, d.dropout_seed, d.dropout_mask);
@@ -1248,12 +1255,16 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
   S2S_TRY(transpose_f32(st, P.Ws, S, Sc, S, k.WsT, Sc));
   }
+  const GemmWs gws = attn_gemm_ws(d, scratch);
+  if (d.ext) {  // external decoder_mlp: dlogp holds d[s_t; c_t] (B*T, S+A)
+    S2S_TRY(copy2d_f32(st, dlogp, S + A, k.DV, S + A, rows, S + A, false));
+  } else {
   // MLP backward for all rows (not on the recurrence)
   hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
-  const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A, nullptr, gws));
+  }
   if (d.dropout > 0.f) {
     hipLaunchKernelGGL(dec_dropout_bwd, dim3(512), dim3(256), 0, st, k);
     S2S_CHECK_HIP(hipGetLastError());
@@ -1355,8 +1366,10 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
   {
     GemmProblem pr[16];
     int n = 0;
-    pr[n++] = GemmProblem{k.DO, k.MM, G.Wo, nullptr, O, d.M, d.M, O, d.M, rows, scale, 1.f};
-    pr[n++] = GemmProblem{k.DU, k.VV, G.Wm, nullptr, Mk, S + A, S + A, Mk, S + A, rows, scale, 1.f};
+    if (!d.ext) {
+      pr[n++] = GemmProblem{k.DO, k.MM, G.Wo, nullptr, O, d.M, d.M, O, d.M, rows, scale, 1.f};
+      pr[n++] = GemmProblem{k.DU, k.VV, G.Wm, nullptr, Mk, S + A, S + A, Mk, S + A, rows, scale, 1.f};
+    }
     pr[n++] = GemmProblem{k.DGA, k.HX, G.Wz, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DGA + S, k.HX, G.Wr, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DGA + 2 * S, k.RHX, G.Wh, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
@@ -1367,8 +1380,10 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
     pr[n++] = GemmProblem{k.DVH, h, G.V, nullptr, Sc, A, A, Sc, A, B * L, scale, 1.f};
     S2S_TRY(gemm_f32(st, pr, n, true, false, attn_gemm_ws(d, scratch)));
   }
-  S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo));
-  S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));
+  if (!d.ext) {
+    S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo));
+    S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));
+  }
   S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd));
   S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc));
   S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));

@@ -112,6 +112,7 @@ AttnDims to_attn(const s2s_attn_dims* d) {
              d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
   a.hk = d->hybridAttendFilterSize;
   a.hf = d->hybridAttendFeatureMaps;
+  a.ext = d->external_mlp ? 1 : 0;
   return a;
 }
 int attn_nparams(const s2s_attn_dims* d) {
@@ -587,6 +588,9 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
 
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d) { return d ? attn_saved_bytes(to_attn(d)) : 0; }
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d) { return d ? attn_scratch_bytes(to_attn(d)) : 0; }
+const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_mlp_input(to_attn(d), saved) : nullptr;
+}
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_alpha(to_attn(d), saved) : nullptr;
 }
@@ -600,12 +604,12 @@ const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved) {
 int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
                  const float* const* params, float* logp, void* saved, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
-  S2S_REQUIRE(d && h && labels && params && logp && saved, "attn: null argument");
+  S2S_REQUIRE(d && h && labels && params && (logp || d->external_mlp) && saved, "attn: null argument");
   AttnParams ap;
   const float** pp = reinterpret_cast<const float**>(&ap);
   for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
-    S2S_REQUIRE(pp[i] != nullptr, "attn: null parameter");
+    S2S_REQUIRE(pp[i] != nullptr || (d->external_mlp && i >= 13 && i <= 16), "attn: null parameter");
   }
   return attn_fwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, logp, saved, scratch, scratch_bytes);
 }
@@ -622,7 +626,8 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
   for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
     gp[i] = grads[i];
-    S2S_REQUIRE(pp[i] != nullptr && gp[i] != nullptr, "attn: null parameter/grad");
+    S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || (d->external_mlp && i >= 13 && i <= 16),
+                "attn: null parameter/grad");
   }
   return attn_bwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, saved, dlogp, dh, dh_accumulate, ag,
                   scale, scratch, scratch_bytes);
@@ -638,6 +643,7 @@ int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims*
                          float* out_score, void* workspace, size_t workspace_bytes) {
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(d && h && params && out && out_len && workspace, "beam search: null argument");
+  S2S_REQUIRE(!d->external_mlp, "beam search: runs the fused Maxout -> Linear -> LogSoftMax decoder_mlp only");
   AttnParams ap;
   const float** pp = reinterpret_cast<const float**>(&ap);
   for (int i = 0; i < attn_nparams(d); ++i) {
@@ -728,6 +734,17 @@ int s2s_relu_fwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, floa
 int s2s_relu_bwd(s2s_ctx* ctx, s2s_stream_t stream, long n, const float* x, const float* dy, float* dx) {
   S2S_TRY(set_device(ctx));
   return relu_bwd(static_cast<hipStream_t>(stream), n, x, dy, dx);
+}
+int s2s_logsoftmax_fwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, const float* x, float* y) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(x && y, "LogSoftMax: null argument");
+  return logsoftmax_fwd(static_cast<hipStream_t>(stream), rows, n, x, y);
+}
+int s2s_logsoftmax_bwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, const float* y, const float* dy,
+                       float* dx) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(y && dy && dx, "LogSoftMax: null argument");
+  return logsoftmax_bwd(static_cast<hipStream_t>(stream), rows, n, y, dy, dx);
 }
 
 int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,

@@ -25,5 +25,7 @@ int smaxpool_bwd(hipStream_t st, int B, int C, int H, int W, int kW, int kH, int
 int swap12(hipStream_t st, int B, int D1, int D2, int D3, const float* x, float* y);
 int relu_fwd(hipStream_t st, long n, const float* x, float* y);
 int relu_bwd(hipStream_t st, long n, const float* x, const float* dy, float* dx);
+int logsoftmax_fwd(hipStream_t st, long rows, int n, const float* x, float* y);
+int logsoftmax_bwd(hipStream_t st, long rows, int n, const float* y, const float* dy, float* dx);
 
 }  // namespace s2s

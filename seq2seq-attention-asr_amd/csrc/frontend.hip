@@ -246,6 +246,34 @@ __global__ void relu_bwd_kernel(const float* __restrict__ x, const float* __rest
   for (long e = blockIdx.x * 256L + threadIdx.x; e < n; e += (long)gridDim.x * 256) dx[e] = x[e] > 0.f ? dy[e] : 0.f;
 }
 
+// nn.LogSoftMax (3p) over rows of n: y = x - max - log(sum exp(x - max)); one wave per row
+__global__ __launch_bounds__(256) void logsoftmax_fwd_kernel(const float* __restrict__ x, long rows, int n,
+                                                             float* __restrict__ y) {
+  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  const float* xr = x + r * n;
+  float m = -INFINITY;
+  for (int j = lane; j < n; j += 64) m = fmaxf(m, xr[j]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int j = lane; j < n; j += 64) s += expf(xr[j] - m);
+  const float lse = m + logf(wave_sum(s));
+  for (int j = lane; j < n; j += 64) y[r * n + j] = xr[j] - lse;
+}
+// dx = dy - exp(y) * sum(dy)
+__global__ __launch_bounds__(256) void logsoftmax_bwd_kernel(const float* __restrict__ y,
+                                                             const float* __restrict__ dy, long rows, int n,
+                                                             float* __restrict__ dx) {
+  const long r = blockIdx.x * 4L + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float s = 0.f;
+  for (int j = lane; j < n; j += 64) s += dy[r * n + j];
+  s = wave_sum(s);
+  for (int j = lane; j < n; j += 64) dx[r * n + j] = dy[r * n + j] - expf(y[r * n + j]) * s;
+}
+
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
 }  // namespace
@@ -446,6 +474,22 @@ int relu_fwd(hipStream_t st, long n, const float* x, float* y) {
 int relu_bwd(hipStream_t st, long n, const float* x, const float* dy, float* dx) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(relu_bwd_kernel, dim3(grid1d(n)), dim3(256), 0, st, x, dy, n, dx);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int logsoftmax_fwd(hipStream_t st, long rows, int n, const float* x, float* y) {
+  S2S_REQUIRE(rows >= 0 && n > 0, "LogSoftMax: bad sizes");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(logsoftmax_fwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, x, rows, n, y);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int logsoftmax_bwd(hipStream_t st, long rows, int n, const float* y, const float* dy, float* dx) {
+  S2S_REQUIRE(rows >= 0 && n > 0, "LogSoftMax: bad sizes");
+  if (rows == 0) return 0;
+  hipLaunchKernelGGL(logsoftmax_bwd_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st, y, dy, rows, n, dx);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

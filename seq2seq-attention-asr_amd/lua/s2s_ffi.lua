@@ -21,7 +21,8 @@ int s2s_gru_bwd(s2s_ctx*, void* stream, int ndir, int B, int L, int D, int H, co
                 float* const* dW, float scale, void* scratch, size_t scratch_bytes);
 typedef struct { int B, L, T; int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
                  float penalty; float dropout; unsigned long long dropout_seed; const float* dropout_mask;
-                 int hybridAttendFilterSize, hybridAttendFeatureMaps; } s2s_attn_dims;
+                 int hybridAttendFilterSize, hybridAttendFeatureMaps; int external_mlp; } s2s_attn_dims;
+const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved);
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
 int s2s_attn_fwd(s2s_ctx*, void* stream, const s2s_attn_dims* d, const float* h, const int* labels,
@@ -72,6 +73,8 @@ int s2s_smaxpool_bwd(s2s_ctx*, void* stream, int B, int C, int H, int W, int kW,
 int s2s_swap12(s2s_ctx*, void* stream, int B, int D1, int D2, int D3, const float* x, float* y);
 int s2s_relu_fwd(s2s_ctx*, void* stream, long n, const float* x, float* y);
 int s2s_relu_bwd(s2s_ctx*, void* stream, long n, const float* x, const float* dy, float* dx);
+int s2s_logsoftmax_fwd(s2s_ctx*, void* stream, long rows, int n, const float* x, float* y);
+int s2s_logsoftmax_bwd(s2s_ctx*, void* stream, long rows, int n, const float* y, const float* dy, float* dx);
 ]]
 
 local C = ffi.load('s2s_hip')

@@ -19,7 +19,8 @@ class s2s_attn_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("annotationDepth", c_int), ("scoreDepth", c_int),
                 ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
                 ("penalty", c_float), ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong),
-                ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int)]
+                ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int),
+                ("external_mlp", c_int)]
 
 
 class s2s_optim_config(ctypes.Structure):
@@ -62,6 +63,7 @@ SIGNATURES = [
     ("s2s_attn_bwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,
                              c_void_p, c_void_p, c_int, P(c_void_p), c_float, c_void_p, c_size_t]),
     ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_mlp_input", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mono_ind", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_dropout_mask", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
@@ -109,6 +111,8 @@ SIGNATURES = [
     ("s2s_swap12", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
     ("s2s_relu_fwd", c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p]),
     ("s2s_relu_bwd", c_int, [c_void_p, c_void_p, c_long, c_void_p, c_void_p, c_void_p]),
+    ("s2s_logsoftmax_fwd", c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p]),
+    ("s2s_logsoftmax_bwd", c_int, [c_void_p, c_void_p, c_long, c_int, c_void_p, c_void_p, c_void_p]),
     ("s2s_comm_unique_id", c_int, [c_void_p]),
     ("s2s_comm_init", c_int, [c_void_p, c_void_p, c_int, c_int]),
     ("s2s_allreduce_sum", c_int, [c_void_p, c_void_p, c_void_p, c_size_t]),

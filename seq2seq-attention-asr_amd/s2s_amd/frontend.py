@@ -115,6 +115,62 @@ class ReLU(Module):
         return self.gradInput
 
 
+class Linear(TemporalConvolution):
+    """nn.Linear(inputSize, outputSize): weight (out, in), bias (out), reset U(+-1/sqrt(in)); rows (N, in) or
+    (B, T, in).  Runs as TemporalConvolution(in, out, 1) (one GEMM over the rows, bias in the epilogue)."""
+
+    def __init__(self, inputSize, outputSize, relu=False, generator=None):
+        super().__init__(inputSize, outputSize, 1, relu=relu, generator=generator)
+
+
+class Maxout(Module):
+    """nn.Maxout(inputDimension, outputDimension, window) (Maxout.lua:5-19): Linear(in, out*window) ->
+    View(out*window, 1) -> TemporalMaxPooling(window, window) -> View(out), on rows (N, in)."""
+
+    def __init__(self, inputDimension, outputDimension, window=4, generator=None):
+        super().__init__()
+        self.inputDim, self.outputDim, self.window = inputDimension, outputDimension, window
+        self.linear = Linear(inputDimension, outputDimension * window, generator=generator)
+        self.pool = TemporalMaxPooling(window, window)
+
+    def parameters(self):
+        return self.linear.parameters()
+
+    def updateOutput(self, input):
+        if input.dim() != 2:
+            raise S2SArgumentError("Maxout: rows (N, inputDimension)")
+        self._u = self.linear.forward(input)
+        N = input.shape[0]
+        self.output = self.pool.forward(self._u.reshape(N, -1, 1)).reshape(N, self.outputDim)
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        N = input.shape[0]
+        du = self.pool.backward(self._u.reshape(N, -1, 1), gradOutput.reshape(N, self.outputDim, 1).contiguous())
+        self.gradInput = self.linear.backward(input, du.reshape(N, -1), scale)
+        return self.gradInput
+
+
+class LogSoftMax(Module):
+    """nn.LogSoftMax over the last dimension."""
+
+    def updateOutput(self, input):
+        _require_cuda_f32(input, "input")
+        n = input.shape[-1]
+        self.output = torch.empty_like(input)
+        check(lib.s2s_logsoftmax_fwd(_ctx(input), stream_ptr(), input.numel() // n, n, dptr(input),
+                                     dptr(self.output)))
+        return self.output
+
+    def backward(self, input, gradOutput, scale=1.0):
+        n = input.shape[-1]
+        go = gradOutput.contiguous()
+        self.gradInput = torch.empty_like(input)
+        check(lib.s2s_logsoftmax_bwd(_ctx(input), stream_ptr(), input.numel() // n, n, dptr(self.output), dptr(go),
+                                     dptr(self.gradInput)))
+        return self.gradInput
+
+
 class SpatialConvolutionMM(Module):
     """nn.SpatialConvolutionMM(nInputPlane, nOutputPlane, kW, kH) (stride 1, no padding): weight
     (out, in*kH*kW), bias (out); reset U(+-1/sqrt(kW*kH*in)).  Input (B, C, H, W) or (C, H, W)."""
@@ -349,3 +405,41 @@ class VGGEncoder(Module):
     def backward(self, input, gradOutput, scale=1.0):
         self.gradInput = self.seq.backward(input, gradOutput, scale)
         return self.gradInput
+
+
+class VGGAttentionModel(Module):
+    """librispeech/model_vgg.lua:loadmodel(opt) end to end: VGGEncoder -> nn.Attention(GRU(S, S),
+    decoder_mlp = Maxout(S+A, M, 7) -> Linear(M, M) -> Maxout(M, M, 7) -> Linear(M, O) -> LogSoftMax
+    (:71-77), scoreDepth, hybrid (off by default), S, A, O, monoAlignPenalty = true, penalty) with the
+    loss seed of librispeech/train.lua (nll = -sum labelmask * logp, dlogp = -labelmask, grads / B).
+    The decoder_mlp runs outside the decoder launches on the saved [s_t; c_t] rows (external_mlp)."""
+
+    def __init__(self, inputFrameSize=40, outputFrameSize=512, hidden=2048, scoreDepth=512, stateDepth=256,
+                 outputDepth=62, mlpDepth=64, penalty=0.0, generator=None):
+        from .nn import GRU, Attention
+        super().__init__()
+        g = generator
+        S, A, M, O = stateDepth, outputFrameSize, mlpDepth, outputDepth
+        self.encoder = VGGEncoder(inputFrameSize, outputFrameSize, hidden, generator=g)
+        mlp = Sequential(Maxout(S + A, M, 7, generator=g), Linear(M, M, generator=g), Maxout(M, M, 7, generator=g),
+                         Linear(M, O, generator=g), LogSoftMax())
+        self.decoder = Attention(GRU(S, S, generator=g), mlp, scoreDepth, 10, 0, S, A, O, True, penalty, generator=g)
+
+    def parameters(self):
+        w1, g1 = self.encoder.parameters()
+        w2, g2 = self.decoder.parameters()
+        return w1 + w2, g1 + g2
+
+    def step(self, x, labels, scale=None, normalizeNLL=False):
+        """One training step on x (B, 3, L, F), labels (B, T) 0-based: forward, nll, backward with
+        gradients accumulated at scale (default 1/B).  Returns (nll (B,), logp (B, T, O))."""
+        from .nn import nll_seed
+        B = x.shape[0]
+        scale = (1.0 / B if B > 1 else 1.0) if scale is None else scale
+        h = self.encoder.forward(x)
+        lab = labels.to(torch.int32).contiguous()
+        logp = self.decoder.forward([h, lab])
+        nll, dlogp = nll_seed(logp, lab, normalizeNLL)
+        dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+        self.encoder.backward(x, dh, scale)
+        return nll, logp

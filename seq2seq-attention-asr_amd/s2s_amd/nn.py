@@ -312,8 +312,14 @@ class Attention(Module):
             raise S2SArgumentError("hybridAttendFilterSize must be in [1, 8] with hybrid attention")
         if not isinstance(decoder_recurrent, GRU) or decoder_recurrent.dimoutput != stateDepth:
             raise S2SArgumentError("decoder_recurrent must be GRU(stateDepth, stateDepth)")
-        if not isinstance(decoder_mlp, MaxoutMLP) or decoder_mlp.inputDim != stateDepth + annotationDepth:
+        # MaxoutMLP (Maxout -> Linear -> LogSoftMax, model_chorowski_baseline.lua:53-59) runs fused in the
+        # decoder launches; any other decoder_mlp module (e.g. the two-Maxout MLP of librispeech/
+        # model_vgg.lua:71-77, built from s2s_amd.frontend) runs outside on the saved [s_t; c_t] rows
+        self.external_mlp = not isinstance(decoder_mlp, MaxoutMLP)
+        if not self.external_mlp and decoder_mlp.inputDim != stateDepth + annotationDepth:
             raise S2SArgumentError("decoder_mlp must be MaxoutMLP(stateDepth + annotationDepth, ...)")
+        if self.external_mlp and not (hasattr(decoder_mlp, "forward") and hasattr(decoder_mlp, "backward")):
+            raise S2SArgumentError("decoder_mlp must be an nn.Module mirror")
         self.scoreDepth, self.stateDepth, self.annotationDepth, self.outputDepth = (scoreDepth, stateDepth,
                                                                                     annotationDepth, outputDepth)
         self.hybridAttendFilterSize, self.hybridAttendFeatureMaps = hybridAttendFilterSize, hybridAttendFeatureMaps
@@ -339,7 +345,10 @@ class Attention(Module):
     def _tensors(self, grads=False):
         o = self.own_grad if grads else self.own
         r = self.decoder_recurrent.gradWeight if grads else self.decoder_recurrent.weight
-        m = self.decoder_mlp.gradWeight if grads else self.decoder_mlp.weight
+        if self.external_mlp:
+            m = [None] * 4  # params 13-16 unused with an external decoder_mlp
+        else:
+            m = self.decoder_mlp.gradWeight if grads else self.decoder_mlp.weight
         out = [o["V"], o["Ws"], o["bs"], o["we"], o["Wy"], o["by"], o["Wc"], o["bc"], o["Wd"], o["bd"],
                r[0], r[1], r[2], m[0], m[1], m[2], m[3]]
         if "hybW" in o:
@@ -347,7 +356,14 @@ class Attention(Module):
         return out
 
     def parameters(self):
-        return self._tensors(False), self._tensors(True)
+        ws, gs = [t for t in self._tensors(False) if t is not None], [t for t in self._tensors(True) if t is not None]
+        if self.external_mlp:
+            w2, g2 = self.decoder_mlp.parameters()
+            ws, gs = ws + list(w2), gs + list(g2)
+        return ws, gs
+
+    def _ptrs(self, grads=False):
+        return ptr_array([t.data_ptr() if t is not None else 0 for t in self._tensors(grads)])
 
     # dropout: injected (B, T, S+A) multipliers for the next forward (parity with an external RNG),
     # else drawn in-kernel from dropout_seed + the forward count
@@ -357,6 +373,14 @@ class Attention(Module):
     def _dims(self, h, T):
         B, L = (1, h.shape[0]) if h.dim() == 2 else (h.shape[0], h.shape[1])
         m = self.decoder_mlp
+        if self.external_mlp:
+            d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
+                                   1, 1, self.penalty, 0.0)
+            d.external_mlp = 1
+            if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
+                d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
+                d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
+            return d
         p = m.dropout if (m.dropout > 0 and self.train) else 0.0
         d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
                                m.mlpDepth, m.window, self.penalty, p)
@@ -406,12 +430,22 @@ class Attention(Module):
         self._labels = lab
         self._saved = _bytes(lib.s2s_attn_saved_bytes(ctypes.byref(d)), dev)
         scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
-        out = torch.empty((d.B, T, self.outputDepth), device=dev, dtype=torch.float32)
-        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
+        out = None if self.external_mlp else torch.empty((d.B, T, self.outputDepth), device=dev, dtype=torch.float32)
         check(lib.s2s_attn_fwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h), dptr(lab),
-                               params, dptr(out), dptr(self._saved), dptr(scr), scr.numel()))
+                               self._ptrs(False), dptr(out), dptr(self._saved), dptr(scr), scr.numel()))
+        if self.external_mlp:  # decoder_mlp over all B*T rows of [s_t; c_t] (RNNAttention.lua:165)
+            self._mlp_in = self.mlp_input().reshape(d.B * T, -1)
+            out = self.decoder_mlp.forward(self._mlp_in).reshape(d.B, T, -1)
         self.output = out if h.dim() == 3 else out[0]
         return self.output
+
+    def mlp_input(self):
+        """(B, T, S+A) decoder_mlp input rows [s_t; c_t] of the last forward (inside the saved buffer)."""
+        d = self._d
+        p = lib.s2s_attn_mlp_input(ctypes.byref(d), dptr(self._saved))
+        off = p - self._saved.data_ptr()
+        n = d.B * d.T * (self.stateDepth + self.annotationDepth)
+        return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T, -1)
 
     def updateGradInput(self, input, gradOutput, scale=1.0):
         h, _ = input
@@ -422,11 +456,12 @@ class Attention(Module):
             go = go[None]
         dh = torch.empty((d.B, d.L, self.annotationDepth), device=dev, dtype=torch.float32)
         scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
-        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
-        grads = ptr_array([t.data_ptr() for t in self._tensors(True)])
+        if self.external_mlp:  # d[s_t; c_t] from the decoder_mlp backward replaces dlogp
+            go = self.decoder_mlp.backward(self._mlp_in, go.reshape(d.B * d.T, -1), scale)
+            go = go.reshape(d.B, d.T, -1).contiguous()
         check(lib.s2s_attn_bwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h),
-                               dptr(self._labels), params, dptr(self._saved), dptr(go), dptr(dh), 0, grads,
-                               float(scale), dptr(scr), scr.numel()))
+                               dptr(self._labels), self._ptrs(False), dptr(self._saved), dptr(go), dptr(dh), 0,
+                               self._ptrs(True), float(scale), dptr(scr), scr.numel()))
         self.gradInput = [dh if h.dim() == 3 else dh[0], None]
         return self.gradInput
 
@@ -451,11 +486,13 @@ class Attention(Module):
         d = self._dims(h, 1)
         self.train = was_train
         dev = h.device
+        if self.external_mlp:
+            raise S2SArgumentError("BeamSearch runs the fused MaxoutMLP decoder_mlp only")
         ws = _bytes(lib.s2s_attn_beam_workspace_bytes(ctypes.byref(d), K, maxlen), dev)
         out = torch.empty((B, maxlen + 1), dtype=torch.int32, device=dev)
         olen = torch.empty(B, dtype=torch.int32, device=dev)
         osc = torch.empty(B, dtype=torch.float32, device=dev)
-        params = ptr_array([t.data_ptr() for t in self._tensors(False)])
+        params = self._ptrs(False)
         check(lib.s2s_attn_beam_search(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h), params,
                                        int(eos), int(K), maxlen, dptr(out), maxlen + 1, dptr(olen), dptr(osc),
                                        dptr(ws), ws.numel()))
