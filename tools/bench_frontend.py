@@ -84,6 +84,27 @@ def main():
                 "ms_per_fwd_bwd": round(ms, 3), "frames_per_s": round(B * L / ms * 1e3, 1),
                 "tflops": round(fl / ms / 1e9, 2), "frac_fp32_mfma_peak": round(fl / ms / 1e9 / PEAK_F32, 4),
                 "dtype": "fp32", "data": "synthetic"})
+    # the whole librispeech/model_vgg.lua training step (config 5 shape): VGG encoder + GRU attention
+    # decoder over L' = 508 frames, T = 200 char targets (O = 29), two-Maxout decoder_mlp, loss seed
+    B, L, F, T = 16, 1024, 40, 200
+    model = s2s_amd.VGGAttentionModel(F, outputFrameSize=512, hidden=2048, outputDepth=29).cuda()
+    x = torch.randn(B, 3, L, F, device="cuda")
+    lab = torch.randint(0, 28, (B, T), device="cuda", dtype=torch.int32)
+    lab[:, -1] = 28
+    for _ in range(args.warmup):
+        model.step(x, lab)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        model.step(x, lab)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    out.append({"model": "VGGAttentionModel (librispeech/model_vgg.lua, BASELINE config 5 shape)",
+                "shape": f"B={B} x (3, L={L}, F={F}), T={T}, O=29", "ms_per_step": round(ms, 3),
+                "frames_per_s": round(B * L / ms * 1e3, 1), "dtype": "fp32", "data": "synthetic",
+                "what": "encoder + decoder forward, nll seed, backward (no optimizer)"})
     for B, L in ((32, 128), (32, 512)):
         D = 123
         enc = s2s_amd.ConvBiLSTMEncoder(D).cuda()
