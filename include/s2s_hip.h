@@ -121,7 +121,13 @@ typedef struct {
    * [s_t; c_t] (s2s_attn_mlp_input; logp may be NULL), s2s_attn_bwd takes d[s_t; c_t] (B, T, S+A) in place of
    * dlogp, and params / grads 13-16 (Wm, bm, Wo, bo) are unused (may be NULL).  Needs dropout == 0. */
   int external_mlp;
+  /* decoder_lstm = 1: decoder_recurrent = nn.LSTM(S, S) without peepholes (the conv + BiLSTM model,
+   * timit/timit.lua:137: s_t = h_t, the carried mem = the cell) instead of nn.GRU(S, S); per-step decoder
+   * kernels.  Params 10-12 are then unused (may be NULL) and params 20-35 are the LSTM's, for q in (i, f, g, o):
+   * Wqx (S, S), bqx (S), Wqh (S, S), bqh (S) (LSTM.lua:25-29); 17-19 stay the hybrid ones (NULL when nF = 0). */
+  int decoder_lstm;
 } s2s_attn_dims;
+#define S2S_ATTN_NPARAMS_LSTM 36
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
 /* Attention:updateOutput (Attention.lua:305-322): h (B, L, A), labels (B, T) -> logp (B, T, O) */

@@ -254,7 +254,8 @@ def vgg_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], scale:
 
 def mlp_fwd(v: Array, layers):
     """A decoder_mlp Sequential on rows v (N, D): layers are ("maxout", W, b, window) (Maxout.lua:14-18:
-    Linear + TemporalMaxPooling(window, window) over consecutive groups), ("linear", W, b), ("logsoftmax",)."""
+    Linear + TemporalMaxPooling(window, window) over consecutive groups), ("linear", W, b), ("relu",),
+    ("logsoftmax",)."""
     cache = []
     h = v
     for L in layers:
@@ -268,6 +269,9 @@ def mlp_fwd(v: Array, layers):
         elif L[0] == "linear":
             cache.append((h,))
             h = h @ L[1].T + L[2]
+        elif L[0] == "relu":
+            cache.append((h,))
+            h = relu_fwd(h)
         else:
             h = orc.log_softmax(h, 1)
             cache.append((h,))
@@ -275,7 +279,7 @@ def mlp_fwd(v: Array, layers):
 
 
 def mlp_bwd(layers, cache, dout: Array, grads, scale: float = 1.0) -> Array:
-    """grads: list of (dW, db) per maxout / linear layer (None for logsoftmax), accumulated."""
+    """grads: list of (dW, db) per maxout / linear layer (None for relu / logsoftmax), accumulated."""
     d = dout
     for L, c, gr in zip(reversed(layers), reversed(cache), reversed(grads)):
         if L[0] == "maxout":
@@ -292,6 +296,8 @@ def mlp_bwd(layers, cache, dout: Array, grads, scale: float = 1.0) -> Array:
             gr[0][...] += scale * (d.T @ h)
             gr[1][...] += scale * d.sum(0)
             d = d @ L[1]
+        elif L[0] == "relu":
+            d = relu_bwd(c[0], d)
         else:
             (y,) = c
             d = d - np.exp(y) * d.sum(1, keepdims=True)

@@ -370,10 +370,13 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
     Vh = temporal_conv(P["V"], None, h, 1)                      # (B, L, Sc)
     s = np.zeros((B, S), dt)
     alpha_prev = np.zeros((B, L), dt)
-    cache = {key: [] for key in ("ws", "alpha", "c", "cin", "yin", "d", "sprev", "mono_ind",
-                                 "z", "r", "hh", "u", "argmax", "m", "logp", "v", "alpha_prev")}
+    keys = ["ws", "alpha", "c", "cin", "yin", "d", "sprev", "mono_ind", "u", "argmax", "m", "logp", "v",
+            "alpha_prev"]
+    keys += ["li", "lf", "lg", "lo", "mprev", "mnew"] if cfg.decoderLSTM else ["z", "r", "hh"]
+    cache = {key: [] for key in keys}
+    mem = np.zeros((B, S), dt)  # the LSTM decoder's carried cell (mem, Attention.lua:152)
     logp_all = np.zeros((B, T, O), dt)
-    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")} if not cfg.decoderLSTM else {}
     hyb = cfg.hybridAttendFeatureMaps > 0
     for t in range(T):
         yprev = np.zeros((B, O), dt)
@@ -394,11 +397,25 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
         yin = yprev @ P["Wy"].T + P["by"]
         cin = c @ P["Wc"].T + P["bc"]
         d = np.concatenate([cin, yin], 1) @ P["Wd"].T + P["bd"]
-        hx = np.concatenate([s, d], 1)
-        z = sigmoid(hx @ Wg["z"].T)
-        r = sigmoid(hx @ Wg["r"].T)
-        hh = np.tanh(np.concatenate([r * s, d], 1) @ Wg["h"].T)
-        s_new = (1.0 - z) * s + z * hh
+        if cfg.decoderLSTM:
+            # LSTM.lua:16-51 with x = d, prev_h = s, prev_c = mem: each gate Linear(x) + Linear(h), biases
+            pre = {q: d @ P[f"dec.W{q}x"].T + P[f"dec.b{q}x"] + s @ P[f"dec.W{q}h"].T + P[f"dec.b{q}h"]
+                   for q in "ifgo"}
+            li, lf, lo = sigmoid(pre["i"]), sigmoid(pre["f"]), sigmoid(pre["o"])
+            lg = np.tanh(pre["g"])
+            mnew = lf * mem + li * lg
+            s_new = lo * np.tanh(mnew)
+            for key, val in (("li", li), ("lf", lf), ("lg", lg), ("lo", lo), ("mprev", mem), ("mnew", mnew)):
+                cache[key].append(val)
+            mem = mnew
+        else:
+            hx = np.concatenate([s, d], 1)
+            z = sigmoid(hx @ Wg["z"].T)
+            r = sigmoid(hx @ Wg["r"].T)
+            hh = np.tanh(np.concatenate([r * s, d], 1) @ Wg["h"].T)
+            s_new = (1.0 - z) * s + z * hh
+            for key, val in (("z", z), ("r", r), ("hh", hh)):
+                cache[key].append(val)
         v = np.concatenate([s_new, c], 1)
         if dropout_mask is not None:
             v = v * dropout_mask[:, t]
@@ -410,7 +427,7 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
         logp = log_softmax(o, 1)
         logp_all[:, t] = logp
         for key, val in (("ws", ws), ("alpha", alpha), ("c", c), ("cin", cin), ("yin", yin), ("d", d),
-                         ("sprev", s), ("mono_ind", ind), ("z", z), ("r", r), ("hh", hh), ("u", u),
+                         ("sprev", s), ("mono_ind", ind), ("u", u),
                          ("argmax", am), ("m", m), ("logp", logp), ("v", v), ("alpha_prev", alpha_prev)):
             cache[key].append(val)
         s = s_new
@@ -420,6 +437,29 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
     cache["h"] = h
     cache["labels"] = labels
     return logp_all, cache
+
+
+def _gru_dec_bwd(P, G, Wg, g_, ds, sp, d, S, scale):
+    """decoder GRU backward (GRU.lua:16-38), x = d, h = s_prev: returns (dd, dL/ds_prev from the cell)."""
+    z, r, hh = g_("z"), g_("r"), g_("hh")
+    dz = ds * (hh - sp)
+    dah = ds * z * (1 - hh * hh)
+    dsp = ds * (1 - z)
+    rhx = np.concatenate([r * sp, d], 1)
+    G["dec.Wh"] += scale * (dah.T @ rhx)
+    drhx = dah @ Wg["h"]
+    dd = drhx[:, S:].copy()
+    dr = drhx[:, :S] * sp
+    dsp += drhx[:, :S] * r
+    daz = dz * z * (1 - z)
+    dar = dr * r * (1 - r)
+    hx = np.concatenate([sp, d], 1)
+    G["dec.Wz"] += scale * (daz.T @ hx)
+    G["dec.Wr"] += scale * (dar.T @ hx)
+    dhx = daz @ Wg["z"] + dar @ Wg["r"]
+    dsp += dhx[:, :S]
+    dd += dhx[:, S:]
+    return dd, dsp
 
 
 def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, G: Dict[str, Array],
@@ -436,9 +476,10 @@ def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, 
     dh = np.zeros_like(h)
     dVh = np.zeros_like(Vh)
     ds_carry = np.zeros((B, S), dt)
+    dmem_carry = np.zeros((B, S), dt)
     dalpha_carry = np.zeros((B, L), dt)
     jw = (L + 1 - np.arange(1, L + 1)).astype(dt)               # (L+1-j), j 1-based
-    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")}
+    Wg = {g: P[f"dec.W{g}"] for g in ("z", "r", "h")} if not cfg.decoderLSTM else {}
     hyb = cfg.hybridAttendFeatureMaps > 0
     kW = cfg.hybridAttendFilterSize
     for t in range(T - 1, -1, -1):
@@ -464,25 +505,26 @@ def attention_bwd(P: Dict[str, Array], cfg: "ModelConfig", cache, dlogp: Array, 
             dv = dv * dropout_mask[:, t]
         ds = dv[:, :S] + ds_carry
         dc = dv[:, S:].copy()
-        # decoder GRU backward (GRU.lua:16-38), x = d, h = s_prev
-        sp, d, z, r, hh = g_("sprev"), g_("d"), g_("z"), g_("r"), g_("hh")
-        dz = ds * (hh - sp)
-        dah = ds * z * (1 - hh * hh)
-        dsp = ds * (1 - z)
-        rhx = np.concatenate([r * sp, d], 1)
-        G["dec.Wh"] += scale * (dah.T @ rhx)
-        drhx = dah @ Wg["h"]
-        dd = drhx[:, S:].copy()
-        dr = drhx[:, :S] * sp
-        dsp += drhx[:, :S] * r
-        daz = dz * z * (1 - z)
-        dar = dr * r * (1 - r)
-        hx = np.concatenate([sp, d], 1)
-        G["dec.Wz"] += scale * (daz.T @ hx)
-        G["dec.Wr"] += scale * (dar.T @ hx)
-        dhx = daz @ Wg["z"] + dar @ Wg["r"]
-        dsp += dhx[:, :S]
-        dd += dhx[:, S:]
+        sp, d = g_("sprev"), g_("d")
+        if cfg.decoderLSTM:
+            # LSTM backward (LSTM.lua:118-136): ds = dL/dh_t, dmem_carry = dL/dc_t from step t+1
+            li, lf, lg, lo, mp, mn = (g_(key) for key in ("li", "lf", "lg", "lo", "mprev", "mnew"))
+            tc = np.tanh(mn)
+            dcell = dmem_carry + ds * lo * (1 - tc * tc)
+            dpre = {"i": dcell * lg * li * (1 - li), "f": dcell * mp * lf * (1 - lf),
+                    "g": dcell * li * (1 - lg * lg), "o": ds * tc * lo * (1 - lo)}
+            dmem_carry = dcell * lf
+            dd = np.zeros_like(d)
+            dsp = np.zeros_like(sp)
+            for q, da in dpre.items():
+                G[f"dec.W{q}x"] += scale * (da.T @ d)
+                G[f"dec.b{q}x"] += scale * da.sum(0)
+                G[f"dec.W{q}h"] += scale * (da.T @ sp)
+                G[f"dec.b{q}h"] += scale * da.sum(0)
+                dd += da @ P[f"dec.W{q}x"]
+                dsp += da @ P[f"dec.W{q}h"]
+        else:
+            dd, dsp = _gru_dec_bwd(P, G, Wg, g_, ds, sp, d, S, scale)
         # d = Wd [c_in; y_in] + bd
         cin, yin = g_("cin"), g_("yin")
         G["Wd"] += scale * (dd.T @ np.concatenate([cin, yin], 1))
@@ -560,6 +602,7 @@ class ModelConfig:
     numLayers: int = 3
     hybridAttendFilterSize: int = 0    # Attention(..., hybridAttendFilterSize, hybridAttendFeatureMaps, ...):
     hybridAttendFeatureMaps: int = 0   # 0 maps = content-only attention (model_chorowski_baseline.lua:39-40)
+    decoderLSTM: bool = False      # decoder_recurrent = nn.LSTM(S, S) (timit/timit.lua:137) instead of GRU(S, S)
 
     @property
     def annotationDepth(self) -> int:

@@ -26,15 +26,21 @@ struct AttnDims {
   // external decoder_mlp: the forward stops at the MLP input [s_t; c_t] (saved VV rows) and the
   // backward takes its gradient in place of dlogp; Wm / bm / Wo / bo are not used
   int ext = 0;
+  // decoder_recurrent = nn.LSTM(S, S) (no peepholes) instead of nn.GRU(S, S): the conv + BiLSTM
+  // model of timit/timit.lua:137 (per-step decoder kernels)
+  int lstm = 0;
 };
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
 struct AttnParams {
   const float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
   const float *hybW = nullptr, *hybb = nullptr, *hybU = nullptr;  // (nF, kW), (nF), (Sc, nF) when hf > 0
+  // decoder LSTM (lstm = 1): for q in (i, f, g, o): Wqx (S, S), bqx (S), Wqh (S, S), bqh (S) (LSTM.lua:25-29)
+  const float* lstm[16] = {};
 };
 struct AttnGrads {
   float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;
   float *hybW = nullptr, *hybb = nullptr, *hybU = nullptr;
+  float* lstm[16] = {};
 };
 
 int attn_check_dims(const AttnDims& d);

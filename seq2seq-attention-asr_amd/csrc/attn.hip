@@ -52,6 +52,10 @@ struct AttnK {
   // d alpha_{t-1} partials q_{l,i} of the step after; PDG [B*NCH][kW][Sc] dG partials; DGT, DCU (bwd)
   float *HGT, *HCU, *QA, *PDG, *DGT, *DCU;
   float *WhT, *GT, *WdT, *WcT, *WsT;
+  // decoder LSTM: LW (4S, 2S) rows [Wqh | Wqx] per gate q in (i, f, g, o), LB (4S) = bqx + bqh (saved),
+  // LC (B*T, S) cell states (saved), LDW (4S, 2S) weight-gradient staging (bwd scratch); GT holds LW^T
+  float *LW, *LB, *LC, *LDW;
+  int lstm;
   // persistent-kernel granule buffers ([2 slots][...]) and abort word; one zeroed region each
   granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gCY, *gD, *gQ;           // forward
   granule_t *gZ, *gR, *gH, *gDD, *gDCY, *gDC, *gPDWS, *gDWS;           // backward
@@ -109,7 +113,7 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   XPlan p;
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && (std::strcmp(m, "step") == 0 || std::strcmp(m, "persist") == 0)) return p;
-  if (d.hf > 0) return p;  // hybrid attention: per-step kernels only
+  if (d.hf > 0 || d.lstm) return p;  // hybrid attention / LSTM decoder: per-step kernels only
   int var = 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
   else if (d.S == 64 && d.A == 128 && d.Sc == 128) var = 2;
@@ -148,7 +152,8 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* HX = sv.take<float>(BT * 2 * S);
   float* RHX = sv.take<float>(BT * 2 * S);
   float* CY = sv.take<float>(BT * 2 * S);
-  float* GSV = sv.take<float>(BT * 3 * S);
+  const long NG = d.lstm ? 4 : 3;  // gate rows per step: GRU z, r, hh / LSTM i, f, g, o
+  float* GSV = sv.take<float>(BT * NG * S);
   float* VV = sv.take<float>(BT * (S + A));
   float* MM = sv.take<float>(BT * M);
   int* AM = sv.take<int>(BT * M);
@@ -161,6 +166,9 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* XZRT = sv.take<float>(2 * S * S);
   float* XWST = sv.take<float>(S * Sc);
   float* VBAR = sv.take<float>(B * Sc);  // mean Vh row per utterance (computed by the forward)
+  float* LW = d.lstm ? sv.take<float>(4 * S * 2 * S) : nullptr;
+  float* LB = d.lstm ? sv.take<float>(4 * S) : nullptr;
+  float* LCS = d.lstm ? sv.take<float>(BT * S) : nullptr;
   const long HK = d.hf > 0 ? d.hk : 0;
   float* HGT = HK ? sv.take<float>(HK * Sc) : nullptr;
   float* HCU = HK ? sv.take<float>(Sc) : nullptr;
@@ -178,7 +186,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* DO = g.take<float>(BT * O);
   float* DU = g.take<float>(BT * Mk);
   float* DV = g.take<float>(BT * (S + A));
-  float* DGA = g.take<float>(BT * 3 * S);
+  float* DGA = g.take<float>(BT * NG * S);
   float* DS = g.take<float>(B * S);
   float* DSP = g.take<float>(B * S);
   float* DSPF = g.take<float>(B * S);
@@ -191,7 +199,8 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* DWEACC = g.take<float>(B * NCH * Sc);
   float* YP = g.take<float>(BT * O);
   float* WhT = g.take<float>(S * S);
-  float* GT = g.take<float>(2 * S * 3 * S);
+  float* GT = g.take<float>(2 * S * NG * S);
+  float* LDW = d.lstm ? g.take<float>(4 * S * 2 * S) : nullptr;
   float* WdT = g.take<float>(2 * S * S);
   float* WcT = g.take<float>(A * S);
   float* WsT = g.take<float>(S * Sc);
@@ -255,6 +264,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
     k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
     k->hk = (int)HK; k->hf = d.hf;
+    k->lstm = d.lstm; k->LW = LW; k->LB = LB; k->LC = LCS; k->LDW = LDW;
     k->HGT = HGT; k->HCU = HCU; k->QA = QA; k->PDG = PDG; k->DGT = DGT; k->DCU = DCU;
     k->MASK = MASK;
     k->Vh = Vh; k->WS = WS; k->E = E; k->ALPHA = ALPHA; k->LSE = LSE; k->IND = IND; k->C = C; k->HX = HX;
@@ -556,6 +566,48 @@ __global__ __launch_bounds__(256) void dec_f7_gru2(AttnK k) {
   if (t + 1 < k.T) k.HX[(row + 1) * 2 * S + n] = snew;
 }
 
+// ---- decoder LSTM (LSTM.lua:16-58 as decoder_recurrent, timit/timit.lua:137): s = h, mem = c
+// LW rows (q*S + n) = [Wqh[n] | Wqx[n]] against HX rows [s_{t-1} | d]; LB = bqx + bqh
+__global__ void dec_lstm_pack(AttnK k) {
+  const int S = k.S;
+  const long n = 4L * S * 2 * S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / (2 * S)), c = (int)(i - (long)r * 2 * S), q = r / S, u = r - q * S;
+    k.LW[i] = c < S ? k.P.lstm[4 * q + 2][(long)u * S + c] : k.P.lstm[4 * q][(long)u * S + c - S];
+    if (c == 0) k.LB[r] = k.P.lstm[4 * q + 1][u] + k.P.lstm[4 * q + 3][u];
+  }
+}
+
+// F6 (LSTM): gate q of unit u = act(LW[q*S+u] . [s_{t-1}; d] + LB)  (N = 4S, K = 2S); act = sigmoid, g: tanh
+__global__ __launch_bounds__(256) void dec_f6_lstm(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.HX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
+                            k.LW + (long)(n0 + (lane & 15)) * 2 * S, 2 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float x = s + k.LB[n];
+  k.GSV[row * 4 * S + n] = (n >= 2 * S && n < 3 * S) ? tanhf(x) : sigmoidf_(x);
+}
+
+// F7 (LSTM): c = f c_{t-1} + i g, s = o tanh(c)
+__global__ void dec_f7_lstm(AttnK k) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x, S = k.S, t = k.t;
+  if (i >= k.B * S) return;
+  const int b = i / S, n = i - b * S;
+  const long row = (long)b * k.T + t;
+  const float* g = k.GSV + row * 4 * S;
+  const float cp = t > 0 ? k.LC[(row - 1) * S + n] : 0.f;
+  const float c = g[S + n] * cp + g[n] * g[2 * S + n];
+  const float snew = g[3 * S + n] * tanhf(c);
+  k.LC[row * S + n] = c;
+  k.VV[row * (S + k.A) + n] = snew;
+  if (t + 1 < k.T) k.HX[(row + 1) * 2 * S + n] = snew;
+}
+
 __global__ void dec_init_fwd(AttnK k) {
   // s_0 = 0 (Recurrent.lua:112 zeros_hidden)
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -647,11 +699,44 @@ __device__ __forceinline__ void dec_gate_grads(const AttnK& k, int b, int t, int
   k.DGA[row * 3 * S + 2 * S + n] = (ds * z) * (1.0f - hh * hh);
 }
 
+// LSTM gate grads of step t from ds = dL/ds_t and the cell carry dcar = dL/dc_t from step t+1
+// (LSTM.lua:118-136 under RNNAttention's BPTT); leaves dL/dc_{t-1} in DSP
+__device__ __forceinline__ void dec_lstm_gate_grads(const AttnK& k, int b, int t, int n, float ds, float dcar) {
+  const int S = k.S;
+  const long row = (long)b * k.T + t;
+  const float* g = k.GSV + row * 4 * S;
+  const float gi = g[n], gf = g[S + n], gg = g[2 * S + n], go = g[3 * S + n];
+  const float c = k.LC[row * S + n], cp = t > 0 ? k.LC[(row - 1) * S + n] : 0.f;
+  const float tc = tanhf(c);
+  const float dc = dcar + ds * go * (1.0f - tc * tc);
+  float* dga = k.DGA + row * 4 * S;
+  dga[n] = dc * gg * (gi * (1.0f - gi));
+  dga[S + n] = dc * cp * (gf * (1.0f - gf));
+  dga[2 * S + n] = dc * gi * (1.0f - gg * gg);
+  dga[3 * S + n] = ds * tc * (go * (1.0f - go));
+  k.DSP[b * S + n] = dc * gf;
+}
+
 __global__ void dec_bwd_init(AttnK k) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= k.B * k.S) return;
   const int b = i / k.S, n = i - b * k.S, t = k.T - 1;
-  dec_gate_grads(k, b, t, n, k.DV[((long)b * k.T + t) * (k.S + k.A) + n]);
+  if (k.lstm) dec_lstm_gate_grads(k, b, t, n, k.DV[((long)b * k.T + t) * (k.S + k.A) + n], 0.f);
+  else dec_gate_grads(k, b, t, n, k.DV[((long)b * k.T + t) * (k.S + k.A) + n]);
+}
+
+// K3 (LSTM): [ds_prev | dd] = LW^T dGA  (N = 2S, K = 4S; GT = LW^T)
+__global__ __launch_bounds__(256) void dec_b3_lstm(AttnK k) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DGA + ((long)brow(b0, lane, k.B) * k.T + t) * 4 * S,
+                            k.GT + (long)(n0 + (lane & 15)) * 4 * S, 4 * S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  if (n < S) k.DSPF[b * S + n] = s;
+  else k.DD[((long)b * k.T + t) * S + n - S] = s;
 }
 
 // K2: dq = Wh[:, :S]^T da_h (N = S, K = S) -> da_r, DSP = ds(1-z) + dq r
@@ -883,7 +968,9 @@ __global__ __launch_bounds__(256) void dec_b8_ws(AttnK k) {
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B || t == 0) return;
   const float carry = k.DSPF[b * S + n] + s;
-  dec_gate_grads(k, b, t - 1, n, k.DV[((long)b * k.T + t - 1) * (S + k.A) + n] + carry);
+  if (k.lstm) dec_lstm_gate_grads(k, b, t - 1, n, k.DV[((long)b * k.T + t - 1) * (S + k.A) + n] + carry,
+                                  k.DSP[b * S + n]);
+  else dec_gate_grads(k, b, t - 1, n, k.DV[((long)b * k.T + t - 1) * (S + k.A) + n] + carry);
 }
 
 __global__ void dec_onehot_prev(AttnK k) {
@@ -1011,7 +1098,7 @@ static unsigned long long* g_dec_stamps[2] = {nullptr, nullptr};
 static int dec_persist_variant(const AttnDims& d) {
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && std::strcmp(m, "step") == 0) return 0;
-  if (d.hf > 0) return 0;
+  if (d.hf > 0 || d.lstm) return 0;
   if ((d.L + LC - 1) / LC > 256) return 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) return 1;
   if (d.S == 64 && d.A == 128 && d.Sc == 128) return 2;
@@ -1193,6 +1280,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   } else {
   ProfScope ps(st, "dec_fwd_steps", 0.0, 0.0);
   if (d.hf > 0) hipLaunchKernelGGL(dec_hyb_fold, dim3((d.Sc + 255) / 256), dim3(256), 0, st, k);
+  if (d.lstm) hipLaunchKernelGGL(dec_lstm_pack, dim3(256), dim3(256), 0, st, k);
   for (int t = 0; t < T; ++t) {
     k.t = t;
     hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
@@ -1200,8 +1288,13 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_f3_combine, dim3(B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
+    if (d.lstm) {
+      hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_f7_lstm, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+    } else {
+      hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
+    }
   }
   S2S_CHECK_HIP(hipGetLastError());
   }
@@ -1244,13 +1337,16 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
   }
   // packed transposes for the backward products
+  if (d.lstm) S2S_TRY(transpose_f32(st, k.LW, 2L * S, 4 * S, 2 * S, k.GT, 4L * S));  // GT = LW^T
   if (!xp.var) {  // (the XCD-local path's operand layouts come from its prologue)
+  if (!d.lstm) {
   S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
   S2S_TRY(transpose_f32(st, P.Wz, 2L * S, S, 2 * S, k.GT, 3L * S));   // GT[c][n]      = Wz[n][c]
   S2S_TRY(transpose_f32(st, P.Wr, 2L * S, S, 2 * S, k.GT + S, 3L * S));
   S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, 2 * S, k.GT + 2 * S, 3L * S));
   // the h-half of Wh reaches ds_{t-1} through dq = Wh[:, :S]^T da_h (K2), not through GT
   hipLaunchKernelGGL(fill2d_kernel, dim3(64), dim3(256), 0, st, k.GT + 2 * S, 3L * S, S, S, 0.f);
+  }
   S2S_TRY(transpose_f32(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
   S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
   S2S_TRY(transpose_f32(st, P.Ws, S, Sc, S, k.WsT, Sc));
@@ -1324,8 +1420,12 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   ProfScope ps(st, "dec_bwd_steps", 0.0, 0.0);
   for (int t = T - 1; t >= 0; --t) {
     k.t = t;
-    hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    if (d.lstm) {
+      hipLaunchKernelGGL(dec_b3_lstm, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    } else {
+      hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+    }
     hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
     if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), 0, st, k);
@@ -1370,9 +1470,14 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
       pr[n++] = GemmProblem{k.DO, k.MM, G.Wo, nullptr, O, d.M, d.M, O, d.M, rows, scale, 1.f};
       pr[n++] = GemmProblem{k.DU, k.VV, G.Wm, nullptr, Mk, S + A, S + A, Mk, S + A, rows, scale, 1.f};
     }
-    pr[n++] = GemmProblem{k.DGA, k.HX, G.Wz, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
-    pr[n++] = GemmProblem{k.DGA + S, k.HX, G.Wr, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
-    pr[n++] = GemmProblem{k.DGA + 2 * S, k.RHX, G.Wh, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+    if (d.lstm) {  // all four gates' [Wqh | Wqx] grads at once, staged in LDW (scattered below)
+      pr[n++] = GemmProblem{k.DGA, k.HX, k.LDW, nullptr, 4L * S, 2L * S, 2L * S, 4 * S, 2 * S, rows, scale, 0.f};
+    } else {
+      pr[n++] = GemmProblem{k.DGA, k.HX, G.Wz, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+      pr[n++] = GemmProblem{k.DGA + S, k.HX, G.Wr, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
+      pr[n++] = GemmProblem{k.DGA + 2 * S, k.RHX, G.Wh, nullptr, 3L * S, 2L * S, 2L * S, S, 2 * S, rows, scale,
+                            1.f};
+    }
     pr[n++] = GemmProblem{k.DD, k.CY, G.Wd, nullptr, S, 2L * S, 2L * S, S, 2 * S, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DCY, k.C, G.Wc, nullptr, 2L * S, A, A, S, A, rows, scale, 1.f};
     pr[n++] = GemmProblem{k.DCY + S, k.YP, G.Wy, nullptr, 2L * S, O, O, S, O, rows, scale, 1.f};
@@ -1385,6 +1490,13 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
     S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));
   }
   S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd));
+  if (d.lstm)
+    for (int q = 0; q < 4; ++q) {  // LSTM.lua:25-29: Linear(S,S)(x) + Linear(S,S)(h), both with bias
+      S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S + S, 2L * S, G.lstm[4 * q], S, S, S, true));      // Wqx
+      S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S, 2L * S, G.lstm[4 * q + 2], S, S, S, true));      // Wqh
+      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 1]));               // bqx
+      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 3]));               // bqh
+    }
   S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc));
   S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));
   S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs));

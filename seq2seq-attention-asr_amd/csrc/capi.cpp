@@ -113,10 +113,20 @@ AttnDims to_attn(const s2s_attn_dims* d) {
   a.hk = d->hybridAttendFilterSize;
   a.hf = d->hybridAttendFeatureMaps;
   a.ext = d->external_mlp ? 1 : 0;
+  a.lstm = d->decoder_lstm ? 1 : 0;
   return a;
 }
 int attn_nparams(const s2s_attn_dims* d) {
+  if (d->decoder_lstm) return S2S_ATTN_NPARAMS_LSTM;
   return d->hybridAttendFeatureMaps > 0 ? S2S_ATTN_NPARAMS_HYBRID : S2S_ATTN_NPARAMS;
+}
+// parameter slots a call may leave NULL: the fused MLP's with an external decoder_mlp, the GRU's with a
+// decoder LSTM, the hybrid ones without hybrid features
+bool attn_param_optional(const s2s_attn_dims* d, int i) {
+  if (d->external_mlp && i >= 13 && i <= 16) return true;
+  if (d->decoder_lstm && i >= 10 && i <= 12) return true;
+  if (d->hybridAttendFeatureMaps <= 0 && i >= 17 && i <= 19) return true;
+  return false;
 }
 
 // ------------------------------------------------------------ model layout
@@ -609,7 +619,7 @@ int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
   const float** pp = reinterpret_cast<const float**>(&ap);
   for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
-    S2S_REQUIRE(pp[i] != nullptr || (d->external_mlp && i >= 13 && i <= 16), "attn: null parameter");
+    S2S_REQUIRE(pp[i] != nullptr || attn_param_optional(d, i), "attn: null parameter");
   }
   return attn_fwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, logp, saved, scratch, scratch_bytes);
 }
@@ -626,8 +636,7 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
   for (int i = 0; i < attn_nparams(d); ++i) {
     pp[i] = params[i];
     gp[i] = grads[i];
-    S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || (d->external_mlp && i >= 13 && i <= 16),
-                "attn: null parameter/grad");
+    S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || attn_param_optional(d, i), "attn: null parameter/grad");
   }
   return attn_bwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, saved, dlogp, dh, dh_accumulate, ag,
                   scale, scratch, scratch_bytes);
@@ -643,7 +652,8 @@ int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims*
                          float* out_score, void* workspace, size_t workspace_bytes) {
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(d && h && params && out && out_len && workspace, "beam search: null argument");
-  S2S_REQUIRE(!d->external_mlp, "beam search: runs the fused Maxout -> Linear -> LogSoftMax decoder_mlp only");
+  S2S_REQUIRE(!d->external_mlp && !d->decoder_lstm,
+              "beam search: runs the GRU decoder with the fused Maxout -> Linear -> LogSoftMax decoder_mlp only");
   AttnParams ap;
   const float** pp = reinterpret_cast<const float**>(&ap);
   for (int i = 0; i < attn_nparams(d); ++i) {

@@ -21,7 +21,7 @@ int s2s_gru_bwd(s2s_ctx*, void* stream, int ndir, int B, int L, int D, int H, co
                 float* const* dW, float scale, void* scratch, size_t scratch_bytes);
 typedef struct { int B, L, T; int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow;
                  float penalty; float dropout; unsigned long long dropout_seed; const float* dropout_mask;
-                 int hybridAttendFilterSize, hybridAttendFeatureMaps; int external_mlp; } s2s_attn_dims;
+                 int hybridAttendFilterSize, hybridAttendFeatureMaps; int external_mlp; int decoder_lstm; } s2s_attn_dims;
 const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved);
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);

@@ -10,4 +10,4 @@ from .nn import (GRU, LSTM, RNN, BiRNN, Attention, MaxoutMLP, nll_seed, Context,
 from .model import ModelConfig, ChorowskiBaseline, param_shapes  # noqa: F401
 from . import optim  # noqa: F401
 from . import frontend, data, checkpoint  # noqa: F401
-from .frontend import ConvBiLSTMEncoder, VGGEncoder, VGGAttentionModel  # noqa: F401
+from .frontend import ConvBiLSTMEncoder, VGGEncoder, VGGAttentionModel, ConvBiLSTMAttentionModel  # noqa: F401

@@ -20,7 +20,7 @@ class s2s_attn_dims(ctypes.Structure):
                 ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
                 ("penalty", c_float), ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong),
                 ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int),
-                ("external_mlp", c_int)]
+                ("external_mlp", c_int), ("decoder_lstm", c_int)]
 
 
 class s2s_optim_config(ctypes.Structure):
@@ -125,6 +125,7 @@ S2S_NORMALIZE_NLL = 2
 S2S_BUCKET_EVENTS = 4
 S2S_ATTN_NPARAMS = 17
 S2S_ATTN_NPARAMS_HYBRID = 20
+S2S_ATTN_NPARAMS_LSTM = 36
 S2S_UNIQUE_ID_BYTES = 128
 
 

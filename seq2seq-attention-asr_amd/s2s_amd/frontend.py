@@ -443,3 +443,42 @@ class VGGAttentionModel(Module):
         dh = self.decoder.backward([h, lab], dlogp, scale)[0]
         self.encoder.backward(x, dh, scale)
         return nll, logp
+
+
+class ConvBiLSTMAttentionModel(Module):
+    """The conv + BiLSTM model timit/timit.lua builds when no model file is given (:106-145), end to end:
+    ConvBiLSTMEncoder (3 x conv(k=3, 256) + ReLU + TemporalMaxPooling(2, 2), BiLSTM 2 x 128) ->
+    nn.Attention(decoder_recurrent = LSTM(400, 400), decoder_mlp = Linear(400 + 256, 2*O) -> ReLU ->
+    Linear(2*O, O) -> LogSoftMax, scoreDepth 150, hybrid attention kW = 5 / 16 maps, monoAlignPenalty
+    true, opt.penalty), with the trainer's loss seed (timit/timit.lua:262-295)."""
+
+    def __init__(self, inputFrameSize=123, numPhonemes=62, hiddenFrameSize=256, outputFrameSize=128,
+                 stateDepth=400, scoreDepth=150, hybridAttendFilterSize=5, hybridAttendFeatureMaps=16, penalty=0.0,
+                 generator=None):
+        from .nn import Attention
+        super().__init__()
+        g = generator
+        S, A, O = stateDepth, 2 * outputFrameSize, numPhonemes
+        self.encoder = ConvBiLSTMEncoder(inputFrameSize, hiddenFrameSize, outputFrameSize, 3, generator=g)
+        mlp = Sequential(Linear(S + A, 2 * O, generator=g), ReLU(), Linear(2 * O, O, generator=g), LogSoftMax())
+        self.decoder = Attention(LSTM(S, S, False, g), mlp, scoreDepth, hybridAttendFilterSize,
+                                 hybridAttendFeatureMaps, S, A, O, True, penalty, generator=g)
+
+    def parameters(self):
+        w1, g1 = self.encoder.parameters()
+        w2, g2 = self.decoder.parameters()
+        return w1 + w2, g1 + g2
+
+    def step(self, x, labels, scale=None, normalizeNLL=False):
+        """One training step on x (B, L, D), labels (B, T) 0-based; gradients accumulate at scale
+        (default 1/B).  Returns (nll (B,), logp (B, T, O))."""
+        from .nn import nll_seed
+        B = x.shape[0]
+        scale = (1.0 / B if B > 1 else 1.0) if scale is None else scale
+        h = self.encoder.forward(x)
+        lab = labels.to(torch.int32).contiguous()
+        logp = self.decoder.forward([h, lab])
+        nll, dlogp = nll_seed(logp, lab, normalizeNLL)
+        dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+        self.encoder.backward(x, dh, scale)
+        return nll, logp

@@ -310,8 +310,15 @@ class Attention(Module):
         nF = int(hybridAttendFeatureMaps or 0)
         if nF > 0 and not 1 <= int(hybridAttendFilterSize or 0) <= 8:
             raise S2SArgumentError("hybridAttendFilterSize must be in [1, 8] with hybrid attention")
-        if not isinstance(decoder_recurrent, GRU) or decoder_recurrent.dimoutput != stateDepth:
-            raise S2SArgumentError("decoder_recurrent must be GRU(stateDepth, stateDepth)")
+        # decoder_recurrent: GRU(S, S) (the Chorowski models) or LSTM(S, S) without peepholes (the conv +
+        # BiLSTM model, timit/timit.lua:137; per-step decoder kernels)
+        self.decoder_lstm = isinstance(decoder_recurrent, LSTM)
+        if self.decoder_lstm:
+            if decoder_recurrent.peepholes or decoder_recurrent.diminput != stateDepth or \
+                    decoder_recurrent.dimoutput != stateDepth:
+                raise S2SArgumentError("decoder_recurrent LSTM must be LSTM(stateDepth, stateDepth) without peepholes")
+        elif not isinstance(decoder_recurrent, GRU) or decoder_recurrent.dimoutput != stateDepth:
+            raise S2SArgumentError("decoder_recurrent must be GRU(stateDepth, stateDepth) or LSTM(stateDepth, stateDepth)")
         # MaxoutMLP (Maxout -> Linear -> LogSoftMax, model_chorowski_baseline.lua:53-59) runs fused in the
         # decoder launches; any other decoder_mlp module (e.g. the two-Maxout MLP of librispeech/
         # model_vgg.lua:71-77, built from s2s_amd.frontend) runs outside on the saved [s_t; c_t] rows
@@ -341,10 +348,50 @@ class Attention(Module):
                         "hybU": _uniform((Sc, nF), 1 / math.sqrt(nF), g)})
         self.own = own
         self.own_grad = {k: torch.zeros_like(v) for k, v in own.items()}
+        # scoreDepth not a multiple of 16 (the conv model's 150, timit/timit.lua:128): the kernels run on
+        # score channels zero-padded to the next multiple of 16 -- padded rows of V / Ws / hybU, bs and
+        # columns of we are zero, so each padded channel adds we_j tanh(0) = 0 to every score (exact)
+        self._scp = (scoreDepth + 15) // 16 * 16
+        self._pad = None
 
-    def _tensors(self, grads=False):
+    _PADDED = {"V": 0, "Ws": 0, "bs": 0, "we": 1, "hybU": 0}  # parameter -> score-channel axis
+
+    def _sync_pad(self, grads_zero=False):
+        """Refresh the zero-padded score-channel copies the kernels read (scoreDepth % 16 != 0)."""
+        if self._scp == self.scoreDepth:
+            return
+        Sc = self.scoreDepth
+        if self._pad is None or self._pad[0]["V"].device != self.own["V"].device:
+            mk = {}
+            for n, ax in self._PADDED.items():
+                if n in self.own:
+                    shp = list(self.own[n].shape)
+                    shp[ax] = self._scp
+                    mk[n] = torch.zeros(shp, dtype=torch.float32, device=self.own[n].device)
+            self._pad = (mk, {n: torch.zeros_like(t) for n, t in mk.items()})
+        with torch.no_grad():
+            for n, t in self._pad[0].items():
+                t.narrow(self._PADDED[n], 0, Sc).copy_(self.own[n])
+            if grads_zero:
+                for t in self._pad[1].values():
+                    t.zero_()
+
+    def _unpad_grads(self):
+        if self._scp == self.scoreDepth:
+            return
+        with torch.no_grad():
+            for n, t in self._pad[1].items():
+                self.own_grad[n].add_(t.narrow(self._PADDED[n], 0, self.scoreDepth))
+
+    def _tensors(self, grads=False, kernel=False):
         o = self.own_grad if grads else self.own
+        if kernel and self._scp != self.scoreDepth:
+            o = dict(o)
+            o.update(self._pad[1] if grads else self._pad[0])
         r = self.decoder_recurrent.gradWeight if grads else self.decoder_recurrent.weight
+        lstm_w = None
+        if self.decoder_lstm:  # params 10-12 unused; the LSTM's 16 at 20-35 (S2S_ATTN_NPARAMS_LSTM)
+            lstm_w, r = list(r), [None] * 3
         if self.external_mlp:
             m = [None] * 4  # params 13-16 unused with an external decoder_mlp
         else:
@@ -353,6 +400,10 @@ class Attention(Module):
                r[0], r[1], r[2], m[0], m[1], m[2], m[3]]
         if "hybW" in o:
             out += [o["hybW"], o["hybb"], o["hybU"]]
+        elif lstm_w is not None:
+            out += [None] * 3
+        if lstm_w is not None:
+            out += lstm_w
         return out
 
     def parameters(self):
@@ -363,7 +414,7 @@ class Attention(Module):
         return ws, gs
 
     def _ptrs(self, grads=False):
-        return ptr_array([t.data_ptr() if t is not None else 0 for t in self._tensors(grads)])
+        return ptr_array([t.data_ptr() if t is not None else 0 for t in self._tensors(grads, kernel=True)])
 
     # dropout: injected (B, T, S+A) multipliers for the next forward (parity with an external RNG),
     # else drawn in-kernel from dropout_seed + the forward count
@@ -374,16 +425,18 @@ class Attention(Module):
         B, L = (1, h.shape[0]) if h.dim() == 2 else (h.shape[0], h.shape[1])
         m = self.decoder_mlp
         if self.external_mlp:
-            d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
+            d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self._scp, self.stateDepth, self.outputDepth,
                                    1, 1, self.penalty, 0.0)
             d.external_mlp = 1
+            d.decoder_lstm = int(self.decoder_lstm)
             if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
                 d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
                 d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
             return d
         p = m.dropout if (m.dropout > 0 and self.train) else 0.0
-        d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self.scoreDepth, self.stateDepth, self.outputDepth,
+        d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self._scp, self.stateDepth, self.outputDepth,
                                m.mlpDepth, m.window, self.penalty, p)
+        d.decoder_lstm = int(self.decoder_lstm)
         if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
             d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
             d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
@@ -427,6 +480,7 @@ class Attention(Module):
         d = self._dims(h, T)
         dev = h.device
         self._d = d
+        self._sync_pad()
         self._labels = lab
         self._saved = _bytes(lib.s2s_attn_saved_bytes(ctypes.byref(d)), dev)
         scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
@@ -459,9 +513,11 @@ class Attention(Module):
         if self.external_mlp:  # d[s_t; c_t] from the decoder_mlp backward replaces dlogp
             go = self.decoder_mlp.backward(self._mlp_in, go.reshape(d.B * d.T, -1), scale)
             go = go.reshape(d.B, d.T, -1).contiguous()
+        self._sync_pad(grads_zero=True)
         check(lib.s2s_attn_bwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h),
                                dptr(self._labels), self._ptrs(False), dptr(self._saved), dptr(go), dptr(dh), 0,
                                self._ptrs(True), float(scale), dptr(scr), scr.numel()))
+        self._unpad_grads()
         self.gradInput = [dh if h.dim() == 3 else dh[0], None]
         return self.gradInput
 
@@ -488,6 +544,7 @@ class Attention(Module):
         dev = h.device
         if self.external_mlp:
             raise S2SArgumentError("BeamSearch runs the fused MaxoutMLP decoder_mlp only")
+        self._sync_pad()
         ws = _bytes(lib.s2s_attn_beam_workspace_bytes(ctypes.byref(d), K, maxlen), dev)
         out = torch.empty((B, maxlen + 1), dtype=torch.int32, device=dev)
         olen = torch.empty(B, dtype=torch.int32, device=dev)

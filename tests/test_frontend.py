@@ -494,3 +494,215 @@ def test_vgg_attention_model_step_matches_oracle(fe):
         lin = m.linear if isinstance(m, fe.Maxout) else m
         pairs += [(f"dmlp{i}.W", lin.gradWeight, g[0]), (f"dmlp{i}.b", lin.gradBias, g[1])]
     _assert_grads(pairs)
+
+
+# --------------------------------------------------------------------------- LSTM decoder (conv + BiLSTM model)
+
+def _lstm_dec_case(rng, S, A, Sc, O, hybrid, mlp_kind):
+    """Decoder parameters of the timit/timit.lua:126-145 model family: LSTM(S, S) decoder_recurrent,
+    hybrid location-aware attention, and either the fused Maxout MLP or an external ReLU MLP."""
+    from oracle import s2s_oracle as orc
+    kW, nF = hybrid
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=4, maxoutWindow=3, numLayers=1, hybridAttendFilterSize=kW,
+                          hybridAttendFeatureMaps=nF, decoderLSTM=True)
+    P = {"V": rng.standard_normal((Sc, A)) * 0.2, "Ws": rng.standard_normal((Sc, S)) * 0.2,
+         "bs": rng.standard_normal(Sc) * 0.1, "we": rng.standard_normal((1, Sc)) * 0.3,
+         "Wy": rng.standard_normal((S, O)) * 0.3, "by": rng.standard_normal(S) * 0.1,
+         "Wc": rng.standard_normal((S, A)) * 0.2, "bc": rng.standard_normal(S) * 0.1,
+         "Wd": rng.standard_normal((S, 2 * S)) * 0.2, "bd": rng.standard_normal(S) * 0.1,
+         "Wm": rng.standard_normal((4 * 3, S + A)) * 0.2, "bm": rng.standard_normal(12) * 0.1,
+         "Wo": rng.standard_normal((O, 4)) * 0.3, "bo": rng.standard_normal(O) * 0.1}
+    if nF:
+        P.update({"hybW": rng.standard_normal((nF, kW)) * 0.3, "hybb": rng.standard_normal(nF) * 0.1,
+                  "hybU": rng.standard_normal((Sc, nF)) * 0.3})
+    for q in "ifgo":
+        P[f"dec.W{q}x"] = rng.standard_normal((S, S)) * 0.2
+        P[f"dec.b{q}x"] = rng.standard_normal(S) * 0.1
+        P[f"dec.W{q}h"] = rng.standard_normal((S, S)) * 0.2
+        P[f"dec.b{q}h"] = rng.standard_normal(S) * 0.1
+    return cfg, P
+
+
+def test_oracle_lstm_decoder_finite_differences():
+    from oracle import s2s_oracle as orc
+    rng = np.random.default_rng(31)
+    cfg, P = _lstm_dec_case(rng, 6, 8, 5, 7, (5, 3), "maxout")
+    B, L, T = 2, 9, 4
+    h = rng.standard_normal((B, L, 8))
+    labels = rng.integers(0, 7, (B, T))
+    logp, cache = orc.attention_fwd(h, labels, P, cfg)
+    dl = rng.standard_normal(logp.shape)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    dh = orc.attention_bwd(P, cfg, cache, dl, G)
+    eps = 1e-6
+    for key in ("dec.Wix", "dec.bfh", "dec.Wgx", "dec.Woh", "Wd", "hybW", "Ws"):
+        for _ in range(2):
+            i = tuple(rng.integers(0, n) for n in P[key].shape)
+            old = P[key][i]
+            P[key][i] = old + eps
+            fp = (orc.attention_fwd(h, labels, P, cfg)[0] * dl).sum()
+            P[key][i] = old - eps
+            fm = (orc.attention_fwd(h, labels, P, cfg)[0] * dl).sum()
+            P[key][i] = old
+            assert abs((fp - fm) / (2 * eps) - G[key][i]) <= 1e-6 * max(1.0, abs(G[key][i])), key
+    i = (1, 3, 2)
+    old = h[i]
+    h[i] = old + eps
+    fp = (orc.attention_fwd(h, labels, P, cfg)[0] * dl).sum()
+    h[i] = old - eps
+    fm = (orc.attention_fwd(h, labels, P, cfg)[0] * dl).sum()
+    h[i] = old
+    assert abs((fp - fm) / (2 * eps) - dh[i]) <= 1e-6
+
+
+def _load_lstm_attention(s2s, fe, P, cfg, mlp):
+    S, A, Sc, O = cfg.stateDepth, cfg.annotationDepth, cfg.scoreDepth, cfg.outputDepth
+    cell = s2s.LSTM(S, S, peepholes=False)
+    att = s2s.Attention(cell, mlp, Sc, cfg.hybridAttendFilterSize, cfg.hybridAttendFeatureMaps, S, A, O, True,
+                        cfg.penalty)
+    with torch.no_grad():
+        for n in ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd") + (("hybW", "hybb", "hybU")
+                                                                                if cfg.hybridAttendFeatureMaps else ()):
+            att.own[n].copy_(torch.tensor(P[n]))
+        for n, t in cell.named().items():
+            t.copy_(torch.tensor(P["dec." + n]))
+        if isinstance(mlp, s2s.MaxoutMLP):
+            for t, n in zip(mlp.weight, ("Wm", "bm", "Wo", "bo")):
+                t.copy_(torch.tensor(P[n]))
+    return att.cuda(), cell
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,T,S,A,Sc,O,hyb", [(4, 30, 6, 32, 64, 48, 11, (5, 16)), (3, 20, 5, 64, 32, 16, 62, (0, 0))])
+def test_lstm_decoder_matches_oracle(fe, B, L, T, S, A, Sc, O, hyb):
+    """decoder_recurrent = LSTM(S, S) (timit/timit.lua:137) with the fused Maxout MLP, hybrid attention on/off."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    rng = np.random.default_rng(B * 100 + L)
+    cfg, P = _lstm_dec_case(rng, S, A, Sc, O, hyb, "maxout")
+    att, cell = _load_lstm_attention(s2s_amd, fe, P, cfg, s2s_amd.MaxoutMLP(S + A, 4, 3, O))
+    h = rng.standard_normal((B, L, A)) * 0.5
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    logp = att.forward([cu(h), cu(labels, torch.int32)])
+    lref, cache = orc.attention_fwd(h, labels, P, cfg)
+    assert_rel(_np(logp), lref, "logp")
+    dl = rng.standard_normal(lref.shape)
+    att.zeroGradParameters()
+    dh = att.backward([cu(h), None], cu(dl), 0.5)[0]
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    dhr = orc.attention_bwd(P, cfg, cache, dl, G, 0.5)
+    torch.cuda.synchronize()
+    pairs = [("dh", dh, dhr)]
+    for n in ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd") + (("hybW", "hybb", "hybU") if hyb[1] else ()):
+        pairs.append(("d" + n, att.own_grad[n], G[n]))
+    for n, g in cell.named(grads=True).items():
+        pairs.append(("d" + n, g, G["dec." + n]))
+    for t, n in zip(att.decoder_mlp.gradWeight, ("Wm", "bm", "Wo", "bo")):
+        pairs.append(("d" + n, t, G[n]))
+    _assert_grads(pairs)
+
+
+@pytest.mark.gpu
+def test_conv_bilstm_model_decoder_external_relu_mlp(fe):
+    """The timit/timit.lua:126-145 decoder as built there: LSTM(S, S) recurrence, hybrid attention (kW = 5,
+    nF = 16), decoder_mlp = Linear(S+A, 2*O) -> ReLU -> Linear(2*O, O) -> LogSoftMax (external_mlp)."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    rng = np.random.default_rng(41)
+    B, L, T, S, A, Sc, O = 3, 14, 6, 32, 64, 48, 11
+    cfg, P = _lstm_dec_case(rng, S, A, Sc, O, (5, 16), "relu")
+    mlp = fe.Sequential(fe.Linear(S + A, 2 * O), fe.ReLU(), fe.Linear(2 * O, O), fe.LogSoftMax())
+    att, cell = _load_lstm_attention(s2s_amd, fe, P, cfg, mlp)
+    lins = [m for m in mlp.modules if isinstance(m, fe.Linear)]
+    layers = [("linear", _np(lins[0].weight), _np(lins[0].bias)), ("relu",),
+              ("linear", _np(lins[1].weight), _np(lins[1].bias)), ("logsoftmax",)]
+    h = rng.standard_normal((B, L, A)) * 0.5
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    logp = att.forward([cu(h), cu(labels, torch.int32)])
+    _, cache = orc.attention_fwd(h, labels, P, cfg)
+    lref, mc = fo.mlp_fwd(cache["v"].reshape(B * T, -1), layers)
+    assert_rel(_np(logp), lref.reshape(B, T, O), "logp")
+    dl = rng.standard_normal((B, T, O))
+    att.zeroGradParameters()
+    dh = att.backward([cu(h), None], cu(dl), 1.0)[0]
+    mg = [(np.zeros_like(Lr[1]), np.zeros_like(Lr[2])) if Lr[0] == "linear" else None for Lr in layers]
+    dv = fo.mlp_bwd(layers, mc, dl.reshape(B * T, O), mg)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    dhr = orc.attention_bwd(P, cfg, cache, None, G, dmlp_in=dv.reshape(B, T, -1))
+    torch.cuda.synchronize()
+    pairs = [("dh", dh, dhr)]
+    for n in ("V", "Ws", "bs", "we", "Wy", "by", "Wc", "bc", "Wd", "bd", "hybW", "hybb", "hybU"):
+        pairs.append(("d" + n, att.own_grad[n], G[n]))
+    for n, g in cell.named(grads=True).items():
+        pairs.append(("d" + n, g, G["dec." + n]))
+    pairs += [("dmlp0.W", lins[0].gradWeight, mg[0][0]), ("dmlp0.b", lins[0].gradBias, mg[0][1]),
+              ("dmlp2.W", lins[1].gradWeight, mg[2][0]), ("dmlp2.b", lins[1].gradBias, mg[2][1])]
+    _assert_grads(pairs)
+
+
+@pytest.mark.gpu
+def test_conv_bilstm_attention_model_step_matches_oracle(fe):
+    """timit/timit.lua:106-145 end to end (conv + BiLSTM encoder, LSTM decoder with hybrid attention, ReLU
+    decoder_mlp, loss seed) at reduced widths; scoreDepth 20 (not a multiple of 16, like the reference's
+    150) runs on zero-padded score channels."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    torch.manual_seed(13)
+    rng = np.random.default_rng(13)
+    B, L, D, T, O = 3, 60, 20, 5, 11
+    model = s2s_amd.ConvBiLSTMAttentionModel(D, numPhonemes=O, hiddenFrameSize=32, outputFrameSize=16, stateDepth=32,
+                                             scoreDepth=20).cuda()
+    enc, dec = model.encoder, model.decoder
+    P = {}
+    convs = [m for m in enc.convlayer.modules if isinstance(m, fe.TemporalConvolution)]
+    for l, m in enumerate(convs):
+        P[f"conv{l}.W"], P[f"conv{l}.b"] = _np(m.weight), _np(m.bias)
+    for pre, c in zip(("f.", "b."), enc.rnn.cells):
+        for k, v in c.named().items():
+            P[pre + k] = _np(v)
+    Pd = {n: _np(t) for n, t in dec.own.items()}
+    for n, t in dec.decoder_recurrent.named().items():
+        Pd["dec." + n] = _np(t)
+    S, A, Sc = 32, 32, 20
+    for name, shp in (("Wm", (3, S + A)), ("bm", (3,)), ("Wo", (O, 1)), ("bo", (O,))):
+        Pd[name] = np.zeros(shp)
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=1, maxoutWindow=3, numLayers=1, hybridAttendFilterSize=5,
+                          hybridAttendFeatureMaps=16, decoderLSTM=True)
+    lins = [m for m in dec.decoder_mlp.modules if isinstance(m, fe.Linear)]
+    layers = [("linear", _np(lins[0].weight), _np(lins[0].bias)), ("relu",),
+              ("linear", _np(lins[1].weight), _np(lins[1].bias)), ("logsoftmax",)]
+    x = rng.standard_normal((B, L, D))
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    model.zeroGradParameters()
+    nll, logp = model.step(cu(x), cu(labels, torch.int32))
+    torch.cuda.synchronize()
+    # oracle: encoder, decoder with the external MLP, loss seed, backward (timit/timit.lua:262-295)
+    h, ecache = fo.conv_bilstm_fwd(x, P)
+    _, acache = orc.attention_fwd(h, labels, Pd, cfg)
+    lref, mc = fo.mlp_fwd(acache["v"].reshape(B * T, -1), layers)
+    lref = lref.reshape(B, T, O)
+    onehot = np.zeros_like(lref)
+    np.put_along_axis(onehot, labels[..., None].astype(np.int64), 1.0, axis=2)
+    assert_rel(_np(logp), lref, "logp")
+    assert_rel(_np(nll), -(onehot * lref).sum((1, 2)), "nll")
+    sc = 1.0 / B
+    mg = [(np.zeros_like(Lr[1]), np.zeros_like(Lr[2])) if Lr[0] == "linear" else None for Lr in layers]
+    dv = fo.mlp_bwd(layers, mc, -onehot.reshape(B * T, O), mg, sc)
+    Gd = {k: np.zeros_like(v) for k, v in Pd.items()}
+    dh = orc.attention_bwd(Pd, cfg, acache, None, Gd, sc, dmlp_in=dv.reshape(B, T, -1))
+    Ge = {k: np.zeros_like(v) for k, v in P.items()}
+    fo.conv_bilstm_bwd(P, ecache, dh, Ge, sc)
+    pairs = []
+    for l, m in enumerate(convs):
+        pairs += [(f"dconv{l}.W", m.gradWeight, Ge[f"conv{l}.W"]), (f"dconv{l}.b", m.gradBias, Ge[f"conv{l}.b"])]
+    for pre, c in zip(("f.", "b."), enc.rnn.cells):
+        pairs += [(f"d{pre}{k}", g, Ge[pre + k]) for k, g in c.named(grads=True).items()]
+    for n, g in dec.own_grad.items():
+        pairs.append(("d" + n, g, Gd[n]))
+    for n, g in dec.decoder_recurrent.named(grads=True).items():
+        pairs.append(("ddec." + n, g, Gd["dec." + n]))
+    pairs += [("dmlp0.W", lins[0].gradWeight, mg[0][0]), ("dmlp2.W", lins[1].gradWeight, mg[2][0]),
+              ("dmlp2.b", lins[1].gradBias, mg[2][1])]
+    _assert_grads(pairs)
