@@ -105,6 +105,26 @@ def main():
                 "shape": f"B={B} x (3, L={L}, F={F}), T={T}, O=29", "ms_per_step": round(ms, 3),
                 "frames_per_s": round(B * L / ms * 1e3, 1), "dtype": "fp32", "data": "synthetic",
                 "what": "encoder + decoder forward, nll seed, backward (no optimizer)"})
+    # the whole timit/timit.lua:106-145 conv + BiLSTM model step at its own sizes (D = 123, LSTM(400) decoder,
+    # scoreDepth 150 -> 160 padded, hybrid attention kW = 5 / 16 maps, O = 62), B = 32, L = 512 -> L' = 62, T = 40
+    B, L, D, T = 32, 512, 123, 40
+    model = s2s_amd.ConvBiLSTMAttentionModel(D).cuda()
+    x = torch.randn(B, L, D, device="cuda")
+    lab = torch.randint(0, 61, (B, T), device="cuda", dtype=torch.int32)
+    for _ in range(args.warmup):
+        model.step(x, lab)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.steps):
+        model.step(x, lab)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.steps
+    out.append({"model": "ConvBiLSTMAttentionModel (timit/timit.lua:106-145)",
+                "shape": f"B={B} x (L={L}, D={D}), T={T}, O=62", "ms_per_step": round(ms, 3),
+                "frames_per_s": round(B * L / ms * 1e3, 1), "dtype": "fp32", "data": "synthetic",
+                "what": "encoder + LSTM/hybrid-attention decoder forward, nll seed, backward (per-step decoder launches)"})
     for B, L in ((32, 128), (32, 512)):
         D = 123
         enc = s2s_amd.ConvBiLSTMEncoder(D).cuda()
