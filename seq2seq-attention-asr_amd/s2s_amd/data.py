@@ -10,10 +10,11 @@ The reference's corpora are HDF5 files written by its Python-2 preprocessing:
 Labels are 1-based class ids (Torch), EOS included (timit/timit.lua:258-262); this module hands the
 C ABI 0-based int32 labels.
 
-h5py is not part of this image: .h5 files are read through h5py when it is importable and refused
-otherwise with that reason.  The same layouts are read from .npz archives whose keys are the HDF5
-paths ("<i>/x", "<i>/chars", "train/x", ...) -- the offline conversion target, and what
-`write_npz` produces (synthetic corpora in the reference's layout).
+.h5 files are read through h5py when it is importable; h5py is not part of this image, so otherwise
+through `s2s_amd.hdf5`, a pure-Python reader of the HDF5 subset h5py writes by default (superblock v0,
+symbol-table groups, contiguous numeric datasets).  The same layouts are also read from .npz archives
+whose keys are the HDF5 paths ("<i>/x", "<i>/chars", "train/x", ...) -- what `write_npz` produces
+(synthetic corpora in the reference's layout).
 
 Batching: the trainer runs one utterance per forward (timit/timit.lua:240-265: variable-length
 utterances, gradients summed over the minibatch, then divided by B, :292-295).  The batched C ABI
@@ -36,9 +37,9 @@ def _read_tree(path):
             return {k: z[k] for k in z.files}
     try:
         import h5py
-    except ImportError as e:  # not in this image; the layout is readable from .npz instead
-        raise ImportError(f"{path}: reading HDF5 needs h5py, which is not installed here; convert the file to "
-                          ".npz with the same dataset paths (s2s_amd.data.write_npz)") from e
+    except ImportError:  # not in this image: the built-in reader of the subset h5py writes by default
+        from .hdf5 import read_tree
+        return read_tree(path)
     out = {}
     with h5py.File(path, "r") as h:
         def visit(name, obj):

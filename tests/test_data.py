@@ -64,17 +64,33 @@ def test_timit_layouts(tmp_path):
     assert (ds39["y"][10] == var["valid/10/y39"]).all()
 
 
-def test_hdf5_without_h5py_is_refused_with_reason(tmp_path):
-    from s2s_amd import data
+PYTABLES_TESTS = "/opt/conda/lib/python3.9/site-packages/tables/tests"
+
+
+def test_hdf5_reader_known_answers():
+    """s2s_amd.hdf5 on real HDF5 files written by the HDF5 C library (PyTables' own test files, shipped in
+    this image's conda tree): float.h5 holds (5, 6) arrays arange(6) + arange(5)[:, None] in float16/32/64
+    (tables/tests/test_types.py ReadFloatTestCase); python3.h5 has datasets inside a subgroup."""
+    import os
+    from s2s_amd import data, hdf5
+    fp = os.path.join(PYTABLES_TESTS, "float.h5")
+    if not os.path.exists(fp):
+        pytest.skip("no HDF5 sample files in this image")
+    t = hdf5.read_tree(fp)
+    ref = np.arange(6) + np.arange(5)[:, None]
+    for dt in ("float16", "float32", "float64"):
+        assert t[dt].dtype == np.dtype(dt) and t[dt].shape == (5, 6)
+        np.testing.assert_array_equal(t[dt], ref.astype(dt))
+    t = data._read_tree(os.path.join(PYTABLES_TESTS, "python3.h5"))
+    assert t["agroup/anarray1"].shape == (7,) and t["agroup/anarray2"].shape == (1,)
+
+
+def test_hdf5_reader_refuses_non_hdf5(tmp_path):
+    from s2s_amd import hdf5
     p = tmp_path / "x.h5"
-    p.write_bytes(b"\x89HDF\r\n\x1a\n")
-    try:
-        import h5py  # noqa: F401
-        pytest.skip("h5py present")
-    except ImportError:
-        pass
-    with pytest.raises(ImportError, match="h5py"):
-        data.loaddata(str(p))
+    p.write_bytes(b"not an hdf5 file at all")
+    with pytest.raises(ValueError, match="not an HDF5 file"):
+        hdf5.read_tree(str(p))
 
 
 def test_checkpoint_roundtrip(tmp_path):
