@@ -1485,26 +1485,27 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
     pr[n++] = GemmProblem{k.DVH, h, G.V, nullptr, Sc, A, A, Sc, A, B * L, scale, 1.f};
     S2S_TRY(gemm_f32(st, pr, n, true, false, attn_gemm_ws(d, scratch)));
   }
+  const GemmWs cws = attn_gemm_ws(d, scratch);  // free again once the GEMMs above are done (stream order)
   if (!d.ext) {
-    S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo));
-    S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm));
+    S2S_TRY(colsum_f32(st, k.DO, O, rows, O, scale, 1.f, G.bo, cws));
+    S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm, cws));
   }
-  S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd));
+  S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd, cws));
   if (d.lstm)
     for (int q = 0; q < 4; ++q) {  // LSTM.lua:25-29: Linear(S,S)(x) + Linear(S,S)(h), both with bias
       S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S + S, 2L * S, G.lstm[4 * q], S, S, S, true));      // Wqx
       S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S, 2L * S, G.lstm[4 * q + 2], S, S, S, true));      // Wqh
-      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 1]));               // bqx
-      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 3]));               // bqh
+      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 1], cws));               // bqx
+      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 3], cws));               // bqh
     }
-  S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc));
-  S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by));
-  S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs));
-  S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we));
+  S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc, cws));
+  S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by, cws));
+  S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs, cws));
+  S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we, cws));
   if (d.hf > 0) {  // hybrid features: dG (sum over utterances, chunks; steps summed in the loop), dcu = sum dws
     k.P = P;
-    S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT));
-    S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, 1.f, 0.f, k.DCU));
+    S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT, cws));
+    S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, 1.f, 0.f, k.DCU, cws));
     const int n = Sc * d.hf + d.hf * d.hk + d.hf;
     hipLaunchKernelGGL(dec_hyb_wgrad, dim3((n + 255) / 256), dim3(256), 0, st, k, G, scale);
     S2S_CHECK_HIP(hipGetLastError());

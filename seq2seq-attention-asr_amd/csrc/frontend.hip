@@ -322,7 +322,7 @@ int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
   S2S_CHECK_HIP(hipGetLastError());
   const long rows = (long)B * L - kW + 1;  // every window start of the flattened batch
   // gradBias += scale * sum_t dY_t ; gradWeight += scale * dY^T [x_t | ... | x_{t+kW-1}]
-  if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db));
+  if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db, ws_of(scratch)));
   if (dW) S2S_TRY(gemm1(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
                         nullptr, ws_of(scratch)));
   if (dx) {

@@ -301,6 +301,32 @@ __global__ void colsum_kernel(const float* __restrict__ X, long ldx, int M, int 
   }
 }
 
+// two-stage column sums: part[p][col] = sum of row slice p (grid (N/64, parts), 64 columns x 4 row
+// groups per workgroup), then out[col] = beta*out + alpha * sum_p part[p][col] in slice order
+constexpr int kColParts = 64;
+__global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, long ldx, int M, int N,
+                                                          float* __restrict__ part) {
+  __shared__ float red[4][65];
+  const int c = threadIdx.x & 63, g = threadIdx.x >> 6;
+  const int col = blockIdx.x * 64 + c;
+  const int chunk = (M + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * chunk, r1 = min(M, r0 + chunk);
+  float s = 0.f;
+  if (col < N)
+    for (int i = r0 + g; i < r1; i += 4) s += X[(long)i * ldx + col];
+  red[g][c] = s;
+  __syncthreads();
+  if (g == 0 && col < N) part[(long)blockIdx.y * N + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+}
+__global__ void colsum_final_kernel(const float* __restrict__ part, int parts, int N, float alpha, float beta,
+                                    float* __restrict__ out) {
+  const int col = blockIdx.x * blockDim.x + threadIdx.x;
+  if (col >= N) return;
+  float t = 0.f;
+  for (int p = 0; p < parts; ++p) t += part[(long)p * N + col];
+  out[col] = (beta == 0.f ? 0.f : beta * out[col]) + alpha * t;
+}
+
 __global__ void copy2d_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, long ldd, int rows,
                               int cols, int accumulate) {
   const long n = (long)rows * cols;
@@ -456,9 +482,19 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
   return 0;
 }
 
-int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out) {
+int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out,
+               GemmWs ws) {
   if (N <= 0) return 0;
-  hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, st, X, ldx, M, N, alpha, beta, out);
+  // row slices of >= 256 rows, at most kColParts; the fixed slice grid keeps the sum order
+  // independent of the workspace size once the two-stage form is taken
+  const int parts = std::min(kColParts, (M + 255) / 256);
+  if (ws.p && parts > 1 && ws.n >= (size_t)kColParts * N) {
+    hipLaunchKernelGGL(colsum_part_kernel, dim3((N + 63) / 64, parts), dim3(256), 0, st, X, ldx, M, N, ws.p);
+    hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, ws.p, parts, N, alpha, beta,
+                       out);
+  } else {
+    hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, st, X, ldx, M, N, alpha, beta, out);
+  }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

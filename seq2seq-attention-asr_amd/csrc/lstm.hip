@@ -392,10 +392,11 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
     }
     S2S_TRY(gemm_f32(st, pr, n, true, false, c.ws));
     for (int q = 0; q < 4; ++q) {
-      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 1]));
-      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 3]));
+      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 1], c.ws));
+      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 3], c.ws));
       if (io.peep && q != 2)
-        S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[kLstmParams + 2 * (q == 3 ? 2 : q) + 1]));
+        S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[kLstmParams + 2 * (q == 3 ? 2 : q) + 1],
+                           c.ws));
     }
   }
   return 0;

@@ -92,7 +92,10 @@ inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float al
 }
 
 // Column sums: out[j] = beta*out[j] + alpha * sum_i X[i*ldx + j], i < M, j < N.
-int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out);
+// With a workspace (>= 64*N floats) tall sums run in two fixed-order stages over up to 64 row slices
+// (many workgroups instead of N/64), same result for any workspace.
+int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out,
+               GemmWs ws = GemmWs{});
 // Strided 2-D copy (rows x cols) dst[r*ldd + c] = src[r*lds + c]  (+ optional accumulate).
 int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd, int rows, int cols, bool accumulate);
 // dst[c*ldd + r] = src[r*lds + c] for the rows x cols block
