@@ -119,6 +119,29 @@ __global__ __launch_bounds__(256) void im2col_kernel(const float* __restrict__ x
   col[(long)r * B * N + (long)b * N + p] = x[(((long)b * C + c) * H + oh + i) * W + ow + j];
 }
 
+// the same with four consecutive panel columns per thread (N % 4 == 0: 16-byte aligned float4 stores);
+// grid (ceil(N/1024), K, B)
+__global__ __launch_bounds__(256) void im2col4_kernel(const float* __restrict__ x, int B, int C, int H, int W,
+                                                      int kH, int kW, int Ho, int Wo, float* __restrict__ col) {
+  const int N = Ho * Wo;
+  const int p = 4 * (blockIdx.x * 256 + threadIdx.x);
+  if (p >= N) return;
+  const int r = blockIdx.y, b = blockIdx.z;
+  const int j = r % kW, i = (r / kW) % kH, c = r / (kW * kH);
+  int oh = p / Wo, ow = p - oh * Wo;
+  const float* xp = x + ((long)b * C + c) * H * W + (long)i * W + j;
+  floatx4 v;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    v[e] = xp[(long)oh * W + ow];
+    if (++ow == Wo) {
+      ow = 0;
+      ++oh;
+    }
+  }
+  *reinterpret_cast<floatx4*>(col + (long)r * B * N + (long)b * N + p) = v;
+}
+
 // dx[b, c, h, w] (+)= sum_{i, j valid} dcol[(c*kH + i)*kW + j][b*N + (h - i)*Wo + (w - j)]
 // grid (ceil(H*W/256), C, B)
 __global__ __launch_bounds__(256) void col2im_kernel(const float* __restrict__ dcol, int B, int C, int H, int W,
@@ -276,6 +299,18 @@ __global__ __launch_bounds__(256) void logsoftmax_bwd_kernel(const float* __rest
 
 inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
 
+void launch_im2col(hipStream_t st, const float* x, int B, int C, int H, int W, int kH, int kW, int Ho, int Wo,
+                   float* col) {
+  const long N = (long)Ho * Wo;
+  const int K = C * kH * kW;
+  if (N % 4 == 0 && (reinterpret_cast<uintptr_t>(col) & 15) == 0)
+    hipLaunchKernelGGL(im2col4_kernel, dim3((unsigned)((N / 4 + 255) / 256), K, B), dim3(256), 0, st, x, B, C, H, W,
+                       kH, kW, Ho, Wo, col);
+  else
+    hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((N + 255) / 256), K, B), dim3(256), 0, st, x, B, C, H, W, kH,
+                       kW, Ho, Wo, col);
+}
+
 }  // namespace
 
 // ------------------------------------------------------------------ TemporalConvolution
@@ -371,8 +406,7 @@ int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
   const int K = Cin * kH * kW;
   S2S_REQUIRE(K <= 65535 && B <= 65535 && (long)B * N < 2147483647L, "SpatialConvolutionMM: sizes exceed the grid");
   float* col = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes);
-  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((N + 255) / 256), K, B), dim3(256), 0, st, x, B, Cin, H, W, kH, kW,
-                     Ho, Wo, col);
+  launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
   S2S_CHECK_HIP(hipGetLastError());
   // y_b (Cout, N) = W (Cout, K) col[:, b*N : (b+1)*N] + bias (per row), ReLU in the epilogue
   for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
@@ -416,8 +450,7 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
   }
   if (dW) {
     if (!col_from_fwd)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
-    hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((N + 255) / 256), K, B), dim3(256), 0, st, x, B, Cin, H, W, kH,
-                       kW, Ho, Wo, col);
+    launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
     S2S_CHECK_HIP(hipGetLastError());
     // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
     S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
