@@ -153,6 +153,9 @@ XCD_CASES = [
     (21, 50, 9, 128, 128, 64, 29, 4, 7, 0.2),
     (5, 200, 7, 128, 128, 64, 29, 4, 7, 0.0),
     (3, 20, 5, 128, 128, 64, 11, 4, 3, 0.0),
+    # edge shapes: one utterance of one frame and one label; one label per utterance, ragged chain
+    (1, 1, 1, 128, 128, 64, 11, 4, 3, 0.0),
+    (9, 3, 1, 512, 512, 256, 62, 8, 7, 0.0),
 ]
 
 
