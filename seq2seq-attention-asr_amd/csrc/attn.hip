@@ -1184,24 +1184,16 @@ static int launch_xcd(const XPlan& xp, bool fwd, hipStream_t st, AttnK& k, XArgs
 // the model step runs it on the side stream beside the encoder).
 static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const GemmWs& gws) {
   const int S = d.S, A = d.A, rows = d.B * d.T;
-  // backward operand layouts first (params only): on the side stream beside the encoder, kernels
-  // run only in the gaps the persistent GRU launches leave, so the independent ones go early and
-  // the dependent GEMM chain last
-  S2S_TRY(transpose_f32(st, k.P.Wh, 2L * S, S, S, x.XWHT, S));
-  S2S_TRY(transpose_f32(st, k.P.Wz, 2L * S, S, S, x.XZRT, 2L * S));
-  S2S_TRY(transpose_f32(st, k.P.Wr, 2L * S, S, S, x.XZRT + S, 2L * S));
-  S2S_TRY(transpose_f32(st, k.P.Ws, S, d.Sc, S, x.XWST, d.Sc));
-  S2S_TRY(copy2d_f32(st, k.P.Wz + S, 2L * S, x.WXD, S, S, S, false));
-  S2S_TRY(copy2d_f32(st, k.P.Wr + S, 2L * S, x.WXD + (long)S * S, S, S, S, false));
-  S2S_TRY(copy2d_f32(st, k.P.Wh + S, 2L * S, x.WXD + 2L * S * S, S, S, S, false));
+  // On the side stream beside the encoder its kernels run only in the gaps the persistent GRU launches
+  // leave: the re-layouts and y_in in one launch, then BKD, then the GEMM chain.
+  hipLaunchKernelGGL(dec_xcd_pack_ops, dim3(1024), dim3(256), 0, st, k, x);
+  hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);  // BKD = Wd_c bc + bd
+  S2S_CHECK_HIP(hipGetLastError());
   // WDC = Wd_c Wc (S x A); WX = WXD WDC (3S x A); WXT = WX^T
   S2S_TRY(gemm1(st, false, false, S, A, S, 1.f, k.P.Wd, 2L * S, k.P.Wc, A, 0.f, x.WDC, A, nullptr, gws));
   S2S_TRY(gemm1(st, false, false, 3 * S, A, S, 1.f, x.WXD, S, x.WDC, A, 0.f, x.WX, A, nullptr, gws));
   S2S_TRY(transpose_f32(st, x.WX, A, 3 * S, A, x.WXT, 3L * S));
-  // y_in -> CY[:, S:]; BKD = Wd_c bc + bd; KD = y_in Wd_y^T + BKD; KX = KD WXD^T
-  hipLaunchKernelGGL(dec_xcd_yin, dim3(256), dim3(256), 0, st, k);
-  hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);
-  S2S_CHECK_HIP(hipGetLastError());
+  // KD = y_in Wd_y^T + BKD; KX = KD WXD^T
   S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
   S2S_TRY(gemm1(st, false, true, rows, 3 * S, S, 1.f, x.KD, S, x.WXD, S, 0.f, x.KX, 3L * S, nullptr, gws));
   return 0;
