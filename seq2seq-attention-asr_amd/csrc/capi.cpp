@@ -254,6 +254,17 @@ int prologue_mode() {
   }();
   return m;
 }
+// S2S_WGRAD_FORK=1 (default): layer l's side-stream weight-gradient GEMMs wait for layer l-1's BPTT
+// sync prep, so the persistent BPTT is dispatched before the GEMM's workgroups take the CUs (the
+// replayed graph otherwise started the GEMM first and layers 2 and 1's BPTT ran 590-618 us instead of
+// 533-540 us, profiles/r01 kernel trace); 0: fork right after layer l's own BPTT + dX (previous layout)
+int wgrad_fork_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("S2S_WGRAD_FORK");
+    return e ? std::atoi(e) : 1;
+  }();
+  return m;
+}
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
                     const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
@@ -361,6 +372,18 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   if (split)
     S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr));
   // ---- encoder backward
+  const bool defer = split && wgrad_fork_mode() == 1;
+  int pending = -1;  // layer whose weight gradients wait for the next BPTT's sync prep
+  auto issue_wgrad = [&](int l) -> int {
+    const GruLayerIO io = layer_io(l);
+    GruLayerGrad gr{};
+    for (int dd = 0; dd < 2; ++dd)
+      for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
+    gr.scale = scale;
+    S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
+    S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
+    return 0;
+  };
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
     const GruLayerIO io = layer_io(l);
@@ -374,10 +397,23 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     gr.lddx = io.ldx;
     gr.dx_accumulate = 0;
     gr.scale = scale;
+    if (defer && pending >= 0) gr.prep_event = ev[1 + pending];
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
-    if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
-    S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
-    S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
+    if (defer) {
+      if (pending >= 0) {  // the layer above: after this BPTT's dispatch point
+        S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1 + pending], 0));
+        S2S_TRY(issue_wgrad(pending));
+      }
+      pending = l;
+      if (l == 0) {  // the last BPTT: nothing left to dispatch ahead of layer 1's GEMMs
+        S2S_TRY(fork_to(st, side, ev[1 + l]));
+        S2S_TRY(issue_wgrad(l));
+      }
+    } else {
+      if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
+      S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
+      S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
+    }
     float* tmp = dYcur;
     dYcur = dYnext;
     dYnext = tmp;

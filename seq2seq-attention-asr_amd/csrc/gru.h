@@ -26,6 +26,7 @@ struct GruLayerGrad {
   int dx_accumulate;
   float* dW[2][3];  // accumulated: dW += scale * ...
   float scale;
+  hipEvent_t prep_event;  // optional: recorded between the persistent BPTT's sync prep and its launch
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);

@@ -441,6 +441,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
       f.UhT[d] = UhT[d]; f.UzrT[d] = UzrT[d]; f.sv[d] = io.saved[d]; f.dy[d] = gr.dy[d]; f.dA[d] = dA + 3L * d * H;
       f.reverse[d] = io.reverse[d];
     }
+    f.prep_event = gr.prep_event;
     S2S_TRY(gru_persist_bwd(st, f, sync));
   } else {
     ProfScope ps(st, "gru_bwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);
@@ -452,6 +453,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
       hipLaunchKernelGGL(gru_bwd_p2, g1, dim3(256), 0, st, a);
     }
     S2S_CHECK_HIP(hipGetLastError());
+    if (gr.prep_event) S2S_CHECK_HIP(hipEventRecord(gr.prep_event, st));
   }
   // dx (+)= dA (B*L, 3*nd*H) . Wx (3*nd*H, D)   (RNN.lua:196 gradInput; both directions summed,
   // which is what the encoder graph's fan-out of the layer input accumulates)

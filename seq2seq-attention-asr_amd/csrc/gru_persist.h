@@ -31,6 +31,7 @@ struct GruPersistBwd {
   float* dA[2];
   long ldA;
   int reverse[2];
+  hipEvent_t prep_event;  // optional: recorded after the sync prep, right before the launch
 };
 
 bool gru_persist_supported(int ndir, int B, int H);

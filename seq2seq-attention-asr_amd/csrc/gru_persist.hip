@@ -627,6 +627,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
   S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
+  if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);
