@@ -844,7 +844,9 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
       if (!e) S2S_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev = ctx->bev;
   }
-  if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
+  // dropout draws from a new seed every step, which would re-capture the graph every step (repeated
+  // capture + destroy of the executable graph segfaulted intermittently in the runtime): eager launches
+  if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr || d->dropout > 0.f)
     return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, bev, d,
                            params, grads, x, labels, scale, flags, logp, nll, workspace);
   GraphKey key;
@@ -856,6 +858,12 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   key.flags = flags;
   key.stream = stream;
   if (!(ctx->have_graph && ctx->key == key)) {
+    // the previous replay may still be in flight (a new dropout seed re-captures every step):
+    // destroying its executable graph under it crashed the runtime, so drain it first
+    if (ctx->exec) {
+      S2S_CHECK_HIP(hipStreamSynchronize(st));
+      if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+    }
     if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
     if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
     ctx->exec = nullptr;

@@ -335,6 +335,31 @@ def test_model_step_dropout_config3(s2s):
         assert_rel(Gg[k], G[k], "grad " + k)
 
 
+def test_model_step_dropout_back_to_back_steps(s2s):
+    """Config 3 trains with a fresh in-kernel dropout seed every step (timit.lua's nn.Dropout draws
+    new masks per forward).  A graph-mode context runs those steps eagerly (a per-step re-capture
+    crashed the runtime intermittently): many steps back to back on a side stream without a host
+    sync complete, a repeated seed reproduces its step bitwise and a new seed changes the masks."""
+    B, L, T = 16, 32, 8
+    cfg_o = orc.ModelConfig()
+    model = s2s.ChorowskiBaseline(s2s.ModelConfig(dropout=0.5), graph=True, overlap=True)
+    x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=5, pad=4, eos=23)
+    xg, lg = cu(x), cu(labels, torch.int32)
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        for _ in range(12):
+            model.step(xg, lg, stream=stream)
+        _, a = model.step(xg, lg, stream=stream, dropout_seed=7)
+        a = a.clone()
+        _, b = model.step(xg, lg, stream=stream, dropout_seed=7)
+        b = b.clone()
+        _, c = model.step(xg, lg, stream=stream, dropout_seed=8)
+    stream.synchronize()
+    assert torch.isfinite(a).all()
+    assert torch.equal(a, b)
+    assert not torch.equal(a, c)
+
+
 def test_labelmask_input_equals_int_labels(s2s):
     rng = np.random.default_rng(5)
     B, L, T, A, Sc, S, O = 2, 12, 4, 32, 32, 16, 9
