@@ -54,11 +54,18 @@ def cpu_worker(args):
     seed, L, T, kw = args
     import numpy as np
     from oracle import s2s_oracle as orc
+    kw = dict(kw)
+    p = kw.pop("dropout", 0.0)  # the oracle takes the dropout as a mask (nn.Dropout, scaled by 1/(1-p))
     cfg = orc.ModelConfig(**kw)
     P = orc.init_params(cfg, seed=1234, dtype=np.float32)
     x, lab = orc.synthetic_batch(cfg, 1, L, T, seed=seed, dtype=np.float32)
     t = time.perf_counter()
-    orc.training_step(x, lab, P, cfg)
+    mask = None
+    if p > 0:
+        rng = np.random.default_rng(seed)
+        width = cfg.stateDepth + 2 * cfg.outputFrameSize
+        mask = ((rng.random((1, T, width)) >= p) / (1.0 - p)).astype(np.float32)
+    orc.training_step(x, lab, P, cfg, dropout_mask=mask)
     return time.perf_counter() - t
 
 
