@@ -261,7 +261,7 @@ def main():
                    "feat_dim": cfg.inputFrameSize, "parallelism": f"dp{world}",
                    "allreduce": ("none" if world == 1 else "flat RCCL after the step" if not bucketed
                                  else f"{len(buckets)} RCCL buckets overlapped with encoder BPTT"),
-                   "launch": "eager" if (args.no_graph or cfg.dropout > 0) else "hipGraph replay",
+                   "launch": "eager" if args.no_graph else "hipGraph replay",
                    "flop_per_step_per_gpu": flop_step},
         "step_tflops_per_gpu": round(flop_step / (ms / 1000.0) / 1e12, 3),
         "optimizer": {"us_per_step": round(opt_us, 2), "what": "adadelta (rho .95, eps 1e-8) + global-norm clip + "

@@ -29,7 +29,11 @@ struct AttnDims {
   // decoder_recurrent = nn.LSTM(S, S) (no peepholes) instead of nn.GRU(S, S): the conv + BiLSTM
   // model of timit/timit.lua:137 (per-step decoder kernels)
   int lstm = 0;
+  // when set, the in-kernel dropout seed is read from this device word (a replayed graph: the host
+  // writes each step's seed there before the replay) instead of dropout_seed
+  const unsigned long long* dropout_seed_dev = nullptr;
 };
+int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
 struct AttnParams {
   const float *V, *Ws, *bs, *we, *Wy, *by, *Wc, *bc, *Wd, *bd, *Wz, *Wr, *Wh, *Wm, *bm, *Wo, *bo;

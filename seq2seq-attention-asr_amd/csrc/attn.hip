@@ -1021,7 +1021,11 @@ __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
   return z ^ (z >> 31);
 }
-__global__ void dec_dropout_fwd(AttnK k, float p, unsigned long long seed, const float* inj) {
+// one word written on the stream (graph replays read each step's dropout seed from it)
+__global__ void set_u64_kernel(unsigned long long* p, unsigned long long v) { *p = v; }
+__global__ void dec_dropout_fwd(AttnK k, float p, unsigned long long seed, const unsigned long long* seedp,
+                                const float* inj) {
+  if (seedp) seed = *seedp;
   const long n = (long)k.B * k.T * (k.S + k.A);
   const float keep = 1.0f / (1.0f - p);
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
@@ -1294,7 +1298,8 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   if (d.ext) return 0;  // external decoder_mlp: the caller runs it on the saved VV rows
   const int rows = B * T;
   if (d.dropout > 0.f) {
-    hipLaunchKernelGGL(dec_dropout_fwd, dim3(512), dim3(256), 0, st, k, d.dropout, d.dropout_seed, d.dropout_mask);
+    hipLaunchKernelGGL(dec_dropout_fwd, dim3(512), dim3(256), 0, st, k, d.dropout, d.dropout_seed, d.dropout_seed_dev,
+                       d.dropout_mask);
     S2S_CHECK_HIP(hipGetLastError());
   }
   S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
@@ -1831,3 +1836,11 @@ extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);
   return 0;
 }
+
+namespace s2s {
+int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v) {
+  hipLaunchKernelGGL(set_u64_kernel, dim3(1), dim3(64), 0, st, p, v);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+}  // namespace s2s

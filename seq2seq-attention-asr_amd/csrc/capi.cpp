@@ -91,6 +91,7 @@ struct s2s_ctx {
   int flags = 0;
   hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
   hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
+  unsigned long long* seed_dev = nullptr;  // dropout seed word read by the replayed graph
   hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
   bool have_graph = false;
   GraphKey key{};
@@ -143,9 +144,12 @@ std::vector<LayerDims> enc_layers(const s2s_model_dims* d) {
   }
   return v;
 }
+const unsigned long long* g_seed_dev = nullptr;  // set while a dropout step is captured (s2s_model_step)
 AttnDims model_attn(const s2s_model_dims* d) {
-  return AttnDims{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
-                  d->mlpDepth, d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
+  AttnDims a{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
+             d->mlpDepth, d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
+  a.dropout_seed_dev = g_seed_dev;
+  return a;
 }
 std::vector<long> param_sizes(const s2s_model_dims* d) {
   std::vector<long> s;
@@ -503,6 +507,7 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   if (!ctx) return;
   if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
   if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+  if (ctx->seed_dev) (void)hipFree(ctx->seed_dev);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -844,14 +849,18 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
       if (!e) S2S_CHECK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     bev = ctx->bev;
   }
-  // dropout draws from a new seed every step, which would re-capture the graph every step (repeated
-  // capture + destroy of the executable graph segfaulted intermittently in the runtime): eager launches
-  if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr || d->dropout > 0.f)
+  if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
     return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, bev, d,
                            params, grads, x, labels, scale, flags, logp, nll, workspace);
+  // dropout draws from a new seed every step: the replayed graph reads it from a device word written
+  // before each replay, so the seed is not part of the graph key (a per-step re-capture cost 2.6 ms
+  // and segfaulted intermittently in the runtime on repeated capture + destroy)
+  const bool dev_seed = d->dropout > 0.f && d->dropout_mask == nullptr;
+  if (dev_seed && !ctx->seed_dev) S2S_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->seed_dev), 64));
   GraphKey key;
   std::memset(&key, 0, sizeof(key));
   key.d = *d;
+  if (dev_seed) key.d.dropout_seed = 0;
   const void* ptrs[7] = {params, grads, x, labels, logp, nll, workspace};
   std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
   key.scale = scale;
@@ -870,8 +879,10 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     ctx->graph = nullptr;
     ctx->have_graph = false;
     S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    g_seed_dev = dev_seed ? ctx->seed_dev : nullptr;
     const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, bev, d,
                                    params, grads, x, labels, scale, flags, logp, nll, workspace);
+    g_seed_dev = nullptr;
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(st, &g);
     if (rc != 0) {
@@ -884,6 +895,7 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     ctx->key = key;
     ctx->have_graph = true;
   }
+  if (dev_seed) S2S_TRY(set_device_u64(st, ctx->seed_dev, d->dropout_seed));
   S2S_CHECK_HIP(hipGraphLaunch(ctx->exec, st));
   return 0;
 }

@@ -337,9 +337,10 @@ def test_model_step_dropout_config3(s2s):
 
 def test_model_step_dropout_back_to_back_steps(s2s):
     """Config 3 trains with a fresh in-kernel dropout seed every step (timit.lua's nn.Dropout draws
-    new masks per forward).  A graph-mode context runs those steps eagerly (a per-step re-capture
-    crashed the runtime intermittently): many steps back to back on a side stream without a host
-    sync complete, a repeated seed reproduces its step bitwise and a new seed changes the masks."""
+    new masks per forward).  A graph-mode context replays one graph and reads each step's seed from a
+    device word (a per-step re-capture crashed the runtime intermittently): many steps back to back
+    without a host sync complete, a repeated seed reproduces its step bitwise and a new seed changes
+    the masks."""
     B, L, T = 16, 32, 8
     cfg_o = orc.ModelConfig()
     model = s2s.ChorowskiBaseline(s2s.ModelConfig(dropout=0.5), graph=True, overlap=True)
