@@ -46,6 +46,12 @@ void s2s_ctx_destroy(s2s_ctx* ctx);
  * only fill the idle CUs (config-2 step 7.39 vs 7.61 ms on MI355X; bitwise-equal results). */
 #define S2S_CTX_OVERLAP 2
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
+/* S2S_CTX_GRAPH keeps one captured step per (dims, buffer pointers, scale, flags, stream) key, up to
+ * `capacity` (default 8, least recently used evicted; an evicted graph's streams are drained before
+ * it is destroyed).  The in-kernel dropout seed is not part of the key (it is read from a device word
+ * the host writes before each replay).  Stats: graphs captured, replays launched, graphs cached. */
+int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
+int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
 
 /* ---------------------------------------------------------------- GRU layer
  * nn.RNN(nn.GRU(D, H), reverse)  (RNN.lua:120-201, GRU.lua:16-51, Recurrent.lua:104-151).
@@ -141,6 +147,14 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
 const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved);
 /* decoder:alpha() (Attention.lua:241-243): device pointer to alpha (B, T, L) inside `saved` */
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved);
+/* decoder:Ws() (Attention.lua:247-249, timit/timit.lua:520): the 'Ws' node is ExpandAs(ws_t, Vh), i.e. the
+ * rows ws_t = W_s s_{t-1} + b_s broadcast over the L frames.  Device pointer to the (B, T, Sc) rows ws_t
+ * inside `saved`; the (B, T, L, Sc) tensor the reference returns is their expansion over L (a view). */
+const float* s2s_attn_ws(const s2s_attn_dims* d, const void* saved);
+/* decoder.Vh.output (Attention.lua:43-47, timit/timit.lua:521): Vh = h V^T, (B, L, Sc) inside `saved`.
+ * decoder:penalty() (Attention.lua:244-246) returns the output of the node named 'penalty', which is
+ * MonotonicAlignment's output = alpha (MonotonicAlignment.lua:40): s2s_attn_alpha serves both. */
+const float* s2s_attn_vh(const s2s_attn_dims* d, const void* saved);
 /* (B, T) MonotonicAlignment indicators 1[penalty_t > 0] of the last forward (MonotonicAlignment.lua:
  * 27-39): the discrete decision behind the penalty gradient (MonotonicAlignment.lua:44-77). */
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
@@ -254,6 +268,11 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
 /* encoder output (the annotations h, B x L x 2*outputFrameSize) of the last step, inside workspace
  * (encoder.output, timit/timit.lua:397). */
 const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace);
+/* the model step's decoder: its s2s_attn_dims and its `saved` buffer inside workspace, for the
+ * decoder accessors above after a step (decoder:alpha(), Ws(), Vh.output, penalty(): timit/timit.lua:
+ * 519-521, 534-536) and s2s_attn_dropout_mask. */
+int s2s_model_attn_dims(const s2s_model_dims* d, s2s_attn_dims* out);
+const void* s2s_model_attn_saved(const s2s_model_dims* d, const void* workspace);
 
 /* ---------------------------------------------------------------- optimizer step
  * After the (all-reduced) backward, timit/timit.lua:292-347 on the flat buffers, fused on the device:

@@ -74,6 +74,8 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
 const float* attn_saved_mlp_input(const AttnDims& d, const void* saved);
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
+const float* attn_saved_ws(const AttnDims& d, const void* saved);  // ws_t rows (B, T, Sc)
+const float* attn_saved_vh(const AttnDims& d, const void* saved);  // Vh (B, L, Sc)
 const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved);
 
 // Attention:BeamSearch (Attention.lua:332-438) for B utterances: h (B, L, A); labels 0-based; out

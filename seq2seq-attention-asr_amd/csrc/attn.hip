@@ -1084,6 +1084,16 @@ const float* attn_saved_alpha(const AttnDims& d, const void* saved) {
   carve(d, &k, (char*)saved, nullptr);
   return k.ALPHA;
 }
+const float* attn_saved_ws(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.WS;
+}
+const float* attn_saved_vh(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.Vh;
+}
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved) {
   AttnK k{};
   carve(d, &k, (char*)saved, nullptr);

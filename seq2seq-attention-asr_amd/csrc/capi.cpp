@@ -86,17 +86,29 @@ struct GraphKey {
 
 constexpr int kMaxBuckets = 17;  // decoder + up to 16 encoder layers
 
+struct CachedGraph {
+  GraphKey key;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  hipStream_t launched_on = nullptr;  // the stream of its last replay (drained before destroy)
+  unsigned long long used = 0;        // LRU clock
+};
+constexpr int kGraphCacheDefault = 8;
+
 struct s2s_ctx {
   int device = 0;
   int flags = 0;
   hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
   hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
-  unsigned long long* seed_dev = nullptr;  // dropout seed word read by the replayed graph
+  unsigned long long* seed_dev = nullptr;  // dropout seed word read by this context's replayed graphs
   hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
-  bool have_graph = false;
-  GraphKey key{};
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
+  // captured model steps, one per GraphKey (least recently used evicted past graph_cap): a caller
+  // alternating shapes / buffers (a data loader's double buffers, length buckets) replays instead of
+  // re-capturing every step
+  std::vector<CachedGraph> graphs;
+  int graph_cap = kGraphCacheDefault;
+  unsigned long long graph_clock = 0;
+  long captures = 0, replays = 0;
   ncclComm_t comm = nullptr;
 };
 
@@ -144,11 +156,9 @@ std::vector<LayerDims> enc_layers(const s2s_model_dims* d) {
   }
   return v;
 }
-const unsigned long long* g_seed_dev = nullptr;  // set while a dropout step is captured (s2s_model_step)
 AttnDims model_attn(const s2s_model_dims* d) {
   AttnDims a{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
              d->mlpDepth, d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
-  a.dropout_seed_dev = g_seed_dev;
   return a;
 }
 std::vector<long> param_sizes(const s2s_model_dims* d) {
@@ -270,9 +280,11 @@ int wgrad_fork_mode() {
   return m;
 }
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
+// seed_dev: the context's dropout seed word when a captured step reads its seed from the device (the
+// host writes it before each replay), else null (the seed is d->dropout_seed)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
                     const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
-                    float* logp, float* nll, void* workspace) {
+                    float* logp, float* nll, void* workspace, const unsigned long long* seed_dev) {
   const bool split = side != nullptr;
   gru_persist_set_exclusive(split ? 1 : 0);
   ModelWs w = model_ws(d, workspace);
@@ -294,7 +306,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, split ? side : st));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
-  const AttnDims ad = model_attn(d);
+  AttnDims ad = model_attn(d);
+  ad.dropout_seed_dev = seed_dev;
   AttnParams ap;
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
@@ -429,6 +442,24 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   return 0;
 }
 
+// Destroy a cached executable graph.  A replay of it may still be running (the host runs ahead of the
+// device): HIP's hipGraphExecDestroy frees the executable's kernel-argument and node storage at once
+// instead of deferring the free to the end of an in-flight launch (CUDA's documented behaviour), so
+// destroying it under a running replay is a use-after-free in the runtime -- the round-1 segfaults
+// inside s2s_model_step, which re-captured (and destroyed the previous exec) on every dropout step.
+// Drain the streams the replay used first.
+int drop_graph(s2s_ctx* ctx, CachedGraph& g) {
+  if (g.exec) {
+    if (g.launched_on) S2S_CHECK_HIP(hipStreamSynchronize(g.launched_on));
+    if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+    (void)hipGraphExecDestroy(g.exec);
+  }
+  if (g.graph) (void)hipGraphDestroy(g.graph);
+  g.exec = nullptr;
+  g.graph = nullptr;
+  return 0;
+}
+
 }  // namespace
 
 // ================================================================== C ABI
@@ -505,8 +536,9 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
 
 void s2s_ctx_destroy(s2s_ctx* ctx) {
   if (!ctx) return;
-  if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
-  if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
+  (void)hipSetDevice(ctx->device);
+  for (auto& g : ctx->graphs) (void)drop_graph(ctx, g);
+  ctx->graphs.clear();
   if (ctx->seed_dev) (void)hipFree(ctx->seed_dev);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
@@ -644,6 +676,12 @@ const float* s2s_attn_mlp_input(const s2s_attn_dims* d, const void* saved) {
 }
 const float* s2s_attn_alpha(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_alpha(to_attn(d), saved) : nullptr;
+}
+const float* s2s_attn_ws(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_ws(to_attn(d), saved) : nullptr;
+}
+const float* s2s_attn_vh(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_vh(to_attn(d), saved) : nullptr;
 }
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_mono_ind(to_attn(d), saved) : nullptr;
@@ -828,6 +866,23 @@ size_t s2s_model_workspace_bytes(const s2s_model_dims* d) {
   return model_ws(d, nullptr).total;
 }
 
+int s2s_model_attn_dims(const s2s_model_dims* d, s2s_attn_dims* out) {
+  S2S_REQUIRE(d != nullptr && out != nullptr, "null argument");
+  std::memset(out, 0, sizeof(*out));
+  out->B = d->B; out->L = d->L; out->T = d->T;
+  out->annotationDepth = 2 * d->outputFrameSize; out->scoreDepth = d->scoreDepth; out->stateDepth = d->stateDepth;
+  out->outputDepth = d->outputDepth; out->mlpDepth = d->mlpDepth; out->maxoutWindow = d->maxoutWindow;
+  out->penalty = d->penalty; out->dropout = d->dropout; out->dropout_seed = d->dropout_seed;
+  out->dropout_mask = d->dropout_mask;
+  return 0;
+}
+
+const void* s2s_model_attn_saved(const s2s_model_dims* d, const void* workspace) {
+  if (!d || !workspace || check_model_dims(d) != 0) return nullptr;
+  ModelWs w = model_ws(d, const_cast<void*>(workspace));
+  return w.attn_saved;
+}
+
 const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace) {
   if (!d || !workspace) return nullptr;
   ModelWs w = model_ws(d, const_cast<void*>(workspace));
@@ -851,38 +906,36 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   }
   if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
     return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, bev, d,
-                           params, grads, x, labels, scale, flags, logp, nll, workspace);
-  // dropout draws from a new seed every step: the replayed graph reads it from a device word written
-  // before each replay, so the seed is not part of the graph key (a per-step re-capture cost 2.6 ms
-  // and segfaulted intermittently in the runtime on repeated capture + destroy)
+                           params, grads, x, labels, scale, flags, logp, nll, workspace, nullptr);
+  // In-kernel dropout draws from a new seed every step: the replayed graph reads it from the context's
+  // device word, written before each replay, so the seed is not part of the graph key.  Injected masks
+  // (or no dropout) leave the seed unread: it is not part of the key either.
   const bool dev_seed = d->dropout > 0.f && d->dropout_mask == nullptr;
   if (dev_seed && !ctx->seed_dev) S2S_CHECK_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->seed_dev), 64));
   GraphKey key;
   std::memset(&key, 0, sizeof(key));
   key.d = *d;
-  if (dev_seed) key.d.dropout_seed = 0;
+  key.d.dropout_seed = 0;
   const void* ptrs[7] = {params, grads, x, labels, logp, nll, workspace};
   std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
   key.scale = scale;
   key.flags = flags;
   key.stream = stream;
-  if (!(ctx->have_graph && ctx->key == key)) {
-    // the previous replay may still be in flight (a new dropout seed re-captures every step):
-    // destroying its executable graph under it crashed the runtime, so drain it first
-    if (ctx->exec) {
-      S2S_CHECK_HIP(hipStreamSynchronize(st));
-      if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+  CachedGraph* hit = nullptr;
+  for (auto& g : ctx->graphs)
+    if (g.key == key) hit = &g;
+  if (!hit) {
+    if ((int)ctx->graphs.size() >= ctx->graph_cap) {  // evict the least recently used
+      size_t lru = 0;
+      for (size_t i = 1; i < ctx->graphs.size(); ++i)
+        if (ctx->graphs[i].used < ctx->graphs[lru].used) lru = i;
+      S2S_TRY(drop_graph(ctx, ctx->graphs[lru]));
+      ctx->graphs.erase(ctx->graphs.begin() + (long)lru);
     }
-    if (ctx->exec) (void)hipGraphExecDestroy(ctx->exec);
-    if (ctx->graph) (void)hipGraphDestroy(ctx->graph);
-    ctx->exec = nullptr;
-    ctx->graph = nullptr;
-    ctx->have_graph = false;
     S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    g_seed_dev = dev_seed ? ctx->seed_dev : nullptr;
     const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, bev, d,
-                                   params, grads, x, labels, scale, flags, logp, nll, workspace);
-    g_seed_dev = nullptr;
+                                   params, grads, x, labels, scale, flags, logp, nll, workspace,
+                                   dev_seed ? ctx->seed_dev : nullptr);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(st, &g);
     if (rc != 0) {
@@ -890,13 +943,46 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
       return rc;
     }
     S2S_CHECK_HIP(ec);
-    ctx->graph = g;
-    S2S_CHECK_HIP(hipGraphInstantiate(&ctx->exec, g, nullptr, nullptr, 0));
-    ctx->key = key;
-    ctx->have_graph = true;
+    CachedGraph cg;
+    cg.key = key;
+    cg.graph = g;
+    const hipError_t ei = hipGraphInstantiate(&cg.exec, g, nullptr, nullptr, 0);
+    if (ei != hipSuccess) {
+      (void)hipGraphDestroy(g);
+      S2S_CHECK_HIP(ei);
+    }
+    ctx->graphs.push_back(cg);
+    hit = &ctx->graphs.back();
+    ctx->captures += 1;
   }
+  hit->used = ++ctx->graph_clock;
+  hit->launched_on = st;
   if (dev_seed) S2S_TRY(set_device_u64(st, ctx->seed_dev, d->dropout_seed));
-  S2S_CHECK_HIP(hipGraphLaunch(ctx->exec, st));
+  S2S_CHECK_HIP(hipGraphLaunch(hit->exec, st));
+  ctx->replays += 1;
+  return 0;
+}
+
+int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  if (captures) *captures = ctx->captures;
+  if (replays) *replays = ctx->replays;
+  if (cached) *cached = (int)ctx->graphs.size();
+  return 0;
+}
+
+int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  S2S_REQUIRE(capacity >= 1 && capacity <= 64, "graph cache capacity must be in [1, 64]");
+  S2S_TRY(set_device(ctx));
+  ctx->graph_cap = capacity;
+  while ((int)ctx->graphs.size() > capacity) {
+    size_t lru = 0;
+    for (size_t i = 1; i < ctx->graphs.size(); ++i)
+      if (ctx->graphs[i].used < ctx->graphs[lru].used) lru = i;
+    S2S_TRY(drop_graph(ctx, ctx->graphs[lru]));
+    ctx->graphs.erase(ctx->graphs.begin() + (long)lru);
+  }
   return 0;
 }
 

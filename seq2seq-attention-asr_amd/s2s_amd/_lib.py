@@ -42,6 +42,8 @@ SIGNATURES = [
     ("s2s_ctx_create", c_int, [c_int, P(c_void_p)]),
     ("s2s_ctx_destroy", None, [c_void_p]),
     ("s2s_ctx_set_flags", c_int, [c_void_p, c_int]),
+    ("s2s_ctx_set_graph_cache", c_int, [c_void_p, c_int]),
+    ("s2s_ctx_graph_stats", c_int, [c_void_p, P(c_long), P(c_long), P(c_int)]),
     ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_gru_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     ("s2s_gru_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
@@ -65,6 +67,10 @@ SIGNATURES = [
     ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mlp_input", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mono_ind", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_ws", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_vh", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_model_attn_dims", c_int, [P(s2s_model_dims), P(s2s_attn_dims)]),
+    ("s2s_model_attn_saved", c_void_p, [P(s2s_model_dims), c_void_p]),
     ("s2s_attn_dropout_mask", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
                              c_void_p]),

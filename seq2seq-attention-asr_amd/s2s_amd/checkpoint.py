@@ -48,7 +48,12 @@ def load_flat(path):
 
 
 def save(path, model, optimizer=None, meta=None):
-    """torch.save(paths.concat(savedir, 'model.t7'), model) for a ChorowskiBaseline (+ its Adadelta)."""
+    """torch.save(paths.concat(savedir, 'model.t7'), model) for a ChorowskiBaseline (+ its Adadelta).
+    The step counter and dropout seed base travel in the metadata, so a resumed run continues the
+    dropout mask sequence instead of replaying it from step 1."""
+    meta = dict(meta or {})
+    meta.setdefault("steps", int(getattr(model, "_steps", 0)))
+    meta.setdefault("dropout_seed_base", str(int(getattr(model, "dropout_seed_base", 0))))
     save_flat(path, model.cfg, model.params, optimizer.state if optimizer is not None else None, meta)
 
 
@@ -62,6 +67,10 @@ def load(path, model=None, optimizer=None):
     elif dataclasses.asdict(model.cfg) != dataclasses.asdict(cfg):
         raise ValueError("checkpoint config differs from the model's")
     model.params.copy_(params.to(model.params.device))
+    if "steps" in meta:
+        model._steps = int(meta["steps"])
+    if "dropout_seed_base" in meta:
+        model.dropout_seed_base = int(meta["dropout_seed_base"])
     if optimizer is not None:
         if state is None or state.numel() != optimizer.state.numel():
             raise ValueError("checkpoint holds no matching optimizer state")

@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib
-from .nn import _bytes, dptr, get_context, stream_ptr
+from .nn import _bytes, dptr, get_context, saved_view, stream_ptr
 
 
 @dataclasses.dataclass
@@ -42,6 +42,25 @@ class ModelConfig:
                    outputDepth=opt.get("numPhonemes", opt.get("outputDepth", 62)),
                    mlpDepth=opt.get("mlpDepth", 64), penalty=opt.get("penalty", 0.0),
                    dropout=opt.get("dropout", 0.0))
+
+
+def _mix64(a: int, b: int) -> int:
+    """splitmix64 of (a, b): the default per-step dropout seed (never 0 for distinct inputs in practice)."""
+    z = (int(a) * 0x9E3779B97F4A7C15 + int(b) + 0x632BE59BD9B4E019) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & 0xFFFFFFFFFFFFFFFF
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & 0xFFFFFFFFFFFFFFFF
+    return z ^ (z >> 31)
+
+
+def _dist_rank() -> int:
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank()
+    except Exception:
+        pass
+    import os
+    return int(os.environ.get("RANK", "0"))
 
 
 def param_shapes(cfg: ModelConfig):
@@ -121,8 +140,13 @@ class ChorowskiBaseline:
         else:
             self.ctx = get_context(self.device.index)
         self._wsbuf = None
+        self._mask_buf = None
+        self._outputs = {}
         self.train = True
         self._steps = 0
+        # default dropout seeds: a per-step counter mixed with the init seed and the data-parallel rank,
+        # so replicas draw independent nn.Dropout masks (the reference draws a fresh mask per forward)
+        self.dropout_seed_base = _mix64(seed, _dist_rank())
         self._check_layout()
 
     def dims(self, B, L, T):
@@ -182,7 +206,8 @@ class ChorowskiBaseline:
     def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None,
              dropout_seed=None, dropout_mask=None, bucket_events=False):
         """One training-step gradient (timit/timit.lua:240-295): grads (+)= scale * d(sum_b nll_b)/dparams,
-        scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O)).
+        scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O)); unless given, both
+        are module-owned buffers overwritten by the next step of the same shape (Torch's self.output).
         With cfg.dropout > 0 (training mode) the decoder MLP input is dropped out with masks drawn
         in-kernel from dropout_seed (default: a per-step counter) or given as dropout_mask
         (B, T, S+A) multipliers.  bucket_events=True records the per-bucket "gradients final" events
@@ -200,21 +225,32 @@ class ChorowskiBaseline:
         lab = labels.to(torch.int32).contiguous()
         if scale is None:
             scale = 1.0 / B if B > 1 else 1.0
-        if logp is None:
-            logp = torch.empty((B, T, self.cfg.outputDepth), device=self.device, dtype=torch.float32)
-        if nll is None:
-            nll = torch.empty(B, device=self.device, dtype=torch.float32)
+        if logp is None or nll is None:
+            # module-owned outputs reused from step to step (as Torch's self.output): stable pointers keep
+            # a graph-mode context replaying one captured step; clone them to keep a step's values
+            o = self._outputs.get((B, T))
+            if o is None:
+                o = (torch.empty((B, T, self.cfg.outputDepth), device=self.device, dtype=torch.float32),
+                     torch.empty(B, device=self.device, dtype=torch.float32))
+                self._outputs[(B, T)] = o
+            logp = o[0] if logp is None else logp
+            nll = o[1] if nll is None else nll
         ws = self.workspace(B, L, T)
         d = self.dims(B, L, T)
         self._steps += 1
         if d.dropout > 0:
-            d.dropout_seed = self._steps if dropout_seed is None else int(dropout_seed)
+            d.dropout_seed = _mix64(self.dropout_seed_base, self._steps) if dropout_seed is None else int(dropout_seed)
             if dropout_mask is not None:
                 S, A = self.cfg.stateDepth, self.cfg.annotationDepth
                 if dropout_mask.shape != (B, T, S + A) or dropout_mask.dtype != torch.float32:
                     raise ValueError("dropout_mask must be float32 (B, T, stateDepth + annotationDepth)")
-                self._mask_keep = dropout_mask.contiguous()
-                d.dropout_mask = self._mask_keep.data_ptr()
+                # copied into a model-owned buffer: its pointer (part of a captured step's key) stays the
+                # same from step to step, so a graph-mode context replays instead of re-capturing
+                n = dropout_mask.numel()
+                if self._mask_buf is None or self._mask_buf.numel() < n:
+                    self._mask_buf = torch.empty(n, device=self.device, dtype=torch.float32)
+                self._mask_buf[:n].copy_(dropout_mask.reshape(-1))
+                d.dropout_mask = self._mask_buf.data_ptr()
         flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
         if bucket_events:
             flags |= _lib.S2S_BUCKET_EVENTS
@@ -246,8 +282,49 @@ class ChorowskiBaseline:
             first = False
             nll[torch.tensor(idx, device=self.device)] = n
             for j, i in enumerate(idx):
-                logps[i] = lp[j]
+                logps[i] = lp[j].clone()  # lp is the module-owned output, reused by the next group
         return nll, logps
+
+    # ---- the decoder's trainer-visible surface after a step (timit/timit.lua:519-521, 534-536)
+    def _attn(self):
+        B, L, T = self._last
+        d = self.dims(B, L, T)
+        ad = _lib.s2s_attn_dims()
+        check(lib.s2s_model_attn_dims(ctypes.byref(d), ctypes.byref(ad)))
+        p = lib.s2s_model_attn_saved(ctypes.byref(d), dptr(self._wsbuf))
+        if not p:
+            check(1)
+        return ad, p
+
+    def decoder_alpha(self):
+        """decoder:alpha() (Attention.lua:241-243) of the last step: (B, T, L)."""
+        ad, sv = self._attn()
+        return saved_view(self._wsbuf, lib.s2s_attn_alpha(ctypes.byref(ad), ctypes.c_void_p(sv)), (ad.B, ad.T, ad.L))
+
+    def decoder_penalty(self):
+        """decoder:penalty() (Attention.lua:244-246): MonotonicAlignment's output, i.e. alpha."""
+        return self.decoder_alpha()
+
+    def decoder_Ws(self):
+        """decoder:Ws() (Attention.lua:247-249): ws_t broadcast over L, (B, T, L, scoreDepth) expand view."""
+        ad, sv = self._attn()
+        ws = saved_view(self._wsbuf, lib.s2s_attn_ws(ctypes.byref(ad), ctypes.c_void_p(sv)),
+                        (ad.B, ad.T, ad.scoreDepth))
+        return ws[:, :, None, :].expand(ad.B, ad.T, ad.L, ad.scoreDepth)
+
+    def decoder_Vh(self):
+        """decoder.Vh.output (Attention.lua:43-47): (B, L, scoreDepth)."""
+        ad, sv = self._attn()
+        return saved_view(self._wsbuf, lib.s2s_attn_vh(ctypes.byref(ad), ctypes.c_void_p(sv)),
+                          (ad.B, ad.L, ad.scoreDepth))
+
+    def dropout_mask_used(self):
+        """(B, T, S+A) nn.Dropout multipliers of the last step (None without dropout)."""
+        ad, sv = self._attn()
+        if ad.dropout <= 0:
+            return None
+        return saved_view(self._wsbuf, lib.s2s_attn_dropout_mask(ctypes.byref(ad), ctypes.c_void_p(sv)),
+                          (ad.B, ad.T, ad.stateDepth + ad.annotationDepth))
 
     def encoder_output(self):
         B, L, T = self._last

@@ -29,6 +29,16 @@ class Context:
         if flags:
             check(lib.s2s_ctx_set_flags(h, flags))
 
+    def set_graph_cache(self, capacity: int):
+        """How many captured steps (one per shape / buffer set) the context keeps (default 8)."""
+        check(lib.s2s_ctx_set_graph_cache(self.handle, int(capacity)))
+
+    def graph_stats(self):
+        """-> (graphs captured, replays launched, graphs cached) of this context."""
+        c, r, n = ctypes.c_long(), ctypes.c_long(), ctypes.c_int()
+        check(lib.s2s_ctx_graph_stats(self.handle, ctypes.byref(c), ctypes.byref(r), ctypes.byref(n)))
+        return c.value, r.value, n.value
+
     def __del__(self):
         try:
             if self.handle:
@@ -569,10 +579,39 @@ class Attention(Module):
     def alpha(self):
         """Attention:alpha() (Attention.lua:241-243): (B, T, L) attention weights of the last forward."""
         d = self._d
-        p = lib.s2s_attn_alpha(ctypes.byref(d), dptr(self._saved))
-        off = p - self._saved.data_ptr()
-        n = d.B * d.T * d.L
-        return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T, d.L)
+        return saved_view(self._saved, lib.s2s_attn_alpha(ctypes.byref(d), dptr(self._saved)), (d.B, d.T, d.L))
+
+    def penalty(self):
+        """Attention:penalty() (Attention.lua:244-246): the output of the graph node named 'penalty', i.e.
+        MonotonicAlignment's output, which is alpha itself (MonotonicAlignment.lua:40) -- (B, T, L)."""
+        return self.alpha()
+
+    def Ws(self):
+        """Attention:Ws() (Attention.lua:247-249): the 'Ws' node ExpandAs(ws_t, Vh) -- the rows
+        ws_t = W_s s_{t-1} + b_s broadcast over the L frames, (B, T, L, scoreDepth) (an expand view of the
+        saved (B, T, scoreDepth) rows, no copy)."""
+        d = self._d
+        ws = saved_view(self._saved, lib.s2s_attn_ws(ctypes.byref(d), dptr(self._saved)), (d.B, d.T, d.scoreDepth))
+        ws = ws[..., :self.scoreDepth]
+        return ws[:, :, None, :].expand(d.B, d.T, d.L, self.scoreDepth)
+
+    @property
+    def Vh_output(self):
+        """decoder.Vh.output (Attention.lua:43-47, timit/timit.lua:521): Vh = h V^T, (B, L, scoreDepth)."""
+        d = self._d
+        vh = saved_view(self._saved, lib.s2s_attn_vh(ctypes.byref(d), dptr(self._saved)), (d.B, d.L, d.scoreDepth))
+        return vh[..., :self.scoreDepth]
+
+
+def saved_view(buf, p, shape):
+    """float32 view of `shape` at device address p inside the byte buffer `buf`."""
+    if not p:
+        raise S2SArgumentError("no such tensor in the saved buffer")
+    off = p - buf.data_ptr()
+    n = math.prod(shape)
+    if off < 0 or off + 4 * n > buf.numel():
+        raise S2SArgumentError("saved-buffer view out of range")
+    return buf[off:off + 4 * n].view(torch.float32).view(*shape)
 
 
 def nll_seed(logp, labels, normalize=False):

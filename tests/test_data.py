@@ -160,7 +160,9 @@ def test_checkpoint_restores_model_and_optimizer(tmp_path):
     m2 = s2s_amd.ChorowskiBaseline(s2s_amd.ModelConfig(**kw), seed=2)
     opt2 = optim.Adadelta(m2, colnormconstr=True)
     _, meta = checkpoint.load(p, m2, opt2)
-    assert meta == {"epoch": 1}
+    assert meta["epoch"] == 1
+    # the step counter and dropout seed base travel too (a resumed run continues the mask sequence)
+    assert m2._steps == m._steps == 1 and m2.dropout_seed_base == m.dropout_seed_base
     assert torch.equal(m2.params, m.params) and torch.equal(opt2.state, opt.state)
     # the restored pair continues identically
     for mm, oo in ((m, opt), (m2, opt2)):
