@@ -28,12 +28,18 @@ CONFIGS = {
     "librispeech_chorowski_b32": (dict(inputFrameSize=80, outputDepth=29), 32, 400, 200),
     # BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64 (fp32 here)
     "timit_chorowski_dropout_b64": (dict(dropout=0.5), 64, 128, 40),
+    # config 2's model on TIMIT-like variable-length utterances (oracle.timit_like_lengths): length-sorted
+    # minibatches of 32, each padded to its longest utterance, masked (s2s_model_dims.frame_lengths /
+    # label_lengths); frames = the utterances' real frames (padding not counted).  L / T: the cap.
+    "timit_ragged_b32": (dict(), 32, 264, 98),
 }
 CONFIG_DESC = {
     "timit_chorowski_b32": ("BASELINE config 2", "timit/model_chorowski_baseline.lua"),
     "librispeech_chorowski_b32": ("BASELINE config 4 shape (1 GPU)", "librispeech/model_chorowski_baseline.lua"),
     "timit_chorowski_dropout_b64": ("BASELINE config 3 (fp32)", "timit/model_chorowski_baseline_dropout.lua"),
+    "timit_ragged_b32": ("BASELINE config 2 model, TIMIT-like variable lengths", "timit/model_chorowski_baseline.lua"),
 }
+RAGGED_BATCHES = 8  # length-sorted minibatches cycled by the ragged workload (one captured graph each)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
@@ -189,24 +195,59 @@ def main():
     model = s2s_amd.ChorowskiBaseline(cfg, graph=not args.no_graph, seed=1234,
                                      overlap=not args.no_overlap)
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
-    x = torch.randn((B, L, cfg.inputFrameSize), generator=g)
-    x[:, :10] = 0
-    x[:, L - 10:] = 0
     eos = 23 if cfg.outputDepth > 23 else cfg.outputDepth - 1
-    labels = torch.randint(0, cfg.outputDepth - 1, (B, T), generator=g)
-    labels[labels >= eos] += 1
-    labels[:, -1] = eos
-    x = x.cuda()
-    labels = labels.to(torch.int32).cuda()
+
+    def make_batch(nb, Lb, Tb, flen=None, tlen=None):
+        x = torch.randn((nb, Lb, cfg.inputFrameSize), generator=g)
+        labels = torch.randint(0, cfg.outputDepth - 1, (nb, Tb), generator=g)
+        labels[labels >= eos] += 1
+        flen = flen if flen is not None else [Lb] * nb
+        tlen = tlen if tlen is not None else [Tb] * nb
+        for b in range(nb):  # 10 zero frames each side of the utterance, EOS last
+            x[b, :10] = 0
+            x[b, max(10, flen[b] - 10):flen[b]] = 0
+            labels[b, tlen[b] - 1] = eos
+        return x.cuda(), labels.to(torch.int32).cuda()
+
+    ragged = args.config == "timit_ragged_b32"
+    if ragged:
+        # RAGGED_BATCHES length-sorted minibatches of B TIMIT-like utterances (oracle.timit_like_lengths's
+        # distribution, restated here so the bench does not import the oracle)
+        import numpy as np
+        rs = np.random.default_rng(77 + rank)
+        dur = np.clip(rs.normal(3.1, 0.9, B * RAGGED_BATCHES), 1.0, 7.8)
+        fl = np.minimum(np.rint(dur * 16000 / 512).astype(int) + 20, L)
+        tl = np.minimum(np.maximum(np.rint(dur * 12.3).astype(int), 1) + 1, T)
+        order = np.argsort(fl, kind="stable")
+        batches = []
+        for i in range(RAGGED_BATCHES):
+            idx = order[i * B:(i + 1) * B]
+            flen, tlen = fl[idx].tolist(), tl[idx].tolist()
+            xb, lb = make_batch(B, max(flen), max(tlen), flen, tlen)
+            batches.append((xb, lb, flen, tlen))
+        args.warmup = max(args.warmup, RAGGED_BATCHES)  # one capture per batch shape, outside the timing
+    else:
+        x, labels = make_batch(B, L, T)
     stream = torch.cuda.Stream()
     scale = s2s_dist.step_scale(B)
+    real_frames = [0]
 
     comm = torch.cuda.Stream()
     buckets = model.grad_buckets()
     bucketed = world > 1 and not args.flat_allreduce
 
+    it = [0]
+
     def step():
-        model.step(x, labels, scale=scale, stream=stream, bucket_events=bucketed)
+        if ragged:
+            xb, lb, flen, tlen = batches[it[0] % RAGGED_BATCHES]
+            it[0] += 1
+            real_frames[0] += sum(flen)
+            model.step(xb, lb, scale=scale, stream=stream, bucket_events=bucketed, frame_lengths=flen,
+                       label_lengths=tlen)
+        else:
+            real_frames[0] += B * L
+            model.step(x, labels, scale=scale, stream=stream, bucket_events=bucketed)
         if bucketed:
             # per-bucket RCCL all-reduce issued as each bucket's gradients become final (decoder,
             # then encoder layers top-down), overlapping the BPTT of the layers below
@@ -222,6 +263,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
+        real_frames[0] = 0
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
@@ -247,10 +289,14 @@ def main():
         e1.record(stream)
     torch.cuda.synchronize()
     opt_us = 1000.0 * e0.elapsed_time(e1) / 20
-    frames_per_step = world * B * L
+    frames_per_step = world * real_frames[0] / args.steps  # every rank runs the same batch schedule
     value = frames_per_step / (ms / 1000.0)
 
-    flop_step = flops_per_utterance(cfg, L, T) * B
+    if ragged:  # algorithmic flops of the real (unpadded) utterances
+        flop_step = sum(flops_per_utterance(cfg, f, t) for _, _, fls, tls in batches for f, t in zip(fls, tls))
+        flop_step /= RAGGED_BATCHES
+    else:
+        flop_step = flops_per_utterance(cfg, L, T) * B
     out = {
         "metric": "log-mel frames/sec fwd+bwd, Chorowski TIMIT baseline",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -267,6 +313,14 @@ def main():
         "optimizer": {"us_per_step": round(opt_us, 2), "what": "adadelta (rho .95, eps 1e-8) + global-norm clip + "
                       "column-norm constraint on the flat buffers (s2s_optim_adadelta_step), not in ms_per_step"},
     }
+    if ragged:
+        out["config"]["ragged"] = {
+            "batches": RAGGED_BATCHES, "utterances": B * RAGGED_BATCHES,
+            "mean_frames": round(sum(sum(b[2]) for b in batches) / (B * RAGGED_BATCHES), 1),
+            "padded_frames_per_step": sum(len(b[2]) * max(b[2]) for b in batches) / RAGGED_BATCHES,
+            "lengths": "TIMIT-like: dur ~ N(3.1 s, 0.9 s) in [1, 7.8] s, hop 512 @ 16 kHz + 20 pad frames, "
+                       "12.3 phones/s + EOS; length-sorted batches, padded + masked; value counts real frames"}
+        x, labels = batches[RAGGED_BATCHES // 2][:2]  # the profiled steps (unmasked, median batch)
     if rank == 0 and not args.no_kernel_timing:
         with torch.cuda.stream(stream):
             out["roofline"], out["kernels"] = s2s_profile.dominant_kernel_roofline(

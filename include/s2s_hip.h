@@ -8,8 +8,11 @@
  *
  * Conventions:
  *   - every buffer is a caller-owned DEVICE pointer, fp32 unless stated, row-major;
- *   - utterances of a call share one length L (and T); the batch axis is leading:
- *     x (B, L, F), h (B, L, A), labels (B, T) int32, 0-based class ids;
+ *   - the batch axis is leading: x (B, L, F), h (B, L, A), labels (B, T) int32, 0-based class ids;
+ *     utterances share the padded length L (and T); variable-length batches pass per-utterance
+ *     lengths (device int32 arrays of B, 1 <= L_b <= L, 1 <= T_b <= T; NULL = all full length) and
+ *     get exactly the reference's per-utterance results (timit/timit.lua:239-295 forwards each
+ *     utterance alone): padding frames / labels contribute nothing;
  *   - weight layouts are the reference's: W (out, in) row-major (LinearZeroBias.lua:8,
  *     nn.Linear, TemporalConvolution (out, in*kW));
  *   - gradients ACCUMULATE (dW += scale * ...), as Torch's accGradParameters; zero them
@@ -59,18 +62,21 @@ int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached
  * the same x (timit/model_chorowski_baseline.lua:22-32) in the same launches; W[d*3 + g] is
  * direction d's gate g in (z, r, h) order, each (H, H+D) with columns [h | x] (GRU.lua:22).
  * y[d] rows: y[d][(b*L + t)*ldy + j]; ldy = 2H with y[1] = y[0] + H reproduces JoinTable(2,2).
- * saved[d]: s2s_gru_saved_bytes(B, L, H) each, written by fwd and read by bwd.           */
+ * saved[d]: s2s_gru_saved_bytes(B, L, H) each, written by fwd and read by bwd.
+ * lengths: (B) frames per utterance or NULL.  With lengths the recurrence is h_t = m_t GRU(h_{t-1}, x_t),
+ * m_t = 1[t < L_b]: y = 0 on padding frames, the reverse direction starts at the utterance's own last
+ * frame, and the backward treats dL/dh_t = 0 there (pass the same lengths to fwd and bwd). */
 size_t s2s_gru_saved_bytes(int B, int L, int H);
 size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H);
 int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
                 const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved,
-                void* scratch, size_t scratch_bytes);
+                const int* lengths, void* scratch, size_t scratch_bytes);
 /* dy[d] rows with stride lddy; dx (may be NULL) = sum over directions, overwritten unless
  * dx_accumulate; dW[d*3+g] += scale * ...  (LinearZeroBias.lua:50-74)                      */
 int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
                 const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy,
-                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch,
-                size_t scratch_bytes);
+                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale,
+                const int* lengths, void* scratch, size_t scratch_bytes);
 
 /* ---------------------------------------------------------------- LSTM layer
  * nn.RNN(nn.LSTM(D, H, peepholes), reverse) for ndir directions -- LSTM.lua:6-136 (gates i, f, g, o,
@@ -132,6 +138,11 @@ typedef struct {
    * kernels.  Params 10-12 are then unused (may be NULL) and params 20-35 are the LSTM's, for q in (i, f, g, o):
    * Wqx (S, S), bqx (S), Wqh (S, S), bqh (S) (LSTM.lua:25-29); 17-19 stay the hybrid ones (NULL when nF = 0). */
   int decoder_lstm;
+  /* variable-length batch (device int32 (B) arrays, or NULL): frames per utterance of h (softmax and
+   * MonotonicAlignment over its own L_b frames; alpha = 0 past them) and labels per utterance (no
+   * MonotonicAlignment gradient at steps >= T_b; the caller's dlogp must be 0 there, s2s_nll_seed does it) */
+  const int* frame_lengths;
+  const int* label_lengths;
 } s2s_attn_dims;
 #define S2S_ATTN_NPARAMS_LSTM 36
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
@@ -227,9 +238,10 @@ int s2s_logsoftmax_bwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, cons
                        float* dx);
 /* ---------------------------------------------------------------- loss seed
  * timit/timit.lua:262-282: nll[b] = -sum(labelmask * logp) (/T if normalize);
- * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).       */
+ * dlogp = -labelmask (never normalised: opt.normalizeGrad is false in every config).
+ * label_lengths (B) or NULL: only steps t < T_b count (normalize: / T_b); dlogp = 0 past them. */
 int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,
-                 int normalize, float* nll, float* dlogp);
+                 const int* label_lengths, int normalize, float* nll, float* dlogp);
 
 /* ---------------------------------------------------------------- whole training step
  * autoencoder:forward({X, labelmask}); nll; autoencoder:backward({X, labelmask}, -labelmask)
@@ -244,6 +256,12 @@ typedef struct {
   float dropout;                   /* as in s2s_attn_dims (model_chorowski_baseline_dropout.lua) */
   unsigned long long dropout_seed;
   const float* dropout_mask;
+  /* variable-length minibatch (device int32 (B) arrays, or NULL = all L / T): the step then equals the
+   * reference's per-utterance loop over utterances of L_b frames and T_b labels (timit/timit.lua:239-295):
+   * masked encoder recurrences (s2s_gru_*), masked attention (s2s_attn_dims), masked loss seed.  The
+   * arrays are read on the device at run time: a captured step replays with new lengths in place. */
+  const int* frame_lengths;
+  const int* label_lengths;
 } s2s_model_dims;
 #define S2S_ZERO_GRADS 1
 #define S2S_NORMALIZE_NLL 2

@@ -694,6 +694,45 @@ def training_step(x: Array, labels: Array, P: Dict[str, Array], cfg: ModelConfig
     return float(nll_b.mean()), G, logp, enc
 
 
+def training_step_ragged(x: Array, labels: Array, flen, tlen, P: Dict[str, Array], cfg: ModelConfig,
+                         normalizeNLL: bool = True):
+    """timit/timit.lua:239-295 literally: a minibatch of variable-length utterances is forwarded and
+    back-propagated ONE UTTERANCE AT A TIME at its own length ("data is variable length", :239-240),
+    gradients summed, then / B (:292-295).  x (B, Lmax, F) and labels (B, Tmax) are padded; utterance b
+    is x[b, :flen[b]], labels[b, :tlen[b]].  Returns (nll per utterance (B,), grads dict,
+    [logp_b (T_b, O)], [enc_b (L_b, A)])."""
+    B = x.shape[0]
+    G = zeros_like_params(P)
+    nlls, logps, encs = [], [], []
+    for b in range(B):
+        Lb, Tb = int(flen[b]), int(tlen[b])
+        nll_b, G_b, logp_b, enc_b = training_step(x[b:b + 1, :Lb], labels[b:b + 1, :Tb], P, cfg, normalizeNLL)
+        for k in G:
+            G[k] += G_b[k]
+        nlls.append(nll_b)
+        logps.append(logp_b[0])
+        encs.append(enc_b[0])
+    if B > 1:
+        for k in G:
+            G[k] /= B
+    return np.array(nlls), G, logps, encs
+
+
+def timit_like_lengths(n: int, seed: int = 0, frames_per_s: float = 16000 / 512, pad: int = 20,
+                       phones_per_s: float = 12.3, max_frames: int = None):
+    """Synthetic TIMIT-like utterance lengths: durations ~ N(3.1 s, 0.9 s) clipped to
+    [1.0, 7.8] s; frames at the reference's hop (librosa hop 512 at 16 kHz, timit/preprocess_timit.py:
+    196-209) plus 10 zero pad frames each side (:274-276); one label per phone (~12.3 phones/s) plus EOS.
+    Returns (frames, labels) int arrays."""
+    rng = np.random.default_rng(seed)
+    dur = np.clip(rng.normal(3.1, 0.9, n), 1.0, 7.8)
+    frames = np.rint(dur * frames_per_s).astype(int) + pad
+    labels = np.maximum(np.rint(dur * phones_per_s).astype(int), 1) + 1
+    if max_frames is not None:
+        frames = np.minimum(frames, max_frames)
+    return frames, labels
+
+
 def synthetic_batch(cfg: ModelConfig, B: int, L: int, T: int, seed: int = 1234, pad: int = 10,
                     eos: int = 23, dtype=np.float64):
     """SURVEY.md §8(d): x ~ N(0,1), zero pad frames each side (timit/preprocess_timit.py:274-276);

@@ -32,6 +32,12 @@ struct AttnDims {
   // when set, the in-kernel dropout seed is read from this device word (a replayed graph: the host
   // writes each step's seed there before the replay) instead of dropout_seed
   const unsigned long long* dropout_seed_dev = nullptr;
+  // variable-length batch (device int32, B each, or null = all full length): frames L_b of each
+  // utterance's annotations (1 <= L_b <= L; alpha = 0 on frames >= L_b, MonotonicAlignment over its L_b
+  // frames) and labels T_b (1 <= T_b <= T; decoder steps >= T_b carry no penalty gradient -- the caller's
+  // dlogp is 0 there, the reference never runs them)
+  const int* flen = nullptr;
+  const int* tlen = nullptr;
 };
 int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
@@ -89,7 +95,8 @@ int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda,
                   int ldb, int* out);
 
 // -log p of the labels and the reference's seed dlogp = -labelmask (timit/timit.lua:262-282).
+// tlen (B, or null): labels per utterance -- steps t >= T_b get dlogp = 0 and no nll term (normalize: / T_b)
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
-             float* dlogp);
+             float* dlogp, const int* tlen = nullptr);
 
 }  // namespace s2s

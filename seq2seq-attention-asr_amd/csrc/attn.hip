@@ -37,6 +37,7 @@ struct AttnK {
   int B, L, T, A, Sc, S, O, M, K, NCH, t;
   float penalty;
   int hk, hf;  // hybrid attention filter size / feature maps (hf = 0: off)
+  const int *flen, *tlen;  // variable-length batch: frames / labels per utterance (null: L / T)
   // params
   AttnParams P;
   const float* h;
@@ -263,6 +264,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   if (k) {
     k->B = d.B; k->L = d.L; k->T = d.T; k->A = d.A; k->Sc = d.Sc; k->S = d.S; k->O = d.O; k->M = d.M; k->K = d.K;
     k->NCH = (int)NCH; k->penalty = d.penalty; k->t = 0;
+    k->flen = d.flen; k->tlen = d.tlen;
     k->hk = (int)HK; k->hf = d.hf;
     k->lstm = d.lstm; k->LW = LW; k->LB = LB; k->LC = LCS; k->LDW = LDW;
     k->HGT = HGT; k->HCU = HCU; k->QA = QA; k->PDG = PDG; k->DGT = DGT; k->DCU = DCU;
@@ -287,6 +289,9 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
 }
 
 __device__ __forceinline__ int brow(int b0, int lane, int B) { return min(b0 + (lane & 15), B - 1); }
+// frames / labels of utterance b in a variable-length batch
+__device__ __forceinline__ int frames_of(const AttnK& k, int b) { return k.flen ? k.flen[b] : k.L; }
+__device__ __forceinline__ int labels_of(const AttnK& k, int b) { return k.tlen ? k.tlen[b] : k.T; }
 
 // ------------------------------------------------------------------ forward step kernels
 
@@ -388,10 +393,11 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
   const float* ws = k.WS + ((long)b * k.T + t) * Sc;
   const float* we = k.P.we;
   const float* ap = (k.hf > 0 && t > 0) ? k.ALPHA + ((long)b * k.T + t - 1) * L : nullptr;  // alpha_{t-1}
+  const int Lb = frames_of(k, b);
   for (int i = 0; i < 4; ++i) {
     const int li = wave * 4 + i, l = ch * LC + li;
     float part = 0.f;
-    if (l < L) {
+    if (l < Lb) {
       const float* vh = k.Vh + ((long)b * L + l) * Sc;
       for (int c4 = lane; c4 < Sc / 4; c4 += 64) {
         float4 v = reinterpret_cast<const float4*>(vh)[c4];
@@ -406,14 +412,14 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
       }
     }
     part = wave_sum(part);
-    if (lane == 0) sc[li] = l < L ? part : -INFINITY;
+    if (lane == 0) sc[li] = l < Lb ? part : -INFINITY;
   }
   __syncthreads();
   float m = -INFINITY;
   for (int i = 0; i < LC; ++i) m = fmaxf(m, sc[i]);
   if (tid < LC) {
     const int l = ch * LC + tid;
-    const float p = l < L ? expf(sc[tid] - m) : 0.f;
+    const float p = l < Lb ? expf(sc[tid] - m) : 0.f;
     pw[tid] = p;
     if (l < L) k.E[((long)b * k.T + t) * L + l] = sc[tid];
   }
@@ -473,12 +479,13 @@ __global__ __launch_bounds__(256) void dec_f3_combine(AttnK k) {
   }
   // alpha_l = exp(e_l - lse) and sum_l (L - l)(alpha_l - alpha_prev_l)   (MonotonicAlignment.lua:27-35)
   const float lse = m + logf(stat[1]);
+  const int Lb = frames_of(k, b);
   float diff = 0.f;
   for (int l = tid; l < L; l += 256) {
-    const float a = expf(k.E[row * L + l] - lse);
+    const float a = expf(k.E[row * L + l] - lse);  // 0 on padding frames (E = -inf)
     k.ALPHA[row * L + l] = a;
     const float ap = t > 0 ? k.ALPHA[(row - 1) * L + l] : 0.f;  // alpha_{t-1} (written by step t-1)
-    diff += (float)(L - l) * (a - ap);
+    diff += (float)(Lb - l) * (a - ap);
   }
   diff = wave_sum(diff);
   if (lane == 0) red[wave] = diff;
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(256) void dec_f3_combine(AttnK k) {
   if (tid == 0) {
     const float d = ((red[0] + red[1]) + red[2]) + red[3];
     const float pen = k.penalty * fmaxf(d, 0.f);
-    k.IND[row] = pen > 0.f ? 1.f : 0.f;
+    k.IND[row] = (pen > 0.f && t < labels_of(k, b)) ? 1.f : 0.f;
   }
 }
 
@@ -814,12 +821,13 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   const float* alpha = k.ALPHA + row * L;
   const float lam = k.penalty;
   const float ind = k.IND[row], indn = t + 1 < T ? k.IND[row + 1] : 0.f;
+  const int Lb = frames_of(k, b);  // MonotonicAlignment's L (alpha = 0 past it)
   // sum_j alpha_j d alpha_j
   float part = 0.f;
   for (int a = tid; a < A; a += 256) part += dc[a] * c[a];
   for (int l = tid; l < L; l += 256)
-    part += alpha[l] * (HYB ? lam * (float)(L - l) * (ind - indn) + hyb_carry(k, b, l)
-                            : lam * (float)(L - l) * (ind - indn));
+    part += alpha[l] * (HYB ? lam * (float)(Lb - l) * (ind - indn) + hyb_carry(k, b, l)
+                            : lam * (float)(Lb - l) * (ind - indn));
   part = wave_sum(part);
   if (lane == 0) redv[wave] = part;
   __syncthreads();
@@ -852,8 +860,8 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     }
     dd = wave_sum(dd);
     const float al = alpha[l];
-    const float dal = HYB ? dd + (lam * (float)(L - l) * (ind - indn) + hyb_carry(k, b, l))
-                          : dd + lam * (float)(L - l) * (ind - indn);
+    const float dal = HYB ? dd + (lam * (float)(Lb - l) * (ind - indn) + hyb_carry(k, b, l))
+                          : dd + lam * (float)(Lb - l) * (ind - indn);
     const float de = al * (dal - ssum);
     float qv[HK];
     if (HYB) {
@@ -993,13 +1001,14 @@ __global__ void fill2d_kernel(float* dst, long ldd, int rows, int cols, float v)
 }
 
 __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
-                                float* dlogp) {
+                                float* dlogp, const int* tlen) {
   const int b = blockIdx.x;
   __shared__ float red[4];
+  const int Tb = tlen ? tlen[b] : T;  // labels of this utterance; later steps are padding
   float s = 0.f;
   for (int i = threadIdx.x; i < T * O; i += blockDim.x) {
     const int t = i / O, o = i - t * O;
-    const bool hit = labels[b * T + t] == o;
+    const bool hit = t < Tb && labels[b * T + t] == o;
     if (hit && logp) s += logp[((long)b * T + t) * O + o];
     if (dlogp) dlogp[((long)b * T + t) * O + o] = hit ? -1.f : 0.f;
   }
@@ -1008,7 +1017,7 @@ __global__ void nll_seed_kernel(int B, int T, int O, const float* logp, const in
   __syncthreads();
   if (threadIdx.x == 0 && nll) {
     float v = -(((red[0] + red[1]) + red[2]) + red[3]);
-    nll[b] = normalize ? v / (float)T : v;
+    nll[b] = normalize ? v / (float)Tb : v;
   }
 }
 
@@ -1113,6 +1122,7 @@ static int dec_persist_variant(const AttnDims& d) {
   const char* m = std::getenv("S2S_DEC_MODE");
   if (m && std::strcmp(m, "step") == 0) return 0;
   if (d.hf > 0 || d.lstm) return 0;
+  if (d.flen || d.tlen) return 0;  // variable-length batches: the XCD-local or the per-step kernels
   if ((d.L + LC - 1) / LC > 256) return 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) return 1;
   if (d.S == 64 && d.A == 128 && d.Sc == 128) return 2;
@@ -1829,8 +1839,8 @@ int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda,
 }
 
 int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* labels, int normalize, float* nll,
-             float* dlogp) {
-  hipLaunchKernelGGL(nll_seed_kernel, dim3(B), dim3(256), 0, st, B, T, O, logp, labels, normalize, nll, dlogp);
+             float* dlogp, const int* tlen) {
+  hipLaunchKernelGGL(nll_seed_kernel, dim3(B), dim3(256), 0, st, B, T, O, logp, labels, normalize, nll, dlogp, tlen);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -127,6 +127,8 @@ AttnDims to_attn(const s2s_attn_dims* d) {
   a.hf = d->hybridAttendFeatureMaps;
   a.ext = d->external_mlp ? 1 : 0;
   a.lstm = d->decoder_lstm ? 1 : 0;
+  a.flen = d->frame_lengths;
+  a.tlen = d->label_lengths;
   return a;
 }
 int attn_nparams(const s2s_attn_dims* d) {
@@ -159,6 +161,8 @@ std::vector<LayerDims> enc_layers(const s2s_model_dims* d) {
 AttnDims model_attn(const s2s_model_dims* d) {
   AttnDims a{d->B, d->L, d->T, 2 * d->outputFrameSize, d->scoreDepth, d->stateDepth, d->outputDepth,
              d->mlpDepth, d->maxoutWindow, d->penalty, d->dropout, d->dropout_seed, d->dropout_mask};
+  a.flen = d->frame_lengths;
+  a.tlen = d->label_lengths;
   return a;
 }
 std::vector<long> param_sizes(const s2s_model_dims* d) {
@@ -341,6 +345,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     }
     io.ldy = 2L * H;
     io.packed = w.pack[l];
+    io.len = d->frame_lengths;
     return io;
   };
   if (w.xpad) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
@@ -357,13 +362,13 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // stream, joined before the decoder (the persistent GRU launches hold every CU, so it runs in the
   // gaps between layers); 1: beside pad + pack, joined before layer 1; 2: inline on the main stream
   if (split && pmode != 2) {
-    S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));  // dlogp = -labelmask
+    S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));  // dlogp = -labelmask
     if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
     S2S_CHECK_HIP(hipEventRecord(ev[14], side));
     if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   } else {
     S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
-    if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp));
+    if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
   }
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   for (int l = 0; l < nl; ++l) S2S_TRY(gru_layer_fwd(st, layer_io(l), w.scratch, w.scratch_bytes));
@@ -376,7 +381,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // ---- loss seed: dlogp = -labelmask needs only the labels (computed beside the encoder when split);
   // the reported nll (timit.lua:268-272) is computed on the side stream at the end of the step
   if (!split)
-    S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp));
+    S2S_TRY(nll_seed(st, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, w.dlogp,
+                     d->label_lengths));
   // ---- decoder backward -> dh
   float* dYcur = w.dY0;
   float* dYnext = w.dY1;
@@ -387,7 +393,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   S2S_TRY(mark_bucket(bev, 0, split ? side : st));
   // the reported nll (timit.lua:268-272) beside the encoder BPTT
   if (split)
-    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr));
+    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr,
+                     d->label_lengths));
   // ---- encoder backward
   const bool defer = split && wgrad_fork_mode() == 1;
   int pending = -1;  // layer whose weight gradients wait for the next BPTT's sync prep
@@ -561,11 +568,13 @@ size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H) {
 }
 
 static int fill_gru_io(GruLayerIO& io, int ndir, int B, int L, int D, int H, const int* reverse, const float* x,
-                       long ldx, const float* const* W, float* const* y, long ldy, void* const* saved) {
+                       long ldx, const float* const* W, float* const* y, long ldy, void* const* saved,
+                       const int* lengths) {
   S2S_REQUIRE(ndir == 1 || ndir == 2, "gru: ndir must be 1 or 2");
   S2S_REQUIRE(reverse && x && W && saved, "gru: null argument");
   S2S_REQUIRE(ldx >= D, "gru: ldx < D");
   io.ndir = ndir; io.B = B; io.L = L; io.D = D; io.H = H; io.x = x; io.ldx = ldx; io.ldy = ldy;
+  io.len = lengths;
   for (int d = 0; d < ndir; ++d) {
     for (int g = 0; g < 3; ++g) {
       io.W[d][g] = W[3 * d + g];
@@ -581,10 +590,10 @@ static int fill_gru_io(GruLayerIO& io, int ndir, int B, int L, int D, int H, con
 
 int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
                 const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved,
-                void* scratch, size_t scratch_bytes) {
+                const int* lengths, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
   GruLayerIO io{};
-  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, y, ldy, saved));
+  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, y, ldy, saved, lengths));
   S2S_REQUIRE(y != nullptr, "gru: null y");
   for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "gru: null y");
   S2S_REQUIRE(ldy >= H, "gru: ldy < H");
@@ -593,11 +602,11 @@ int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
 
 int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse,
                 const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy,
-                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch,
-                size_t scratch_bytes) {
+                long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale,
+                const int* lengths, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
   GruLayerIO io{};
-  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, nullptr, H, saved));
+  S2S_TRY(fill_gru_io(io, ndir, B, L, D, H, reverse, x, ldx, W, nullptr, H, saved, lengths));
   S2S_REQUIRE(dy && dW, "gru: null dy/dW");
   GruLayerGrad gr{};
   for (int d = 0; d < ndir; ++d) {
@@ -837,11 +846,11 @@ int s2s_logsoftmax_bwd(s2s_ctx* ctx, s2s_stream_t stream, long rows, int n, cons
 }
 
 int s2s_nll_seed(s2s_ctx* ctx, s2s_stream_t stream, int B, int T, int O, const float* logp, const int* labels,
-                 int normalize, float* nll, float* dlogp) {
+                 const int* label_lengths, int normalize, float* nll, float* dlogp) {
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(logp && labels && nll, "nll: null argument");
   S2S_REQUIRE(B > 0 && T > 0 && O > 0, "nll: empty dims");
-  return nll_seed(static_cast<hipStream_t>(stream), B, T, O, logp, labels, normalize, nll, dlogp);
+  return nll_seed(static_cast<hipStream_t>(stream), B, T, O, logp, labels, normalize, nll, dlogp, label_lengths);
 }
 
 size_t s2s_model_param_count(const s2s_model_dims* d) {

@@ -17,6 +17,10 @@ struct GruLayerIO {
   int Dx = 0;       // x columns [D, Dx) are readable zeros (0 = D; Dx <= round_up(D, 32)):
                     // the input GEMMs then run over K = Dx on aligned, unguarded tiles
   const float* packed = nullptr;  // gru_layer_pack output for these weights (null: pack per call)
+  // variable-length batch: (B) device int32 frames per utterance, 1 <= len_b <= L (null: all L).  The
+  // recurrence is h_t = m_t GRU(h_{t-1}, x_t), m_t = 1[t < len_b]: outputs are 0 on the padding frames and
+  // the reverse direction starts at each utterance's own last frame (RNN.lua:142-145 on the utterance alone)
+  const int* len = nullptr;
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]

@@ -40,6 +40,7 @@ struct GruFwdDir {
 struct GruFwdArgs {
   GruFwdDir d[2];
   int B, L, H, step;
+  const int* len;  // (B) frames per utterance or null
 };
 
 __global__ __launch_bounds__(256) void gru_fwd_p1(GruFwdArgs a) {
@@ -93,8 +94,9 @@ __global__ __launch_bounds__(256) void gru_fwd_p2(GruFwdArgs a) {
   float* sv = g.sv + row * 5 * H;
   const float z = sv[n], hp = sv[3 * H + n];
   sv[2 * H + n] = hh;
-  // GRU.lua:27-30: v1 = (-z)+1; v2 = v1*h; h' = v2 + z*hh
-  g.y[row * g.ldy + n] = (-z + 1.0f) * hp + z * hh;
+  // GRU.lua:27-30: v1 = (-z)+1; v2 = v1*h; h' = v2 + z*hh  (0 on a padding frame)
+  const bool valid = !a.len || t < a.len[b];
+  g.y[row * g.ldy + n] = valid ? (-z + 1.0f) * hp + z * hh : 0.f;
 }
 
 struct GruBwdDir {
@@ -112,13 +114,15 @@ struct GruBwdDir {
 struct GruBwdArgs {
   GruBwdDir d[2];
   int B, L, H, step;  // step = forward step index being back-propagated (L-1 .. 0)
+  const int* len;     // (B) frames per utterance or null: dL/dh_t = 0 on padding frames
 };
+__device__ __forceinline__ bool frame_valid(const int* len, int b, int t) { return !len || t < len[b]; }
 
 __device__ __forceinline__ void gru_gate_grads(const GruBwdDir& g, int B, int L, int H, int b, int t, int k,
-                                               float dhcarry) {
+                                               float dhcarry, const int* len) {
   const long row = (long)b * L + t;
   const float* sv = g.sv + row * 5 * H;
-  const float dh = g.dy[row * g.lddy + k] + dhcarry;
+  const float dh = frame_valid(len, b, t) ? g.dy[row * g.lddy + k] + dhcarry : 0.f;
   const float z = sv[k], hh = sv[2 * H + k], hp = sv[3 * H + k];
   float* dA = g.dA + row * g.ldA;
   dA[k] = dh * (hh - hp) * (z * (1.0f - z));          // da_z
@@ -133,7 +137,7 @@ __global__ void gru_bwd_init(GruBwdArgs a) {
   const int b = idx / a.H, k = idx - b * a.H;
   const int t = g.reverse ? 0 : a.L - 1;
   g.dhc[idx] = 0.f;
-  gru_gate_grads(g, a.B, a.L, a.H, b, t, k, 0.f);
+  gru_gate_grads(g, a.B, a.L, a.H, b, t, k, 0.f, a.len);
 }
 
 __global__ __launch_bounds__(256) void gru_bwd_p1(GruBwdArgs a) {
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(256) void gru_bwd_p1(GruBwdArgs a) {
   const float* sv = g.sv + row * 5 * H;
   const float z = sv[k], r = sv[H + k], hp = sv[3 * H + k];
   g.dA[row * g.ldA + H + k] = (dq * hp) * (r * (1.0f - r));  // da_r
-  const float dh = g.dy[row * g.lddy + k] + g.dhc[b * H + k];
+  const float dh = frame_valid(a.len, b, t) ? g.dy[row * g.lddy + k] + g.dhc[b * H + k] : 0.f;
   g.dhp[b * H + k] = dh * (-z + 1.0f) + dq * r;
 }
 
@@ -170,10 +174,10 @@ __global__ __launch_bounds__(256) void gru_bwd_p2(GruBwdArgs a) {
   const float s = skinny_reduce(red, acc, wave, lane, tid);
   const int b = b0 + (tid >> 4), k = n0 + (tid & 15);
   if (b >= B || step == 0) return;
-  const float dhprev = g.dhp[b * H + k] + s;
-  g.dhc[b * H + k] = dhprev;
   const int tn = g.reverse ? t + 1 : t - 1;
-  gru_gate_grads(g, B, L, H, b, tn, k, dhprev);
+  const float dhprev = frame_valid(a.len, b, tn) ? g.dhp[b * H + k] + s : 0.f;
+  g.dhc[b * H + k] = dhprev;
+  gru_gate_grads(g, B, L, H, b, tn, k, dhprev, a.len);
 }
 
 // Pack W{z,r,h} (H, H+D) into kernel layouts.
@@ -369,8 +373,10 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   a.B = B;
   a.L = L;
   a.H = H;
+  a.len = io.len;
   if (use_persistent(nd, B, H)) {
     GruPersistFwd f{};
+    f.len = io.len;
     f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 3L * nd * H; f.ldy = io.ldy;
     if (fuse) {
       f.x = io.x; f.ldx = io.ldx; f.Kx = Kx; f.Wx = Wx;
@@ -434,8 +440,10 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   a.B = B;
   a.L = L;
   a.H = H;
+  a.len = io.len;
   if (use_persistent(nd, B, H)) {
     GruPersistBwd f{};
+    f.len = io.len;
     f.ndir = nd; f.B = B; f.L = L; f.H = H; f.lddy = gr.lddy; f.ldA = ldA;
     for (int d = 0; d < nd; ++d) {
       f.UhT[d] = UhT[d]; f.UzrT[d] = UzrT[d]; f.sv[d] = io.saved[d]; f.dy[d] = gr.dy[d]; f.dA[d] = dA + 3L * d * H;

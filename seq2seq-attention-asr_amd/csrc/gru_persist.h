@@ -20,6 +20,7 @@ struct GruPersistFwd {
   long ldy;
   float* sv[2];
   int reverse[2];
+  const int* len = nullptr;  // (B) frames per utterance (null: all L)
 };
 struct GruPersistBwd {
   int ndir, B, L, H;
@@ -32,6 +33,7 @@ struct GruPersistBwd {
   long ldA;
   int reverse[2];
   hipEvent_t prep_event;  // optional: recorded after the sync prep, right before the launch
+  const int* len = nullptr;  // (B) frames per utterance (null: all L)
 };
 
 bool gru_persist_supported(int ndir, int B, int H);

@@ -80,6 +80,7 @@ struct PArgs {
   int allow_local;       // 0 forces write-through (sc1) hand-offs even on an XCD-local chain
   unsigned* abort_word;
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
+  const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
   unsigned long long* stamps;  // diagnostic: [grid][L][6] s_memrealtime, or nullptr
 };
 
@@ -237,6 +238,9 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), on = c1 * 16 + (tid & 15);  // this thread's output
   const bool live = ob < B;
+  // variable-length batch: h_t = m_t GRU(h_{t-1}, x_t), m_t = 1[t < len_b] -- the reverse direction then
+  // starts from h = 0 at the utterance's own last frame, as the reference's per-utterance nn.RNN does
+  const int lenb = (a.len && live) ? a.len[ob] : L;
   // r tiles: units [jt, jt + 16) of h_{t-1} are chunk it of wave wt in the sweep layout
   const int jt = c1 * 16 - H, wt = (jt % 64) / 16, it = jt / 64;
   float zreg = 0.f, hreg = 0.f;
@@ -342,6 +346,7 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
       const float hh = tanhf(sum + xph);
       const float hp = hreg;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
+      if (t >= lenb) hreg = 0.f;
       if (loc) {  // first
         if (live) put_sent(g.s0 + s * slot + (long)ob * H + on, hreg);
       } else {
@@ -390,6 +395,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), ok_ = c * 16 + (tid & 15);
   const bool live = ob < B;
+  const int lenb = (a.len && live) ? a.len[ob] : L;  // masked frames: dL/dh_t = 0 (forward h_t = 0)
   float dhc = 0.f, dhp = 0.f;
   bool aborted = false;
 
@@ -404,7 +410,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
       const long row = (long)ob * L + t;
       const float* sv = g.sv + row * 5 * H;
       v.z = sv[ok_]; v.r = sv[H + ok_]; v.hh = sv[2 * H + ok_]; v.hp = sv[3 * H + ok_];
-      v.dy = g.dy[row * g.lddy + ok_];
+      v.dy = t < lenb ? g.dy[row * g.lddy + ok_] : 0.f;
     }
     return v;
   };
@@ -486,7 +492,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     acc = mfma_chunks<2 * NC>(azr, wzr);
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    if (live && s > 0) dhc = dhp + sm;
+    if (live && s > 0) dhc = tn < lenb ? dhp + sm : 0.f;
     if (s > 0) gate(tn, nxt, nxt.dy + dhc, p + 1, live);
     cur = nxt;
     GRU_STAMP(5);
@@ -595,6 +601,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   for (int d = 0; d < f.ndir; ++d)
     a.d[d] = PDir{f.xp[d], f.ldxp, f.Uzr[d], f.Uh[d], f.y[d], f.ldy, f.sv[d], nullptr, 0, nullptr, 0, f.reverse[d],
                   gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
+  a.len = f.len;
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
@@ -623,6 +630,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
                   b.reverse[d], gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
+  a.len = b.len;
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];

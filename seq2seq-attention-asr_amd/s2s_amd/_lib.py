@@ -20,7 +20,8 @@ class s2s_attn_dims(ctypes.Structure):
                 ("stateDepth", c_int), ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int),
                 ("penalty", c_float), ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong),
                 ("dropout_mask", c_void_p), ("hybridAttendFilterSize", c_int), ("hybridAttendFeatureMaps", c_int),
-                ("external_mlp", c_int), ("decoder_lstm", c_int)]
+                ("external_mlp", c_int), ("decoder_lstm", c_int), ("frame_lengths", c_void_p),
+                ("label_lengths", c_void_p)]
 
 
 class s2s_optim_config(ctypes.Structure):
@@ -32,7 +33,8 @@ class s2s_model_dims(ctypes.Structure):
     _fields_ = [("B", c_int), ("L", c_int), ("T", c_int), ("inputFrameSize", c_int), ("hiddenFrameSize", c_int),
                 ("outputFrameSize", c_int), ("numLayers", c_int), ("scoreDepth", c_int), ("stateDepth", c_int),
                 ("outputDepth", c_int), ("mlpDepth", c_int), ("maxoutWindow", c_int), ("penalty", c_float),
-                ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong), ("dropout_mask", c_void_p)]
+                ("dropout", c_float), ("dropout_seed", ctypes.c_ulonglong), ("dropout_mask", c_void_p),
+                ("frame_lengths", c_void_p), ("label_lengths", c_void_p)]
 
 
 # every symbol include/s2s_hip.h declares: (name, restype, argtypes)
@@ -47,10 +49,10 @@ SIGNATURES = [
     ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_gru_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     ("s2s_gru_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
-                            P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_size_t]),
+                            P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_void_p, c_size_t]),
     ("s2s_gru_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
                             P(c_void_p), P(c_void_p), P(c_void_p), c_long, c_void_p, c_long, c_int, P(c_void_p),
-                            c_float, c_void_p, c_size_t]),
+                            c_float, c_void_p, c_void_p, c_size_t]),
     ("s2s_lstm_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_lstm_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("s2s_lstm_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p,
@@ -72,8 +74,8 @@ SIGNATURES = [
     ("s2s_model_attn_dims", c_int, [P(s2s_model_dims), P(s2s_attn_dims)]),
     ("s2s_model_attn_saved", c_void_p, [P(s2s_model_dims), c_void_p]),
     ("s2s_attn_dropout_mask", c_void_p, [P(s2s_attn_dims), c_void_p]),
-    ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_int, c_void_p,
-                             c_void_p]),
+    ("s2s_nll_seed", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                             c_void_p, c_void_p]),
     ("s2s_model_param_count", c_size_t, [P(s2s_model_dims)]),
     ("s2s_model_param_offset", c_long, [P(s2s_model_dims), c_int, P(c_long)]),
     ("s2s_model_workspace_bytes", c_size_t, [P(s2s_model_dims)]),

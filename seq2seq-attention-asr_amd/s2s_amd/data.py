@@ -17,10 +17,11 @@ whose keys are the HDF5 paths ("<i>/x", "<i>/chars", "train/x", ...) -- what `wr
 (synthetic corpora in the reference's layout).
 
 Batching: the trainer runs one utterance per forward (timit/timit.lua:240-265: variable-length
-utterances, gradients summed over the minibatch, then divided by B, :292-295).  The batched C ABI
-needs equal (L, T) inside a launch, so a minibatch is split into equal-shape groups
-(`bucket_by_shape`) that accumulate into the same gradient with scale 1/B
-(`ChorowskiBaseline.step_ragged`) -- exactly the per-utterance sum, no padding or masking.
+utterances, gradients summed over the minibatch, then divided by B, :292-295).  The batched C ABI takes
+padded (B, L_max) batches with per-utterance frame / label lengths (s2s_model_dims.frame_lengths /
+label_lengths): masked recurrences, masked attention and loss seed give the per-utterance results
+(`ChorowskiBaseline.step_ragged` sorts by length, pads and steps, accumulating with scale 1/B).
+`bucket_by_shape` groups exactly equal shapes (no padding at all) for callers that want that.
 """
 import os
 from collections import OrderedDict

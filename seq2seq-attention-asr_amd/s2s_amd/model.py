@@ -12,7 +12,7 @@ import torch
 
 from . import _lib
 from ._lib import check, lib
-from .nn import _bytes, dptr, get_context, saved_view, stream_ptr
+from .nn import _bytes, dptr, get_context, lengths_tensor, saved_view, stream_ptr
 
 
 @dataclasses.dataclass
@@ -142,6 +142,7 @@ class ChorowskiBaseline:
         self._wsbuf = None
         self._mask_buf = None
         self._outputs = {}
+        self._lenbufs = {}
         self.train = True
         self._steps = 0
         # default dropout seeds: a per-step counter mixed with the init seed and the data-parallel rank,
@@ -204,14 +205,17 @@ class ChorowskiBaseline:
         check(lib.s2s_stream_wait_bucket(self.ctx.handle, ctypes.c_void_p(stream.cuda_stream), i))
 
     def step(self, x, labels, scale=None, zero_grads=True, normalizeNLL=True, logp=None, nll=None, stream=None,
-             dropout_seed=None, dropout_mask=None, bucket_events=False):
+             dropout_seed=None, dropout_mask=None, bucket_events=False, frame_lengths=None, label_lengths=None):
         """One training-step gradient (timit/timit.lua:240-295): grads (+)= scale * d(sum_b nll_b)/dparams,
         scale = 1/B when B > 1 (timit.lua:292-295).  Returns (nll (B,), logp (B, T, O)); unless given, both
         are module-owned buffers overwritten by the next step of the same shape (Torch's self.output).
         With cfg.dropout > 0 (training mode) the decoder MLP input is dropped out with masks drawn
         in-kernel from dropout_seed (default: a per-step counter) or given as dropout_mask
         (B, T, S+A) multipliers.  bucket_events=True records the per-bucket "gradients final" events
-        that dist.allreduce_buckets waits on."""
+        that dist.allreduce_buckets waits on.
+        frame_lengths / label_lengths: (B,) frames and labels per utterance of a padded variable-length
+        batch (each in [1, L] / [1, T]): the step then equals the reference's per-utterance loop over the
+        unpadded utterances (timit/timit.lua:239-295); logp rows past T_b are padding."""
         if x.dim() == 2:
             x = x[None]
         if labels.dim() == 1:
@@ -251,6 +255,24 @@ class ChorowskiBaseline:
                     self._mask_buf = torch.empty(n, device=self.device, dtype=torch.float32)
                 self._mask_buf[:n].copy_(dropout_mask.reshape(-1))
                 d.dropout_mask = self._mask_buf.data_ptr()
+        if frame_lengths is not None or label_lengths is not None:
+            fl = lengths_tensor(frame_lengths if frame_lengths is not None else [L] * B, B, L, "cpu")
+            tl = lengths_tensor(label_lengths if label_lengths is not None else [T] * B, B, T, "cpu")
+            # model-owned (2, B) device buffer: a stable pointer (part of a captured step's key) whose
+            # contents the replayed kernels read at run time; written on the step's stream
+            buf = self._lenbufs.get(B)
+            if buf is None:
+                buf = torch.empty((2, B), dtype=torch.int32, device=self.device)
+                self._lenbufs[B] = buf
+            host = torch.stack([fl, tl]).pin_memory()
+            if stream is not None:
+                with torch.cuda.stream(stream):
+                    buf.copy_(host, non_blocking=True)
+            else:
+                buf.copy_(host, non_blocking=True)
+            self._len_host = host  # kept alive until the copy has run
+            d.frame_lengths = buf[0].data_ptr()
+            d.label_lengths = buf[1].data_ptr()
         flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
         if bucket_events:
             flags |= _lib.S2S_BUCKET_EVENTS
@@ -260,29 +282,39 @@ class ChorowskiBaseline:
         self._last = (B, L, T)
         return nll, logp
 
-    def step_ragged(self, xs, labels, max_batch=None, normalizeNLL=True):
+    def step_ragged(self, xs, labels, max_batch=None, normalizeNLL=True, stream=None):
         """The reference's minibatch over variable-length utterances (timit/timit.lua:240-295: one
-        forward/backward per utterance, gradients summed, then / B): utterances are grouped by equal
-        (L, T) (data.bucket_by_shape) and each group runs as one batched step accumulating into the same
-        gradient with scale 1/B (B = all utterances), so the result is the per-utterance sum exactly.
+        forward/backward per utterance, gradients summed, then / B) as padded, length-masked batched steps:
+        utterances sorted by length, cut into batches of at most max_batch (default: all), each padded to its
+        longest utterance and run with frame_lengths / label_lengths, accumulating into the same gradient
+        with scale 1/B (B = all utterances) -- the per-utterance sum up to fp32 reassociation.
         xs: list of (L_i, F) float32 CUDA tensors; labels: list of (T_i,) 0-based int tensors.
-        Returns nll (B,) in input order and the per-utterance logp list."""
-        from .data import bucket_by_shape
+        Returns nll (B,) in input order and the per-utterance logp list ((T_i, O) each)."""
         if len(xs) != len(labels) or not xs:
             raise ValueError("step_ragged needs one label sequence per utterance")
         B = len(xs)
         scale = 1.0 / B if B > 1 else 1.0
         nll = torch.empty(B, device=self.device, dtype=torch.float32)
         logps = [None] * B
+        order = sorted(range(B), key=lambda i: (xs[i].shape[0], labels[i].shape[0]))
+        nb = max_batch or B
         first = True
-        for idx in bucket_by_shape([(x.shape[0], y.shape[0]) for x, y in zip(xs, labels)], max_batch):
-            x = torch.stack([xs[i] for i in idx]).contiguous()
-            y = torch.stack([labels[i].to(torch.int32) for i in idx]).contiguous()
-            n, lp = self.step(x, y, scale=scale, zero_grads=first, normalizeNLL=normalizeNLL)
+        for c0 in range(0, B, nb):
+            idx = order[c0:c0 + nb]
+            Ls = [xs[i].shape[0] for i in idx]
+            Ts = [labels[i].shape[0] for i in idx]
+            L, T, F = max(Ls), max(Ts), xs[idx[0]].shape[1]
+            x = torch.zeros((len(idx), L, F), device=self.device, dtype=torch.float32)
+            y = torch.zeros((len(idx), T), device=self.device, dtype=torch.int32)
+            for j, i in enumerate(idx):
+                x[j, :Ls[j]] = xs[i]
+                y[j, :Ts[j]] = labels[i].to(torch.int32)
+            n, lp = self.step(x, y, scale=scale, zero_grads=first, normalizeNLL=normalizeNLL, stream=stream,
+                              frame_lengths=Ls, label_lengths=Ts)
             first = False
             nll[torch.tensor(idx, device=self.device)] = n
             for j, i in enumerate(idx):
-                logps[i] = lp[j].clone()  # lp is the module-owned output, reused by the next group
+                logps[i] = lp[j, :Ts[j]].clone()  # lp is the module-owned output, reused by the next batch
         return nll, logps
 
     # ---- the decoder's trainer-visible surface after a step (timit/timit.lua:519-521, 534-536)

@@ -78,6 +78,18 @@ class S2SArgumentError(ValueError):
     pass
 
 
+def lengths_tensor(lengths, n, maxlen, device):
+    """(n,) int32 device tensor of per-utterance lengths, each in [1, maxlen] (checked on the host: the
+    kernels trust them)."""
+    t = torch.as_tensor(lengths).to(torch.int64).reshape(-1)
+    if t.numel() != n:
+        raise S2SArgumentError(f"lengths: {t.numel()} values for {n} utterances")
+    tc = t.cpu()
+    if int(tc.min()) < 1 or int(tc.max()) > maxlen:
+        raise S2SArgumentError(f"lengths must be in [1, {maxlen}]")
+    return tc.to(torch.int32).to(device)
+
+
 def _uniform(shape, stdv, gen=None):
     return (torch.rand(shape, generator=gen, dtype=torch.float64) * 2 - 1).mul_(stdv).float()
 
@@ -201,6 +213,18 @@ class _GruSeq(Module):
             return input.shape
         raise S2SArgumentError("input dimension must be 2D or 3D")  # RNN.lua:128
 
+    # variable-length batch: (B,) frames per utterance (the reference forwards each utterance alone,
+    # timit/timit.lua:239-240); None = every utterance has all L frames
+    lengths = None
+
+    def _lengths_ptr(self, B, L, dev):
+        if self.lengths is None:
+            return ctypes.c_void_p(0)
+        if self.lstm:
+            raise S2SArgumentError("lengths: variable-length batches run on the GRU encoder only")
+        self._len_dev = lengths_tensor(self.lengths, B, L, dev)
+        return dptr(self._len_dev)
+
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
         B, L, D = self._shape(input)
@@ -223,8 +247,8 @@ class _GruSeq(Module):
             self._saved = [_bytes(lib.s2s_gru_saved_bytes(B, L, H), dev) for _ in range(nd)]
             scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
             sv = ptr_array([s.data_ptr() for s in self._saved])
-            check(lib.s2s_gru_fwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, y, nd * H, sv, dptr(scr),
-                                  scr.numel()))
+            check(lib.s2s_gru_fwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, y, nd * H, sv,
+                                  self._lengths_ptr(B, L, dev), dptr(scr), scr.numel()))
         self._dims = (B, L, D)
         self.output = out if input.dim() == 3 else out[0]
         return self.output
@@ -248,7 +272,7 @@ class _GruSeq(Module):
         else:
             scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
             check(lib.s2s_gru_bwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv, dy, nd * H, dptr(dx),
-                                  D, 0, dW, float(scale), dptr(scr), scr.numel()))
+                                  D, 0, dW, float(scale), self._lengths_ptr(B, L, dev), dptr(scr), scr.numel()))
         self.gradInput = dx if input.dim() == 3 else dx[0]
         return self.gradInput
 
@@ -430,6 +454,20 @@ class Attention(Module):
     # else drawn in-kernel from dropout_seed + the forward count
     dropout_mask = None
     dropout_seed = 0x5eed
+    # variable-length batch: (B,) frames of h and labels per utterance (None = all L / T)
+    frame_lengths = None
+    label_lengths = None
+
+    def _set_lengths(self, d, B, L, T, dev):
+        self._len_keep = []
+        if self.frame_lengths is not None:
+            t = lengths_tensor(self.frame_lengths, B, L, dev)
+            self._len_keep.append(t)
+            d.frame_lengths = t.data_ptr()
+        if self.label_lengths is not None:
+            t = lengths_tensor(self.label_lengths, B, T, dev)
+            self._len_keep.append(t)
+            d.label_lengths = t.data_ptr()
 
     def _dims(self, h, T):
         B, L = (1, h.shape[0]) if h.dim() == 2 else (h.shape[0], h.shape[1])
@@ -442,6 +480,7 @@ class Attention(Module):
             if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
                 d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
                 d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
+            self._set_lengths(d, B, L, T, h.device)
             return d
         p = m.dropout if (m.dropout > 0 and self.train) else 0.0
         d = _lib.s2s_attn_dims(B, L, T, self.annotationDepth, self._scp, self.stateDepth, self.outputDepth,
@@ -450,6 +489,7 @@ class Attention(Module):
         if self.hybridAttendFeatureMaps and self.hybridAttendFeatureMaps > 0:
             d.hybridAttendFilterSize = int(self.hybridAttendFilterSize)
             d.hybridAttendFeatureMaps = int(self.hybridAttendFeatureMaps)
+        self._set_lengths(d, B, L, T, h.device)
         if p > 0:
             self._fwd_count = getattr(self, "_fwd_count", 0) + 1
             d.dropout_seed = (self.dropout_seed * 1000003 + self._fwd_count) & ((1 << 64) - 1)
@@ -614,14 +654,16 @@ def saved_view(buf, p, shape):
     return buf[off:off + 4 * n].view(torch.float32).view(*shape)
 
 
-def nll_seed(logp, labels, normalize=False):
-    """timit/timit.lua:262-282: per-utterance nll and dlogp = -labelmask."""
+def nll_seed(logp, labels, normalize=False, label_lengths=None):
+    """timit/timit.lua:262-282: per-utterance nll and dlogp = -labelmask (label_lengths: (B,) labels per
+    utterance of a variable-length batch; steps past them carry no loss and dlogp = 0)."""
     B, T, O = logp.shape
     lab = labels.to(torch.int32).contiguous()
     nll = torch.empty(B, device=logp.device, dtype=torch.float32)
     dlogp = torch.empty_like(logp)
+    tl = lengths_tensor(label_lengths, B, T, logp.device) if label_lengths is not None else None
     check(lib.s2s_nll_seed(get_context(logp.device.index).handle, stream_ptr(), B, T, O, dptr(logp), dptr(lab),
-                           int(normalize), dptr(nll), dptr(dlogp)))
+                           dptr(tl), int(normalize), dptr(nll), dptr(dlogp)))
     return nll, dlogp
 
 

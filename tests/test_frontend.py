@@ -14,6 +14,9 @@ import torch.nn.functional as F
 from oracle import frontend_oracle as fo
 
 RTOL = 1e-4
+# ill-conditioned tensors: bar = max(RTOL, FLOOR_FACTOR x the fp32 restatement's own error), see
+# tests/test_gpu_fullsize.py
+FLOOR_FACTOR = 16
 
 
 def rel_err(g, r):
@@ -305,7 +308,7 @@ def test_vgg_encoder_matches_oracle(fe):
     import s2s_amd
     rng = np.random.default_rng(12)
     B, L, Fq = 2, 40, 40
-    enc = s2s_amd.VGGEncoder(Fq, outputFrameSize=128, hidden=256).cuda()
+    enc = s2s_amd.VGGEncoder(Fq, outputFrameSize=128, hidden=256, generator=torch.Generator().manual_seed(12)).cuda()
     mods = enc.seq.modules
     convs = [m for m in mods if isinstance(m, fe.SpatialConvolutionMM)]
     lins = [m for m in mods if isinstance(m, fe.TemporalConvolution)]
@@ -330,7 +333,17 @@ def test_vgg_encoder_matches_oracle(fe):
         pairs += [(f"dvgg{l}.W", m.gradWeight, G[f"vgg{l}.W"]), (f"dvgg{l}.b", m.gradBias, G[f"vgg{l}.b"])]
     for l, m in enumerate(lins):
         pairs += [(f"dlin{l}.W", m.gradWeight, G[f"lin{l}.W"]), (f"dlin{l}.b", m.gradBias, G[f"lin{l}.b"])]
-    _assert_grads(pairs)
+    # default init: the conv weight gradients are sums that cancel to ~1e-3 of their terms, beyond what fp32
+    # arithmetic of the reference algorithm itself reaches -- the bar per tensor is max(1e-4, 16 x the fp32
+    # restatement's own error on these inputs) (tests/test_gpu_fullsize.py explains the floor)
+    P32 = {k: v.astype(np.float32) for k, v in P.items()}
+    _, cache32 = fo.vgg_fwd(x.astype(np.float32), P32)
+    G32 = {k: np.zeros_like(v) for k, v in P32.items()}
+    fo.vgg_bwd(P32, cache32, dy.astype(np.float32), G32)
+    floor = {n: rel_err(G32[n[1:]], r) for n, _, r in pairs}
+    errs = {n: rel_err(_np(g), r) for n, g, r in pairs}
+    bad = {n: f"{errs[n]:.2e} (fp32 floor {floor[n]:.2e})" for n in errs if not errs[n] <= max(RTOL, FLOOR_FACTOR * floor[n])}
+    assert not bad, bad
 
 
 # --------------------------------------------------------------------------- external decoder_mlp (VGG model)
