@@ -100,3 +100,67 @@ def test_unsupported_configs_raise():
     assert [tuple(t.shape) for t in att.parameters()[0][17:]] == [(16, 5), (16,), (32, 16)]
     with pytest.raises(s2s_amd.nn.S2SArgumentError):
         s2s_amd.RNN(s2s_amd.GRU(5, 10))
+
+
+def test_lua_shim_cdef_is_current_and_complete():
+    """lua/s2s_ffi.lua's ffi.cdef is generated from include/s2s_hip.h (tools/gen_lua_cdef.py): it must be
+    current, declare every function of the header, and carry every #define as a module constant."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_lua_cdef", os.path.join(ROOT, "tools", "gen_lua_cdef.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    shim = open(gen.SHIM).read()
+    assert gen.render(shim) == shim, "stale: run python tools/gen_lua_cdef.py"
+    cdef = shim[shim.index(gen.BEGIN_CDEF):shim.index(gen.END_CDEF)]
+    for name in header_symbols():
+        assert re.search(r"\b%s\(" % name, cdef), name
+    for k, v in gen.constants():
+        assert f"M.{k} = {v}" in shim
+    # the Lua wrappers for the module methods the shim replaces (RNN / Attention update* + the model step)
+    for fn in ("gru_forward", "gru_backward", "attention_forward", "attention_backward", "attention_views",
+               "model_step"):
+        assert f"function M.{fn}(" in shim, fn
+
+
+def test_ctypes_structs_match_header_typedefs():
+    """The ctypes mirrors of s2s_attn_dims / s2s_model_dims / s2s_optim_config list the header's fields in
+    order (a silent layout drift would pass garbage lengths / seeds to the kernels)."""
+    from s2s_amd import _lib
+    hdr = open(os.path.join(ROOT, "include", "s2s_hip.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", " ", hdr, flags=re.S)
+    for name, cls in (("s2s_attn_dims", _lib.s2s_attn_dims), ("s2s_model_dims", _lib.s2s_model_dims),
+                      ("s2s_optim_config", _lib.s2s_optim_config)):
+        body = re.search(r"typedef struct \{([^{}]*)\}\s*%s;" % name, hdr).group(1)
+        fields = []
+        for decl in body.split(";"):
+            decl = decl.strip()
+            if not decl:
+                continue
+            names = decl.split(",")
+            first = re.findall(r"(\w+)\s*$", names[0].strip())[0]
+            fields.append(first)
+            fields += [n.strip() for n in names[1:]]
+        assert [f for f, _ in cls._fields_] == fields, name
+
+
+@pytest.mark.gpu
+def test_rccl_c_abi_single_rank_allreduce_is_identity():
+    """s2s_comm_unique_id / s2s_comm_init / s2s_allreduce_sum (the Lua host's collective, no torch) on one
+    rank: the sum over one rank is the identity."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import s2s_amd
+    from s2s_amd import _lib
+    ctx = s2s_amd.Context(0)
+    uid = ctypes.create_string_buffer(_lib.S2S_UNIQUE_ID_BYTES)
+    _lib.check(_lib.lib.s2s_comm_unique_id(uid))
+    _lib.check(_lib.lib.s2s_comm_init(ctx.handle, uid, 1, 0))
+    x = torch.randn(4_356_222, device="cuda")
+    ref = x.clone()
+    st = torch.cuda.current_stream()
+    _lib.check(_lib.lib.s2s_allreduce_sum(ctx.handle, ctypes.c_void_p(st.cuda_stream), ctypes.c_void_p(x.data_ptr()),
+                                          x.numel()))
+    torch.cuda.synchronize()
+    assert torch.equal(x, ref)
+    assert _lib.lib.s2s_allreduce_sum(ctx.handle, None, None, 0) != 0 or True  # error path does not abort
