@@ -42,6 +42,14 @@ CONFIG_DESC = {
 RAGGED_BATCHES = 8  # length-sorted minibatches cycled by the ragged workload (one captured graph each)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SIMDS = 1024                    # 256 CUs x 4 SIMDs (MfmaUtil's SIMD_NUM)
+HOP_US = 0.22                   # one XCD-local hand-off, measured (tools/pingpong.hip)
+# hand-off seams per recurrence step of each persistent kernel: the latency floor of a
+# launch is seams x steps x HOP_US -- the recurrences are chains of dependent hand-offs
+SEAMS = {"gru_fwd_persist": 2, "gru_bwd_persist": 2, "dec_fwd_xcd": 5, "dec_bwd_xcd": 5}
+# PMC passes (one rocprofv3 run each; MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass)
+PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
+              ("SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"))
 
 
 def flops_per_utterance(cfg, L, T):
@@ -98,10 +106,10 @@ def cpu_baseline(kw, L, T, seconds_budget):
 
 
 def pmc_counters(config):
-    """Per-kernel HBM traffic from rocprofv3 PMC counters, measured in two child passes (FETCH_SIZE and
-    WRITE_SIZE cannot share one pass: MI355X_MICROARCH.md, rocprofv3 PMC slots) of a short eager run
-    of this same workload.  Called before this process touches the GPU.  Returns
-    {kernel name: {"FETCH_SIZE": KB per dispatch, "WRITE_SIZE": KB per dispatch}} or None."""
+    """Per-kernel PMC counters from rocprofv3, one child pass per PMC_PASSES entry (FETCH_SIZE and WRITE_SIZE
+    cannot share one pass: MI355X_MICROARCH.md, rocprofv3 PMC slots) of a short eager run of this same
+    workload: HBM traffic and MFMA instruction / busy counts.  Called before this process touches the GPU.
+    Returns {kernel name: {counter: value per dispatch}} or None."""
     import csv
     import glob
     import shutil
@@ -111,9 +119,9 @@ def pmc_counters(config):
     if not exe:
         return None
     out = {}
-    for ctr in ("FETCH_SIZE", "WRITE_SIZE"):
+    for ctrs in PMC_PASSES:
         d = tempfile.mkdtemp(prefix="s2s_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
-        cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", ctr, "--output-format", "csv", "-d", d, "-o", "pmc",
+        cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", *ctrs, "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu",
                "--no-kernel-timing", "--no-pmc", "--no-graph", "--config", config]
         try:
@@ -126,15 +134,56 @@ def pmc_counters(config):
         acc = {}
         for f in files:
             for r in csv.DictReader(open(f)):
-                if r.get("Counter_Name") != ctr:
+                ctr = r.get("Counter_Name")
+                if ctr not in ctrs:
                     continue
-                a = acc.setdefault(r["Kernel_Name"], [0.0, 0])
-                a[0] += float(r["Counter_Value"])
-                a[1] += 1
-        for k, (v, n) in acc.items():
-            out.setdefault(k, {})[ctr] = v / n
+                a = acc.setdefault((r["Kernel_Name"], ctr), {})
+                # one row per dispatch and counter (values summed over the counter's instances); keyed by
+                # dispatch so a counter reported in several rows of one dispatch adds up
+                key = r.get("Dispatch_Id") or len(a)
+                a[key] = a.get(key, 0.0) + float(r["Counter_Value"])
+        for (k, ctr), per in acc.items():
+            out.setdefault(k, {})[ctr] = sum(per.values()) / len(per)
         shutil.rmtree(d, ignore_errors=True)
     return out
+
+
+def mfma_of(pmc, family, avg_us):
+    """MFMA evidence per launch of a kernel family: F32 MFMA flops executed (MOPS x 512), MFMA-busy SIMD cycles
+    and the busy fraction of the SIMDs over the dispatch (GRBM_GUI_ACTIVE / 8 = the dispatch's cycles:
+    rocprofv3 sums it over the 8 XCDs, MI355X_MICROARCH.md DVFS note)."""
+    if not pmc:
+        return None
+    family = SYMBOL.get(family, family)
+    rows = [v for k, v in pmc.items() if family in k and "SQ_INSTS_VALU_MFMA_MOPS_F32" in v]
+    if not rows:
+        return None
+    mops = sum(v["SQ_INSTS_VALU_MFMA_MOPS_F32"] for v in rows) / len(rows)
+    busy = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for v in rows) / len(rows)
+    grbm = sum(v.get("GRBM_GUI_ACTIVE", 0.0) for v in rows) / len(rows)
+    cycles = grbm / 8.0
+    out = {"SQ_INSTS_VALU_MFMA_MOPS_F32": round(mops), "mfma_flops_per_launch": round(512.0 * mops),
+           "SQ_VALU_MFMA_BUSY_CYCLES": round(busy), "GRBM_GUI_ACTIVE": round(grbm),
+           "mfma_busy_frac": round(busy / (cycles * SIMDS), 4) if cycles > 0 else None,
+           "clock_GHz_from_GRBM": round(cycles / (avg_us * 1e3), 3) if avg_us else None,
+           "source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, eager run"}
+    return out
+
+
+def latency_floor(name, steps, avg_us):
+    """The hand-off chain a persistent recurrence cannot beat: seams per step x steps x one measured hop."""
+    seams = SEAMS.get(name)
+    if not seams or not avg_us:
+        return None
+    floor = seams * steps * HOP_US
+    return {"seams_per_step": seams, "steps": steps, "hop_us": HOP_US, "floor_us": round(floor, 1),
+            "frac": round(floor / avg_us, 4),
+            "what": "seams x steps x one XCD-local hand-off (tools/pingpong.hip); the compute inside each seam "
+                    "is on top of it"}
+
+
+# live-timing family -> the kernel symbol rocprofv3 reports
+SYMBOL = {"dec_fwd_xcd": "dec_xcd_fwd", "dec_bwd_xcd": "dec_xcd_bwd"}
 
 
 def traffic_of(pmc, family):
@@ -143,6 +192,7 @@ def traffic_of(pmc, family):
     HBM), so the read side is doubled."""
     if not pmc:
         return None, None
+    family = SYMBOL.get(family, family)
     rows = [v for k, v in pmc.items() if family in k and "FETCH_SIZE" in v and "WRITE_SIZE" in v]
     if not rows:
         return None, None
@@ -323,12 +373,25 @@ def main():
         x, labels = batches[RAGGED_BATCHES // 2][:2]  # the profiled steps (unmasked, median batch)
     if rank == 0 and not args.no_kernel_timing:
         with torch.cuda.stream(stream):
-            out["roofline"], out["kernels"] = s2s_profile.dominant_kernel_roofline(
+            out["roofline"], out["kernels"], dec = s2s_profile.dominant_kernel_roofline(
                 model, x, labels, stream, PEAK_FP32_MFMA_TFLOPS, PEAK_HBM_GBS)
         if out["roofline"]:
-            t, detail = traffic_of(pmc, out["roofline"]["kernel"])
-            out["roofline"]["traffic"] = round(t) if t is not None else None
-            out["roofline"]["traffic_detail"] = detail
+            r = out["roofline"]
+            t, detail = traffic_of(pmc, r["kernel"])
+            r["traffic"] = round(t) if t is not None else None
+            r["traffic_detail"] = detail
+            r["mfma_counters"] = mfma_of(pmc, r["kernel"], r["avg_launch_us"])
+            r["latency_floor"] = latency_floor(r["kernel"], L, r["avg_launch_us"])
+        # the decoder recurrences (the attention path): priced against HBM (the attention
+        # re-streams Vh and h every step) and against their own hand-off latency floor
+        out["roofline_decoder"] = []
+        for e in dec:
+            t, detail = traffic_of(pmc, e["kernel"])
+            e["traffic"] = round(t) if t is not None else None
+            e["traffic_detail"] = detail
+            e["mfma_counters"] = mfma_of(pmc, e["kernel"], e["avg_launch_us"])
+            e["latency_floor"] = latency_floor(e["kernel"], T, e["avg_launch_us"])
+            out["roofline_decoder"].append(e)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(kw, L, T, args.cpu_seconds)
     if rank == 0:

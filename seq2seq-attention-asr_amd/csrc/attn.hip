@@ -1129,6 +1129,15 @@ static int dec_persist_variant(const AttnDims& d) {
   return 0;
 }
 
+// algorithmic flops of one decoder recurrence launch (T P_step + T L (2 Sc + A) per utterance,
+// times 2; the backward does twice the forward's products)
+static double dec_flops(const AttnDims& d, bool bwd) {
+  const double S = d.S, Sc = d.Sc, A = d.A, O = d.O, Mk = (double)d.M * d.K;
+  const double p_step = S * Sc + O * S + A * S + 2 * S * S + 3 * S * 2 * S + (S + A) * Mk + d.M * O;
+  const double f = 2.0 * d.B * ((double)d.T * p_step + (double)d.T * d.L * (2 * Sc + A));
+  return bwd ? 2.0 * f : f;
+}
+
 // A persistent launch must be fully co-resident (its workgroups wait on each other).
 static bool co_resident(const void* fn, int grid, size_t dyn_lds) {
   int dev = 0, cus = 0, per_cu = 0;
@@ -1273,7 +1282,9 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_xcd_vbar, dim3((d.Sc + 63) / 64, B), dim3(256), 0, side ? side : st, k, x);
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
-      ProfScope ps(st, "dec_fwd_xcd", 0.0, 0.0);
+      // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
+      // per forward; flops = the step products + the attention contractions
+      ProfScope ps(st, "dec_fwd_xcd", dec_flops(d, false), 4.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
       S2S_TRY(launch_xcd(xp, true, st, k, x));
     }
     // alpha / MonotonicAlignment indicators from the saved scores: only the backward (and alpha())
@@ -1394,7 +1405,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
-      ProfScope ps(st, "dec_bwd_xcd", 0.0, 0.0);
+      ProfScope ps(st, "dec_bwd_xcd", dec_flops(d, true), 8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
       S2S_TRY(launch_xcd(xp, false, st, k, x));
     }
     // dVh / dwe (dec_xcd_dvh) beside the alpha^T dc GEMMs when split; both feed dh

@@ -11,6 +11,7 @@ BOUND = {"gemm_f32": "mfma", "gru_fwd_persist": "mfma", "gru_bwd_persist": "mfma
 # dispatch durations (within 1 %, profiles/r01), whereas a side-stream GEMM's bracket also counts
 # the time it waits for CU residency behind them (117 us by events vs 90 us by rocprofv3).
 CRITICAL = ("gru_bwd_persist", "gru_fwd_persist")
+DECODER = ("dec_fwd_xcd", "dec_bwd_xcd")
 
 
 def collect():
@@ -52,9 +53,9 @@ def dominant_kernel_roofline(model, x, labels, stream, peak_tflops, peak_gbs):
     agg = profile_step(model, x, labels, stream)
     kernels = {k: {"launches_per_step": round(v["launches"], 2), "us_per_step": round(v["total_us"], 2),
                    "avg_us": round(v["total_us"] / max(v["launches"], 1e-9), 3)} for k, v in agg.items()}
-    single = {k: v for k, v in agg.items() if not k.endswith("_steps") and v["flops"] > 0}
+    single = {k: v for k, v in agg.items() if not k.endswith("_steps") and v["flops"] > 0 and k not in DECODER}
     if not single:
-        return None, kernels
+        return None, kernels, []
     crit = {k: v for k, v in single.items() if k in CRITICAL}
     name, v = max((crit or single).items(), key=lambda kv: kv[1]["total_us"])
     avg_us = v["total_us"] / v["launches"]
@@ -71,4 +72,18 @@ def dominant_kernel_roofline(model, x, labels, stream, peak_tflops, peak_gbs):
                           else "largest live time"),
             "algorithmic_flops_per_launch": v["flops"] / v["launches"],
             "algorithmic_bytes_per_launch": v["bytes"] / v["launches"]}
-    return roof, kernels
+    # the decoder recurrences: HBM-priced (algorithmic bytes) with their flop rate beside it
+    dec = []
+    for k in DECODER:
+        if k not in agg or agg[k]["launches"] <= 0 or agg[k]["bytes"] <= 0:
+            continue
+        d = agg[k]
+        us = d["total_us"] / d["launches"]
+        gbs = d["bytes"] / d["launches"] / (us * 1e-6) / 1e9
+        dec.append({"kernel": k, "bound": "hbm", "achieved": round(gbs, 1), "peak": peak_gbs, "unit": "GB/s",
+                    "frac": round(gbs / peak_gbs, 4), "avg_launch_us": round(us, 2),
+                    "algorithmic_bytes_per_launch": d["bytes"] / d["launches"],
+                    "algorithmic_flops_per_launch": d["flops"] / d["launches"],
+                    "tflops": round(d["flops"] / d["launches"] / (us * 1e-6) / 1e12, 3),
+                    "mfma_frac": round(d["flops"] / d["launches"] / (us * 1e-6) / 1e12 / peak_tflops, 4)})
+    return roof, kernels, dec

@@ -22,7 +22,31 @@ def per_kernel(d, ctr):
     return acc
 
 
+def mfma_table(d):
+    """MFMA pass: per kernel F32 MFMA ops (x512 = flops), MFMA-busy cycles and the busy fraction of the
+    1024 SIMDs over the dispatch (GRBM_GUI_ACTIVE / 8 cycles: rocprofv3 sums it over the 8 XCDs)."""
+    p = os.path.join(d, "pmc_MFMA")
+    mops = per_kernel(p, "SQ_INSTS_VALU_MFMA_MOPS_F32")
+    busy = per_kernel(p, "SQ_VALU_MFMA_BUSY_CYCLES")
+    grbm = per_kernel(p, "GRBM_GUI_ACTIVE")
+    out = csv.writer(sys.stdout)
+    out.writerow(["kernel", "dispatches", "mfma_f32_flops_per_dispatch", "mfma_busy_cycles_per_dispatch",
+                  "grbm_gui_active_per_dispatch", "mfma_busy_frac"])
+    rows = []
+    for k in mops:
+        n = mops[k][1]
+        m = mops[k][0] / n
+        b = busy.get(k, [0.0, 1])[0] / busy.get(k, [0.0, 1])[1]
+        g = grbm.get(k, [0.0, 1])[0] / grbm.get(k, [0.0, 1])[1]
+        rows.append((k, n, 512 * m, b, g, b / (g / 8 * 1024) if g else 0.0))
+    rows.sort(key=lambda r: -r[2])
+    for k, n, f, b, g, u in rows:
+        out.writerow([k, n, round(f), round(b), round(g), round(u, 4)])
+
+
 def main():
+    if sys.argv[1] == "--mfma":
+        return mfma_table(sys.argv[2])
     d = sys.argv[1]
     f = per_kernel(os.path.join(d, "pmc_FETCH_SIZE"), "FETCH_SIZE")
     w = per_kernel(os.path.join(d, "pmc_WRITE_SIZE"), "WRITE_SIZE")
