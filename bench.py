@@ -32,13 +32,21 @@ CONFIGS = {
     # minibatches of 32, each padded to its longest utterance, masked (s2s_model_dims.frame_lengths /
     # label_lengths); frames = the utterances' real frames (padding not counted).  L / T: the cap.
     "timit_ragged_b32": (dict(), 32, 264, 98),
+    # BASELINE config 5 single-GPU shape: librispeech/model_vgg.lua (VGG conv stack on (B, 3, 1024, 40),
+    # 1x1 layers 2048, A = 512, S = 256, Sc = 512, two-Maxout decoder_mlp, 29 chars), B = 16 per GPU
+    "librispeech_vgg_b16": (dict(inputFrameSize=40, outputDepth=29), 16, 1024, 200),
 }
 CONFIG_DESC = {
     "timit_chorowski_b32": ("BASELINE config 2", "timit/model_chorowski_baseline.lua"),
     "librispeech_chorowski_b32": ("BASELINE config 4 shape (1 GPU)", "librispeech/model_chorowski_baseline.lua"),
     "timit_chorowski_dropout_b64": ("BASELINE config 3 (fp32)", "timit/model_chorowski_baseline_dropout.lua"),
     "timit_ragged_b32": ("BASELINE config 2 model, TIMIT-like variable lengths", "timit/model_chorowski_baseline.lua"),
+    "librispeech_vgg_b16": ("BASELINE config 5 (1 GPU)", "librispeech/model_vgg.lua"),
 }
+# operand precision of the hoisted GEMMs per config (BASELINE.json: configs 3 and 5 are bf16 MFMA); the
+# recurrences (GRU / attention steps) stay fp32 in every config
+PRECISION = {"timit_chorowski_dropout_b64": "bf16", "librispeech_vgg_b16": "bf16"}
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # MI355X_MICROARCH.md: dense BF16 matrix peak
 RAGGED_BATCHES = 8  # length-sorted minibatches cycled by the ragged workload (one captured graph each)
 PEAK_FP32_MFMA_TFLOPS = 157.3   # MI355X_MICROARCH.md: F32 matrix peak (v_mfma_f32_32x32x2_f32)
 PEAK_HBM_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -49,7 +57,8 @@ HOP_US = 0.22                   # one XCD-local hand-off, measured (tools/pingpo
 SEAMS = {"gru_fwd_persist": 2, "gru_bwd_persist": 2, "dec_fwd_xcd": 5, "dec_bwd_xcd": 5}
 # PMC passes (one rocprofv3 run each; MI355X_MICROARCH.md: FETCH_SIZE and WRITE_SIZE cannot share a pass)
 PMC_PASSES = (("FETCH_SIZE",), ("WRITE_SIZE",),
-              ("SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_VALU_MFMA_BUSY_CYCLES", "GRBM_GUI_ACTIVE"))
+              ("SQ_INSTS_VALU_MFMA_MOPS_F32", "SQ_INSTS_VALU_MFMA_MOPS_BF16", "SQ_VALU_MFMA_BUSY_CYCLES",
+               "GRBM_GUI_ACTIVE"))
 
 
 def flops_per_utterance(cfg, L, T):
@@ -105,7 +114,7 @@ def cpu_baseline(kw, L, T, seconds_budget):
                       f"{wall:.1f} s wall"}
 
 
-def pmc_counters(config):
+def pmc_counters(config, precision):
     """Per-kernel PMC counters from rocprofv3, one child pass per PMC_PASSES entry (FETCH_SIZE and WRITE_SIZE
     cannot share one pass: MI355X_MICROARCH.md, rocprofv3 PMC slots) of a short eager run of this same
     workload: HBM traffic and MFMA instruction / busy counts.  Called before this process touches the GPU.
@@ -123,7 +132,7 @@ def pmc_counters(config):
         d = tempfile.mkdtemp(prefix="s2s_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
         cmd = ["timeout", "-s", "KILL", "150", exe, "--pmc", *ctrs, "--output-format", "csv", "-d", d, "-o", "pmc",
                "--", sys.executable, os.path.abspath(__file__), "--steps", "2", "--warmup", "1", "--no-cpu",
-               "--no-kernel-timing", "--no-pmc", "--no-graph", "--config", config]
+               "--no-kernel-timing", "--no-pmc", "--no-graph", "--config", config, "--precision", precision]
         try:
             subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=170, check=True)
         except Exception:
@@ -149,7 +158,7 @@ def pmc_counters(config):
 
 
 def mfma_of(pmc, family, avg_us):
-    """MFMA evidence per launch of a kernel family: F32 MFMA flops executed (MOPS x 512), MFMA-busy SIMD cycles
+    """MFMA evidence per launch of a kernel family: MFMA flops executed ((F32 + BF16 MOPS) x 512), MFMA-busy SIMD cycles
     and the busy fraction of the SIMDs over the dispatch (GRBM_GUI_ACTIVE / 8 = the dispatch's cycles:
     rocprofv3 sums it over the 8 XCDs, MI355X_MICROARCH.md DVFS note)."""
     if not pmc:
@@ -159,14 +168,17 @@ def mfma_of(pmc, family, avg_us):
     if not rows:
         return None
     mops = sum(v["SQ_INSTS_VALU_MFMA_MOPS_F32"] for v in rows) / len(rows)
+    mops16 = sum(v.get("SQ_INSTS_VALU_MFMA_MOPS_BF16", 0.0) for v in rows) / len(rows)
     busy = sum(v.get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0) for v in rows) / len(rows)
     grbm = sum(v.get("GRBM_GUI_ACTIVE", 0.0) for v in rows) / len(rows)
     cycles = grbm / 8.0
-    out = {"SQ_INSTS_VALU_MFMA_MOPS_F32": round(mops), "mfma_flops_per_launch": round(512.0 * mops),
+    out = {"SQ_INSTS_VALU_MFMA_MOPS_F32": round(mops), "SQ_INSTS_VALU_MFMA_MOPS_BF16": round(mops16),
+           "mfma_flops_per_launch": round(512.0 * (mops + mops16)),
            "SQ_VALU_MFMA_BUSY_CYCLES": round(busy), "GRBM_GUI_ACTIVE": round(grbm),
            "mfma_busy_frac": round(busy / (cycles * SIMDS), 4) if cycles > 0 else None,
            "clock_GHz_from_GRBM": round(cycles / (avg_us * 1e3), 3) if avg_us else None,
-           "source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, eager run"}
+           "source": "rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 "
+                     "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE, eager run"}
     return out
 
 
@@ -203,6 +215,117 @@ def traffic_of(pmc, family):
                                             "source": "rocprofv3 --pmc, 2 passes, eager run"}
 
 
+def cpu_vgg_baseline(L, T, seconds_budget):
+    """CPU restatement of librispeech/model_vgg.lua (oracle/frontend_oracle.py, numpy fp32) on the host:
+    one process, BLAS threads on every core, whole utterances (B = 1, the reference's per-utterance loop)."""
+    import numpy as np
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    from oracle import frontend_oracle as fo
+    P, layers, cfg = fo.vgg_random_case(seed=1234)
+    rng = np.random.default_rng(5)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        x = rng.standard_normal((1, 3, L, 40)).astype(np.float32)
+        lab = rng.integers(0, cfg.outputDepth - 1, (1, T)).astype(np.int32)
+        fo.vgg_model_step(x, lab, P, layers, cfg)
+        n += 1
+        wall = time.perf_counter() - t0
+        if wall >= seconds_budget:
+            break
+    return {"value": round(n * L / wall, 1), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"{n} utterances (3 x {L} x 40 log-mel planes, T={T}, B=1 each, fp32) of librispeech/model_vgg.lua, "
+                      f"oracle/frontend_oracle.py (numpy restatement, not Torch7), one process, BLAS on {cores} "
+                      f"threads, {wall:.1f} s wall"}
+
+
+def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
+    """BASELINE config 5: librispeech/model_vgg.lua training step (VGG encoder -> attention decoder with the
+    two-Maxout decoder_mlp -> loss seed -> backward), B = 16 utterances of 1024 frames per GPU, eager
+    launches (the host-side Sequential of the front-end), all-reduce of every gradient when N > 1."""
+    kw, B, L, T = CONFIGS[args.config]
+    g = torch.Generator().manual_seed(1234 + rank)
+    model = s2s_amd.VGGAttentionModel(kw["inputFrameSize"], outputFrameSize=512, hidden=2048,
+                                      outputDepth=kw["outputDepth"], generator=torch.Generator().manual_seed(1234),
+                                      precision=args.precision).cuda()
+    x = torch.randn((B, 3, L, kw["inputFrameSize"]), generator=g).cuda()
+    labels = torch.randint(0, kw["outputDepth"] - 1, (B, T), generator=g)
+    labels[:, -1] = kw["outputDepth"] - 1
+    labels = labels.to(torch.int32).cuda()
+    grads = model.parameters()[1]
+
+    def step():
+        model.zeroGradParameters()
+        model.step(x, labels)
+        if world > 1:  # one flat all-reduce per gradient tensor list (RCCL)
+            for gt in grads:
+                dist.all_reduce(gt)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = 1000.0 * elapsed / args.steps
+    value = world * B * L / (ms / 1000.0)
+    out = {"metric": "log-mel frames/sec fwd+bwd, librispeech/model_vgg.lua",
+           "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+           "dtype": args.precision,
+           "precision_note": ("bf16 operands / fp32 accumulation in every GEMM (VGG convolutions, 1x1 layers, Vh, "
+                              "decoder folds and MLP, weight gradients); decoder recurrence fp32; fp32 master weights"
+                              if args.precision == "bf16" else "fp32 everywhere"),
+           "data": "synthetic (N(0,1) 3-plane log-mel-shaped input, uniform char labels, random-init weights)",
+           "config": {"workload": f"{CONFIG_DESC[args.config][0]}: {args.config}", "model": CONFIG_DESC[args.config][1],
+                      "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
+                      "feat_dim": kw["inputFrameSize"], "annotation_frames": (L - 8) // 2,
+                      "parallelism": f"dp{world}", "launch": "eager"}}
+    if rank == 0 and not args.no_kernel_timing:
+        from s2s_amd import _lib
+        from s2s_amd import profile as s2s_profile
+        _lib.check(_lib.lib.s2s_prof_enable(1))
+        s2s_profile.collect()
+        for _ in range(2):
+            step()
+        torch.cuda.synchronize()
+        agg = s2s_profile.collect()
+        _lib.lib.s2s_prof_enable(0)
+        fam = "gemm_bf16" if args.precision == "bf16" else "gemm_f32"
+        out["kernels"] = {k: {"launches_per_step": v["launches"] / 2, "us_per_step": round(v["total_us"] / 2, 1)}
+                          for k, v in agg.items()}
+        if fam in agg and agg[fam]["launches"] > 0:
+            v = agg[fam]
+            avg = v["total_us"] / v["launches"]
+            ach = v["flops"] / v["launches"] / (avg * 1e-6) / 1e12
+            peak = PEAK_BF16_MFMA_TFLOPS if args.precision == "bf16" else PEAK_FP32_MFMA_TFLOPS
+            t, detail = traffic_of(pmc, "gemm_" + ("bf16" if args.precision == "bf16" else "f32"))
+            out["roofline"] = {"kernel": fam, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
+                               "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+                               "traffic": round(t) if t is not None else None, "traffic_detail": detail,
+                               "avg_launch_us": round(avg, 2), "launches_per_step": v["launches"] / 2,
+                               "selection": "the GEMM family: the VGG step's MFMA-bound work (largest live time)",
+                               "mfma_counters": mfma_of(pmc, "gemm_" + ("bf16" if args.precision == "bf16" else "f32"),
+                                                        avg)}
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_vgg_baseline(L, T, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -217,15 +340,19 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC traffic passes")
+    ap.add_argument("--precision", choices=("auto", "fp32", "bf16", "bf16-all"), default="auto",
+                    help="operand precision of the hoisted GEMMs (auto: BASELINE's per config)")
     ap.add_argument("--flat-allreduce", action="store_true",
                     help="N>1: one all-reduce of the whole gradient after the step instead of the bucketed, "
                          "overlapped one")
     args = ap.parse_args()
+    if args.precision == "auto":
+        args.precision = PRECISION.get(args.config, "fp32")
 
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
     pmc = None
     if world0 == 1 and not args.no_pmc and not args.no_kernel_timing:
-        pmc = pmc_counters(args.config)  # child processes, before this one initialises the GPU
+        pmc = pmc_counters(args.config, args.precision)  # child processes, before this one initialises the GPU
 
     import torch
     import torch.distributed as dist
@@ -241,9 +368,11 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     kw, B, L, T = CONFIGS[args.config]
+    if args.config == "librispeech_vgg_b16":
+        return run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist)
     cfg = s2s_amd.ModelConfig(**kw)
     model = s2s_amd.ChorowskiBaseline(cfg, graph=not args.no_graph, seed=1234,
-                                     overlap=not args.no_overlap)
+                                     overlap=not args.no_overlap, precision=args.precision)
     g = torch.Generator(device="cpu").manual_seed(1234 + rank)
     eos = 23 if cfg.outputDepth > 23 else cfg.outputDepth - 1
 
@@ -351,7 +480,11 @@ def main():
         "metric": "log-mel frames/sec fwd+bwd, Chorowski TIMIT baseline",
         "value": round(value, 1), "unit": "frames/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
-        "dtype": "fp32", "data": "synthetic (N(0,1) log-mel-shaped features, uniform labels, random-init weights)",
+        "dtype": args.precision,
+        "precision_note": ("fp32 everywhere (exact f32 MFMA)" if args.precision == "fp32" else
+                           "bf16 operands / fp32 accumulation in the hoisted GEMMs (x-projections, Vh, MLP, dX, "
+                           "weight gradients); recurrences fp32; fp32 master weights"),
+        "data": "synthetic (N(0,1) log-mel-shaped features, uniform labels, random-init weights)",
         "config": {"workload": f"{CONFIG_DESC[args.config][0]}: {args.config}", "model": CONFIG_DESC[args.config][1],
                    "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
                    "feat_dim": cfg.inputFrameSize, "parallelism": f"dp{world}",

@@ -54,6 +54,17 @@ int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
  * it is destroyed).  The in-kernel dropout seed is not part of the key (it is read from a device word
  * the host writes before each replay).  Stats: graphs captured, replays launched, graphs cached. */
 int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
+/* Operand precision of the hoisted GEMMs of the context's calls (the recurrences stay fp32):
+ *   S2S_PREC_FP32 (default): exact f32 MFMA (v_mfma_f32_32x32x2_f32) everywhere;
+ *   S2S_PREC_BF16_GEMM: the forward and data-gradient GEMMs (front-end convolutions, x-projections, Vh,
+ *     decoder MLP, dX / dh) round their operands to bf16 when staged (v_mfma_f32_16x16x32_bf16, fp32
+ *     accumulation and output, fp32 master weights / activations in HBM); weight gradients and the
+ *     decoder's weight folds stay fp32 (cancelling sums: BASELINE configs 3 and 5);
+ *   S2S_PREC_BF16_ALL: the weight-gradient GEMMs in bf16 too. */
+#define S2S_PREC_FP32 0
+#define S2S_PREC_BF16_GEMM 1
+#define S2S_PREC_BF16_ALL 2
+int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
 int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
 
 /* ---------------------------------------------------------------- GRU layer

@@ -331,3 +331,33 @@ def vgg_model_step(x: Array, labels: Array, P: Dict[str, Array], mlp_layers, cfg
     dh = orc.attention_bwd(Pd, cfg, acache, None, G, scale, dmlp_in=dv.reshape(B, T, -1))
     vgg_bwd(P, ecache, dh, G, scale)
     return nll, logp, G, mgrads
+
+
+def vgg_random_case(F: int = 40, hidden: int = 2048, out: int = 512, S: int = 256, Sc: int = 512, O: int = 29,
+                    M: int = 64, seed: int = 1234, dtype=np.float32):
+    """Parameters of a librispeech/model_vgg.lua model at the reference's default init (U(+-1/sqrt(fan_in)),
+    nn.Linear / SpatialConvolutionMM / TemporalConvolution resets) as (P, mlp layers, decoder cfg) for
+    vgg_model_step: the CPU-baseline workload of bench.py's config-5 line (a port of the reference, timed)."""
+    rng = np.random.default_rng(seed)
+
+    def u(shape, fan_in):
+        return (rng.uniform(-1.0, 1.0, shape) / np.sqrt(fan_in)).astype(dtype)
+
+    P = {}
+    for l, (ci, co) in enumerate(VGG_CONVS):
+        P[f"vgg{l}.W"], P[f"vgg{l}.b"] = u((co, ci * 9), ci * 9), u((co,), ci * 9)
+    for l, (di, do) in enumerate(vgg_dims(F, hidden, out)):
+        P[f"lin{l}.W"], P[f"lin{l}.b"] = u((do, di), di), u((do,), di)
+    A = out
+    for name, shape, fan in (("V", (Sc, A), A), ("Ws", (Sc, S), S), ("bs", (Sc,), S), ("we", (1, Sc), Sc),
+                             ("Wy", (S, O), O), ("by", (S,), O), ("Wc", (S, A), A), ("bc", (S,), A),
+                             ("Wd", (S, 2 * S), 2 * S), ("bd", (S,), 2 * S), ("dec.Wz", (S, 2 * S), 2 * S),
+                             ("dec.Wr", (S, 2 * S), 2 * S), ("dec.Wh", (S, 2 * S), 2 * S)):
+        P[name] = u(shape, fan)
+    k = 7
+    layers = [("maxout", u((M * k, S + A), S + A), u((M * k,), S + A), k), ("linear", u((M, M), M), u((M,), M)),
+              ("maxout", u((M * k, M), M), u((M * k,), M), k), ("linear", u((O, M), M), u((O,), M)),
+              ("logsoftmax",)]
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=k, numLayers=1)
+    return P, layers, cfg

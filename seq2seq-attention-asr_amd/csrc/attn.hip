@@ -1216,6 +1216,7 @@ static int launch_xcd(const XPlan& xp, bool fwd, hipStream_t st, AttnK& k, XArgs
 // Weight folds and teacher-forced constants of the XCD-local decoder (params and labels only, so
 // the model step runs it on the side stream beside the encoder).
 static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const GemmWs& gws) {
+  WgradPrecision wp;  // the weight folds Wx' = W_d Wd_c Wc are reused by every step: fp32
   const int S = d.S, A = d.A, rows = d.B * d.T;
   // On the side stream beside the encoder its kernels run only in the gaps the persistent GRU launches
   // leave: the re-layouts and y_in in one launch, then BKD, then the GEMM chain.
@@ -1473,6 +1474,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
 // step runs it on a side stream beside the encoder BPTT.
 int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                    const void* saved, const AttnGrads& G, float scale, void* scratch) {
+  WgradPrecision wp;
   AttnK k{};
   XArgs x{};
   carve(d, &k, (char*)saved, (char*)scratch, &x);

@@ -80,6 +80,7 @@ struct GraphKey {
   const void* ptrs[7];
   float scale;
   int flags;
+  int precision;
   void* stream;
   bool operator==(const GraphKey& o) const { return std::memcmp(this, &o, sizeof(GraphKey)) == 0; }
 };
@@ -98,6 +99,7 @@ constexpr int kGraphCacheDefault = 8;
 struct s2s_ctx {
   int device = 0;
   int flags = 0;
+  int precision = S2S_PREC_FP32;  // S2S_PREC_*: operand precision of the hoisted GEMMs
   hipStream_t side = nullptr;     // weight-gradient GEMMs run here beside the critical path
   hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
   unsigned long long* seed_dev = nullptr;  // dropout seed word read by this context's replayed graphs
@@ -114,9 +116,12 @@ struct s2s_ctx {
 
 namespace {
 
+// every compute entry point starts here: the device, and the context's GEMM precision for this call
 int set_device(s2s_ctx* ctx) {
   S2S_REQUIRE(ctx != nullptr, "null context");
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
+  set_gemm_precision(ctx->precision == S2S_PREC_FP32 ? kGemmF32 : kGemmBf16);
+  set_wgrad_bf16(ctx->precision == S2S_PREC_BF16_ALL);
   return 0;
 }
 
@@ -562,6 +567,14 @@ int s2s_ctx_set_flags(s2s_ctx* ctx, int flags) {
   return 0;
 }
 
+int s2s_ctx_set_precision(s2s_ctx* ctx, int precision) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  S2S_REQUIRE(precision == S2S_PREC_FP32 || precision == S2S_PREC_BF16_GEMM || precision == S2S_PREC_BF16_ALL,
+              "unknown precision");
+  ctx->precision = precision;
+  return 0;
+}
+
 size_t s2s_gru_saved_bytes(int B, int L, int H) { return sizeof(float) * (size_t)B * L * 5 * H; }
 size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H) {
   return gru_layer_scratch_bytes(ndir, B, L, D, H);
@@ -929,6 +942,7 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   std::memcpy(key.ptrs, ptrs, sizeof(ptrs));
   key.scale = scale;
   key.flags = flags;
+  key.precision = ctx->precision;
   key.stream = stream;
   CachedGraph* hit = nullptr;
   for (auto& g : ctx->graphs)
@@ -1100,3 +1114,15 @@ int s2s_allreduce_sum(s2s_ctx* ctx, s2s_stream_t stream, float* buf, size_t coun
 
 // diagnostic: 1 runs the decoder's off-path kernels (vbar, alpha/indicators, dVh) on the side stream
 extern "C" void s2s_debug_dec_side(int on) { g_dec_side = on; }
+
+// diagnostic (not part of the C ABI header): one GEMM C = alpha op(A) op(B) + beta C through the library's
+// MFMA GEMM (bf16 = 1: the bf16-operand kernels), on the legacy default stream; for the layout tests
+extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float alpha, const float* A, long lda,
+                              const float* B, long ldb, float beta, float* C, long ldc, int bf16, float* ws,
+                              size_t ws_floats) {
+  s2s::set_gemm_precision(bf16 ? s2s::kGemmBf16 : s2s::kGemmF32);
+  const int rc = s2s::gemm1(nullptr, transA != 0, transB != 0, M, N, K, alpha, A, lda, B, ldb, beta, C, ldc, nullptr,
+                            s2s::GemmWs{ws, ws ? ws_floats : 0});
+  s2s::set_gemm_precision(s2s::kGemmF32);
+  return rc;
+}

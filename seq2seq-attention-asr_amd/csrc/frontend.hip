@@ -358,8 +358,11 @@ int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
   const long rows = (long)B * L - kW + 1;  // every window start of the flattened batch
   // gradBias += scale * sum_t dY_t ; gradWeight += scale * dY^T [x_t | ... | x_{t+kW-1}]
   if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db, ws_of(scratch)));
-  if (dW) S2S_TRY(gemm1(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
-                        nullptr, ws_of(scratch)));
+  if (dW) {
+    WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
+    S2S_TRY(gemm1(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
+                  nullptr, ws_of(scratch)));
+  }
   if (dx) {
     S2S_TRY(gemm1(st, false, false, B * L, kW * Din, Dout, 1.f, dyp, Dout, W, (long)kW * Din, 0.f, dU,
                   (long)kW * Din));
@@ -453,6 +456,7 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
     launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
     S2S_CHECK_HIP(hipGetLastError());
     // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
+    WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
     S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
   }
   if (dx) {

@@ -168,6 +168,201 @@ __device__ __forceinline__ void gemm_mainloop(floatx16 (&acc)[BM / 64][BN / 64],
   }
 }
 
+// ------------------------------------------------------------------ bf16 MFMA variant
+// Same problem batching, XCD dealing and split-K as gemm_f32_kernel; the fp32 operands are rounded to bf16
+// (RNE, v_cvt_pk_bf16_f32) while staged into LDS and multiplied with v_mfma_f32_16x16x32_bf16 (fp32
+// accumulate; 16x the f32-MFMA rate), fp32 master operands in HBM, fp32 output.
+//  * K-tile HBK = 64 (one barrier per 64-deep step); LDS rows of 64 bf16 + 8 pad (144-byte rows:
+//    conflict-free ds_read_b128 per 16-lane group);
+//  * each wave owns a (BM/2) x (BN/2) sub-tile = FM x FN accumulators of 16 x 16 (4 x 4 at 128 x 128);
+//    lane l reads k = 8 (l >> 4) .. +7 of row l & 15 per 32-deep k-step (the bf16 A/B maps);
+//  * k-contiguous operands: float4 global loads -> 4 bf16 -> ds_write_b64; row-contiguous ones
+//    (A of TN, B of NN): a 4 (k) x 4 (rows) block per thread, transposed in registers, 4 ds_write_b64.
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+constexpr int HBK = 64, HLD = HBK + 8;
+
+// k-contiguous operand, R rows x HBK k: thread f (of R * 16 float4) -> row f / 16, k quad f % 16
+template <int R, bool FAST>
+__device__ __forceinline__ void hload_kc(floatx4 (&v)[R / 16], const float* X, long ld, int r0, int rmax, int k0,
+                                         int kend) {
+#pragma unroll
+  for (int j = 0; j < R / 16; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    const int gr = r0 + (f >> 4), k = k0 + 4 * (f & 15);
+    if (FAST) {
+      v[j] = *reinterpret_cast<const floatx4*>(X + (long)gr * ld + k);
+    } else {
+      const float* row = X + (long)min(gr, rmax - 1) * ld;
+      float e[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const float x = row[min(k + c, kend - 1)];
+        e[c] = (gr < rmax && k + c < kend) ? x : 0.f;
+      }
+      v[j] = floatx4{e[0], e[1], e[2], e[3]};
+    }
+  }
+}
+template <int R>
+__device__ __forceinline__ void hstore_kc(__bf16* Xs, const floatx4 (&v)[R / 16]) {
+#pragma unroll
+  for (int j = 0; j < R / 16; ++j) {
+    const int f = threadIdx.x + 256 * j;
+    *reinterpret_cast<bf16x4*>(Xs + (f >> 4) * HLD + 4 * (f & 15)) = __builtin_convertvector(v[j], bf16x4);
+  }
+}
+// row-contiguous operand (element (r, k) at X[k * ld + r]): thread block b (of R * HBK / 16) -> rows
+// 4 (b % (R/4)) .. +3, k 4 (b / (R/4)) .. +3; v[4 j + c] = the float4 of rows at k + c
+template <int R, bool FAST>
+__device__ __forceinline__ void hload_rc(floatx4 (&v)[R / 16], const float* X, long ld, int r0, int rmax, int k0,
+                                         int kend) {
+#pragma unroll
+  for (int j = 0; j < R / 64; ++j) {
+    const int b = threadIdx.x + 256 * j;
+    const int r = r0 + 4 * (b % (R / 4)), kb = k0 + 4 * (b / (R / 4));
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int k = kb + c;
+      if (FAST) {
+        v[4 * j + c] = *reinterpret_cast<const floatx4*>(X + (long)k * ld + r);
+      } else {
+        const float* row = X + (long)min(k, kend - 1) * ld;
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float x = row[min(r + q, rmax - 1)];
+          e[q] = (k < kend && r + q < rmax) ? x : 0.f;
+        }
+        v[4 * j + c] = floatx4{e[0], e[1], e[2], e[3]};
+      }
+    }
+  }
+}
+template <int R>
+__device__ __forceinline__ void hstore_rc(__bf16* Xs, const floatx4 (&v)[R / 16]) {
+#pragma unroll
+  for (int j = 0; j < R / 64; ++j) {
+    const int b = threadIdx.x + 256 * j;
+    const int r = 4 * (b % (R / 4)), kb = 4 * (b / (R / 4));
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 col = {v[4 * j][q], v[4 * j + 1][q], v[4 * j + 2][q], v[4 * j + 3][q]};
+      *reinterpret_cast<bf16x4*>(Xs + (r + q) * HLD + kb) = __builtin_convertvector(col, bf16x4);
+    }
+  }
+}
+
+template <bool TA, bool TB, int BM, int BN, bool FAST>
+__device__ __forceinline__ void gemm_mainloop_bf16(floatx4 (&acc)[BM / 32][BN / 32], __bf16 (&As)[2][BM * HLD],
+                                                   __bf16 (&Bs)[2][BN * HLD], const float* __restrict__ A,
+                                                   const float* __restrict__ Bm, long lda, long ldb, int m0, int n0,
+                                                   int M, int N, int kbeg, int kend, int nk, int wy, int wx,
+                                                   int lane) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  floatx4 ra[BM / 16], rb[BN / 16];
+  if (TA) hload_rc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend); else hload_kc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend);
+  if (TB) hload_kc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend); else hload_rc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend);
+  if (TA) hstore_rc<BM>(As[0], ra); else hstore_kc<BM>(As[0], ra);
+  if (TB) hstore_kc<BN>(Bs[0], rb); else hstore_rc<BN>(Bs[0], rb);
+  __syncthreads();
+  const int lr = lane & 15, lq = 8 * (lane >> 4);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < nk;
+    if (more) {
+      const int k0 = kbeg + (kt + 1) * HBK;
+      if (TA) hload_rc<BM, FAST>(ra, A, lda, m0, M, k0, kend); else hload_kc<BM, FAST>(ra, A, lda, m0, M, k0, kend);
+      if (TB) hload_kc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend); else hload_rc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend);
+    }
+#pragma unroll
+    for (int s = 0; s < HBK / 32; ++s) {
+      bf16x8 a[FM], b[FN];
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+        a[f] = *reinterpret_cast<const bf16x8*>(As[buf] + (wy * WM + 16 * f + lr) * HLD + 32 * s + lq);
+#pragma unroll
+      for (int g = 0; g < FN; ++g)
+        b[g] = *reinterpret_cast<const bf16x8*>(Bs[buf] + (wx * WN + 16 * g + lr) * HLD + 32 * s + lq);
+#pragma unroll
+      for (int f = 0; f < FM; ++f)
+#pragma unroll
+        for (int g = 0; g < FN; ++g)
+          acc[f][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[g], acc[f][g], 0, 0, 0);
+    }
+    if (more) {
+      if (TA) hstore_rc<BM>(As[buf ^ 1], ra); else hstore_kc<BM>(As[buf ^ 1], ra);
+      if (TB) hstore_kc<BN>(Bs[buf ^ 1], rb); else hstore_rc<BN>(Bs[buf ^ 1], rb);
+    }
+    __syncthreads();
+  }
+}
+
+template <bool TA, bool TB, int BM, int BN>
+__global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmLaunch Lc) {
+  constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 16, FN = WN / 16;
+  __shared__ __attribute__((aligned(16))) __bf16 As[2][BM * HLD];
+  __shared__ __attribute__((aligned(16))) __bf16 Bs[2][BN * HLD];
+  const int lin = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (lin >= Lc.nblocks) return;
+  int pi = 0;
+  while (pi + 1 < Lc.nprob && lin >= Lc.q[pi + 1].base) ++pi;
+  const GemmTile& q = Lc.q[pi];
+  int loc = lin - q.base;
+  const int tn = loc % q.tiles_n;
+  loc /= q.tiles_n;
+  const int tm = loc % q.tiles_m, s = loc / q.tiles_m;
+  const int M = q.p.M, N = q.p.N, K = q.p.K;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = s * q.kslice, kend = min(K, kbeg + q.kslice);
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g) acc[f][g] = floatx4{0.f, 0.f, 0.f, 0.f};
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wy = wave >> 1, wx = wave & 1;
+  const int nk = (kend - kbeg + HBK - 1) / HBK;
+  if (nk > 0) {
+    const int Mr = max(M, q.p.Mread), Nr = max(N, q.p.Nread);
+    const bool fast = q.vecA && q.vecB && m0 + BM <= Mr && n0 + BN <= Nr && (kend - kbeg) % HBK == 0;
+    if (fast)
+      gemm_mainloop_bf16<TA, TB, BM, BN, true>(acc, As, Bs, q.p.A, q.p.B, q.p.lda, q.p.ldb, m0, n0, M, N, kbeg, kend,
+                                               nk, wy, wx, lane);
+    else
+      gemm_mainloop_bf16<TA, TB, BM, BN, false>(acc, As, Bs, q.p.A, q.p.B, q.p.lda, q.p.ldb, m0, n0, M, N, kbeg,
+                                                kend, nk, wy, wx, lane);
+  }
+  // epilogue (16 x 16 accumulator map: column lane & 15, rows 4 (lane >> 4) + r)
+  const float alpha = q.p.alpha, beta = q.p.beta;
+  const float* __restrict__ bias = q.p.bias;
+  float* __restrict__ C = q.p.C;
+  float* __restrict__ part = q.part;
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int g = 0; g < FN; ++g) {
+      const int col = n0 + wx * WN + 16 * g + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wy * WM + 16 * f + 4 * (lane >> 4) + r;
+        if (row < M && col < N) {
+          if (part) {
+            part[((long)s * M + row) * N + col] = acc[f][g][r];
+          } else {
+            float v = alpha * acc[f][g][r];
+            if (bias) v += bias[col];
+            if (q.p.rbias) v += q.p.rbias[row];
+            float* c = C + (long)row * q.p.ldc + col;
+            if (beta != 0.f) v += beta * *c;
+            if (q.p.relu) v = fmaxf(v, 0.f);
+            *c = v;
+          }
+        }
+      }
+    }
+}
+
 template <bool TA, bool TB, int BM, int BN>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
@@ -370,6 +565,13 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 
 }  // namespace
 
+static thread_local int g_gemm_prec = kGemmF32;
+static thread_local bool g_wgrad_bf16 = false;
+void set_gemm_precision(int p) { g_gemm_prec = p; }
+int gemm_precision() { return g_gemm_prec; }
+void set_wgrad_bf16(bool on) { g_wgrad_bf16 = on; }
+bool wgrad_bf16() { return g_wgrad_bf16; }
+
 struct GemmPlan {
   int bm = 64, bn = 64, kslice = 0, nblocks = 0;
 };
@@ -377,10 +579,11 @@ struct GemmPlan {
 // Pick the tile shape and a uniform K slice for the batch from a simple time model: every CU
 // (256) works through ceil(blocks / 256) blocks of bm*bn*kslice MACs at a per-shape efficiency,
 // plus the split slabs' HBM round trip and the reduce launch.
-static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats) {
+static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf16) {
   int kmax = 0;
   for (int i = 0; i < n; ++i) kmax = p[i].K > kmax ? p[i].K : kmax;
-  const int kfull = (kmax + BK - 1) / BK * BK;
+  const int kq = bf16 ? HBK : BK;  // K-slices are whole K-tiles of the kernel
+  const int kfull = (kmax + kq - 1) / kq * kq;
   auto count = [&](GemmPlan& pl) {  // blocks and slab floats of a plan; false if the slabs do not fit
     long blocks = 0;
     double slab = 0;
@@ -397,7 +600,7 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats) {
   if (const char* o = std::getenv("S2S_GEMM_PLAN")) {  // "bm:bn:kslice" (diagnostics)
     int bm = 0, bn = 0, ks = 0;
     if (std::sscanf(o, "%d:%d:%d", &bm, &bn, &ks) == 3 && (bm == 128 || bm == 64) && (bn == 128 || bn == 64) &&
-        !(bm == 64 && bn == 128) && ks % BK == 0) {
+        !(bm == 64 && bn == 128) && ks % kq == 0) {
       pl.bm = bm; pl.bn = bn; pl.kslice = ks > 0 ? ks : kfull;
       if (count(pl)) return pl;
     }
@@ -410,10 +613,20 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats) {
   // encoder fwd+bwd.)
   pl.bm = 64; pl.bn = 64; pl.kslice = kfull;
   count(pl);
+  if (bf16) {  // bf16: the largest tile that still fills the chip (more MFMA work per staged byte); 64-row
+    // tiles when every problem has <= 64 rows (the convolutions' Cout = 64 outputs)
+    int mmax = 0;
+    for (int i = 0; i < n; ++i) mmax = std::max(mmax, p[i].M);
+    GemmPlan big = pl;
+    big.bm = mmax <= 64 ? 64 : 128;
+    big.bn = 128;
+    count(big);
+    if (big.nblocks >= 256) pl = big;
+  }
   const int tiles = pl.nblocks;
   while (tiles < 512 && pl.nblocks < 1024 && pl.kslice / 2 >= 512) {
     GemmPlan nx = pl;
-    nx.kslice = (pl.kslice / 2 + BK - 1) / BK * BK;
+    nx.kslice = (pl.kslice / 2 + kq - 1) / kq * kq;
     if (!count(nx)) break;
     pl = nx;
   }
@@ -421,7 +634,14 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats) {
 }
 
 template <bool TA, bool TB>
-static void launch_tiles(hipStream_t st, const GemmPlan& pl, dim3 grid, const GemmLaunch& L) {
+static void launch_tiles(hipStream_t st, const GemmPlan& pl, dim3 grid, const GemmLaunch& L, bool bf16) {
+  if (bf16) {
+    if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, 128, 128>), grid, dim3(256), 0, st, L);
+    else if (pl.bn == 128) hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, 64, 128>), grid, dim3(256), 0, st, L);
+    else if (pl.bm == 128) hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, 128, 64>), grid, dim3(256), 0, st, L);
+    else hipLaunchKernelGGL((gemm_bf16_kernel<TA, TB, 64, 64>), grid, dim3(256), 0, st, L);
+    return;
+  }
   if (pl.bm == 128 && pl.bn == 128) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 128, 128>), grid, dim3(256), 0, st, L);
   else if (pl.bm == 128) hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 128, 64>), grid, dim3(256), 0, st, L);
   else hipLaunchKernelGGL((gemm_f32_kernel<TA, TB, 64, 64>), grid, dim3(256), 0, st, L);
@@ -438,7 +658,8 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
     use[used++] = q;
   }
   if (used == 0) return 0;
-  const GemmPlan pl = plan_gemm(use, used, ws.p ? ws.n : 0);
+  const bool bf16 = gemm_precision() == kGemmBf16;
+  const GemmPlan pl = plan_gemm(use, used, ws.p ? ws.n : 0, bf16);
   GemmLaunch L{};
   L.nprob = used;
   int base = 0;
@@ -467,12 +688,12 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
     bytes += 4.0 * ((double)t.p.M * t.p.K + (double)t.p.K * t.p.N + (double)t.p.M * t.p.N * (t.p.beta != 0.f ? 2 : 1));
   }
   L.nblocks = base;
-  ProfScope ps(st, "gemm_f32", flops, bytes);
+  ProfScope ps(st, bf16 ? "gemm_bf16" : "gemm_f32", flops, bytes);
   const dim3 grid((unsigned)((base + 7) / 8 * 8));
-  if (!transA && !transB) launch_tiles<false, false>(st, pl, grid, L);
-  else if (!transA && transB) launch_tiles<false, true>(st, pl, grid, L);
-  else if (transA && !transB) launch_tiles<true, false>(st, pl, grid, L);
-  else launch_tiles<true, true>(st, pl, grid, L);
+  if (!transA && !transB) launch_tiles<false, false>(st, pl, grid, L, bf16);
+  else if (!transA && transB) launch_tiles<false, true>(st, pl, grid, L, bf16);
+  else if (transA && !transB) launch_tiles<true, false>(st, pl, grid, L, bf16);
+  else launch_tiles<true, true>(st, pl, grid, L, bf16);
   if (split) {
     long mn_max = 0;
     for (int i = 0; i < used; ++i)

@@ -490,6 +490,7 @@ float* gru_layer_dA(const GruLayerIO& io, void* scratch) {
 // dW += scale * dA_g^T . [h_{t-1} | q ; x]   (LinearZeroBias.lua:67-74 summed over all steps).
 // Off the recurrence: the model step runs it on a side stream beside the next layer's BPTT.
 int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws) {
+  WgradPrecision wp;
   const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H;
   const long ldA = 3L * nd * H;
   GemmProblem probs[12];

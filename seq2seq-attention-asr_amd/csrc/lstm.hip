@@ -390,7 +390,10 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
       pr[n++] = GemmProblem{dAd + H, sv + SV_CP * H, G[18], nullptr, ldA, lsv, H, H, H, B * L, gr.scale, 1.f};
       pr[n++] = GemmProblem{dAd + 3 * H, sv + SV_C * H, G[20], nullptr, ldA, lsv, H, H, H, B * L, gr.scale, 1.f};
     }
+    {
+    WgradPrecision wp;  // weight gradients: fp32 under S2S_PREC_BF16_GEMM
     S2S_TRY(gemm_f32(st, pr, n, true, false, c.ws));
+  }
     for (int q = 0; q < 4; ++q) {
       S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 1], c.ws));
       S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 3], c.ws));

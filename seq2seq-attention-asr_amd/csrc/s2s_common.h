@@ -75,6 +75,24 @@ struct GemmProblem {
   int relu = 0;                  // epilogue max(v, 0) after bias and beta (fused nn.ReLU)
 };
 constexpr int kMaxGemmBatch = 16;
+// Operand precision of the hoisted GEMMs of the calling thread's current C-ABI call (the context's
+// S2S_PREC_*, set at every entry): fp32 (exact f32 MFMA) or bf16 operands with fp32 accumulation.
+enum GemmPrecision { kGemmF32 = 0, kGemmBf16 = 1 };
+void set_gemm_precision(int p);
+int gemm_precision();
+// S2S_PREC_BF16_GEMM keeps the weight-gradient GEMMs (and the decoder's weight folds) in fp32: a weight
+// gradient is a sum over B*L rows whose terms cancel, and bf16 operand rounding there costs ~5e-2
+// normwise at config 3 (measured) against ~1e-3 elsewhere.  The wgrad sites open this scope; under
+// S2S_PREC_BF16_ALL (g_wgrad_bf16) it keeps bf16.
+void set_wgrad_bf16(bool on);
+bool wgrad_bf16();
+struct WgradPrecision {
+  int prev;
+  WgradPrecision() : prev(gemm_precision()) {
+    if (!wgrad_bf16()) set_gemm_precision(kGemmF32);
+  }
+  ~WgradPrecision() { set_gemm_precision(prev); }
+};
 // Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs
 // fit; without a workspace every problem runs unsplit.  Concurrent calls need disjoint ones.
 struct GemmWs {

@@ -20,6 +20,7 @@ int s2s_ctx_create(int device, s2s_ctx** out);
 void s2s_ctx_destroy(s2s_ctx* ctx);
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
 int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
+int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
 int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
 size_t s2s_gru_saved_bytes(int B, int L, int H);
 size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H);
@@ -89,6 +90,9 @@ local M = {C = C}
 -- BEGIN GENERATED CONSTANTS (tools/gen_lua_cdef.py)
 M.S2S_CTX_GRAPH = 1
 M.S2S_CTX_OVERLAP = 2
+M.S2S_PREC_FP32 = 0
+M.S2S_PREC_BF16_GEMM = 1
+M.S2S_PREC_BF16_ALL = 2
 M.S2S_ATTN_NPARAMS = 17
 M.S2S_ATTN_NPARAMS_HYBRID = 20
 M.S2S_ATTN_NPARAMS_LSTM = 36

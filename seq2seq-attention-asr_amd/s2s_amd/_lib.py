@@ -45,6 +45,7 @@ SIGNATURES = [
     ("s2s_ctx_destroy", None, [c_void_p]),
     ("s2s_ctx_set_flags", c_int, [c_void_p, c_int]),
     ("s2s_ctx_set_graph_cache", c_int, [c_void_p, c_int]),
+    ("s2s_ctx_set_precision", c_int, [c_void_p, c_int]),
     ("s2s_ctx_graph_stats", c_int, [c_void_p, P(c_long), P(c_long), P(c_int)]),
     ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_gru_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
@@ -135,6 +136,9 @@ S2S_ATTN_NPARAMS = 17
 S2S_ATTN_NPARAMS_HYBRID = 20
 S2S_ATTN_NPARAMS_LSTM = 36
 S2S_UNIQUE_ID_BYTES = 128
+S2S_PREC_FP32 = 0
+S2S_PREC_BF16_GEMM = 1
+S2S_PREC_BF16_ALL = 2
 
 
 class S2SError(RuntimeError):

@@ -415,9 +415,12 @@ class VGGAttentionModel(Module):
     The decoder_mlp runs outside the decoder launches on the saved [s_t; c_t] rows (external_mlp)."""
 
     def __init__(self, inputFrameSize=40, outputFrameSize=512, hidden=2048, scoreDepth=512, stateDepth=256,
-                 outputDepth=62, mlpDepth=64, penalty=0.0, generator=None):
+                 outputDepth=62, mlpDepth=64, penalty=0.0, generator=None, precision="fp32"):
         from .nn import GRU, Attention
         super().__init__()
+        # "bf16": every hoisted GEMM of the step (the VGG convolutions and 1x1 layers, Vh, decoder folds, the
+        # decoder_mlp Linears, all weight gradients) on bf16 MFMA with fp32 accumulation (BASELINE config 5)
+        self.precision = precision
         g = generator
         S, A, M, O = stateDepth, outputFrameSize, mlpDepth, outputDepth
         self.encoder = VGGEncoder(inputFrameSize, outputFrameSize, hidden, generator=g)
@@ -433,15 +436,16 @@ class VGGAttentionModel(Module):
     def step(self, x, labels, scale=None, normalizeNLL=False):
         """One training step on x (B, 3, L, F), labels (B, T) 0-based: forward, nll, backward with
         gradients accumulated at scale (default 1/B).  Returns (nll (B,), logp (B, T, O))."""
-        from .nn import nll_seed
+        from .nn import nll_seed, precision
         B = x.shape[0]
         scale = (1.0 / B if B > 1 else 1.0) if scale is None else scale
-        h = self.encoder.forward(x)
-        lab = labels.to(torch.int32).contiguous()
-        logp = self.decoder.forward([h, lab])
-        nll, dlogp = nll_seed(logp, lab, normalizeNLL)
-        dh = self.decoder.backward([h, lab], dlogp, scale)[0]
-        self.encoder.backward(x, dh, scale)
+        with precision(self.precision, x.device.index):
+            h = self.encoder.forward(x)
+            lab = labels.to(torch.int32).contiguous()
+            logp = self.decoder.forward([h, lab])
+            nll, dlogp = nll_seed(logp, lab, normalizeNLL)
+            dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+            self.encoder.backward(x, dh, scale)
         return nll, logp
 
 
@@ -472,13 +476,14 @@ class ConvBiLSTMAttentionModel(Module):
     def step(self, x, labels, scale=None, normalizeNLL=False):
         """One training step on x (B, L, D), labels (B, T) 0-based; gradients accumulate at scale
         (default 1/B).  Returns (nll (B,), logp (B, T, O))."""
-        from .nn import nll_seed
+        from .nn import nll_seed, precision
         B = x.shape[0]
         scale = (1.0 / B if B > 1 else 1.0) if scale is None else scale
-        h = self.encoder.forward(x)
-        lab = labels.to(torch.int32).contiguous()
-        logp = self.decoder.forward([h, lab])
-        nll, dlogp = nll_seed(logp, lab, normalizeNLL)
-        dh = self.decoder.backward([h, lab], dlogp, scale)[0]
-        self.encoder.backward(x, dh, scale)
+        with precision(self.precision, x.device.index):
+            h = self.encoder.forward(x)
+            lab = labels.to(torch.int32).contiguous()
+            logp = self.decoder.forward([h, lab])
+            nll, dlogp = nll_seed(logp, lab, normalizeNLL)
+            dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+            self.encoder.backward(x, dh, scale)
         return nll, logp

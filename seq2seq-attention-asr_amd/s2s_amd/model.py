@@ -118,7 +118,7 @@ class ChorowskiBaseline:
     """autoencoder = decoder({encoder(x), labelmask}) with flat params/grads on one device."""
 
     def __init__(self, cfg: ModelConfig = None, device=None, seed: int = 1234, graph: bool = False,
-                 overlap: bool = False):
+                 overlap: bool = False, precision: str = "fp32"):
         self.cfg = cfg or ModelConfig()
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         shapes = param_shapes(self.cfg)
@@ -134,11 +134,14 @@ class ChorowskiBaseline:
             off += sz
         self.params = flat.to(self.device)
         self.grads = torch.zeros_like(self.params)
-        if graph or overlap:
+        if graph or overlap or precision != "fp32":
             from .nn import Context
             self.ctx = Context(self.device.index, graph=graph, overlap=overlap)
+            # "bf16": the step's hoisted GEMMs on bf16 MFMA, fp32 accumulation (BASELINE config 3)
+            self.ctx.set_precision(precision)
         else:
             self.ctx = get_context(self.device.index)
+        self.precision = precision
         self._wsbuf = None
         self._mask_buf = None
         self._outputs = {}

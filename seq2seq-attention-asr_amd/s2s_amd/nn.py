@@ -6,6 +6,7 @@ Protocol kept from Torch7: `forward(input)` = `updateOutput`,
 accumulate, `training()` / `evaluate()`.  2-D inputs are one utterance (the reference's
 SGD mode, Recurrent.lua:67-77); 3-D inputs are a batch of equal-length utterances.
 """
+import contextlib
 import ctypes
 import math
 
@@ -29,6 +30,13 @@ class Context:
         if flags:
             check(lib.s2s_ctx_set_flags(h, flags))
 
+    def set_precision(self, precision: str):
+        """"fp32" (default), "bf16" (forward / data-gradient GEMMs on bf16 operands, weight gradients fp32) or
+        "bf16-all" (weight gradients too): operand precision of the hoisted GEMMs (s2s_ctx_set_precision)."""
+        p = {"fp32": _lib.S2S_PREC_FP32, "bf16": _lib.S2S_PREC_BF16_GEMM, "bf16-all": _lib.S2S_PREC_BF16_ALL}[precision]
+        check(lib.s2s_ctx_set_precision(self.handle, p))
+        self.precision = precision
+
     def set_graph_cache(self, capacity: int):
         """How many captured steps (one per shape / buffer set) the context keeps (default 8)."""
         check(lib.s2s_ctx_set_graph_cache(self.handle, int(capacity)))
@@ -48,6 +56,20 @@ class Context:
 
 
 _CTX = {}
+
+
+@contextlib.contextmanager
+def precision(p: str, device=None):
+    """with s2s_amd.precision("bf16"): the default context's hoisted GEMMs (front-end convolutions,
+    x-projections, Vh, decoder MLP, weight-gradient / dX GEMMs) take bf16 operands with fp32
+    accumulation inside the block (s2s_ctx_set_precision); "fp32" restores exact f32 MFMA."""
+    ctx = get_context(device)
+    prev = getattr(ctx, "precision", "fp32")
+    ctx.set_precision(p)
+    try:
+        yield ctx
+    finally:
+        ctx.set_precision(prev)
 
 
 def get_context(device=None) -> Context:

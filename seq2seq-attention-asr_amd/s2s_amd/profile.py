@@ -31,6 +31,7 @@ def profile_step(model, x, labels, stream, reps=3):
     # same stream layout as the timed steps (weight-gradient GEMMs on the side stream), eager so the
     # library can bracket every launch with events
     model.ctx = Context(model.device.index, graph=False, overlap=True)
+    model.ctx.set_precision(getattr(model, "precision", "fp32"))
     try:
         model.step(x, labels, stream=stream)  # warm
         stream.synchronize()

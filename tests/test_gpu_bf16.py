@@ -1,0 +1,133 @@
+"""GPU: the bf16-operand MFMA GEMMs (S2S_PREC_BF16_GEMM, BASELINE configs 3 and 5).
+
+Two kinds of checks:
+* exactness of the kernel: every transpose form, guarded and unguarded tiles, split-K, against numpy
+  on the SAME bf16-rounded operands (round-to-nearest-even, what v_cvt_pk_bf16_f32 does) accumulated in
+  float64 -- only the fp32 accumulation order differs: max|gpu - ref| <= 2e-5 max|ref|;
+* the accuracy bf16 buys at model level, against the float64 oracle (tests below state their bars).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_gemm
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                   ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p, ctypes.c_long, ctypes.c_float, ctypes.c_void_p,
+                   ctypes.c_long, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+    return _lib
+
+
+def bf16_round(a):
+    """float32 -> nearest bf16 (ties to even), returned as float64."""
+    u = np.ascontiguousarray(a, dtype=np.float32).view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16) << 16
+    return r.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+@pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(256, 384, 512), (77, 45, 133), (64, 64, 8192), (1000, 2048, 96), (64, 40000, 576)])
+def test_bf16_gemm_exact_on_rounded_operands(lib, tA, tB, M, N, K):
+    rng = np.random.default_rng(M + N + K + 7 * tA + 3 * tB)
+    A = rng.standard_normal((K, M) if tA else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tB else (K, N)).astype(np.float32)
+    C0 = rng.standard_normal((M, N)).astype(np.float32)
+    Ag, Bg, Cg = (torch.tensor(v, device="cuda") for v in (A, B, C0))
+    ws = torch.empty(8 << 20, device="cuda")
+    rc = lib.lib.s2s_debug_gemm(tA, tB, M, N, K, 0.5, Ag.data_ptr(), A.shape[1], Bg.data_ptr(), B.shape[1], 0.25,
+                                Cg.data_ptr(), N, 1, ws.data_ptr(), ws.numel())
+    assert rc == 0
+    torch.cuda.synchronize()
+    Ar, Br = bf16_round(A), bf16_round(B)
+    ref = 0.5 * ((Ar.T if tA else Ar) @ (Br.T if tB else Br)) + 0.25 * C0.astype(np.float64)
+    err = np.abs(Cg.cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err <= 2e-5, err
+    # and it is really bf16: the fp32 product differs from the rounded-operand one by far more
+    exact = 0.5 * ((A.T if tA else A).astype(np.float64) @ (B.T if tB else B).astype(np.float64)) + 0.25 * C0
+    assert np.abs(ref - exact).max() / np.abs(exact).max() > 1e-4
+
+
+def _rel(a, r):
+    """relative L2 error ||a - r|| / ||r||"""
+    a = np.asarray(a, np.float64).ravel()
+    r = np.asarray(r, np.float64).ravel()
+    return float(np.linalg.norm(a - r) / max(np.linalg.norm(r), 1e-30))
+
+
+# The bf16 tolerance (stated against the float64 oracle).  bf16 operands carry a unit roundoff of 2^-9 per
+# operand; the forward outputs stay within ~1e-4.  The gradients move more: the forward's rounding flips
+# near-tie DISCRETE decisions (which of a Maxout group's 7 units wins, which ReLU units are active), and a
+# flipped decision routes a whole gradient row elsewhere -- for any bf16 implementation, not a kernel error
+# (the bf16 GEMM kernel itself is exact on rounded operands: test_bf16_gemm_exact_on_rounded_operands).  So the
+# bar is on relative L2 error: logp <= 1e-3, every gradient <= BF16_GRAD_RTOL, on every tensor that the fp32
+# restatement itself gets to 1e-5 (measured: 1-6e-2 at config 3, <= 1.4e-1 at config 5).
+BF16_LOGP_RTOL = 1e-3
+BF16_GRAD_RTOL = 0.2
+
+
+@pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
+def test_model_step_bf16_config3_dims(lib, prec):
+    """BASELINE config 3 (model_chorowski_baseline_dropout.lua, bf16 MFMA): the whole step with bf16 GEMM
+    operands (injected dropout masks, reduced L / T for the oracle) against the float64 oracle."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    cfg_o = orc.ModelConfig()
+    model = s2s_amd.ChorowskiBaseline(s2s_amd.ModelConfig(dropout=0.5), precision=prec)
+    P = orc.unflatten(model.params.cpu().double().numpy(), cfg_o)
+    B, L, T = 16, 48, 16
+    x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=3, pad=10, eos=23)
+    rng = np.random.default_rng(4)
+    mask = (rng.random((B, T, cfg_o.stateDepth + 2 * cfg_o.outputFrameSize)) >= 0.5) / 0.5
+    nll, logp = model.step(torch.tensor(x, dtype=torch.float32, device="cuda"),
+                           torch.tensor(labels, dtype=torch.int32, device="cuda"),
+                           dropout_mask=torch.tensor(mask, dtype=torch.float32, device="cuda"))
+    torch.cuda.synchronize()
+    _, G, lref, _ = orc.training_step(x, labels, P, cfg_o, dropout_mask=mask)
+    errs = {"logp": _rel(logp.cpu().numpy(), lref)}
+    Gg = orc.unflatten(model.grads.cpu().double().numpy(), cfg_o)
+    errs.update({"grad " + k: _rel(Gg[k], G[k]) for k in G})
+    print(f"config 3 {prec} max rel errs:", {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: f"{v:.2e}" for k, v in errs.items() if not v <= (BF16_LOGP_RTOL if k == "logp" else BF16_GRAD_RTOL)}
+    assert not bad, bad
+    assert errs["logp"] > 1e-6  # bf16 really ran (fp32 reaches ~2e-7 here)
+
+
+def test_vgg_model_step_bf16_config5(lib):
+    """BASELINE config 5 (librispeech/model_vgg.lua, bf16): full width (1x1 layers 2048), B = 1, L = 256,
+    T = 50, against the float64 oracle; tensors the fp32 restatement cannot pin to 1e-5 (cancelling sums,
+    tests/test_gpu_fullsize.py) are reported, not judged."""
+    import s2s_amd
+    import vgg_case as vc
+    from s2s_amd import frontend as fe
+    g = torch.Generator().manual_seed(5)
+    B, L, T = 1, 256, 50
+    model = s2s_amd.VGGAttentionModel(40, outputFrameSize=512, hidden=2048, outputDepth=29, generator=g,
+                                      precision="bf16").cuda()
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((B, 3, L, 40))
+    labels = np.append(rng.integers(0, 28, (B, T - 1)), np.full((B, 1), 28), axis=1).astype(np.int32)
+    model.zeroGradParameters()
+    nll, logp = model.step(torch.tensor(x, dtype=torch.float32, device="cuda"),
+                           torch.tensor(labels, dtype=torch.int32, device="cuda"))
+    torch.cuda.synchronize()
+    nll64, logp64, G64, mg64 = vc.oracle_step(model, fe, x, labels, np.float64)
+    nll32, logp32, G32, mg32 = vc.oracle_step(model, fe, x, labels, np.float32)
+    errs = {"logp": _rel(logp.cpu().numpy(), logp64)}
+    floor = {"logp": _rel(logp32, logp64)}
+    for (name, gpu, r64), (_, _, r32) in zip(vc.grad_pairs(model, fe, G64, mg64), vc.grad_pairs(model, fe, G32, mg32)):
+        errs[name] = _rel(gpu.detach().cpu().numpy(), r64)
+        floor[name] = _rel(r32, r64)
+    print("config 5 bf16 max rel errs (fp32 floor):", {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
+    bad = {k: f"{errs[k]:.2e}" for k in errs
+           if floor[k] <= 1e-5 and not errs[k] <= (BF16_LOGP_RTOL if k == "logp" else BF16_GRAD_RTOL)}
+    assert not bad, bad

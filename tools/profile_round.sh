@@ -19,7 +19,7 @@ for c in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 150 rocprofv3 --pmc $c --output-format csv -d "$out/pmc_$c" -o pmc -- \
     python "$root/bench.py" --steps 2 --warmup 1 --no-cpu --no-kernel-timing --no-pmc --no-graph > /dev/null
 done
-timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+timeout -s KILL 150 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
   --output-format csv -d "$out/pmc_MFMA" -o pmc -- \
   python "$root/bench.py" --steps 2 --warmup 1 --no-cpu --no-kernel-timing --no-pmc --no-graph > /dev/null
 python "$root/tools/pmc_table.py" "$out" > "$out/pmc_hbm.csv"
