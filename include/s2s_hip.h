@@ -187,11 +187,30 @@ const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
  * B utterances at once, in evaluate() mode: h (B, L, A); eos and the output tokens 0-based; out (B, ldo),
  * ldo >= maxseqlength + 1, the best finished hypothesis of each utterance padded with -1; out_len (B);
  * out_score (B, may be NULL) its summed log-probability.  Hypotheses finish on eos or at maxseqlength;
- * K in [1, 16].  Blocks until done (it polls for the end of the search).  Content-only attention. */
+ * K in [1, 16].  Blocks until done (it polls for the end of the search).  Content or hybrid attention
+ * (alpha_{t-1} carried per hypothesis), GRU or LSTM decoder_recurrent (the cell carried: the reference's
+ * hidden {alpha, s, mem}, Attention.lua:360-403), fused decoder_mlp; frame_lengths must be NULL. */
 size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength);
 int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
                          const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len,
                          float* out_score, void* workspace, size_t workspace_bytes);
+/* The same search in stages, for an external decoder_mlp (external_mlp = 1; also usable with the fused one):
+ *   s2s_attn_beam_init;  for count = 0 .. maxseqlength: s2s_attn_beam_step(count) -> [run the decoder_mlp on
+ *   the (B*K, S+A) rows at s2s_attn_beam_mlp_input -> (B*K, O) log-probabilities] -> s2s_attn_beam_advance(count,
+ *   logp; NULL with the fused decoder_mlp) -> stop once s2s_attn_beam_done reports 1;  s2s_attn_beam_finish.
+ * Rows are hypothesis r = b*K + j (inactive ones are computed and ignored).  The workspace holds all state. */
+int s2s_attn_beam_init(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
+                       const float* const* params, int eos, int K, int maxseqlength, void* workspace,
+                       size_t workspace_bytes);
+int s2s_attn_beam_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* const* params, int K,
+                       int maxseqlength, int count, void* workspace, size_t workspace_bytes);
+const float* s2s_attn_beam_mlp_input(const s2s_attn_dims* d, int K, int maxseqlength, void* workspace);
+int s2s_attn_beam_advance(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int eos, int K,
+                          int maxseqlength, int count, const float* logp, void* workspace, size_t workspace_bytes);
+int s2s_attn_beam_done(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength,
+                       void* workspace, int* all_done);
+int s2s_attn_beam_finish(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength,
+                         int* out, int ldo, int* out_len, float* out_score, void* workspace);
 /* WagnerFischer(a, b) (utils.lua:3-27) for n pairs on the device: a (n, lda) with lengths alen, b (n, ldb)
  * with blen, out (n) the edit distances (PER/CER numerators, timit/timit.lua:396-410). */
 int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b,

@@ -793,11 +793,13 @@ def optimizer_step(x: Array, g: Array, state: Dict[str, Array], rho: float = 0.9
 # Decode path: Attention:BeamSearch (Attention.lua:332-438) and WagnerFischer (utils.lua:3-27)
 # ----------------------------------------------------------------------------
 
-def decoder_step(h: Array, Vh: Array, s: Array, yprev: int, alpha_prev: Array, P: Dict[str, Array],
-                 cfg: "ModelConfig"):
-    """One decoder_base forward for one utterance (Attention.lua:51-184) in evaluate() mode:
-    h (L, A), Vh (L, Sc), s (S), yprev the previous label (-1 = zeros_y), alpha_prev (L).
-    Returns (logp (O), s_new (S), alpha (L))."""
+def decoder_step(h: Array, Vh: Array, state, yprev: int, P: Dict[str, Array], cfg: "ModelConfig", mlp=None):
+    """One decoder_base forward for one utterance (Attention.lua:51-184) in evaluate() mode, the step of
+    attention_fwd above for a single row: h (L, A), Vh (L, Sc), state = the reference's hidden
+    {alpha_prev (L), s (S), mem (S)} (Attention.lua:360-403; mem is the LSTM decoder's cell, unused by the
+    GRU), yprev the previous label (-1 = zeros_y).  mlp: an external decoder_mlp, v = [s; c] (S + A) ->
+    log-probabilities (O); None = the fused MaxoutMLP.  Returns (logp (O), new state)."""
+    alpha_prev, s, mem = state
     O, M, k = cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
     ws = P["Ws"] @ s + P["bs"]
     Z = ws[None, :] + Vh
@@ -812,45 +814,59 @@ def decoder_step(h: Array, Vh: Array, s: Array, yprev: int, alpha_prev: Array, P
     yin = P["Wy"] @ y + P["by"]
     cin = P["Wc"] @ c + P["bc"]
     d = P["Wd"] @ np.concatenate([cin, yin]) + P["bd"]
-    hx = np.concatenate([s, d])
-    z = sigmoid(P["dec.Wz"] @ hx)
-    r = sigmoid(P["dec.Wr"] @ hx)
-    hh = np.tanh(P["dec.Wh"] @ np.concatenate([r * s, d]))
-    s_new = (1.0 - z) * s + z * hh
-    u = P["Wm"] @ np.concatenate([s_new, c]) + P["bm"]
-    m = u.reshape(M, k).max(1)
-    logp = log_softmax(P["Wo"] @ m + P["bo"], 0)
-    return logp, s_new, alpha
+    if cfg.decoderLSTM:  # LSTM.lua:16-51, x = d, prev_h = s, prev_c = mem
+        pre = {q: P[f"dec.W{q}x"] @ d + P[f"dec.b{q}x"] + P[f"dec.W{q}h"] @ s + P[f"dec.b{q}h"] for q in "ifgo"}
+        mem = sigmoid(pre["f"]) * mem + sigmoid(pre["i"]) * np.tanh(pre["g"])
+        s_new = sigmoid(pre["o"]) * np.tanh(mem)
+    else:
+        hx = np.concatenate([s, d])
+        z = sigmoid(P["dec.Wz"] @ hx)
+        r = sigmoid(P["dec.Wr"] @ hx)
+        hh = np.tanh(P["dec.Wh"] @ np.concatenate([r * s, d]))
+        s_new = (1.0 - z) * s + z * hh
+    v = np.concatenate([s_new, c])
+    if mlp is not None:
+        logp = np.asarray(mlp(v)).reshape(-1)
+    else:
+        u = P["Wm"] @ v + P["bm"]
+        m = u.reshape(M, k).max(1)
+        logp = log_softmax(P["Wo"] @ m + P["bo"], 0)
+    return logp, (alpha, s_new, mem)
+
+
+def decoder_zero_state(L: int, S: int, dtype=np.float64):
+    """zeros_hidden (Recurrent.lua:112) of the dimhidden {L, S, S} hidden (Attention.lua:318)."""
+    return np.zeros(L, dtype), np.zeros(S, dtype), np.zeros(S, dtype)
 
 
 def beam_search(h: Array, P: Dict[str, Array], cfg: "ModelConfig", eos: int, K: int = 5,
-                maxseqlength: Optional[int] = None):
+                maxseqlength: Optional[int] = None, mlp=None):
     """Attention:BeamSearch (Attention.lua:332-438) for one utterance h (L, A), 0-based labels.
     Step 0 from zeros_y / zero hidden (:356-367), torch.topk(K) sorted (:369); then while fewer
     than K hypotheses finished and count < maxseqlength (:384): every active hypothesis k is
     extended (p_next[k] = logp + p_beam[k], :386-399), topk(K) over the flattened candidates
     (:400-402), of which the first K - finished are taken (:408): eos or count == maxseqlength
-    finishes (:413-417), else it survives with its parent's hidden state.  Returns
-    (prediction = the finished hypothesis of highest score (first maximum, :432-434), score)."""
+    finishes (:413-417), else it survives with its parent's hidden {alpha, s, mem}.  mlp: an external
+    decoder_mlp (decoder_step).  Returns (prediction = the finished hypothesis of highest score
+    (first maximum, :432-434), score)."""
     L = h.shape[0]
     maxlen = maxseqlength or L
     Vh = h @ P["V"].T
-    S = cfg.stateDepth
-    logp, s, a = decoder_step(h, Vh, np.zeros(S, h.dtype), -1, np.zeros(L, h.dtype), P, cfg)
+    logp, st = decoder_step(h, Vh, decoder_zero_state(L, cfg.stateDepth, h.dtype), -1, P, cfg, mlp)
     order = np.argsort(-logp, kind="stable")[:K]
     beams, fin = [], []
     for j in order:
         if j == eos:
             fin.append(([int(j)], float(logp[j])))
         else:
-            beams.append(([int(j)], (s, a), float(logp[j])))
+            beams.append(([int(j)], st, float(logp[j])))
     count = 0
     while len(fin) < K and count < maxlen:
         count += 1
         nexts = []
-        for seq, (sp, ap), pb in beams:
-            lp, sn, an = decoder_step(h, Vh, sp, seq[-1], ap, P, cfg)
-            nexts.append((lp + pb, (sn, an)))
+        for seq, sp, pb in beams:
+            lp, sn = decoder_step(h, Vh, sp, seq[-1], P, cfg, mlp)
+            nexts.append((lp + pb, sn))
         flat = np.concatenate([n[0] for n in nexts])
         O = nexts[0][0].size
         top = np.argsort(-flat, kind="stable")[:K]

@@ -90,6 +90,18 @@ const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved);
 size_t attn_beam_workspace_bytes(const AttnDims& d, int K, int maxlen);
 int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K,
                      int maxlen, int* out, int ldo, int* out_len, float* out_score, void* ws, size_t ws_bytes);
+// the same search in stages (an external decoder_mlp runs between step and advance on beam_mlp_input's
+// (B*K, S+A) rows and hands back (B*K, O) log-probabilities)
+int attn_beam_init(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K, int maxlen,
+                   void* ws, size_t ws_bytes);
+int attn_beam_step(hipStream_t st, const AttnDims& d, const AttnParams& P, int K, int maxlen, int count, void* ws,
+                   size_t ws_bytes);
+const float* attn_beam_mlp_input(const AttnDims& d, int K, int maxlen, void* ws);
+int attn_beam_advance(hipStream_t st, const AttnDims& d, int eos, int K, int maxlen, int count, const float* logp_ext,
+                      void* ws, size_t ws_bytes);
+int attn_beam_done(hipStream_t st, const AttnDims& d, int K, int maxlen, void* ws, int* all_done);
+int attn_beam_finish(hipStream_t st, const AttnDims& d, int K, int maxlen, void* ws, int* out, int ldo, int* out_len,
+                     float* out_score);
 // WagnerFischer (utils.lua:3-27) over n sequence pairs (row-major, lengths alen / blen)
 int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda, const int* b, const int* blen,
                   int ldb, int* out);

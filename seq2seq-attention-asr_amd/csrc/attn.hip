@@ -1561,10 +1561,14 @@ int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
 namespace {
 
 struct BeamK {
-  int B, K, maxlen, eos, S, O;
+  int B, K, maxlen, eos, S, O, L, hyb, lstm;
   int *nact, *nfin, *done;
   int *yprev, *hist, *hlen, *fseq, *flen, *lab2;
-  float *pbeam, *s, *fscore;
+  // per hypothesis, double-buffered by step parity: decoder state s, attention alpha (hybrid attention's
+  // location features read alpha_{t-1}) and the LSTM cell (mem) -- the reference's hidden {alpha, s, mem}
+  // (Attention.lua:360-403)
+  float *pbeam, *s, *fscore, *alpha, *mem;
+  float* mlp_in;  // (R, S + A) decoder_mlp input rows of the current step (external decoder_mlp)
 };
 
 // hypothesis row r = b*K + k gets utterance b's annotations (grid.y = utterance)
@@ -1576,7 +1580,12 @@ __global__ void beam_rep_h(const float* h, float* hr, int K, long per) {
 
 __global__ void beam_init(BeamK q) {
   const int R = q.B * q.K;
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * q.S; i += gridDim.x * blockDim.x) q.s[i] = 0.f;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * q.S; i += gridDim.x * blockDim.x) {
+    q.s[i] = 0.f;
+    if (q.lstm) q.mem[i] = 0.f;
+  }
+  if (q.hyb)
+    for (long i = blockIdx.x * blockDim.x + threadIdx.x; i < (long)R * q.L; i += gridDim.x * blockDim.x) q.alpha[i] = 0.f;
   for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
     q.pbeam[r] = 0.f;
     q.yprev[r] = -1;
@@ -1590,14 +1599,21 @@ __global__ void beam_init(BeamK q) {
   }
 }
 
-// s_{t-1} and y_{t-1} of every hypothesis row into the t = 1 slots of the T = 2 problem
+// s_{t-1} and y_{t-1} of every hypothesis row into the t = 1 slots of the T = 2 problem; alpha_{t-1} (hybrid)
+// and the LSTM cell c_{t-1} into its t = 0 slots (what the step kernels read as the previous step's)
 __global__ void beam_prep(AttnK k, BeamK q, int par) {
-  const int R = q.B * q.K, S = q.S;
+  const int R = q.B * q.K, S = q.S, L = q.L;
   const float* s = q.s + (long)par * R * S;
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < R * S; i += gridDim.x * blockDim.x) {
     const int r = i / S, n = i - r * S;
     k.HX[((long)r * 2 + 1) * 2 * S + n] = s[i];
+    if (q.lstm) k.LC[((long)r * 2) * S + n] = q.mem[(long)par * R * S + i];
   }
+  if (q.hyb)
+    for (long i = blockIdx.x * blockDim.x + threadIdx.x; i < (long)R * L; i += gridDim.x * blockDim.x) {
+      const long r = i / L, l = i - r * L;
+      k.ALPHA[(r * 2) * L + l] = q.alpha[(long)par * R * L + i];
+    }
   for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < R; r += gridDim.x * blockDim.x) {
     q.lab2[2 * r] = q.yprev[r];
     q.lab2[2 * r + 1] = 0;
@@ -1683,6 +1699,12 @@ __global__ __launch_bounds__(256) void beam_update(AttnK k, BeamK q, int count) 
     for (int x = tid; x < len; x += 256) hnew[(long)dst * L1 + x] = hcur[(long)src * L1 + x];
     const float* sv = k.VV + ((long)src * 2 + 1) * (S + k.A);
     for (int n = tid; n < S; n += 256) snew[(long)dst * S + n] = sv[n];
+    if (q.lstm)
+      for (int n = tid; n < S; n += 256)
+        q.mem[(long)nxt * R * S + (long)dst * S + n] = k.LC[((long)src * 2 + 1) * S + n];
+    if (q.hyb)
+      for (int l = tid; l < q.L; l += 256)
+        q.alpha[(long)nxt * R * q.L + (long)dst * q.L + l] = k.ALPHA[((long)src * 2 + 1) * q.L + l];
     if (tid == 0) {
       hnew[(long)dst * L1 + len] = ntok[e];
       lnew[dst] = len + 1;
@@ -1694,6 +1716,22 @@ __global__ __launch_bounds__(256) void beam_update(AttnK k, BeamK q, int count) 
     q.nfin[b] += nf;
     q.nact[b] = nn;
     q.done[b] = (q.nfin[b] >= K || count >= q.maxlen) ? 1 : 0;
+  }
+}
+
+// external decoder_mlp: the step's [s_t; c_t] rows (t = 1 slots) out, the caller's log-probabilities in
+__global__ void beam_mlp_rows(AttnK k, BeamK q) {
+  const int R = q.B * q.K, W = q.S + k.A;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (long)R * W; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / W, c = i - r * W;
+    q.mlp_in[i] = k.VV[(r * 2 + 1) * W + c];
+  }
+}
+__global__ void beam_put_logp(AttnK k, BeamK q, const float* logp) {
+  const int R = q.B * q.K, O = q.O;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < (long)R * O; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / O, o = i - r * O;
+    k.LOGP[(r * 2 + 1) * O + o] = logp[i];
   }
 }
 
@@ -1744,6 +1782,8 @@ AttnDims beam_dims(const AttnDims& d, int K) {
   d2.T = 2;
   d2.dropout = 0.f;  // evaluate() mode
   d2.dropout_mask = nullptr;
+  d2.flen = nullptr;  // rows are hypotheses; every utterance's annotations are searched whole
+  d2.tlen = nullptr;
   return d2;
 }
 
@@ -1761,7 +1801,8 @@ BeamLayout beam_layout(const AttnDims& d, int K, int maxlen) {
   l.state = l.scratch + up(attn_scratch_bytes(d2));
   const size_t ints = 3 * (size_t)d.B + R /*yprev*/ + 2 * R * L1 /*hist*/ + 2 * R /*hlen*/ + R * L1 /*fseq*/ +
                       R /*flen*/ + 2 * R /*lab2*/;
-  const size_t floats = R /*pbeam*/ + 2 * R * d.S /*s*/ + R /*fscore*/;
+  const size_t floats = R /*pbeam*/ + 2 * R * d.S /*s*/ + R /*fscore*/ + 2 * R * d.L /*alpha*/ + 2 * R * d.S /*mem*/ +
+                        R * (size_t)(d.S + d.A) /*mlp_in*/;
   l.fstate = l.state + up(4 * ints);
   l.total = l.fstate + up(4 * floats);
   return l;
@@ -1771,22 +1812,34 @@ BeamLayout beam_layout(const AttnDims& d, int K, int maxlen) {
 
 size_t attn_beam_workspace_bytes(const AttnDims& d, int K, int maxlen) { return beam_layout(d, K, maxlen).total; }
 
-int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K,
-                     int maxlen, int* out, int ldo, int* out_len, float* out_score, void* ws, size_t ws_bytes) {
+// The beam's device state inside the workspace (beam_layout): the T = 2 decoder problem of R = B*K rows and
+// the per-hypothesis bookkeeping.  Every stage re-derives the same views from (d, K, maxlen, ws).
+struct BeamView {
+  AttnDims d2;
+  AttnK k;
+  BeamK q;
+  float* hrep;
+  GemmWs gws;
+};
+static int beam_view(const AttnDims& d, const AttnParams& P, int eos, int K, int maxlen, void* ws, size_t ws_bytes,
+                     BeamView& v) {
   S2S_TRY(attn_check_dims(d));
-  S2S_REQUIRE(d.hf == 0, "beam search: hybrid attention not supported");
   S2S_REQUIRE(K >= 1 && K <= kBeamMaxK && K <= d.O, "beam search: K must be in [1, 16] and <= outputDepth");
-  S2S_REQUIRE(maxlen >= 1 && eos >= 0 && eos < d.O && ldo >= maxlen + 1, "beam search: bad eos / maxlen / ldo");
+  S2S_REQUIRE(maxlen >= 1 && eos >= 0 && eos < d.O, "beam search: bad eos / maxlen");
+  S2S_REQUIRE(!d.flen, "beam search: frame lengths unsupported (search an utterance's own frames)");
   const BeamLayout bl = beam_layout(d, K, maxlen);
   S2S_REQUIRE(ws && ws_bytes >= bl.total, "beam search: workspace too small");
-  const AttnDims d2 = beam_dims(d, K);
+  v.d2 = beam_dims(d, K);
   char* base = static_cast<char*>(ws);
-  float* hrep = reinterpret_cast<float*>(base + bl.hrep);
-  AttnK k{};
-  carve(d2, &k, base + bl.saved, base + bl.scratch);
-  const int B = d.B, R = B * K, S = d.S, L = d.L, L1 = maxlen + 1;
-  BeamK q{};
-  q.B = B; q.K = K; q.maxlen = maxlen; q.eos = eos; q.S = S; q.O = d.O;
+  v.hrep = reinterpret_cast<float*>(base + bl.hrep);
+  v.k = AttnK{};
+  carve(v.d2, &v.k, base + bl.saved, base + bl.scratch);
+  const int B = d.B, R = B * K, S = d.S, L1 = maxlen + 1;
+  BeamK& q = v.q;
+  q = BeamK{};
+  q.B = B; q.K = K; q.maxlen = maxlen; q.eos = eos; q.S = S; q.O = d.O; q.L = d.L;
+  q.hyb = d.hf > 0 ? 1 : 0;
+  q.lstm = d.lstm ? 1 : 0;
   int* ip = reinterpret_cast<int*>(base + bl.state);
   q.nact = ip; ip += B;
   q.nfin = ip; ip += B;
@@ -1800,45 +1853,126 @@ int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const At
   float* fp = reinterpret_cast<float*>(base + bl.fstate);
   q.pbeam = fp; fp += R;
   q.s = fp; fp += 2L * R * S;
-  q.fscore = fp;
-  k.P = P;
-  k.h = hrep;
-  k.labels = q.lab2;
-  k.logp = nullptr;
+  q.fscore = fp; fp += R;
+  q.alpha = fp; fp += 2L * R * d.L;
+  q.mem = fp; fp += 2L * R * S;
+  q.mlp_in = fp;
+  v.k.P = P;
+  v.k.h = v.hrep;
+  v.k.labels = q.lab2;
+  v.k.logp = nullptr;
+  v.k.t = 1;
+  v.gws = attn_gemm_ws(v.d2, base + bl.scratch);
+  return 0;
+}
+
+int attn_beam_init(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K, int maxlen,
+                   void* ws, size_t ws_bytes) {
+  BeamView v;
+  S2S_TRY(beam_view(d, P, eos, K, maxlen, ws, ws_bytes, v));
+  const int B = d.B, R = B * K, L = d.L;
   // annotations and Vh once per hypothesis row (Attention.lua:356-357: vh = Vh:forward(annotations))
-  hipLaunchKernelGGL(beam_rep_h, dim3(64, B), dim3(256), 0, st, h, hrep, K, (long)L * d.A);
-  const GemmWs gws = attn_gemm_ws(d2, base + bl.scratch);
-  S2S_TRY(gemm1(st, false, true, R * L, d.Sc, d.A, 1.f, hrep, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
-  hipLaunchKernelGGL(beam_init, dim3(64), dim3(256), 0, st, q);
+  hipLaunchKernelGGL(beam_rep_h, dim3(64, B), dim3(256), 0, st, h, v.hrep, K, (long)L * d.A);
+  S2S_TRY(gemm1(st, false, true, R * L, d.Sc, d.A, 1.f, v.hrep, d.A, P.V, d.A, 0.f, v.k.Vh, d.Sc, nullptr, v.gws));
+  hipLaunchKernelGGL(beam_init, dim3(64), dim3(256), 0, st, v.q);
+  if (d.hf > 0) hipLaunchKernelGGL(dec_hyb_fold, dim3((d.Sc + 255) / 256), dim3(256), 0, st, v.k);
+  if (d.lstm) hipLaunchKernelGGL(dec_lstm_pack, dim3(256), dim3(256), 0, st, v.k);
   S2S_CHECK_HIP(hipGetLastError());
-  const int bt = (R + 15) / 16, rows = 2 * R;
-  std::vector<int> done(B);
-  k.t = 1;
-  for (int count = 0; count <= maxlen; ++count) {
-    hipLaunchKernelGGL(beam_prep, dim3(64), dim3(256), 0, st, k, q, count & 1);
-    hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, R), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f3_combine, dim3(R), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+  return 0;
+}
+
+// one decoder_base forward of every active hypothesis (Attention.lua:386-399); with the fused decoder_mlp
+// through the log-probabilities, with an external one up to its input rows (beam mlp_in)
+int attn_beam_step(hipStream_t st, const AttnDims& d, const AttnParams& P, int K, int maxlen, int count, void* ws,
+                   size_t ws_bytes) {
+  BeamView v;
+  S2S_TRY(beam_view(d, P, 0, K, maxlen, ws, ws_bytes, v));
+  AttnK& k = v.k;
+  const int R = d.B * K, S = d.S, bt = (R + 15) / 16, rows = 2 * R;
+  hipLaunchKernelGGL(beam_prep, dim3(64), dim3(256), 0, st, k, v.q, count & 1);
+  hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, R), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_f3_combine, dim3(R), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+  if (d.lstm) {
+    hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f7_lstm, dim3((R * S + 255) / 256), dim3(256), 0, st, k);
+  } else {
     hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
+  }
+  if (d.ext) {
+    hipLaunchKernelGGL(beam_mlp_rows, dim3(256), dim3(256), 0, st, k, v.q);
+  } else {
     S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
-                  (long)d.M * d.K, P.bm, gws));
+                  (long)d.M * d.K, P.bm, v.gws));
     hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
-    hipLaunchKernelGGL(beam_update, dim3(B), dim3(256), 0, st, k, q, count);
-    S2S_CHECK_HIP(hipGetLastError());
+  }
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+const float* attn_beam_mlp_input(const AttnDims& d, int K, int maxlen, void* ws) {
+  BeamView v;
+  AttnParams P{};
+  if (beam_view(d, P, 0, K, maxlen, ws, beam_layout(d, K, maxlen).total, v) != 0) return nullptr;
+  return v.q.mlp_in;
+}
+
+// topk + bookkeeping of the step (Attention.lua:400-430); logp_ext: (R, O) log-probabilities of an external
+// decoder_mlp (null with the fused one)
+int attn_beam_advance(hipStream_t st, const AttnDims& d, int eos, int K, int maxlen, int count, const float* logp_ext,
+                      void* ws, size_t ws_bytes) {
+  BeamView v;
+  AttnParams P{};
+  S2S_TRY(beam_view(d, P, eos, K, maxlen, ws, ws_bytes, v));
+  S2S_REQUIRE(!d.ext || logp_ext, "beam search: an external decoder_mlp needs the step's log-probabilities");
+  if (logp_ext) hipLaunchKernelGGL(beam_put_logp, dim3(256), dim3(256), 0, st, v.k, v.q, logp_ext);
+  hipLaunchKernelGGL(beam_update, dim3(d.B), dim3(256), 0, st, v.k, v.q, count);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int attn_beam_done(hipStream_t st, const AttnDims& d, int K, int maxlen, void* ws, int* all_done) {
+  BeamView v;
+  AttnParams P{};
+  S2S_TRY(beam_view(d, P, 0, K, maxlen, ws, beam_layout(d, K, maxlen).total, v));
+  std::vector<int> done(d.B);
+  S2S_CHECK_HIP(hipMemcpyAsync(done.data(), v.q.done, sizeof(int) * d.B, hipMemcpyDeviceToHost, st));
+  S2S_CHECK_HIP(hipStreamSynchronize(st));
+  bool all = true;
+  for (int x : done) all = all && x;
+  *all_done = all ? 1 : 0;
+  return 0;
+}
+
+int attn_beam_finish(hipStream_t st, const AttnDims& d, int K, int maxlen, void* ws, int* out, int ldo, int* out_len,
+                     float* out_score) {
+  BeamView v;
+  AttnParams P{};
+  S2S_TRY(beam_view(d, P, 0, K, maxlen, ws, beam_layout(d, K, maxlen).total, v));
+  S2S_REQUIRE(ldo >= maxlen + 1, "beam search: ldo < maxseqlength + 1");
+  hipLaunchKernelGGL(beam_final, dim3(d.B), dim3(256), 0, st, v.q, out, ldo, out_len, out_score);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int attn_beam_search(hipStream_t st, const AttnDims& d, const float* h, const AttnParams& P, int eos, int K,
+                     int maxlen, int* out, int ldo, int* out_len, float* out_score, void* ws, size_t ws_bytes) {
+  S2S_REQUIRE(!d.ext, "beam search: an external decoder_mlp runs through the stepwise calls");
+  S2S_REQUIRE(ldo >= maxlen + 1, "beam search: ldo < maxseqlength + 1");
+  S2S_TRY(attn_beam_init(st, d, h, P, eos, K, maxlen, ws, ws_bytes));
+  for (int count = 0; count <= maxlen; ++count) {
+    S2S_TRY(attn_beam_step(st, d, P, K, maxlen, count, ws, ws_bytes));
+    S2S_TRY(attn_beam_advance(st, d, eos, K, maxlen, count, nullptr, ws, ws_bytes));
     if ((count & 3) == 3 || count == maxlen) {  // stop once every utterance has K finished hypotheses
-      S2S_CHECK_HIP(hipMemcpyAsync(done.data(), q.done, sizeof(int) * B, hipMemcpyDeviceToHost, st));
-      S2S_CHECK_HIP(hipStreamSynchronize(st));
-      bool all = true;
-      for (int v : done) all = all && v;
+      int all = 0;
+      S2S_TRY(attn_beam_done(st, d, K, maxlen, ws, &all));
       if (all) break;
     }
   }
-  hipLaunchKernelGGL(beam_final, dim3(B), dim3(256), 0, st, q, out, ldo, out_len, out_score);
-  S2S_CHECK_HIP(hipGetLastError());
-  return 0;
+  return attn_beam_finish(st, d, K, maxlen, ws, out, ldo, out_len, out_score);
 }
 
 int edit_distance(hipStream_t st, int n, const int* a, const int* alen, int lda, const int* b, const int* blen,

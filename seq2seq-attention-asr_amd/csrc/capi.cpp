@@ -748,21 +748,73 @@ size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqle
   return attn_beam_workspace_bytes(to_attn(d), K, maxseqlength);
 }
 
+static int beam_params(const s2s_attn_dims* d, const float* const* params, AttnParams& ap) {
+  S2S_REQUIRE(params, "beam search: null parameters");
+  const float** pp = reinterpret_cast<const float**>(&ap);
+  for (int i = 0; i < attn_nparams(d); ++i) {
+    pp[i] = params[i];
+    S2S_REQUIRE(pp[i] != nullptr || attn_param_optional(d, i), "beam search: null parameter");
+  }
+  return 0;
+}
+
 int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
                          const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len,
                          float* out_score, void* workspace, size_t workspace_bytes) {
   S2S_TRY(set_device(ctx));
-  S2S_REQUIRE(d && h && params && out && out_len && workspace, "beam search: null argument");
-  S2S_REQUIRE(!d->external_mlp && !d->decoder_lstm,
-              "beam search: runs the GRU decoder with the fused Maxout -> Linear -> LogSoftMax decoder_mlp only");
-  AttnParams ap;
-  const float** pp = reinterpret_cast<const float**>(&ap);
-  for (int i = 0; i < attn_nparams(d); ++i) {
-    pp[i] = params[i];
-    S2S_REQUIRE(pp[i] != nullptr, "beam search: null parameter");
-  }
+  S2S_REQUIRE(d && h && out && out_len && workspace, "beam search: null argument");
+  AttnParams ap{};
+  S2S_TRY(beam_params(d, params, ap));
   return attn_beam_search(static_cast<hipStream_t>(stream), to_attn(d), h, ap, eos, K, maxseqlength, out, ldo,
                           out_len, out_score, workspace, workspace_bytes);
+}
+
+int s2s_attn_beam_init(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h,
+                       const float* const* params, int eos, int K, int maxseqlength, void* workspace,
+                       size_t workspace_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && h && workspace, "beam search: null argument");
+  AttnParams ap{};
+  S2S_TRY(beam_params(d, params, ap));
+  return attn_beam_init(static_cast<hipStream_t>(stream), to_attn(d), h, ap, eos, K, maxseqlength, workspace,
+                        workspace_bytes);
+}
+
+int s2s_attn_beam_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* const* params, int K,
+                       int maxseqlength, int count, void* workspace, size_t workspace_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && workspace && count >= 0 && count <= maxseqlength, "beam search: bad step");
+  AttnParams ap{};
+  S2S_TRY(beam_params(d, params, ap));
+  return attn_beam_step(static_cast<hipStream_t>(stream), to_attn(d), ap, K, maxseqlength, count, workspace,
+                        workspace_bytes);
+}
+
+const float* s2s_attn_beam_mlp_input(const s2s_attn_dims* d, int K, int maxseqlength, void* workspace) {
+  return d && workspace ? attn_beam_mlp_input(to_attn(d), K, maxseqlength, workspace) : nullptr;
+}
+
+int s2s_attn_beam_advance(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int eos, int K,
+                          int maxseqlength, int count, const float* logp, void* workspace, size_t workspace_bytes) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && workspace && count >= 0 && count <= maxseqlength, "beam search: bad step");
+  return attn_beam_advance(static_cast<hipStream_t>(stream), to_attn(d), eos, K, maxseqlength, count, logp, workspace,
+                           workspace_bytes);
+}
+
+int s2s_attn_beam_done(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength,
+                       void* workspace, int* all_done) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && workspace && all_done, "beam search: null argument");
+  return attn_beam_done(static_cast<hipStream_t>(stream), to_attn(d), K, maxseqlength, workspace, all_done);
+}
+
+int s2s_attn_beam_finish(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength,
+                         int* out, int ldo, int* out_len, float* out_score, void* workspace) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(d && out && out_len && workspace, "beam search: null argument");
+  return attn_beam_finish(static_cast<hipStream_t>(stream), to_attn(d), K, maxseqlength, workspace, out, ldo, out_len,
+                          out_score);
 }
 
 int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b,

@@ -43,6 +43,12 @@ const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
 size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength);
 int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len, float* out_score, void* workspace, size_t workspace_bytes);
+int s2s_attn_beam_init(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const float* const* params, int eos, int K, int maxseqlength, void* workspace, size_t workspace_bytes);
+int s2s_attn_beam_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* const* params, int K, int maxseqlength, int count, void* workspace, size_t workspace_bytes);
+const float* s2s_attn_beam_mlp_input(const s2s_attn_dims* d, int K, int maxseqlength, void* workspace);
+int s2s_attn_beam_advance(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int eos, int K, int maxseqlength, int count, const float* logp, void* workspace, size_t workspace_bytes);
+int s2s_attn_beam_done(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength, void* workspace, int* all_done);
+int s2s_attn_beam_finish(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, int K, int maxseqlength, int* out, int ldo, int* out_len, float* out_score, void* workspace);
 int s2s_edit_distance(s2s_ctx* ctx, s2s_stream_t stream, int n, const int* a, const int* alen, int lda, const int* b, const int* blen, int ldb, int* out);
 size_t s2s_tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW);
 int s2s_tconv_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W, const float* b, float* y);
@@ -208,6 +214,40 @@ function M.attention_views(d, saved)
    local sv = vptr(saved)
    return {alpha = C.s2s_attn_alpha(d, sv), penalty = C.s2s_attn_alpha(d, sv), Ws = C.s2s_attn_ws(d, sv),
            Vh = C.s2s_attn_vh(d, sv)}
+end
+
+-- decoder:BeamSearch(annotations, eos, K, maxseqlength) (Attention.lua:332-438) for B utterances; eos and the
+-- tokens 0-based.  workspace: a CudaTensor (float; its storage also backs the decoder_mlp input view).
+-- mlp (optional): an external decoder_mlp module (d.external_mlp = 1), run between the search's step and
+-- advance calls on the (B*K, S+A) hypothesis rows.  Returns out (B, maxlen+1) -1 padded, lengths, scores.
+function M.beam_search(ctx, stream, d, h, params, eos, K, maxlen, workspace, mlp)
+   local B = d.B
+   local bytes = tonumber(C.s2s_attn_beam_workspace_bytes(d, K, maxlen))
+   workspace:resize(math.ceil(bytes / 4))
+   local out = torch.CudaIntTensor(B, maxlen + 1)
+   local len, score = torch.CudaIntTensor(B), torch.CudaTensor(B)
+   local P, ws, n = ptrs('const float*', params), vptr(workspace), 4 * workspace:nElement()
+   if mlp == nil then
+      M.check(C.s2s_attn_beam_search(ctx, stream, d, dptr(h), P, eos, K, maxlen, iptr(out), maxlen + 1, iptr(len),
+                                     dptr(score), ws, n))
+      return out, len, score
+   end
+   local R, W = B * K, d.stateDepth + d.annotationDepth
+   local off = tonumber(ffi.cast('const float*', C.s2s_attn_beam_mlp_input(d, K, maxlen, ws)) - dptr(workspace))
+   local rows = torch.CudaTensor(workspace:storage(), workspace:storageOffset() + off, torch.LongStorage{R, W})
+   local done = ffi.new('int[1]')
+   M.check(C.s2s_attn_beam_init(ctx, stream, d, dptr(h), P, eos, K, maxlen, ws, n))
+   for count = 0, maxlen do
+      M.check(C.s2s_attn_beam_step(ctx, stream, d, P, K, maxlen, count, ws, n))
+      local logp = mlp:forward(rows):contiguous()
+      M.check(C.s2s_attn_beam_advance(ctx, stream, d, eos, K, maxlen, count, dptr(logp), ws, n))
+      if count % 4 == 3 or count == maxlen then
+         M.check(C.s2s_attn_beam_done(ctx, stream, d, K, maxlen, ws, done))
+         if done[0] ~= 0 then break end
+      end
+   end
+   M.check(C.s2s_attn_beam_finish(ctx, stream, d, K, maxlen, iptr(out), maxlen + 1, iptr(len), dptr(score), ws))
+   return out, len, score
 end
 
 -- the whole autoencoder:forward({X, labelmask}) + NLL + backward(-labelmask) on flat buffers

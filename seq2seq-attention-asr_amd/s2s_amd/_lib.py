@@ -88,6 +88,16 @@ SIGNATURES = [
     ("s2s_attn_beam_workspace_bytes", c_size_t, [P(s2s_attn_dims), c_int, c_int]),
     ("s2s_attn_beam_search", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, c_int, c_int, c_int,
                                      c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_size_t]),
+    ("s2s_attn_beam_init", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, c_int, c_int, c_int,
+                                   c_void_p, c_size_t]),
+    ("s2s_attn_beam_step", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_int, c_int, c_int, c_void_p,
+                                   c_size_t]),
+    ("s2s_attn_beam_mlp_input", c_void_p, [P(s2s_attn_dims), c_int, c_int, c_void_p]),
+    ("s2s_attn_beam_advance", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_int, c_int, c_int, c_int, c_void_p,
+                                      c_void_p, c_size_t]),
+    ("s2s_attn_beam_done", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_int, c_int, c_void_p, P(c_int)]),
+    ("s2s_attn_beam_finish", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_int, c_int, c_void_p, c_int, c_void_p,
+                                     c_void_p, c_void_p]),
     ("s2s_edit_distance", c_int, [c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p, c_int,
                                   c_void_p]),
     ("s2s_optim_state_bytes", c_size_t, [c_size_t]),

@@ -600,7 +600,9 @@ class Attention(Module):
         """decoder:BeamSearch(annotations, eos, K, maxseqlength) (Attention.lua:332-438) in evaluate()
         mode.  annotations (L, A) -> 1-D int tensor (the prediction, 0-based tokens, eos last when it
         finished on eos); (B, L, A) -> (tokens (B, maxseqlength + 1) padded with -1, lengths (B),
-        scores (B)).  maxseqlength defaults to L (:337)."""
+        scores (B)).  maxseqlength defaults to L (:337).  Content or hybrid attention, GRU or LSTM
+        decoder_recurrent; an external decoder_mlp runs between the search's step and advance calls on
+        the (B*K, S+A) hypothesis rows."""
         h = annotations
         if h.dim() not in (2, 3):
             raise S2SArgumentError("annotations must be 2d or 3d")
@@ -608,23 +610,54 @@ class Attention(Module):
         single = h.dim() == 2
         if single:
             h = h[None]
+        h = h.contiguous()
         B, L = h.shape[0], h.shape[1]
         maxlen = int(maxseqlength or L)
         was_train, self.train = self.train, False
         d = self._dims(h, 1)
         self.train = was_train
+        d.frame_lengths = d.label_lengths = None  # the utterances' whole annotation sequences are searched
         dev = h.device
-        if self.external_mlp:
-            raise S2SArgumentError("BeamSearch runs the fused MaxoutMLP decoder_mlp only")
         self._sync_pad()
         ws = _bytes(lib.s2s_attn_beam_workspace_bytes(ctypes.byref(d), K, maxlen), dev)
         out = torch.empty((B, maxlen + 1), dtype=torch.int32, device=dev)
         olen = torch.empty(B, dtype=torch.int32, device=dev)
         osc = torch.empty(B, dtype=torch.float32, device=dev)
         params = self._ptrs(False)
-        check(lib.s2s_attn_beam_search(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h), params,
-                                       int(eos), int(K), maxlen, dptr(out), maxlen + 1, dptr(olen), dptr(osc),
-                                       dptr(ws), ws.numel()))
+        ctx, st = get_context(dev.index).handle, stream_ptr()
+        if not self.external_mlp:
+            check(lib.s2s_attn_beam_search(ctx, st, ctypes.byref(d), dptr(h), params, int(eos), int(K), maxlen,
+                                           dptr(out), maxlen + 1, dptr(olen), dptr(osc), dptr(ws), ws.numel()))
+        else:
+            R, W = B * int(K), self.stateDepth + self.annotationDepth
+            p = lib.s2s_attn_beam_mlp_input(ctypes.byref(d), int(K), maxlen, dptr(ws))
+            off = p - ws.data_ptr()
+            rows = ws[off:off + 4 * R * W].view(torch.float32).view(R, W)
+            mlp_train = getattr(self.decoder_mlp, "train", None)
+            if mlp_train is not None:
+                self.decoder_mlp.train = False
+            done = ctypes.c_int(0)
+            try:
+                check(lib.s2s_attn_beam_init(ctx, st, ctypes.byref(d), dptr(h), params, int(eos), int(K), maxlen,
+                                             dptr(ws), ws.numel()))
+                for count in range(maxlen + 1):
+                    check(lib.s2s_attn_beam_step(ctx, st, ctypes.byref(d), params, int(K), maxlen, count, dptr(ws),
+                                                 ws.numel()))
+                    logp = self.decoder_mlp.forward(rows).contiguous()
+                    if logp.shape != (R, self.outputDepth) or logp.dtype != torch.float32:
+                        raise S2SArgumentError("decoder_mlp must map (B*K, S+A) rows to (B*K, outputDepth) fp32")
+                    check(lib.s2s_attn_beam_advance(ctx, st, ctypes.byref(d), int(eos), int(K), maxlen, count,
+                                                    dptr(logp), dptr(ws), ws.numel()))
+                    if (count & 3) == 3 or count == maxlen:
+                        check(lib.s2s_attn_beam_done(ctx, st, ctypes.byref(d), int(K), maxlen, dptr(ws),
+                                                     ctypes.byref(done)))
+                        if done.value:
+                            break
+                check(lib.s2s_attn_beam_finish(ctx, st, ctypes.byref(d), int(K), maxlen, dptr(out), maxlen + 1,
+                                               dptr(olen), dptr(osc), dptr(ws)))
+            finally:
+                if mlp_train is not None:
+                    self.decoder_mlp.train = mlp_train
         if single:
             return out[0, :int(olen[0].item())]
         return out, olen, osc

@@ -722,3 +722,94 @@ def test_conv_bilstm_attention_model_step_matches_oracle(fe):
     pairs += [("dmlp0.W", lins[0].gradWeight, mg[0][0]), ("dmlp2.W", lins[1].gradWeight, mg[2][0]),
               ("dmlp2.b", lins[1].gradBias, mg[2][1])]
     _assert_grads(pairs)
+
+
+# --------------------------------------------------------------------------- beam search, every decoder variant
+
+def _check_beam(att, h, P, cfg, eos, K, maxlen, mlp=None):
+    """decoder:BeamSearch on the device vs the oracle's per-utterance search (Attention.lua:332-438).  A
+    hypothesis may flip only at an fp32-vs-fp64 near tie, so a differing prediction must score (teacher-forced,
+    oracle) within 1e-4 of the oracle's best; the reported score equals the oracle's rescoring of the GPU's
+    own prediction."""
+    from oracle import s2s_oracle as orc
+    B = h.shape[0]
+    toks, lens, scores = att.BeamSearch(cu(h), eos, K, maxlen)
+    toks, lens, scores = toks.cpu().numpy(), lens.cpu().numpy(), scores.cpu().numpy()
+
+    def rescore(b, seq):
+        st, Vh, tot, y = orc.decoder_zero_state(h.shape[1], cfg.stateDepth), h[b] @ P["V"].T, 0.0, -1
+        for tok in seq:
+            lp, st = orc.decoder_step(h[b], Vh, st, y, P, cfg, mlp)
+            tot, y = tot + lp[tok], tok
+        return tot
+
+    agree = 0
+    for b in range(B):
+        seq = [int(t) for t in toks[b, :lens[b]]]
+        assert all(t == -1 for t in toks[b, lens[b]:])
+        assert seq[-1] == eos or len(seq) == maxlen + 1
+        ref_seq, ref_score = orc.beam_search(h[b], P, cfg, eos, K, maxlen, mlp=mlp)
+        mine = rescore(b, seq)
+        assert abs(mine - scores[b]) <= 1e-4 * max(1.0, abs(mine)), (b, mine, scores[b])
+        if seq == list(ref_seq):
+            agree += 1
+        else:
+            assert mine >= ref_score - 1e-4 * max(1.0, abs(ref_score)), (b, seq, ref_seq, mine, ref_score)
+    assert agree >= B - 1
+    return toks, lens
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("hyb,K,maxlen", [((5, 16), 4, 10), ((0, 0), 3, 8), ((5, 16), 1, 6)])
+def test_beam_search_lstm_decoder_matches_oracle(fe, hyb, K, maxlen):
+    """BeamSearch with the timit/timit.lua:137 LSTM decoder_recurrent (the cell carried per hypothesis) and
+    hybrid location-aware attention (alpha_{t-1} carried), fused Maxout MLP."""
+    import s2s_amd
+    rng = np.random.default_rng(K * 10 + maxlen)
+    B, L, S, A, Sc, O, eos = 5, 24, 32, 64, 48, 11, 2
+    cfg, P = _lstm_dec_case(rng, S, A, Sc, O, hyb, "maxout")
+    att, _ = _load_lstm_attention(s2s_amd, fe, P, cfg, s2s_amd.MaxoutMLP(S + A, 4, 3, O))
+    h = rng.standard_normal((B, L, A)) * 1.5
+    toks, lens = _check_beam(att, h, P, cfg, eos, K, maxlen)
+    one = att.BeamSearch(cu(h[1]), eos, K, maxlen).cpu().numpy()
+    assert list(one) == list(toks[1, :lens[1]])
+
+
+@pytest.mark.gpu
+def test_beam_search_gru_hybrid_matches_oracle(fe):
+    """BeamSearch with the Chorowski GRU decoder and hybrid attention (kW = 5, nF = 8)."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    torch.manual_seed(3)
+    rng = np.random.default_rng(17)
+    B, L, S, A, Sc, O, M, Kw, eos = 4, 26, 32, 64, 64, 13, 4, 3, 3
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=Kw, numLayers=1, hybridAttendFilterSize=5,
+                          hybridAttendFeatureMaps=8)
+    att = s2s_amd.Attention(s2s_amd.GRU(S, S), s2s_amd.MaxoutMLP(S + A, M, Kw, O), Sc, 5, 8, S, A, O, True,
+                            0.0).cuda()
+    with torch.no_grad():
+        att.own["hybU"].mul_(4.0)  # location features visibly steer the scores
+    P = {n: _np(t) for n, t in att.own.items()}
+    P.update({f"dec.W{g}": _np(t) for g, t in zip("zrh", att.decoder_recurrent.weight)})
+    P.update({n: _np(t) for n, t in zip(("Wm", "bm", "Wo", "bo"), att.decoder_mlp.weight)})
+    h = rng.standard_normal((B, L, A)) * 1.5
+    _check_beam(att, h, P, cfg, eos, 4, 9)
+
+
+@pytest.mark.gpu
+def test_beam_search_external_mlp_matches_oracle(fe):
+    """BeamSearch of the timit/timit.lua:126-145 decoder as built there: LSTM recurrence, hybrid attention, and the
+    external decoder_mlp Linear -> ReLU -> Linear -> LogSoftMax run between the search's step and advance calls."""
+    import s2s_amd
+    rng = np.random.default_rng(43)
+    B, L, S, A, Sc, O, eos = 4, 20, 32, 64, 48, 11, 2
+    cfg, P = _lstm_dec_case(rng, S, A, Sc, O, (5, 16), "relu")
+    mlp = fe.Sequential(fe.Linear(S + A, 2 * O), fe.ReLU(), fe.Linear(2 * O, O), fe.LogSoftMax())
+    att, _ = _load_lstm_attention(s2s_amd, fe, P, cfg, mlp)
+    lins = [m for m in mlp.modules if isinstance(m, fe.Linear)]
+    layers = [("linear", _np(lins[0].weight), _np(lins[0].bias)), ("relu",),
+              ("linear", _np(lins[1].weight), _np(lins[1].bias)), ("logsoftmax",)]
+    ext = lambda v: fo.mlp_fwd(v[None], layers)[0][0]  # noqa: E731
+    h = rng.standard_normal((B, L, A)) * 1.5
+    _check_beam(att, h, P, cfg, eos, 3, 8, mlp=ext)

@@ -253,12 +253,20 @@ def test_wagner_fischer_known_answers():
     assert orc.wagner_fischer([1, 2, 3], [1, 2, 3]) == 0
 
 
-def test_beam_search_step_matches_teacher_forced_forward():
+@pytest.mark.parametrize("variant", ["gru", "hybrid", "lstm", "hybrid_lstm"])
+def test_beam_search_step_matches_teacher_forced_forward(variant):
     """decoder_step restates the training forward's step: the beam search's score of its best
     hypothesis equals the teacher-forced log-likelihood of that sequence (attention_fwd with the
-    hypothesis as labels), and K = 1 is greedy decoding."""
-    cfg = tiny_cfg()
+    hypothesis as labels), and K = 1 is greedy decoding -- for the content / hybrid attention and the
+    GRU / LSTM decoder_recurrent (the carried hidden {alpha, s, mem})."""
+    kw = dict(hybridAttendFeatureMaps=3, hybridAttendFilterSize=5) if "hybrid" in variant else {}
+    cfg = tiny_cfg(decoderLSTM="lstm" in variant, **kw)
     P = orc.init_params(cfg, seed=13)
+    if cfg.decoderLSTM:  # LSTM(S, S) gates (LSTM.lua:25-29); init_params draws the GRU's
+        prng, S = np.random.default_rng(5), cfg.stateDepth
+        for q in "ifgo":
+            P.update({f"dec.W{q}x": prng.standard_normal((S, S)) * 0.4, f"dec.b{q}x": prng.standard_normal(S) * 0.1,
+                      f"dec.W{q}h": prng.standard_normal((S, S)) * 0.4, f"dec.b{q}h": prng.standard_normal(S) * 0.1})
     rng = np.random.default_rng(3)
     h = rng.standard_normal((9, cfg.annotationDepth))
     for K in (1, 3):
@@ -266,12 +274,27 @@ def test_beam_search_step_matches_teacher_forced_forward():
         logp, _ = orc.attention_fwd(h[None], np.array([seq]), P, cfg)
         assert abs(logp[0, np.arange(len(seq)), seq].sum() - score) < 1e-10
         assert seq[-1] == 2 or len(seq) == 7
-    greedy, y, s, a = [], -1, np.zeros(cfg.stateDepth), np.zeros(9)
+    greedy, y, st = [], -1, orc.decoder_zero_state(9, cfg.stateDepth)
     Vh = h @ P["V"].T
     for _ in range(7):
-        lp, s, a = orc.decoder_step(h, Vh, s, y, a, P, cfg)
+        lp, st = orc.decoder_step(h, Vh, st, y, P, cfg)
         y = int(np.argmax(lp))
         greedy.append(y)
         if y == 2:
             break
     assert orc.beam_search(h, P, cfg, eos=2, K=1, maxseqlength=6)[0] == greedy
+
+
+def test_beam_search_external_mlp_equals_fused():
+    """An external decoder_mlp (the Maxout -> Linear -> LogSoftMax stack as a callable) searches exactly
+    like the fused MaxoutMLP."""
+    from oracle import frontend_oracle as fo
+    cfg = tiny_cfg()
+    P = orc.init_params(cfg, seed=17)
+    h = np.random.default_rng(4).standard_normal((9, cfg.annotationDepth))
+    layers = [("maxout", P["Wm"], P["bm"], cfg.maxoutWindow), ("linear", P["Wo"], P["bo"]), ("logsoftmax",)]
+    mlp = lambda v: fo.mlp_fwd(v[None], layers)[0][0]  # noqa: E731
+    for K in (1, 4):
+        a = orc.beam_search(h, P, cfg, eos=2, K=K, maxseqlength=6)
+        b = orc.beam_search(h, P, cfg, eos=2, K=K, maxseqlength=6, mlp=mlp)
+        assert a[0] == b[0] and abs(a[1] - b[1]) < 1e-12
