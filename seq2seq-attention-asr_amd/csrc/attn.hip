@@ -1663,11 +1663,12 @@ __global__ __launch_bounds__(256) void beam_update(AttnK k, BeamK q, int count) 
     }
     __syncthreads();
   }
-  // the first K - finished of the sorted candidates extend their parents (Attention.lua:413-430)
+  // the first K - finished of the sorted candidates extend their parents (Attention.lua:413-430); at
+  // count 0 the one zero-state row offers all K (:369-387), later the K - finished survivors
   if (tid == 0) {
     int nf = 0, nn = 0;
     const int fin = q.nfin[b];
-    for (int m = 0; m < nact && m < nsel; ++m) {
+    for (int m = 0; m < K - fin && m < nsel; ++m) {
       const int i = sel[m] / O, j = sel[m] - i * O;
       if (j == q.eos || (count > 0 && count == q.maxlen)) {
         fpar[nf] = i; ftok[nf] = j; fsc[nf] = selv[m]; fdst[nf] = fin + nf; ++nf;

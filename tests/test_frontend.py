@@ -813,3 +813,29 @@ def test_beam_search_external_mlp_matches_oracle(fe):
     ext = lambda v: fo.mlp_fwd(v[None], layers)[0][0]  # noqa: E731
     h = rng.standard_normal((B, L, A)) * 1.5
     _check_beam(att, h, P, cfg, eos, 3, 8, mlp=ext)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [2, 3, 4])
+def test_beam_search_keeps_K_hypotheses_from_the_first_step(fe, K):
+    """Attention.lua:369-387: the first step (one zero-state row) seeds all K hypotheses, eos among them
+    finishing at once.  Swept over maxseqlength so an eos ranked k-th at step 0 and ties in later
+    selections both come up (this case's utterance 1 finishes on eos at step 0 for K = 4)."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    torch.manual_seed(3)
+    rng = np.random.default_rng(17)
+    B, L, S, A, Sc, O, M, Kw, eos = 4, 26, 32, 64, 64, 13, 4, 3, 3
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=M, maxoutWindow=Kw, numLayers=1, hybridAttendFilterSize=5,
+                          hybridAttendFeatureMaps=8)
+    att = s2s_amd.Attention(s2s_amd.GRU(S, S), s2s_amd.MaxoutMLP(S + A, M, Kw, O), Sc, 5, 8, S, A, O, True,
+                            0.0).cuda()
+    with torch.no_grad():
+        att.own["hybU"].mul_(4.0)
+    P = {n: _np(t) for n, t in att.own.items()}
+    P.update({f"dec.W{g}": _np(t) for g, t in zip("zrh", att.decoder_recurrent.weight)})
+    P.update({n: _np(t) for n, t in zip(("Wm", "bm", "Wo", "bo"), att.decoder_mlp.weight)})
+    h = rng.standard_normal((B, L, A)) * 1.5
+    for maxlen in (1, 2, 3, 5, 8):
+        _check_beam(att, h, P, cfg, eos, K, maxlen)
