@@ -49,6 +49,14 @@ __device__ __forceinline__ void put_granule_pair(granule_t* base, long idx, floa
   if (active) put_granule(base + idx, v, tag, local);
 #endif
 }
+// two adjacent granules j, j+1 of one lane (j % 2 == 0) as one 16-byte store
+__device__ __forceinline__ void put_granule2(__amdgpu_buffer_rsrc_t rs, long byte_off, float v0, float v1, unsigned tag,
+                                             bool local = false) {
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4 d = {__float_as_uint(v0), tag, __float_as_uint(v1), tag};
+  if (local) __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)byte_off, 0, 1);
+  else __builtin_amdgcn_raw_buffer_store_b128(d, rs, (int)byte_off, 0, 16);
+}
 // four adjacent granules j..j+3 of one lane (j % 2 == 0) as two 16-byte write-through stores
 __device__ __forceinline__ void put_granule4(__amdgpu_buffer_rsrc_t rs, long byte_off, float v0, float v1, float v2,
                                              float v3, unsigned tag, bool local = false) {

@@ -30,7 +30,9 @@ def report(name, st, nph, labels):
 
 
 def main():
-    B, L, T = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (32, 128, 40)
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    B, L, T = (int(a) for a in args[:3]) if len(args) > 2 else (32, 128, 40)
+
     cfg = s2s_amd.ModelConfig()
     model = s2s_amd.ChorowskiBaseline(cfg)
     x = torch.randn(B, L, cfg.inputFrameSize, device="cuda")
