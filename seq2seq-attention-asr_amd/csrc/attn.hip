@@ -1995,8 +1995,9 @@ int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* 
 
 }  // namespace s2s
 
-// Diagnostic (not part of the C ABI header): device buffers of (grid * T * 8) uint64 that the
-// persistent decoder kernels fill with s_memrealtime stamps at phase ends; nullptr turns it off.
+// Diagnostic (not part of the C ABI header): device buffers of uint64 s_memrealtime stamps the persistent
+// decoder kernels fill at phase ends -- (grid, T, 8) for attn_persist.inc, (chains * 32, T, 16) for
+// dec_xcd.inc (tools/xdec_stamps.py, tools/xdec_substamps.py); nullptr turns it off.
 // diagnostic: 0 forces write-through (sc1) hand-offs in every XCD-local decoder chain
 extern "C" void s2s_debug_dec_local(int allow) { s2s::g_dec_allow_local = allow; }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {

@@ -37,7 +37,7 @@ def main():
     model = s2s_amd.ChorowskiBaseline(cfg)
     x = torch.randn(B, L, cfg.inputFrameSize, device="cuda")
     lab = torch.randint(0, cfg.outputDepth, (B, T), device="cuda", dtype=torch.int32)
-    nst = 8 * 32 * T * 8
+    nst = 8 * 32 * T * 16
     sf = torch.zeros(nst, dtype=torch.int64, device="cuda")
     sb = torch.zeros_like(sf)
     fn = _lib.lib.s2s_debug_dec_stamps
@@ -50,8 +50,8 @@ def main():
     fn(None, None)
     U = (B + 7) // 8  # attn.hip dec_xcd_plan
     nch = (B + U - 1) // U
-    f = sf.cpu().numpy().reshape(8 * 32, T, 8)[: nch * 32].reshape(nch, 32, T, 8).astype(np.float64)
-    b = sb.cpu().numpy().reshape(8 * 32, T, 8)[: nch * 32].reshape(nch, 32, T, 8)[:, :, ::-1].astype(np.float64)
+    f = sf.cpu().numpy().reshape(8 * 32, T, 16)[: nch * 32].reshape(nch, 32, T, 16).astype(np.float64)
+    b = sb.cpu().numpy().reshape(8 * 32, T, 16)[: nch * 32].reshape(nch, 32, T, 16)[:, :, ::-1].astype(np.float64)
     report("decoder forward", f, 6, ["(loop)", "F1 ws,us", "F2 attention", "F3 combine", "F4 gx,z,r,q", "F5 hh,s"])
     report("decoder backward", b, 7, ["(loop)", "G gate grads", "B2 dq,da_r", "B3 dc,us'", "B4 attention",
                                        "B45 dws", "B5 ds"])
