@@ -81,15 +81,15 @@ struct PArgs {
   unsigned* abort_word;
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
-  unsigned long long* stamps;  // diagnostic: [grid][L][6] s_memrealtime, or nullptr
+  unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
 };
 
 // diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
-// end and p2 sweep start / done / end
+// end and p2 sweep start / done / end; forward p1 sub-phases: 6 = MFMA issued, 7 = reduced
 #define GRU_STAMP(ph)                                                                      \
   do {                                                                                     \
     if (a.stamps && threadIdx.x == 0)                                                      \
-      a.stamps[((long)lw * a.L + s) * 6 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
+      a.stamps[((long)lw * a.L + s) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 unsigned long long* g_gru_stamps[2] = {nullptr, nullptr};
 
@@ -273,7 +273,6 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   float xz_n = 0.f, xh_n = 0.f;
   if (a.fused) xp_wait(0);
   xp_load(0, xz_n, xh_n);
-
   for (int s = 0; s < L; ++s) {
     const int t = g.reverse ? L - 1 - s : s;
     const long row = (long)ob * L + t;
@@ -298,12 +297,10 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
           if (i == it) *reinterpret_cast<float4*>(&hprev[lane & 15][4 * (lane >> 4)]) = av[i];
       }
     }
+    GRU_STAMP(6);
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
-    if (s + 1 < L) {  // next step's x-projection (xnext_lds was set before the reduce barrier)
-      if (a.fused && !__builtin_amdgcn_readfirstlane(xnext_lds[s & 1])) xp_wait(s + 1);
-      xp_load(s + 1, xz_n, xh_n);
-    }
+    GRU_STAMP(7);
     {
       const float gate = sigmoidf_(sum + xpv);
       float* sv = g.sv + row * 5 * H;
@@ -325,6 +322,13 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
           sv[4 * H + j] = q;
         }
       }
+    }
+    // next step's x-projection, after this step's hand-off is published: its load latency (and the
+    // fused producers' readiness poll) stays off the q / h critical path (xnext_lds was set before
+    // the reduce barrier)
+    if (s + 1 < L) {
+      if (a.fused && !__builtin_amdgcn_readfirstlane(xnext_lds[s & 1])) xp_wait(s + 1);
+      xp_load(s + 1, xz_n, xh_n);
     }
     GRU_STAMP(2);
     if (!isz) continue;

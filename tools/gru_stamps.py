@@ -19,7 +19,7 @@ from s2s_amd import _lib  # noqa: E402
 
 
 def analyse(name, st, nwg, ndir, ntile, prod1, cons1, prod2, cons2):
-    """st: (grid, L, 6) stamps in us; prodX / consX: workgroup offsets within a chain."""
+    """st: (grid, L, 8) stamps in us; prodX / consX: workgroup offsets within a chain."""
     L = st.shape[1]
     rows = []
     for d in range(ndir):
@@ -44,8 +44,8 @@ def main():
     ndir = 2
     ntile = (B + 15) // 16
     nf, nb = ndir * (2 * H // 16) * ntile, ndir * (H // 16) * ntile
-    sf = torch.zeros(nf * L * 6, dtype=torch.int64, device="cuda")
-    sb = torch.zeros(nb * L * 6, dtype=torch.int64, device="cuda")
+    sf = torch.zeros(nf * L * 8, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(nb * L * 8, dtype=torch.int64, device="cuda")
     fn = _lib.lib.s2s_debug_gru_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     x = torch.randn(B, L, D, device="cuda")
@@ -56,12 +56,15 @@ def main():
     model.step(x, lab)
     torch.cuda.synchronize()
     fn(None, None)
-    tf = sf.cpu().numpy().reshape(nf, L, 6).astype(np.float64) * 0.01
-    tb = sb.cpu().numpy().reshape(nb, L, 6).astype(np.float64) * 0.01
+    tf = sf.cpu().numpy().reshape(nf, L, 8).astype(np.float64) * 0.01
+    tb = sb.cpu().numpy().reshape(nb, L, 8).astype(np.float64) * 0.01
     z = list(range(H // 16))
     zr = list(range(2 * H // 16))
     r = list(range(H // 16, 2 * H // 16))
     analyse("gru forward ", tf, nf // ndir, ndir, ntile, prod1=z, cons1=zr, prod2=r, cons2=z)
+    t = tf[:, 2:]  # per-workgroup means of the forward p1 sub-phases
+    print(f"  p1 per workgroup: MFMA {(t[..., 6] - t[..., 1]).mean():.2f}  reduce {(t[..., 7] - t[..., 6]).mean():.2f}"
+          f"  gate + publish {(t[..., 2] - t[..., 7]).mean():.2f} us")
     # backward stamps are indexed by time step s (processed L-1 .. 0): flip to processing order
     tbp = tb[:, ::-1, :].copy()
     allc = list(range(H // 16))
