@@ -393,10 +393,17 @@ int tmaxpool_bwd(hipStream_t st, int B, int L, int D, int kW, int dW, const int*
 }
 
 // ------------------------------------------------------------------ SpatialConvolutionMM
+// scratch: split-K slabs | im2col panel (K, B N) | dcol (K, B N) | dyt (Cout, B N); under bf16 the implicit
+// forward / input gradient keep their re-laid-out weights (Cin Cout kH kW) in the panel / dcol region
+static size_t sconv_dcol_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
+  const size_t K = (size_t)Cin * kH * kW, BN = (size_t)B * (H - kH + 1) * (W - kW + 1);
+  return align256(std::max(sizeof(float) * K * BN, sconv_implicit_scratch_bytes(B, Cin, H, W, Cout, kH, kW)));
+}
 size_t sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
   const size_t N = (size_t)(H - kH + 1) * (W - kW + 1);
   const size_t K = (size_t)Cin * kH * kW;
-  return kWsBytes + 2 * align256(sizeof(float) * K * B * N) + align256(sizeof(float) * (size_t)Cout * B * N);
+  return kWsBytes + 2 * sconv_dcol_bytes(B, Cin, H, W, Cout, kH, kW) +
+         align256(sizeof(float) * (size_t)Cout * B * N);
 }
 
 int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
@@ -408,7 +415,10 @@ int sconv_fwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
   const long N = (long)Ho * Wo;
   const int K = Cin * kH * kW;
   S2S_REQUIRE(K <= 65535 && B <= 65535 && (long)B * N < 2147483647L, "SpatialConvolutionMM: sizes exceed the grid");
+  // bf16 operands: implicit GEMM straight from x (no im2col panel in HBM)
   float* col = reinterpret_cast<float*>(static_cast<char*>(scratch) + kWsBytes);
+  if (gemm_precision() == kGemmBf16 && kH == kW && (kW == 3 || kW == 1))  // re-laid-out weights in the panel region
+    return sconv_fwd_implicit(st, B, Cin, H, W, Cout, kH, kW, relu, x, Wt, bias, y, col);
   launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
   S2S_CHECK_HIP(hipGetLastError());
   // y_b (Cout, N) = W (Cout, K) col[:, b*N : (b+1)*N] + bias (per row), ReLU in the epilogue
@@ -439,8 +449,8 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
               "SpatialConvolutionMM: sizes exceed the grid");
   char* base = static_cast<char*>(scratch) + kWsBytes;
   float* col = reinterpret_cast<float*>(base);
-  float* dcol = reinterpret_cast<float*>(base + align256(sizeof(float) * K * BN));
-  float* dyt = reinterpret_cast<float*>(base + 2 * align256(sizeof(float) * K * BN));
+  float* dcol = reinterpret_cast<float*>(base + sconv_dcol_bytes(B, Cin, H, W, Cout, kH, kW));
+  float* dyt = reinterpret_cast<float*>(base + 2 * sconv_dcol_bytes(B, Cin, H, W, Cout, kH, kW));
   hipLaunchKernelGGL(nchw_to_cbn_kernel, dim3((unsigned)((N + 255) / 256), Cout, B), dim3(256), 0, st, dy, y, relu, B,
                      Cout, (int)N, dyt);
   S2S_CHECK_HIP(hipGetLastError());
@@ -451,14 +461,18 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
     hipLaunchKernelGGL(rowsum_final_kernel, dim3((Cout + 255) / 256), dim3(256), 0, st, part, Cout, scale, 1.f, db);
     S2S_CHECK_HIP(hipGetLastError());
   }
+  // bf16 forward / input gradient are implicit GEMMs (no panels); the weight gradient keeps the panel
+  const bool implicit = gemm_precision() == kGemmBf16 && kH == kW && (kW == 3 || kW == 1);
   if (dW) {
-    if (!col_from_fwd)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
-    launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
+    if (!col_from_fwd || implicit)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
+      launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
     S2S_CHECK_HIP(hipGetLastError());
     // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
     WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
     S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
   }
+  if (dx && implicit)  // dx = transposed convolution of dyt, the re-laid-out weights in the dcol region
+    return sconv_dx_implicit(st, B, Cin, H, W, Cout, kH, kW, Wt, dyt, dx, dx_accumulate, dcol);
   if (dx) {
     // dcol (K, B*N) = W^T dyt ; dx = col2im(dcol)
     S2S_TRY(gemm1(st, true, false, K, (int)BN, Cout, 1.f, Wt, K, dyt, BN, 0.f, dcol, BN));

@@ -34,6 +34,12 @@ namespace {
 
 constexpr int BK = 32, LDK = BK + 4;
 
+// Out-of-range lanes of the guarded operand loaders read this zero instead of branching around the
+// load: a conditional value (cond ? x : 0) let the compiler sink each load into an exec-masked block
+// followed by its own vmcnt(0) wait, serialising a tile's loads; a select between two addresses
+// keeps every load of the tile in flight together.
+__device__ float g_zero_f32 = 0.f;
+
 struct GemmTile {
   GemmProblem p;
   float* part;  // split-K partial slabs (splits x M x N) or nullptr
@@ -63,8 +69,7 @@ __device__ __forceinline__ void load_kc(floatx4 (&v)[R / 32], const float* X, lo
       float e[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = row[min(k + c, kend - 1)];
-        e[c] = (gr < rmax && k + c < kend) ? x : 0.f;
+        e[c] = *((gr < rmax && k + c < kend) ? row + k + c : &g_zero_f32);
       }
       v[j] = floatx4{e[0], e[1], e[2], e[3]};
     }
@@ -93,8 +98,7 @@ __device__ __forceinline__ void load_rc(floatx4 (&v)[R / 32], const float* X, lo
       float e[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = row[min(r + c, rmax - 1)];
-        e[c] = (k < kend && r + c < rmax) ? x : 0.f;
+        e[c] = *((k < kend && r + c < rmax) ? row + r + c : &g_zero_f32);
       }
       v[j] = floatx4{e[0], e[1], e[2], e[3]};
     }
@@ -197,8 +201,7 @@ __device__ __forceinline__ void hload_kc(floatx4 (&v)[R / 16], const float* X, l
       float e[4];
 #pragma unroll
       for (int c = 0; c < 4; ++c) {
-        const float x = row[min(k + c, kend - 1)];
-        e[c] = (gr < rmax && k + c < kend) ? x : 0.f;
+        e[c] = *((gr < rmax && k + c < kend) ? row + k + c : &g_zero_f32);
       }
       v[j] = floatx4{e[0], e[1], e[2], e[3]};
     }
@@ -231,8 +234,7 @@ __device__ __forceinline__ void hload_rc(floatx4 (&v)[R / 16], const float* X, l
         float e[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const float x = row[min(r + q, rmax - 1)];
-          e[q] = (k < kend && r + q < rmax) ? x : 0.f;
+          e[q] = *((k < kend && r + q < rmax) ? row + r + q : &g_zero_f32);
         }
         v[4 * j + c] = floatx4{e[0], e[1], e[2], e[3]};
       }
@@ -563,6 +565,8 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
     dst[i] = alpha * src[i] + (beta == 0.f ? 0.f : beta * dst[i]);
 }
 
+#include "conv_bf16.inc"
+
 }  // namespace
 
 static thread_local int g_gemm_prec = kGemmF32;
@@ -755,6 +759,97 @@ int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alph
   hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, n, alpha, beta);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
+}
+
+// ------------------------------------------------------------------ implicit-GEMM convolutions (conv_bf16.inc)
+static int conv_launch(hipStream_t st, bool dx, ConvArgs& c, const float* W, void* scratch, const char* name) {
+  S2S_REQUIRE(c.M > 0 && c.K > 0 && c.N > 0, "conv: bad sizes");
+  S2S_REQUIRE(c.g.kH == c.g.kW && (c.g.kW == 3 || c.g.kW == 1), "conv: implicit bf16 path for 3x3 / 1x1 kernels");
+  const int kk = c.g.kH * c.g.kW;
+  float* wr = static_cast<float*>(scratch);
+  __bf16* xh = reinterpret_cast<__bf16*>(static_cast<char*>(scratch) +
+                                         (sconv_implicit_wscratch_bytes(c.g.Cin, c.g.Cout, c.g.kH, c.g.kW) + 255) / 256 * 256);
+  // tap-major K over a channels-last bf16 copy when the gathered tensor's channels fill whole K-tiles
+  // (every VGG layer but the first)
+  const int C = dx ? c.g.Cout : c.g.Cin;
+  const bool tapk = C % HBK == 0;
+  if (tapk) {
+    const long P = dx ? (long)c.g.B * c.g.Ho * c.g.Wo : (long)c.g.H * c.g.W;  // dx: dyt (Cout, B Ho Wo) as one image
+    const int nb = dx ? 1 : c.g.B;
+    S2S_REQUIRE(P < (1L << 31) / 64, "conv: image too large");
+    hipLaunchKernelGGL(nchw_to_nhwc_bf16, dim3((unsigned)((P + 63) / 64), C / 64, nb), dim3(256), 0, st, c.X, nullptr, C,
+                       (int)P, xh);
+    c.Xh = xh;
+    c.xhlen = (long)nb * P * C;
+  }
+  if (dx || tapk) {  // weights in the GEMM's K order (the first layer's forward reads W as it is)
+    hipLaunchKernelGGL(conv_w_relayout, dim3(std::min(1024, (c.g.Cout * c.g.Cin * kk + 255) / 256)), dim3(256), 0,
+                       st, W, c.g.Cout, c.g.Cin, kk, dx ? 1 : 0, tapk ? 1 : 0, wr);
+    S2S_CHECK_HIP(hipGetLastError());
+    c.A = wr;
+  } else {
+    c.A = W;
+  }
+  const long tiles_n = (c.N + kConvBN - 1) / kConvBN;
+  c.tiles_m = (c.M + kConvBM - 1) / kConvBM;
+  S2S_REQUIRE(tiles_n * c.tiles_m < 2147483647L / 8, "conv: too many tiles");
+  c.nblocks = (int)(tiles_n * c.tiles_m);
+  const double flops = 2.0 * c.M * (double)c.N * c.K;
+  const double bytes = 4.0 * ((double)c.M * c.K + (double)c.N * c.K / kk + (double)c.M * c.N);
+  ProfScope ps(st, name, flops, bytes);
+  const dim3 grid((unsigned)((c.nblocks + 7) / 8 * 8));
+#define S2S_CONV_LAUNCH(DXV, KWV, TK) hipLaunchKernelGGL((conv_bf16_kernel<DXV, KWV, TK>), grid, dim3(256), 0, st, c)
+  if (c.g.kW == 3) {
+    if (dx) { if (tapk) S2S_CONV_LAUNCH(true, 3, true); else S2S_CONV_LAUNCH(true, 3, false); }
+    else { if (tapk) S2S_CONV_LAUNCH(false, 3, true); else S2S_CONV_LAUNCH(false, 3, false); }
+  } else {
+    if (dx) { if (tapk) S2S_CONV_LAUNCH(true, 1, true); else S2S_CONV_LAUNCH(true, 1, false); }
+    else { if (tapk) S2S_CONV_LAUNCH(false, 1, true); else S2S_CONV_LAUNCH(false, 1, false); }
+  }
+#undef S2S_CONV_LAUNCH
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+size_t sconv_implicit_wscratch_bytes(int Cin, int Cout, int kH, int kW) {
+  return sizeof(float) * (size_t)Cin * Cout * kH * kW;
+}
+size_t sconv_implicit_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
+  const size_t act = std::max((size_t)B * Cin * H * W, (size_t)B * Cout * (H - kH + 1) * (W - kW + 1));
+  return (sconv_implicit_wscratch_bytes(Cin, Cout, kH, kW) + 255) / 256 * 256 + 2 * act;
+}
+
+int sconv_fwd_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
+                       const float* Wt, const float* bias, float* y, void* scratch) {
+  ConvArgs c{};
+  c.g = ConvGeom{B, Cin, H, W, Cout, kH, kW, H - kH + 1, W - kW + 1};
+  S2S_REQUIRE((long)B * Cin * H * W < (1L << 29) && (long)B * Cout * c.g.Ho * c.g.Wo < (1L << 29),
+              "conv: implicit bf16 path needs tensors below 2^29 elements (32-bit byte offsets)");
+  c.X = x;
+  c.xlen = (long)B * Cin * H * W;
+  c.bias = bias;
+  c.Y = y;
+  c.M = Cout;
+  c.K = Cin * kH * kW;
+  c.N = (long)B * c.g.Ho * c.g.Wo;
+  c.relu = relu;
+  return conv_launch(st, false, c, Wt, scratch, "conv_fwd_bf16");
+}
+
+int sconv_dx_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, const float* Wt,
+                      const float* dyt, float* dx, int accumulate, void* scratch) {
+  ConvArgs c{};
+  c.g = ConvGeom{B, Cin, H, W, Cout, kH, kW, H - kH + 1, W - kW + 1};
+  S2S_REQUIRE((long)B * Cin * H * W < (1L << 29) && (long)B * Cout * c.g.Ho * c.g.Wo < (1L << 29),
+              "conv: implicit bf16 path needs tensors below 2^29 elements (32-bit byte offsets)");
+  c.X = dyt;
+  c.xlen = (long)Cout * B * c.g.Ho * c.g.Wo;
+  c.Y = dx;
+  c.M = Cin;
+  c.K = Cout * kH * kW;
+  c.N = (long)B * H * W;
+  c.accumulate = accumulate;
+  return conv_launch(st, true, c, Wt, scratch, "conv_dx_bf16");
 }
 
 }  // namespace s2s

@@ -125,6 +125,16 @@ struct GemmWs {
 constexpr size_t kGemmWsFloats = size_t(8) << 20;  // 32 MiB
 // All problems of one call share transA/transB.
 int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB, GemmWs ws = GemmWs{});
+// Implicit-GEMM SpatialConvolutionMM on bf16 MFMA (conv_bf16.inc): no im2col panel.  Forward y (B, Cout, Ho,
+// Wo) = conv(x) + bias (per channel), ReLU when relu; input gradient dx (B, Cin, H, W) (+)= transposed
+// convolution of dyt (Cout, B Ho Wo) -- the ReLU-masked output gradient -- with W.  scratch:
+// sconv_implicit_scratch_bytes (the weights in the GEMM's K order and a channels-last bf16 copy of the input).
+size_t sconv_implicit_wscratch_bytes(int Cin, int Cout, int kH, int kW);
+size_t sconv_implicit_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW);
+int sconv_fwd_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, int relu, const float* x,
+                       const float* Wt, const float* bias, float* y, void* scratch);
+int sconv_dx_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, const float* Wt,
+                      const float* dyt, float* dx, int accumulate, void* scratch);
 inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
                  const float* B, long ldb, float beta, float* C, long ldc, const float* bias = nullptr,
                  GemmWs ws = GemmWs{}) {

@@ -458,9 +458,10 @@ class ConvBiLSTMAttentionModel(Module):
 
     def __init__(self, inputFrameSize=123, numPhonemes=62, hiddenFrameSize=256, outputFrameSize=128,
                  stateDepth=400, scoreDepth=150, hybridAttendFilterSize=5, hybridAttendFeatureMaps=16, penalty=0.0,
-                 generator=None):
+                 generator=None, precision="fp32"):
         from .nn import Attention
         super().__init__()
+        self.precision = precision  # "fp32" | "bf16" | "bf16-all" (s2s_amd.precision) for the step's GEMMs
         g = generator
         S, A, O = stateDepth, 2 * outputFrameSize, numPhonemes
         self.encoder = ConvBiLSTMEncoder(inputFrameSize, hiddenFrameSize, outputFrameSize, 3, generator=g)

@@ -102,17 +102,18 @@ def test_model_step_bf16_config3_dims(lib, prec):
     assert errs["logp"] > 1e-6  # bf16 really ran (fp32 reaches ~2e-7 here)
 
 
-def test_vgg_model_step_bf16_config5(lib):
+@pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
+def test_vgg_model_step_bf16_config5(lib, prec):
     """BASELINE config 5 (librispeech/model_vgg.lua, bf16): full width (1x1 layers 2048), B = 1, L = 256,
     T = 50, against the float64 oracle; tensors the fp32 restatement cannot pin to 1e-5 (cancelling sums,
-    tests/test_gpu_fullsize.py) are reported, not judged."""
+    tests/test_gpu_fullsize.py) are reported, not judged.  bf16-all also takes the weight gradients in bf16."""
     import s2s_amd
     import vgg_case as vc
     from s2s_amd import frontend as fe
     g = torch.Generator().manual_seed(5)
     B, L, T = 1, 256, 50
     model = s2s_amd.VGGAttentionModel(40, outputFrameSize=512, hidden=2048, outputDepth=29, generator=g,
-                                      precision="bf16").cuda()
+                                      precision=prec).cuda()
     rng = np.random.default_rng(5)
     x = rng.standard_normal((B, 3, L, 40))
     labels = np.append(rng.integers(0, 28, (B, T - 1)), np.full((B, 1), 28), axis=1).astype(np.int32)
@@ -127,7 +128,46 @@ def test_vgg_model_step_bf16_config5(lib):
     for (name, gpu, r64), (_, _, r32) in zip(vc.grad_pairs(model, fe, G64, mg64), vc.grad_pairs(model, fe, G32, mg32)):
         errs[name] = _rel(gpu.detach().cpu().numpy(), r64)
         floor[name] = _rel(r32, r64)
-    print("config 5 bf16 max rel errs (fp32 floor):", {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
+    print(f"config 5 {prec} max rel errs (fp32 floor):", {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
     bad = {k: f"{errs[k]:.2e}" for k in errs
            if floor[k] <= 1e-5 and not errs[k] <= (BF16_LOGP_RTOL if k == "logp" else BF16_GRAD_RTOL)}
     assert not bad, bad
+
+
+@pytest.mark.parametrize("B,Cin,H,W,Cout,relu", [(2, 3, 20, 12, 64, True), (2, 64, 17, 11, 64, False),
+                                                   (1, 128, 9, 13, 128, True), (3, 5, 7, 6, 7, False),
+                                                   (2, 64, 40, 21, 128, False)])
+def test_bf16_implicit_conv_exact_on_rounded_operands(lib, B, Cin, H, W, Cout, relu):
+    """SpatialConvolutionMM under bf16 runs as implicit GEMMs (conv_bf16.inc: no im2col / col2im panels):
+    the forward and the input gradient equal float64 convolutions of the bf16-rounded operands up to the
+    fp32 accumulation order (<= 2e-5 max|ref|); ragged pixel tiles, K = 27 / 45 / 576 / 1152, two channel
+    tiles, ReLU on and off."""
+    import s2s_amd
+    from s2s_amd import frontend as fe
+    from numpy.lib.stride_tricks import sliding_window_view as win
+    rng = np.random.default_rng(B * 1000 + Cin + H)
+    conv = fe.SpatialConvolutionMM(Cin, Cout, 3, 3, relu=relu)
+    x = rng.standard_normal((B, Cin, H, W)).astype(np.float32)
+    Wt = (rng.standard_normal((Cout, Cin * 9)) * 0.2).astype(np.float32)
+    bias = (rng.standard_normal(Cout) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((B, Cout, H - 2, W - 2)).astype(np.float32)
+    conv.weight = torch.tensor(Wt, device="cuda")
+    conv.bias = torch.tensor(bias, device="cuda")
+    conv.gradWeight = torch.zeros_like(conv.weight)
+    conv.gradBias = torch.zeros_like(conv.bias)
+    xg, dyg = torch.tensor(x, device="cuda"), torch.tensor(dy, device="cuda")
+    with s2s_amd.precision("bf16"):
+        y = conv.forward(xg).clone()
+        dx = conv.backward(xg, dyg).clone()
+    torch.cuda.synchronize()
+    xr, Wr = bf16_round(x), bf16_round(Wt).reshape(Cout, Cin, 3, 3)
+    pre = np.einsum("bchwij,ocij->bohw", win(xr, (3, 3), axis=(2, 3)), Wr) + bias.astype(np.float64)[None, :, None, None]
+    yref = np.maximum(pre, 0.0) if relu else pre
+    err = np.abs(y.cpu().numpy() - yref).max() / np.abs(yref).max()
+    assert err <= 2e-5, ("y", err)
+    dyt = dy.astype(np.float64) * (pre > 0) if relu else dy.astype(np.float64)
+    dyr = bf16_round(dyt.astype(np.float32))
+    pad = np.pad(dyr, ((0, 0), (0, 0), (2, 2), (2, 2)))
+    dxref = np.einsum("bohwij,ocij->bchw", win(pad, (3, 3), axis=(2, 3)), Wr[:, :, ::-1, ::-1])
+    err = np.abs(dx.cpu().numpy() - dxref).max() / np.abs(dxref).max()
+    assert err <= 2e-5, ("dx", err)
