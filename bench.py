@@ -311,22 +311,22 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
         torch.cuda.synchronize()
         agg = s2s_profile.collect()
         _lib.lib.s2s_prof_enable(0)
-        fam = "gemm_bf16" if args.precision == "bf16" else "gemm_f32"
+        bf16 = args.precision != "fp32"
+        fam = "gemm_bf16" if bf16 else "gemm_f32"
         out["kernels"] = {k: {"launches_per_step": v["launches"] / 2, "us_per_step": round(v["total_us"] / 2, 1)}
                           for k, v in agg.items()}
         if fam in agg and agg[fam]["launches"] > 0:
             v = agg[fam]
             avg = v["total_us"] / v["launches"]
             ach = v["flops"] / v["launches"] / (avg * 1e-6) / 1e12
-            peak = PEAK_BF16_MFMA_TFLOPS if args.precision == "bf16" else PEAK_FP32_MFMA_TFLOPS
-            t, detail = traffic_of(pmc, "gemm_" + ("bf16" if args.precision == "bf16" else "f32"))
+            peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
+            t, detail = traffic_of(pmc, "gemm_" + ("bf16" if bf16 else "f32"))
             out["roofline"] = {"kernel": fam, "bound": "mfma", "achieved": round(ach, 2), "peak": peak,
                                "unit": "TFLOP/s", "frac": round(ach / peak, 4),
                                "traffic": round(t) if t is not None else None, "traffic_detail": detail,
                                "avg_launch_us": round(avg, 2), "launches_per_step": v["launches"] / 2,
                                "selection": "the GEMM family: the VGG step's MFMA-bound work (largest live time)",
-                               "mfma_counters": mfma_of(pmc, "gemm_" + ("bf16" if args.precision == "bf16" else "f32"),
-                                                        avg)}
+                               "mfma_counters": mfma_of(pmc, "gemm_" + ("bf16" if bf16 else "f32"), avg)}
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_vgg_baseline(L, T, args.cpu_seconds)
     if rank == 0:

@@ -14,6 +14,7 @@ cp "$src/pmc_hbm.csv" "$dst/pmc_hbm.csv"
 [ -f "$src/stamps_gru.txt" ] && grep -v amdgpu.ids "$src/stamps_gru.txt" > "$dst/stamps_gru.txt"
 [ -f "$src/stamps_dec.txt" ] && grep -v amdgpu.ids "$src/stamps_dec.txt" > "$dst/stamps_dec.txt"
 grep -E "^(CPU\(s\)|Model name|Thread|Core|Socket)" "$src/host_cpu.txt" > "$dst/host_cpu.txt" || true
+for f in "$src"/bench_*.json; do [ -f "$f" ] && cp "$f" "$dst/"; done
 cat > "$dst/command.txt" <<TXT
 # produced by tools/profile_round.sh $r on one MI355X (gpurun), collected by tools/profile_collect.sh
 # bench line (driver command):             python bench.py
@@ -22,5 +23,6 @@ cat > "$dst/command.txt" <<TXT
 #                                           rocprofv3 --pmc WRITE_SIZE --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu --no-kernel-timing --no-pmc --no-graph
 # MFMA evidence (pmc_mfma.csv), one pass:   rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F32 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu --no-kernel-timing --no-pmc --no-graph
 # per-phase stamps (stamps_*.txt):          python tools/gru_stamps.py; python tools/xdec_stamps.py
+# secondary bench lines (bench_<config>.json): tools/bench_lines.sh (python bench.py --config <config>)
 TXT
 echo "collected $src -> $dst"
