@@ -271,6 +271,30 @@ function M.model_step(ctx, stream, d, params, grads, x, labels, scale, flags, lo
                             dptr(logp), dptr(nll), vptr(workspace), workspace:nElement()))
 end
 
+-- the trainer's post-backward block (timit/timit.lua:292-347): clip, L2, optim.adadelta, column-norm
+-- constraint, on the flat parameters / gradients; state is a CudaByteTensor kept across steps
+-- (zeroed on first use, as optim.adadelta's paramVariance / accDelta start at 0).
+function M.adadelta_step(ctx, stream, d, opt, params, grads, state, gradnorm)
+   local n = params:nElement()
+   if not M._mats or M._mats_d ~= d then
+      local nm = C.s2s_model_weight_matrices(d, nil)
+      M._mats = ffi.new('long[?]', 3 * nm)
+      C.s2s_model_weight_matrices(d, M._mats)
+      M._nmats, M._mats_d = nm, d
+   end
+   local bytes = tonumber(C.s2s_optim_state_bytes(n))
+   if state:nElement() ~= bytes then
+      state:resize(bytes)
+      M.check(C.s2s_optim_reset(ctx, stream, vptr(state), n))
+   end
+   local cfg = ffi.new('s2s_optim_config')
+   cfg.rho, cfg.eps = opt.rho or 0.95, opt.eps or 1e-8
+   cfg.maxnorm, cfg.weightDecay = opt.maxnorm or 1e20, opt.weightDecay or 0
+   cfg.colnorm_max = opt.colnormconstr and (opt.colnorm_max or 1) or 0
+   M.check(C.s2s_optim_adadelta_step(ctx, stream, cfg, dptr(params), dptr(grads), n, vptr(state), M._mats,
+                                     M._nmats, gradnorm and dptr(gradnorm) or nil))
+end
+
 -- nn.TemporalConvolution(Din, Dout, kW) on a (L x Din) or (B x L x Din) CudaTensor, as the conv + BiLSTM
 -- encoder's convlayer uses it (timit/timit.lua:113-121); relu = true fuses the nn.ReLU that follows.
 function M.tconv_forward(ctx, stream, m, x, relu, output)

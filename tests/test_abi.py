@@ -118,7 +118,7 @@ def test_lua_shim_cdef_is_current_and_complete():
         assert f"M.{k} = {v}" in shim
     # the Lua wrappers for the module methods the shim replaces (RNN / Attention update* + the model step)
     for fn in ("gru_forward", "gru_backward", "attention_forward", "attention_backward", "attention_views",
-               "model_step", "beam_search"):
+               "model_step", "beam_search", "adadelta_step"):
         assert f"function M.{fn}(" in shim, fn
 
 
