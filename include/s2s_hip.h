@@ -331,9 +331,15 @@ const void* s2s_model_attn_saved(const s2s_model_dims* d, const void* workspace)
  * `gradients` is left clipped / decayed in place as the reference leaves it.  state: the optimizer's
  * paramVariance / accDelta (s2s_optim_state_bytes, zero it with s2s_optim_reset).  mats: n_mats
  * (offset, rows, cols) weight matrices of the flat buffer (s2s_model_weight_matrices for the model).
- * gradnorm (device float, may be NULL) receives ||g|| before clipping (timit.lua:297 gradnorms). */
+ * gradnorm (device float, may be NULL) receives ||g|| before clipping (timit.lua:297 gradnorms).
+ * gradnoise_eta != 0 adds the trainer's gradient noise after the L2 term (timit.lua:310-315, gradnoise =
+ * {eta, gamma, t}, :185-189): t += 1 (the counter lives in `state`, 0 after s2s_optim_reset), sigma =
+ * sqrt(eta / (1 + t)^gamma), g += sigma * N(0, 1); the normals are a counter-based function of
+ * (gradnoise_seed, t, element), identical on every data-parallel rank for the same seed. */
 typedef struct {
   float rho, eps, maxnorm, weightDecay, colnorm_max;
+  float gradnoise_eta, gradnoise_gamma;
+  unsigned long long gradnoise_seed;
 } s2s_optim_config;
 size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);

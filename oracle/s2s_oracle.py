@@ -762,18 +762,48 @@ def column_norm_constraint(W: Array, maxval: float = 1.0) -> Array:
     return W / div
 
 
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+
+
+def _mix64(z):
+    """splitmix64's finaliser on uint64 arrays (wrapping arithmetic)."""
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def gradient_noise(n: int, seed: int, t: int) -> Array:
+    """The N(0, 1) draws of gradient-noise step t (timit.lua:310-315 uses torch.randn; the device
+    optimizer uses this counter-based form so every rank and launch geometry agree): key =
+    mix64(seed * G + t); h_i = mix64(key + i * G); u1 = (h >> 40 + 1) / 2^24, u2 = ((h >> 16) & 0xffffff)
+    / 2^24; z = sqrt(-2 ln u1) cos(2 pi u2).  Restates csrc/optim.hip noise_normal."""
+    with np.errstate(over="ignore"):
+        key = _mix64(np.array([seed], dtype=np.uint64) * _GOLDEN + np.uint64(t))[0]
+        h = _mix64(key + np.arange(n, dtype=np.uint64) * _GOLDEN)
+    u1 = ((h >> np.uint64(40)) + np.uint64(1)).astype(np.float64) / 16777216.0
+    u2 = ((h >> np.uint64(16)) & np.uint64(0xFFFFFF)).astype(np.float64) / 16777216.0
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
 def optimizer_step(x: Array, g: Array, state: Dict[str, Array], rho: float = 0.95, eps: float = 1e-8,
-                   maxnorm: float = 1e20, weightDecay: float = 0.0, colnorm_max: float = 0.0, mats=()):
+                   maxnorm: float = 1e20, weightDecay: float = 0.0, colnorm_max: float = 0.0, mats=(),
+                   gradnoise_eta: float = 0.0, gradnoise_gamma: float = 0.55, gradnoise_seed: int = 0x5EED):
     """One optimizer step on the flat buffers after the (1/B-scaled) backward:
     clip on the global norm (timit.lua:297-302), L2 (:305-308), optim.adadelta (3p) -- v = rho v +
     (1-rho) g^2; delta = sqrt(u + eps) / sqrt(v + eps) * g; x -= delta; u = rho u + (1-rho) delta^2 --
     and the column-norm constraint on every weight matrix (:344-346).  mats: (offset, rows, cols).
+    Gradient noise (:310-315) when gradnoise_eta != 0: t += 1 (state["gradnoise_t"]), g += N(0, 1) *
+    (eta / (1 + t)^gamma)^0.5 with the draws of gradient_noise.
     Updates x, g, state in place; returns ||g|| before clipping."""
     gn = float(np.sqrt((g * g).sum()))
     if gn > maxnorm:
         g *= maxnorm / gn
     if weightDecay > 0:
         g += weightDecay * x
+    if gradnoise_eta != 0:
+        t = state["gradnoise_t"] = state.get("gradnoise_t", 0) + 1
+        sigma = (gradnoise_eta / (1 + t) ** gradnoise_gamma) ** 0.5
+        g += gradient_noise(g.size, gradnoise_seed, t) * sigma
     v = state.setdefault("paramVariance", np.zeros_like(x))
     u = state.setdefault("accDelta", np.zeros_like(x))
     v *= rho

@@ -1099,8 +1099,9 @@ int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_c
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(cfg != nullptr, "optim: null config");
   S2S_REQUIRE(cfg->rho >= 0.f && cfg->rho < 1.f && cfg->eps > 0.f && cfg->maxnorm > 0.f, "optim: bad config");
-  return optim_adadelta_step(static_cast<hipStream_t>(stream), cfg->rho, cfg->eps, cfg->maxnorm, cfg->weightDecay,
-                             cfg->colnorm_max, params, grads, n, state, mats, n_mats, gradnorm);
+  const OptimConfig c{cfg->rho,           cfg->eps,           cfg->maxnorm,       cfg->weightDecay,
+                      cfg->colnorm_max,   cfg->gradnoise_eta, cfg->gradnoise_gamma, cfg->gradnoise_seed};
+  return optim_adadelta_step(static_cast<hipStream_t>(stream), c, params, grads, n, state, mats, n_mats, gradnorm);
 }
 
 int s2s_model_bucket_count(const s2s_model_dims* d) {

@@ -401,7 +401,6 @@ static size_t sconv_dcol_bytes(int B, int Cin, int H, int W, int Cout, int kH, i
 }
 size_t sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
   const size_t N = (size_t)(H - kH + 1) * (W - kW + 1);
-  const size_t K = (size_t)Cin * kH * kW;
   return kWsBytes + 2 * sconv_dcol_bytes(B, Cin, H, W, Cout, kH, kW) +
          align256(sizeof(float) * (size_t)Cout * B * N);
 }

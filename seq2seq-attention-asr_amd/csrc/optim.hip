@@ -2,6 +2,7 @@
 // what timit/timit.lua:292-347 does after the backward, minus the host round trips --
 //   gradient clipping on the global norm       (timit.lua:297-302: if ||g|| > maxnorm: g *= maxnorm/||g||)
 //   L2 regularisation                          (timit.lua:305-308: g += weightDecay * x)
+//   gradient noise                             (timit.lua:310-315: t += 1; g += N(0, 1) * sqrt(eta / (1+t)^gamma))
 //   optim.adadelta (3p, rho / eps config)      (timit.lua:179, exp_logmel7_chorowski_normNLL_colnorm.lua:32-33)
 //   TrainUtils.columnNormConstraint(maxval)    (timit.lua:344-346, TrainUtils.lua:52-104) on every weight matrix
 // The 1/B normalisation (timit.lua:292-295) is the model step's `scale`.
@@ -9,7 +10,10 @@
 // HBM-bound elementwise work: the norm is a two-pass deterministic reduction (fixed per-block
 // order, then one block over the partials), the update one pass reading x, g, v, u and writing
 // x, g, v, u (32 B per parameter), the constraint one wave per weight row.  No host sync: the clip
-// factor stays on the device.
+// factor, the noise counter t and sigma stay on the device, so a captured graph replays them.
+// The reference draws the noise with torch.randn; here it is a counter-based normal of (seed, t, i)
+// (splitmix64 -> Box-Muller), so any launch geometry -- and every data-parallel rank, which all hold
+// the same all-reduced gradients -- draws the same noise.
 #include "s2s_common.h"
 
 #include <algorithm>
@@ -25,7 +29,7 @@ struct OptState {
   float* v;        // optim.adadelta paramVariance
   float* u;        // optim.adadelta accDelta
   float* partial;  // [kNormBlocks] sums of squares
-  float* scal;     // [0] ||g||, [1] clip factor
+  float* scal;     // [0] ||g||, [1] clip factor, [2] noise sigma, [3] noise counter t (uint32 bits)
 };
 
 OptState carve_state(void* state, size_t n) {
@@ -49,8 +53,26 @@ __global__ __launch_bounds__(256) void opt_sumsq(const float* __restrict__ g, si
   if (threadIdx.x == 0) partial[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
 }
 
-__global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb, float maxnorm, float* scal,
-                                                    float* gradnorm_out) {
+constexpr unsigned long long kGolden = 0x9e3779b97f4a7c15ull;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+// N(0, 1) for element i of the step keyed by mix64(seed * kGolden + t): u1 in (0, 1], u2 in [0, 1)
+// from 24-bit fields of mix64(key + i * kGolden), z = sqrt(-2 ln u1) cos(2 pi u2)
+// (oracle/s2s_oracle.py: gradient_noise restates it)
+__device__ __forceinline__ float noise_normal(unsigned long long key, size_t i) {
+  const unsigned long long h = mix64(key + (unsigned long long)i * kGolden);
+  const float u1 = (float)((h >> 40) + 1) * (1.0f / 16777216.0f);
+  const float u2 = (float)((h >> 16) & 0xffffffull) * (1.0f / 16777216.0f);
+  return sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958647692f * u2);
+}
+
+__global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb, float maxnorm, float eta,
+                                                    float gamma, float* scal, float* gradnorm_out) {
   __shared__ float red[4];
   float s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
@@ -61,6 +83,11 @@ __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb
     const float gn = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
     scal[0] = gn;
     scal[1] = gn > maxnorm ? maxnorm / gn : 1.f;
+    if (eta != 0.f) {  // gradnoise.t = (gradnoise.t or 0) + 1; sigma = (eta / (1 + t)^gamma)^0.5
+      const unsigned t = __float_as_uint(scal[3]) + 1u;
+      scal[3] = __uint_as_float(t);
+      scal[2] = (float)sqrt((double)eta / pow(1.0 + (double)t, (double)gamma));
+    }
     if (gradnorm_out) *gradnorm_out = gn;
   }
 }
@@ -69,13 +96,17 @@ __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb
 //   delta = sqrt(u + eps) / std * g;  x -= delta;  u = rho u + (1-rho) delta^2
 __global__ __launch_bounds__(256) void opt_adadelta(float* __restrict__ x, float* __restrict__ g,
                                                     float* __restrict__ v, float* __restrict__ u, size_t n,
-                                                    const float* scal, float rho, float eps, float wd) {
+                                                    const float* scal, float rho, float eps, float wd,
+                                                    int noise, unsigned long long seed) {
   const float clip = scal[1];
+  const float sigma = noise ? scal[2] : 0.f;
+  const unsigned long long key = noise ? mix64(seed * kGolden + __float_as_uint(scal[3])) : 0ull;
   for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += 256ull * gridDim.x) {
     float gi = g[i];
     if (clip != 1.f) gi = gi * clip;
     const float xi = x[i];
     if (wd != 0.f) gi = gi + wd * xi;
+    if (noise) gi = gi + noise_normal(key, i) * sigma;
     const float vi = v[i] * rho + (1.f - rho) * (gi * gi);
     const float sd = sqrtf(vi + eps);
     const float ui = u[i];
@@ -118,16 +149,20 @@ size_t optim_state_bytes(size_t n) {
   return sizeof(float) * (2 * nn + kNormBlocks + 64);
 }
 
-int optim_adadelta_step(hipStream_t st, float rho, float eps, float maxnorm, float wd, float colnorm_max,
-                        float* x, float* g, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
+int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
+                        const long* mats, int n_mats, float* gradnorm) {
+  const float rho = c.rho, eps = c.eps, wd = c.weightDecay, colnorm_max = c.colnorm_max;
+  const int noise = c.gradnoise_eta != 0.f;
   S2S_REQUIRE(x && g && state && n > 0, "optim: null argument");
   S2S_REQUIRE(colnorm_max <= 0.f || (mats && n_mats > 0 && n_mats <= kMaxMats), "optim: bad weight-matrix table");
   const OptState s = carve_state(state, n);
   const int nb = (int)std::min<size_t>(kNormBlocks, (n + 255) / 256);
   hipLaunchKernelGGL(opt_sumsq, dim3(nb), dim3(256), 0, st, g, n, s.partial);
-  hipLaunchKernelGGL(opt_finalize, dim3(1), dim3(256), 0, st, s.partial, nb, maxnorm, s.scal, gradnorm);
+  hipLaunchKernelGGL(opt_finalize, dim3(1), dim3(256), 0, st, s.partial, nb, c.maxnorm, c.gradnoise_eta,
+                     c.gradnoise_gamma, s.scal, gradnorm);
   const int ne = (int)std::min<size_t>(2048, (n + 255) / 256);
-  hipLaunchKernelGGL(opt_adadelta, dim3(ne), dim3(256), 0, st, x, g, s.v, s.u, n, s.scal, rho, eps, wd);
+  hipLaunchKernelGGL(opt_adadelta, dim3(ne), dim3(256), 0, st, x, g, s.v, s.u, n, s.scal, rho, eps, wd, noise,
+                     c.gradnoise_seed);
   if (colnorm_max > 0.f) {
     MatTable t{};
     t.n = n_mats;
@@ -147,7 +182,7 @@ int optim_adadelta_step(hipStream_t st, float rho, float eps, float maxnorm, flo
   return 0;
 }
 
-// zero paramVariance / accDelta (optim.adadelta's lazily created state)
+// zero paramVariance / accDelta (optim.adadelta's lazily created state) and the noise counter t
 int optim_state_reset(hipStream_t st, void* state, size_t n) {
   S2S_CHECK_HIP(hipMemsetAsync(state, 0, optim_state_bytes(n), st));
   return 0;

@@ -191,7 +191,11 @@ struct Bump {
 // ---------------------------------------------------------------- optimizer (optim.hip)
 size_t optim_state_bytes(size_t n);
 int optim_state_reset(hipStream_t st, void* state, size_t n);
-int optim_adadelta_step(hipStream_t st, float rho, float eps, float maxnorm, float wd, float colnorm_max,
-                        float* x, float* g, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+struct OptimConfig {
+  float rho, eps, maxnorm, weightDecay, colnorm_max, gradnoise_eta, gradnoise_gamma;
+  unsigned long long gradnoise_seed;
+};
+int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
+                        const long* mats, int n_mats, float* gradnorm);
 
 }  // namespace s2s

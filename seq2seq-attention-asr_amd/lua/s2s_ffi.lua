@@ -77,7 +77,7 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
 const float* s2s_model_encoder_output(const s2s_model_dims* d, const void* workspace);
 int s2s_model_attn_dims(const s2s_model_dims* d, s2s_attn_dims* out);
 const void* s2s_model_attn_saved(const s2s_model_dims* d, const void* workspace);
-typedef struct { float rho, eps, maxnorm, weightDecay, colnorm_max; } s2s_optim_config;
+typedef struct { float rho, eps, maxnorm, weightDecay, colnorm_max; float gradnoise_eta, gradnoise_gamma; unsigned long long gradnoise_seed; } s2s_optim_config;
 size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params, float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
@@ -291,6 +291,9 @@ function M.adadelta_step(ctx, stream, d, opt, params, grads, state, gradnorm)
    cfg.rho, cfg.eps = opt.rho or 0.95, opt.eps or 1e-8
    cfg.maxnorm, cfg.weightDecay = opt.maxnorm or 1e20, opt.weightDecay or 0
    cfg.colnorm_max = opt.colnormconstr and (opt.colnorm_max or 1) or 0
+   local gn = opt.gradnoise or {}   -- the trainer's gradnoise = {eta, gamma, t} (timit.lua:185-189)
+   cfg.gradnoise_eta, cfg.gradnoise_gamma = gn.eta or 0, gn.gamma or 0.55
+   cfg.gradnoise_seed = gn.seed or 0x5EED
    M.check(C.s2s_optim_adadelta_step(ctx, stream, cfg, dptr(params), dptr(grads), n, vptr(state), M._mats,
                                      M._nmats, gradnorm and dptr(gradnorm) or nil))
 end

@@ -26,7 +26,8 @@ class s2s_attn_dims(ctypes.Structure):
 
 class s2s_optim_config(ctypes.Structure):
     _fields_ = [("rho", c_float), ("eps", c_float), ("maxnorm", c_float), ("weightDecay", c_float),
-                ("colnorm_max", c_float)]
+                ("colnorm_max", c_float), ("gradnoise_eta", c_float), ("gradnoise_gamma", c_float),
+                ("gradnoise_seed", ctypes.c_ulonglong)]
 
 
 class s2s_model_dims(ctypes.Structure):

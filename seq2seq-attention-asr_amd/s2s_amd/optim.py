@@ -31,11 +31,15 @@ def weight_matrices(cfg):
 
 class Adadelta:
     """optim.adadelta with the reference trainer's surroundings (timit/timit.lua:292-347):
-    opt.maxnorm (gradient clip), opt.weightDecay (L2), opt.colnormconstr (max row norm 1).
+    opt.maxnorm (gradient clip), opt.weightDecay (L2), opt.colnormconstr (max row norm 1) and the
+    gradient noise table gradnoise = {eta, gamma} (timit.lua:185-189, 310-315; the configs set eta = 0,
+    timit.lua's own default is 1e-3).  The noise counter t lives in self.state (checkpointed with it);
+    gradnoise_seed must be equal on every data-parallel rank so the replicas stay identical.
     params / grads: flat float32 CUDA tensors (ChorowskiBaseline.getParameters()), or pass the model."""
 
     def __init__(self, model=None, params=None, grads=None, mats=None, rho=0.95, eps=1e-8, maxnorm=1e20,
-                 weightDecay=0.0, colnormconstr=False, colnorm_max=1.0):
+                 weightDecay=0.0, colnormconstr=False, colnorm_max=1.0, gradnoise_eta=0.0, gradnoise_gamma=0.55,
+                 gradnoise_seed=0x5EED):
         if model is not None:
             params, grads = model.getParameters()
             if mats is None:
@@ -45,7 +49,8 @@ class Adadelta:
             raise ValueError("params / grads must be flat contiguous float32 CUDA tensors of one size")
         self.params, self.grads = params, grads
         self.n = params.numel()
-        self.cfg = _lib.s2s_optim_config(rho, eps, maxnorm, weightDecay, colnorm_max if colnormconstr else 0.0)
+        self.cfg = _lib.s2s_optim_config(rho, eps, maxnorm, weightDecay, colnorm_max if colnormconstr else 0.0,
+                                         gradnoise_eta, gradnoise_gamma, gradnoise_seed)
         mats = list(mats or [])
         self._mats = (ctypes.c_long * max(1, 3 * len(mats)))(*[v for m in mats for v in m])
         self._nmats = len(mats)

@@ -571,12 +571,13 @@ def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B
             assert torch.equal(a, b), f"{name} differs (rep {rep}): max |d| = {(a - b).abs().max().item():.3e}"
 
 
-@pytest.mark.parametrize("maxnorm,wd,colnorm", [(1e20, 0.0, False), (0.5, 0.0, True), (1e20, 1e-3, True)])
-def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm):
+@pytest.mark.parametrize("maxnorm,wd,colnorm,eta", [(1e20, 0.0, False, 0.0), (0.5, 0.0, True, 0.0),
+                                                    (1e20, 1e-3, True, 0.0), (0.5, 1e-3, True, 1e-3)])
+def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm, eta):
     """Device optimizer step (s2s_optim_adadelta_step) vs the oracle's restatement of
-    timit.lua:292-347: global-norm clip, L2, optim.adadelta (rho .95, eps 1e-8,
-    exp_logmel7_chorowski_normNLL_colnorm.lua:32-33), column-norm constraint -- three steps on the
-    Chorowski flat layout, fp32 on the GPU vs float64."""
+    timit.lua:292-347: global-norm clip, L2, gradient noise (eta 1e-3, gamma .55: timit.lua:185-189's
+    default table), optim.adadelta (rho .95, eps 1e-8, exp_logmel7_chorowski_normNLL_colnorm.lua:32-33),
+    column-norm constraint -- three steps on the Chorowski flat layout, fp32 on the GPU vs float64."""
     cfg = s2s.ModelConfig()
     mats = s2s.optim.weight_matrices(cfg)
     n = sum(int(np.prod(s)) for _, s in s2s.param_shapes(cfg))
@@ -585,14 +586,15 @@ def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm):
     xg = cu(x)
     gg = torch.empty_like(xg)
     opt = s2s.optim.Adadelta(params=xg, grads=gg, mats=mats, rho=0.95, eps=1e-8, maxnorm=maxnorm, weightDecay=wd,
-                             colnormconstr=colnorm)
+                             colnormconstr=colnorm, gradnoise_eta=eta, gradnoise_seed=99)
     xr, st = x.astype(np.float64), {}
     for it in range(3):
         g = (rng.standard_normal(n) * 1e-3).astype(np.float32)
         gg.copy_(cu(g))
         opt.step()
         gr = g.astype(np.float64)
-        gn = orc.optimizer_step(xr, gr, st, 0.95, 1e-8, maxnorm, wd, 1.0 if colnorm else 0.0, mats)
+        gn = orc.optimizer_step(xr, gr, st, 0.95, 1e-8, maxnorm, wd, 1.0 if colnorm else 0.0, mats,
+                                gradnoise_eta=eta, gradnoise_seed=99)
         torch.cuda.synchronize()
         assert abs(opt.gradnorm.item() - gn) <= 1e-5 * gn
         assert_rel(gg.cpu().numpy(), gr, f"g[{it}]", 1e-5)

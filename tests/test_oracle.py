@@ -298,3 +298,20 @@ def test_beam_search_external_mlp_equals_fused():
         a = orc.beam_search(h, P, cfg, eos=2, K=K, maxseqlength=6)
         b = orc.beam_search(h, P, cfg, eos=2, K=K, maxseqlength=6, mlp=mlp)
         assert a[0] == b[0] and abs(a[1] - b[1]) < 1e-12
+
+
+def test_gradient_noise_draws_and_schedule():
+    """timit.lua:310-315: t counts optimizer steps from 1, sigma = (eta / (1 + t)^gamma)^0.5, and the
+    counter-based draws are standard normal, deterministic in (seed, t) and fresh per step."""
+    z = orc.gradient_noise(200000, 7, 1)
+    assert abs(z.mean()) < 0.01 and abs(z.std() - 1) < 0.01
+    assert np.array_equal(z, orc.gradient_noise(200000, 7, 1))
+    assert np.corrcoef(z, orc.gradient_noise(200000, 7, 2))[0, 1] < 0.01
+    assert np.corrcoef(z, orc.gradient_noise(200000, 8, 1))[0, 1] < 0.01
+    n = 1000
+    x, st = np.zeros(n), {}
+    for t in (1, 2):
+        g = np.zeros(n)
+        orc.optimizer_step(x, g, st, gradnoise_eta=1e-3, gradnoise_gamma=0.55, gradnoise_seed=3)
+        np.testing.assert_allclose(g, orc.gradient_noise(n, 3, t) * (1e-3 / (1 + t) ** 0.55) ** 0.5, rtol=1e-12)
+    assert st["gradnoise_t"] == 2
