@@ -422,9 +422,18 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       gr.dy[dd] = dYcur + dd * H;
     }
     gr.lddy = 2L * H;
-    gr.dx = l == 0 ? nullptr : dYnext;
-    gr.lddx = io.ldx;
-    gr.dx_accumulate = 0;
+    // this layer's dX is the dy of the layer below: produced inside that layer's BPTT launch (or by one
+    // GEMM in front of it), so the critical path has no GEMM between two BPTT launches
+    gr.dx = nullptr;
+    if (l + 1 < nl) {
+      const GruLayerIO up = layer_io(l + 1);
+      gr.ydA = w.dA[l + 1];
+      gr.yldA = 3L * up.ndir * up.H;
+      gr.yK = 3 * up.ndir * up.H;
+      gr.yN = up.D;
+      gr.yWx = gru_layer_packed_wx(up, &gr.yldw);
+      S2S_REQUIRE(gr.yWx != nullptr && up.ldx == 2L * H, "model step: dX of layer above needs packed weights");
+    }
     gr.scale = scale;
     if (defer && pending >= 0) gr.prep_event = ev[1 + pending];
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));

@@ -31,6 +31,14 @@ struct GruLayerGrad {
   float* dW[2][3];  // accumulated: dW += scale * ...
   float scale;
   hipEvent_t prep_event;  // optional: recorded between the persistent BPTT's sync prep and its launch
+  // optional: dy[0] (both directions, dy[1] = dy[0] + H) is the layer above's dX, ydA (B*L, yK; stride
+  // yldA) . yWx (yK, yN; stride yldw), not yet computed -- the persistent BPTT's spare slots produce it
+  // in-launch (gru_persist_fused_dy), otherwise one GEMM in front of the BPTT
+  const float* ydA;
+  long yldA;
+  int yK, yN;
+  const float* yWx;
+  long yldw;
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
@@ -47,5 +55,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
                        size_t scratch_bytes);
 int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws);
 float* gru_layer_dA(const GruLayerIO& io, void* scratch);
+// the x-weights (3 ndir H, Kx) rows of a packed layer (gru_layers_pack) and their row stride Kx
+const float* gru_layer_packed_wx(const GruLayerIO& io, long* ldw);
 
 }  // namespace s2s

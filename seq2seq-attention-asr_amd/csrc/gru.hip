@@ -441,9 +441,21 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   a.L = L;
   a.H = H;
   a.len = io.len;
-  if (use_persistent(nd, B, H)) {
+  const bool persist = use_persistent(nd, B, H);
+  const bool yfuse = gr.ydA && persist && (nd == 1 || gr.dy[1] == gr.dy[0] + H) &&
+                     gru_persist_fused_dy(nd, B, H, gr.yK, gr.yldw, gr.lddy);
+  if (gr.ydA && !yfuse) {  // the layer above's dX as one GEMM in front of the BPTT (same order as in-launch)
+    GemmProblem p{gr.ydA, gr.yWx, const_cast<float*>(gr.dy[0]), nullptr, gr.yldA, gr.yldw, gr.lddy, B * L, gr.yN,
+                  gr.yK, 1.f, 0.f};
+    p.Nread = (int)gr.yldw;
+    S2S_TRY(gemm_f32(st, &p, 1, false, false, layer_gemm_ws(scratch, nd, B, L, D, H)));
+  }
+  if (persist) {
     GruPersistBwd f{};
     f.len = io.len;
+    if (yfuse) {
+      f.ydA = gr.ydA; f.yldA = gr.yldA; f.yK = gr.yK; f.yWx = gr.yWx; f.yldw = gr.yldw;
+    }
     f.ndir = nd; f.B = B; f.L = L; f.H = H; f.lddy = gr.lddy; f.ldA = ldA;
     for (int d = 0; d < nd; ++d) {
       f.UhT[d] = UhT[d]; f.UzrT[d] = UzrT[d]; f.sv[d] = io.saved[d]; f.dy[d] = gr.dy[d]; f.dA[d] = dA + 3L * d * H;
@@ -471,6 +483,12 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     S2S_TRY(gemm_f32(st, &p, 1, false, false, layer_gemm_ws(scratch, nd, B, L, D, H)));
   }
   return 0;
+}
+
+const float* gru_layer_packed_wx(const GruLayerIO& io, long* ldw) {
+  const int Kx = io.Dx > io.D ? io.Dx : io.D;
+  *ldw = Kx;
+  return io.packed ? pack_view(io.packed, io.ndir, io.H).Wx : nullptr;
 }
 
 float* gru_layer_dA(const GruLayerIO& io, void* scratch) {

@@ -34,9 +34,18 @@ struct GruPersistBwd {
   int reverse[2];
   hipEvent_t prep_event;  // optional: recorded after the sync prep, right before the launch
   const int* len = nullptr;  // (B) frames per utterance (null: all L)
+  // optional fused dy: dy[0] .. (the dy buffer, both directions at column d H) = ydA (B*L, yK; row stride
+  // yldA) . yWx (yK, ndir H; row stride yldw) -- the dX of the layer above, computed by the spare slots
+  const float* ydA = nullptr;
+  long yldA = 0;
+  int yK = 0;
+  const float* yWx = nullptr;
+  long yldw = 0;
 };
 
 bool gru_persist_supported(int ndir, int B, int H);
+// the backward's spare slots can produce its dy (the dX GEMM of the layer above) in-launch
+bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy);
 bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx);
 // 1 = persistent GRU launches reserve their CU (see kExclLds); set around a step whose weight-gradient
 // GEMMs run on a side stream

@@ -58,11 +58,17 @@ struct PDir {
 // every loop bound is uniform).  Hand-off (cross-XCD): write-through stores, every
 // wave drains, one agent-scope add per tile to the slice's counter; a consumer polls the counter
 // (sc1) and then reads xp with sc1 loads (MI355X guide, visibility table row 1).
+// The backward uses the same producers for its dy (fused dX of the layer above, gemm_f32's 64x64 NN
+// kernel order): x = that layer's gate gradients dA (K = 3 nd H' columns), W = its x-weights (K, D')
+// read row-contiguous (nn = 1), xp = this layer's dy; slices follow the BPTT's processing order
+// (flip = 1: processing index s is time L-1-s for the forward direction).
 struct XProj {
   const float* x;
   long ldx;
   int K;            // padded input width (% 32 == 0): x and W hold K readable columns
-  const float* W;   // (nd*3H, K) x-weights, direction d's rows [3H d, 3H (d+1))
+  const float* W;   // nn = 0: (nd*ncd, ldw) x-weights, direction d's rows [ncd d, ncd (d+1)); nn = 1: (K, ldw)
+  long ldw;
+  int nn, ncd, flip;
   float* xp;
   long ldxp;
   int tpt;          // steps per slice (64 / B)
@@ -109,14 +115,15 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
   const XProj& q = a.xq;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wy = wave >> 1, wx = wave & 1, li = lane & 31, lk = lane >> 5;
-  const int B = a.B, L = a.L, H3 = 3 * a.H, nd = q.nslices > 0 ? q.nwork / (q.nslices * q.ntn) : 1;
+  const int B = a.B, L = a.L, H3 = q.ncd, nd = q.nslices > 0 ? q.nwork / (q.nslices * q.ntn) : 1;
   constexpr int LDK = 36;
   float* As[2] = {lds, lds + 64 * LDK};
   float* Bs[2] = {lds + 128 * LDK, lds + 192 * LDK};
   for (int w = p; w < q.nwork; w += nprod) {
     const int sl = w / (nd * q.ntn), rem = w - sl * nd * q.ntn, d = rem / q.ntn, ct = rem - d * q.ntn;
-    const int rev = a.d[d].reverse;
-    // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows
+    const int rev = a.d[d].reverse ^ q.flip;
+    // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows (nn: B columns 4 (f / 32) ..
+    // + 3 of k row f % 32, gemm_f32's row-contiguous loader)
     const float* arow[2];
     bool aval[2];
     const float* brow[2];
@@ -126,7 +133,9 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
       aval[j] = jt < q.tpt && s < L;
       const int t = rev ? L - 1 - s : s;
       arow[j] = q.x + (aval[j] ? ((long)b * L + t) * q.ldx : 0);
-      brow[j] = q.W + (long)(d * H3 + ct * 64 + r) * q.K;
+      const int f = tid + 256 * j;
+      brow[j] = q.nn ? q.W + (long)(f & 31) * q.ldw + d * H3 + ct * 64 + 4 * (f >> 5)
+                     : q.W + (long)(d * H3 + ct * 64 + r) * q.ldw;
     }
     const int kq = 4 * (tid & 7);
     floatx4 ra[2], rb[2];
@@ -134,7 +143,8 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         ra[j] = aval[j] ? *reinterpret_cast<const floatx4*>(arow[j] + k0 + kq) : floatx4{0.f, 0.f, 0.f, 0.f};
-        rb[j] = *reinterpret_cast<const floatx4*>(brow[j] + k0 + kq);
+        rb[j] = q.nn ? *reinterpret_cast<const floatx4*>(brow[j] + (long)k0 * q.ldw)
+                     : *reinterpret_cast<const floatx4*>(brow[j] + k0 + kq);
       }
     };
     auto lstore = [&](int buf) {
@@ -142,7 +152,15 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
       for (int j = 0; j < 2; ++j) {
         const int f = tid + 256 * j;
         *reinterpret_cast<floatx4*>(As[buf] + (f >> 3) * LDK + 4 * (f & 7)) = ra[j];
-        *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = rb[j];
+        if (q.nn) {
+          float* pb = Bs[buf] + (4 * (f >> 5)) * LDK + (f & 31);
+          pb[0] = rb[j][0];
+          pb[LDK] = rb[j][1];
+          pb[2 * LDK] = rb[j][2];
+          pb[3 * LDK] = rb[j][3];
+        } else {
+          *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = rb[j];
+        }
       }
     };
     floatx16 acc;
@@ -372,9 +390,17 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
   __shared__ unsigned tb_lds;
+  __shared__ int ynext_lds[1];
+  extern __shared__ __attribute__((aligned(16))) float ylds[];  // producer tiles (fused dy)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
-  if (cs.chain >= a.nchains) return;  // idle slot of the placement grid
+  if (cs.chain >= a.nchains) {  // spare slot of the placement grid: dy producer (or idle)
+    if (a.fused) {
+      const int gch = 8 * ((a.nchains + 7) / 8);
+      xproj_produce(a, ylds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
+    }
+    return;
+  }
   const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
   const PDir& g = a.d[dir];
   const int ncol = H / 16;
@@ -414,7 +440,8 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
       const long row = (long)ob * L + t;
       const float* sv = g.sv + row * 5 * H;
       v.z = sv[ok_]; v.r = sv[H + ok_]; v.hh = sv[2 * H + ok_]; v.hp = sv[3 * H + ok_];
-      v.dy = t < lenb ? g.dy[row * g.lddy + ok_] : 0.f;
+      const float* pdy = g.dy + row * g.lddy + ok_;  // fused dy: written through by the producers
+      v.dy = t >= lenb ? 0.f : a.fused ? __hip_atomic_load(pdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pdy;
     }
     return v;
   };
@@ -441,7 +468,33 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     }
   };
 
+  // fused dy: processing index q's slice must be complete before its dy row is read.  Every load in
+  // front of a sweep delays that sweep's first check (vmcnt retires in order), so readiness is not
+  // polled per step: `yready` slices are known complete, and only a step that needs a slice past
+  // them refreshes it -- the 64 lanes of wave 0 read the next 64 slice counters at once (one round
+  // trip, then a barrier), so once the producers are ahead one refresh covers every slice they finished
+  int yready = 0;
+  auto dy_need = [&](int q) {
+    const int need = q / a.xq.tpt;
+    if (need < yready) return;
+    if (wave == 0) {
+      unsigned spins = 0;
+      while (true) {
+        const int sl = yready + lane;
+        const bool rd = sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl);
+        const unsigned long long nr = __ballot(!rd);
+        const int upto = nr ? yready + (int)__builtin_ctzll(nr) : yready + 64;
+        if (upto > need || spin_give_up(spins, a.abort_word)) {
+          if (lane == 0) ynext_lds[0] = upto;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    yready = __builtin_amdgcn_readfirstlane(ynext_lds[0]);
+  };
   const int tl = g.reverse ? 0 : L - 1;
+  if (a.fused) dy_need(0);
   Row cur = load_row(tl);
   gate(tl, cur, cur.dy, 0, live);
 
@@ -474,6 +527,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     GRU_STAMP(2);
     // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
     const int tn = g.reverse ? t + 1 : t - 1;
+    if (a.fused && s > 0) dy_need(p + 1);
     const Row nxt = s > 0 ? load_row(tn) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     float4 azr[2 * NC];
     GRU_STAMP(3);
@@ -554,6 +608,14 @@ bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx) {
   return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
 }
 
+int g_fuse_dy = 1;  // s2s_debug_gru_fused_dy(0) (diagnostic): the dX GEMM in front of the BPTT instead
+
+bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy) {
+  if (!g_fuse_xproj || !g_fuse_dy || B > 64 || K % 32 != 0 || H % 64 != 0 || ldw % 4 != 0 || lddy < (long)ndir * H) return false;
+  const int MT = (B + 15) / 16, nchains = ndir * MT, nmem = H / 16;
+  return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
+}
+
 bool gru_persist_supported(int ndir, int B, int H) {
   if (!(H == 64 || H == 128 || H == 256 || H == 512)) return false;
   const int MT = (B + 15) / 16;
@@ -611,7 +673,8 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.stamps = g_gru_stamps[0];
   if (f.x) {  // fused x-projection by the grid's spare slots
     XProj& q = a.xq;
-    q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.xp = const_cast<float*>(f.xp[0]); q.ldxp = f.ldxp;
+    q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.ldw = f.Kx; q.nn = 0; q.ncd = 3 * f.H; q.flip = 0;
+    q.xp = const_cast<float*>(f.xp[0]); q.ldxp = f.ldxp;
     q.tpt = 64 / f.B;
     q.nslices = (f.L + q.tpt - 1) / q.tpt;
     q.ntn = 3 * f.H / 64;
@@ -630,7 +693,8 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   const int MT = (b.B + 15) / 16;
   granule_t* gr[2][3];
   float* sr[2][3];
-  carve_granules(static_cast<char*>(sync), b.B, b.L, b.H, &a.abort_word, gr, sr, &a.census);
+  unsigned* xcount = nullptr;
+  carve_granules(static_cast<char*>(sync), b.B, b.L, b.H, &a.abort_word, gr, sr, &a.census, &xcount);
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
                   b.reverse[d], gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
@@ -638,8 +702,20 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
+  if (b.ydA) {  // fused dy (the layer above's dX) by the grid's spare slots
+    XProj& q = a.xq;
+    q.x = b.ydA; q.ldx = b.yldA; q.K = b.yK; q.W = b.yWx; q.ldw = b.yldw; q.nn = 1; q.ncd = b.H; q.flip = 1;
+    q.xp = const_cast<float*>(b.dy[0]); q.ldxp = b.lddy;
+    q.tpt = 64 / b.B;
+    q.nslices = (b.L + q.tpt - 1) / q.tpt;
+    q.ntn = b.H / 64;
+    q.nwork = q.nslices * b.ndir * q.ntn;
+    q.done = xcount;
+    a.fused = 1;
+  }
   S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
+  // the recurrence's algorithmic work only (a fused dy's GEMM runs on the spare slots beside it)
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);
@@ -652,6 +728,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
 // diagnostic: 0 forces write-through (sc1) hand-offs in every chain (tests cover both forms)
 extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
 extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
+extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);

@@ -40,6 +40,9 @@ def analyse(name, st, nwg, ndir, ntile, prod1, cons1, prod2, cons2):
 
 def main():
     B, L, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (32, 128, 256)
+    # S2S_GRU_LAYERS=2: the stamped backward is the lower layer's, whose dy (the upper layer's dX) the
+    # BPTT launch produces itself (fused dy)
+    nl = int(os.environ.get("S2S_GRU_LAYERS", "1"))
     D = 2 * H
     ndir = 2
     ntile = (B + 15) // 16
@@ -49,9 +52,13 @@ def main():
     fn = _lib.lib.s2s_debug_gru_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     x = torch.randn(B, L, D, device="cuda")
-    cfg = s2s_amd.ModelConfig(inputFrameSize=D, hiddenFrameSize=H, outputFrameSize=H, numLayers=1)
+    cfg = s2s_amd.ModelConfig(inputFrameSize=D, hiddenFrameSize=H, outputFrameSize=H, numLayers=nl)
     model = s2s_amd.ChorowskiBaseline(cfg, graph=False)
     lab = torch.randint(0, cfg.outputDepth, (B, 8), device="cuda", dtype=torch.int32)
+    if os.environ.get("S2S_GRU_FUSED") == "0":  # separate x-projection / dX GEMMs (A/B)
+        _lib.lib.s2s_debug_gru_fused_xproj(0)
+    if os.environ.get("S2S_GRU_LOCAL") == "0":  # force the tagged-granule hand-offs (A/B)
+        _lib.lib.s2s_debug_gru_local(0)
     fn(sf.data_ptr(), sb.data_ptr())
     model.step(x, lab)
     torch.cuda.synchronize()
@@ -69,6 +76,14 @@ def main():
     tbp = tb[:, ::-1, :].copy()
     allc = list(range(H // 16))
     analyse("gru backward", tbp, nb // ndir, ndir, ntile, prod1=allc, cons1=allc, prod2=allc, cons2=allc)
+    t0 = tbp[:, 0, 0].min()
+    ends = tbp[:, :, 5].max(0)  # per processing step: the last workgroup's end
+    per = np.diff(ends)
+    q = len(per) // 4
+    print("  backward step time by quarter of the sweep: " + ", ".join(f"{per[i * q:(i + 1) * q].mean():.2f}"
+                                                                    for i in range(4)) + " us")
+    print(f"  backward: first step starts at +0, step 8 at {tbp[:, 8, 0].mean() - t0:.1f} us, last step ends at "
+          f"{tbp[:, -1, 5].max() - t0:.1f} us")
 
 
 if __name__ == "__main__":
