@@ -167,12 +167,19 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
     const int nk = q.K / 32;
-    gload(0);
-    lstore(0);
+    const bool act = tid < 256;  // a backward block's 5th (row loader) wave only joins the barriers
+    if (act) {
+      gload(0);
+      lstore(0);
+    }
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {  // gemm_f32's double-buffered 64x64 main loop, same MFMA order
       const int buf = kt & 1;
       const bool more = kt + 1 < nk;
+      if (!act) {
+        __syncthreads();
+        continue;
+      }
       if (more) gload((kt + 1) * 32);
       floatx4 av[4], bv[4];
       const float* pa = As[buf] + (wy * 32 + li) * LDK + 16 * lk;
@@ -193,6 +200,7 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
     const int col = d * H3 + ct * 64 + wx * 32 + li;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
+      if (!act) break;
       const int tr = wy * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, jt = tr / B, b = tr - jt * B, s = sl * q.tpt + jt;
       if (jt < q.tpt && s < L) {
         const int t = rev ? L - 1 - s : s;
@@ -385,12 +393,21 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
 
 // ------------------------------------------------------------------------------ backward
 // chain (dir, mt) has nmem = H/16 members c, each the same column tile in both seams.
+// Backward blocks have a 5th wave that only moves the saved activations and dy of the coming steps
+// from HBM into an LDS ring (kRowRing steps): vmcnt is per wave and retires in order, so a row load
+// issued by a recurrence wave would hold that wave's next sweep check for the HBM latency (measured:
+// most of the p2 hand-off), while the loader wave's waits delay nothing but itself.  The loader joins
+// every block barrier of the recurrence waves: [P] before the loop, [A] and [B] (the p1 / p2 reduces)
+// per step; it writes row q + 2 between [A] and [B] of step q, which the recurrence waves read after
+// [B] of step q + 1.
+constexpr int kRowRing = 4;
+constexpr int kBwdThreads = 320;
 template <int NC>
-__global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
+__global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
   __shared__ unsigned tb_lds;
-  __shared__ int ynext_lds[1];
+  __shared__ __attribute__((aligned(16))) float rowq[kRowRing][5][256];  // [step % ring][z r hh hp dy][thread]
   extern __shared__ __attribute__((aligned(16))) float ylds[];  // producer tiles (fused dy)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
@@ -410,11 +427,74 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
-  rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
-  rearm_rect(g.s1, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
-  rearm_rect(g.s2, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  const bool loader = wave == 4;
+  if (!loader) {
+    rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+    rearm_rect(g.s1, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+    rearm_rect(g.s2, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  }
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
+
+  if (loader) {
+    // lane l: utterance b0 + (l >> 2) of the tile, units c * 16 + 4 (l & 3) .. + 3
+    const int bl = b0 + (lane >> 2), u = c * 16 + 4 * (lane & 3);
+    const bool lv = bl < B;
+    const int lenl = (a.len && lv) ? a.len[bl] : L;
+    const __amdgpu_buffer_rsrc_t dyr = rsrc_of(g.dy);
+    // fused dy: `yready` slices are known complete; a step past them refreshes all 64 slice counters
+    // ahead at once (one round trip), so the poll is rare once the producers are ahead
+    int yready = 0;
+    auto dy_ready = [&](int q) {
+      const int need = q / a.xq.tpt;
+      unsigned spins = 0;
+      while (need >= yready) {
+        const int sl = yready + lane;
+        const unsigned long long nr = __ballot(!(sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl)));
+        const int upto = nr ? yready + (int)__builtin_ctzll(nr) : yready + 64;
+        if (upto <= need && spin_give_up(spins, a.abort_word)) break;
+        yready = upto;
+      }
+    };
+    auto issue = [&](int q, float4 (&r)[5]) {  // loads of processing step q
+#pragma unroll
+      for (int v = 0; v < 5; ++v) r[v] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!lv || q >= L) return;
+      const int t = g.reverse ? q : L - 1 - q;
+      const long row = (long)bl * L + t;
+      const float* sv = g.sv + row * 5 * H + u;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) r[v] = *reinterpret_cast<const float4*>(sv + v * H);
+      if (t >= lenl) return;
+      if (a.fused) {  // this step's dy slice must be complete (written through by the producers)
+        dy_ready(q);
+        r[4] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              dyr, (int)(4 * (row * g.lddy + u)), 0, 16));
+      } else {
+        r[4] = *reinterpret_cast<const float4*>(g.dy + row * g.lddy + u);
+      }
+    };
+    auto put = [&](int q, const float4 (&r)[5]) {
+#pragma unroll
+      for (int v = 0; v < 5; ++v) *reinterpret_cast<float4*>(&rowq[q % kRowRing][v][4 * lane]) = r[v];
+    };
+    float4 ra[5], rb[5];
+    issue(0, ra);
+    issue(1, rb);
+    put(0, ra);
+    put(1, rb);
+    issue(2, ra);
+    __syncthreads();  // [P]
+    for (int p = 0; p < L; ++p) {
+      __syncthreads();  // [A]
+      if (abort_lds) return;
+      put(p + 2, ra);   // loaded during the previous step
+      __syncthreads();  // [B]
+      if (abort_lds) return;
+      issue(p + 3, ra);
+    }
+    return;
+  }
 
   float4 wh[NC], wzr[2 * NC];
   load_wfrag(wh, g.Wa + (long)(c * 16 + (lane & 15)) * H, wave, lane);
@@ -429,21 +509,13 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
   float dhc = 0.f, dhp = 0.f;
   bool aborted = false;
 
-  // saved activations of one step for this thread's (utterance, unit): loaded one step ahead, while
-  // the previous hand-off is in flight, so no dependent global load sits on the recurrence
+  // saved activations and dy of one step for this thread's (utterance, unit), from the loader's ring
   struct Row {
     float z, r, hh, hp, dy;
   };
-  auto load_row = [&](int t) {
-    Row v{0.f, 0.f, 0.f, 0.f, 0.f};
-    if (live) {
-      const long row = (long)ob * L + t;
-      const float* sv = g.sv + row * 5 * H;
-      v.z = sv[ok_]; v.r = sv[H + ok_]; v.hh = sv[2 * H + ok_]; v.hp = sv[3 * H + ok_];
-      const float* pdy = g.dy + row * g.lddy + ok_;  // fused dy: written through by the producers
-      v.dy = t >= lenb ? 0.f : a.fused ? __hip_atomic_load(pdy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *pdy;
-    }
-    return v;
+  auto load_row = [&](int q) {
+    const float(*r)[256] = rowq[q % kRowRing];
+    return Row{r[0][tid], r[1][tid], r[2][tid], r[3][tid], r[4][tid]};
   };
   // gate gradients of dh = dy_t + carry at time t (rows that are live), published as hand-off
   // step pn (tag tb + pn + 1, slot pn & 1; sentinel slot pn) when `pub`; every lane calls it
@@ -468,34 +540,9 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     }
   };
 
-  // fused dy: processing index q's slice must be complete before its dy row is read.  Every load in
-  // front of a sweep delays that sweep's first check (vmcnt retires in order), so readiness is not
-  // polled per step: `yready` slices are known complete, and only a step that needs a slice past
-  // them refreshes it -- the 64 lanes of wave 0 read the next 64 slice counters at once (one round
-  // trip, then a barrier), so once the producers are ahead one refresh covers every slice they finished
-  int yready = 0;
-  auto dy_need = [&](int q) {
-    const int need = q / a.xq.tpt;
-    if (need < yready) return;
-    if (wave == 0) {
-      unsigned spins = 0;
-      while (true) {
-        const int sl = yready + lane;
-        const bool rd = sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl);
-        const unsigned long long nr = __ballot(!rd);
-        const int upto = nr ? yready + (int)__builtin_ctzll(nr) : yready + 64;
-        if (upto > need || spin_give_up(spins, a.abort_word)) {
-          if (lane == 0) ynext_lds[0] = upto;
-          break;
-        }
-      }
-    }
-    __syncthreads();
-    yready = __builtin_amdgcn_readfirstlane(ynext_lds[0]);
-  };
   const int tl = g.reverse ? 0 : L - 1;
-  if (a.fused) dy_need(0);
-  Row cur = load_row(tl);
+  __syncthreads();  // [P]
+  Row cur = load_row(0);
   gate(tl, cur, cur.dy, 0, live);
 
   for (int p = 0; p < L; ++p) {
@@ -527,8 +574,6 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     GRU_STAMP(2);
     // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
     const int tn = g.reverse ? t + 1 : t - 1;
-    if (a.fused && s > 0) dy_need(p + 1);
-    const Row nxt = s > 0 ? load_row(tn) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     float4 azr[2 * NC];
     GRU_STAMP(3);
     {
@@ -550,6 +595,7 @@ __global__ __launch_bounds__(256) void gru_bwd_persist(PArgs a) {
     acc = mfma_chunks<2 * NC>(azr, wzr);
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
+    const Row nxt = s > 0 ? load_row(p + 1) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     if (live && s > 0) dhc = tn < lenb ? dhp + sm : 0.f;
     if (s > 0) gate(tn, nxt, nxt.dy + dhc, p + 1, live);
     cur = nxt;
@@ -579,7 +625,7 @@ int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
   } else {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
-    hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(256), shm, st, a);
+    hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(kBwdThreads), shm, st, a);
   }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
