@@ -223,13 +223,20 @@ __device__ __forceinline__ bool xproj_ready(const XProj& q, int d, int sl) {
 // ------------------------------------------------------------------------------ forward
 // chain (dir, mt) has nmem = 2H/16 members c1 (chain_slot placement, handoff.h); z-column
 // workgroups (c1 < H/16) also own the candidate tile of the same units.
+// Like the backward, forward blocks carry a 5th wave that loads the x-projections of coming steps into
+// an LDS ring (and, with the fused x-projection, waits for their slices), so no global load or counter
+// poll sits in front of a recurrence wave's sweep.  It joins the barriers [P], [A] (p1 reduce) and, in
+// z-column blocks, [B] (p2 reduce); step q + 2's values are written between [A] of step q and [A] of
+// step q + 1, after which the recurrence waves read them.
+constexpr int kRowRing = 4;  // steps of loaded operands in flight (LDS ring)
+constexpr int kFwdThreads = 320;
 template <int NC>  // NC = H / 64
-__global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
+__global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
   __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
-  __shared__ int xnext_lds[2];
+  __shared__ __attribute__((aligned(16))) float xring[kRowRing][2][256];  // [step % ring][gate | candidate][thread]
   extern __shared__ __attribute__((aligned(16))) float xlds[];  // producer tiles (fused x-projection)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
@@ -251,9 +258,63 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   // z tiles publish h, r tiles q
-  rearm_rect(isz ? g.s0 : g.s1, (long)B * H, L, H, b0, min(16, B - b0), isz ? c1 * 16 : c1 * 16 - H, 16);
+  const bool loader = wave == 4;
+  if (!loader)
+    rearm_rect(isz ? g.s0 : g.s1, (long)B * H, L, H, b0, min(16, B - b0), isz ? c1 * 16 : c1 * 16 - H, 16);
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
+
+  if (loader) {
+    // lane l: utterance b0 + (l >> 2) of the tile, columns c1 * 16 + 4 (l & 3) .. + 3
+    const int bl = b0 + (lane >> 2), col = c1 * 16 + 4 * (lane & 3);
+    const bool lv = bl < B;
+    const __amdgpu_buffer_rsrc_t xr = rsrc_of(g.xp);
+    int xready = 0;  // fused: slices known complete (one refresh of 64 counters at a time)
+    auto issue = [&](int q, float4 (&r)[2]) {
+      r[0] = r[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!lv || q >= L) return;
+      const int t = g.reverse ? L - 1 - q : q;
+      const long off = ((long)bl * L + t) * g.ldxp + col;
+      if (a.fused) {
+        const int need = q / a.xq.tpt;
+        unsigned spins = 0;
+        while (need >= xready) {
+          const int sl = xready + lane;
+          const unsigned long long nr = __ballot(!(sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl)));
+          const int upto = nr ? xready + (int)__builtin_ctzll(nr) : xready + 64;
+          if (upto <= need && spin_give_up(spins, a.abort_word)) break;
+          xready = upto;
+        }
+        r[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * off), 0, 16));
+        if (isz)
+          r[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * (off + 2 * H)), 0, 16));
+      } else {
+        r[0] = *reinterpret_cast<const float4*>(g.xp + off);
+        if (isz) r[1] = *reinterpret_cast<const float4*>(g.xp + off + 2 * H);
+      }
+    };
+    auto put = [&](int q, const float4 (&r)[2]) {
+      *reinterpret_cast<float4*>(&xring[q % kRowRing][0][4 * lane]) = r[0];
+      *reinterpret_cast<float4*>(&xring[q % kRowRing][1][4 * lane]) = r[1];
+    };
+    float4 ra[2], rb[2];
+    issue(0, ra);
+    issue(1, rb);
+    put(0, ra);
+    put(1, rb);
+    issue(2, ra);
+    __syncthreads();  // [P]
+    for (int s = 0; s < L; ++s) {
+      __syncthreads();  // [A]
+      if (abort_lds) return;
+      put(s + 2, ra);   // loaded during the previous step
+      issue(s + 3, ra);
+      if (!isz) continue;
+      __syncthreads();  // [B]
+      if (abort_lds) return;
+    }
+    return;
+  }
 
   float4 w1[NC], w2[NC];
   load_wfrag(w1, g.Wa + (long)(c1 * 16 + (lane & 15)) * H, wave, lane);
@@ -272,40 +333,11 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
   float zreg = 0.f, hreg = 0.f;
   bool aborted = false;
 
-  // x-projection operands of step s (this thread's gate column, and the candidate column for z tiles),
-  // loaded one step ahead; with the fused x-projection only after the slice's counter says ready
-  auto xp_load = [&](int s, float& xz, float& xh) {
-    const int t = g.reverse ? L - 1 - s : s;
-    const float* p = g.xp + ((long)ob * L + t) * g.ldxp;
-    xz = 0.f;
-    xh = 0.f;
-    if (!live) return;
-    if (a.fused) {
-      xz = __hip_atomic_load(p + on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (isz) xh = __hip_atomic_load(p + 2 * H + on, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      xz = p[on];
-      if (isz) xh = p[2 * H + on];
-    }
-  };
-  auto xp_wait = [&](int s) {  // blocking: thread 0 polls, then a barrier
-    if (tid == 0) {
-      unsigned spins = 0;
-      while (!xproj_ready(a.xq, dir, s / a.xq.tpt))
-        if (spin_give_up(spins, a.abort_word)) break;
-    }
-    __syncthreads();
-  };
-  float xz_n = 0.f, xh_n = 0.f;
-  if (a.fused) xp_wait(0);
-  xp_load(0, xz_n, xh_n);
+  __syncthreads();  // [P]
   for (int s = 0; s < L; ++s) {
     const int t = g.reverse ? L - 1 - s : s;
     const long row = (long)ob * L + t;
     // ---- p1: [z | r] = sig(Uzr h_{t-1} + xp)
-    const float xpv = xz_n, xph_s = xh_n;
-    if (a.fused && tid == 0)  // double-buffered: a lagging thread may still read the previous step's
-      xnext_lds[s & 1] = (s + 1 < L && xproj_ready(a.xq, dir, (s + 1) / a.xq.tpt)) ? 1 : 0;
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     bool ok = true;
     GRU_STAMP(0);
@@ -327,6 +359,8 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
     GRU_STAMP(7);
+    // this step's x-projections from the loader's ring (written before [A] of the previous step)
+    const float xpv = xring[s % kRowRing][0][tid], xph = xring[s % kRowRing][1][tid];
     {
       const float gate = sigmoidf_(sum + xpv);
       float* sv = g.sv + row * 5 * H;
@@ -349,17 +383,9 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
         }
       }
     }
-    // next step's x-projection, after this step's hand-off is published: its load latency (and the
-    // fused producers' readiness poll) stays off the q / h critical path (xnext_lds was set before
-    // the reduce barrier)
-    if (s + 1 < L) {
-      if (a.fused && !__builtin_amdgcn_readfirstlane(xnext_lds[s & 1])) xp_wait(s + 1);
-      xp_load(s + 1, xz_n, xh_n);
-    }
     GRU_STAMP(2);
     if (!isz) continue;
     // ---- p2: hh = tanh(Uh q + xp_h); h = (1-z) h_{t-1} + z hh
-    const float xph = xph_s;
     acc = floatx4{0.f, 0.f, 0.f, 0.f};
     ok = true;
     GRU_STAMP(3);
@@ -400,7 +426,6 @@ __global__ __launch_bounds__(256) void gru_fwd_persist(PArgs a) {
 // every block barrier of the recurrence waves: [P] before the loop, [A] and [B] (the p1 / p2 reduces)
 // per step; it writes row q + 2 between [A] and [B] of step q, which the recurrence waves read after
 // [B] of step q + 1.
-constexpr int kRowRing = 4;
 constexpr int kBwdThreads = 320;
 template <int NC>
 __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
@@ -621,7 +646,7 @@ int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
   if (fwd) {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
-    hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(256), shm, st, a);
+    hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(kFwdThreads), shm, st, a);
   } else {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
