@@ -220,6 +220,21 @@ __device__ __forceinline__ bool xproj_ready(const XProj& q, int d, int sl) {
          (unsigned)q.ntn;
 }
 
+// loader wave: wait until slice `need` of direction d is complete.  `ready` = slices known complete; a
+// refresh reads the 64 counters ahead at once (lane i: slice ready + i) and advances to the first one not
+// yet complete.  MUST run with all 64 lanes active (wave-uniform call site): an inactive lane's ballot bit
+// reads as "complete", which would advance `ready` past a slice still being produced.
+__device__ __forceinline__ void xproj_wait(const XProj& q, int d, int need, int& ready, int lane, unsigned* abort_word) {
+  unsigned spins = 0;
+  while (need >= ready) {
+    const int sl = ready + lane;
+    const unsigned long long nr = __ballot(!(sl >= q.nslices || xproj_ready(q, d, sl)));
+    const int upto = nr ? ready + (int)__builtin_ctzll(nr) : ready + 64;
+    if (upto <= need && spin_give_up(spins, abort_word)) break;
+    ready = upto;
+  }
+}
+
 // ------------------------------------------------------------------------------ forward
 // chain (dir, mt) has nmem = 2H/16 members c1 (chain_slot placement, handoff.h); z-column
 // workgroups (c1 < H/16) also own the candidate tile of the same units.
@@ -272,19 +287,12 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     int xready = 0;  // fused: slices known complete (one refresh of 64 counters at a time)
     auto issue = [&](int q, float4 (&r)[2]) {
       r[0] = r[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!lv || q >= L) return;
+      if (q >= L) return;
+      if (a.fused) xproj_wait(a.xq, dir, q / a.xq.tpt, xready, lane, a.abort_word);  // all lanes
+      if (!lv) return;
       const int t = g.reverse ? L - 1 - q : q;
       const long off = ((long)bl * L + t) * g.ldxp + col;
       if (a.fused) {
-        const int need = q / a.xq.tpt;
-        unsigned spins = 0;
-        while (need >= xready) {
-          const int sl = xready + lane;
-          const unsigned long long nr = __ballot(!(sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl)));
-          const int upto = nr ? xready + (int)__builtin_ctzll(nr) : xready + 64;
-          if (upto <= need && spin_give_up(spins, a.abort_word)) break;
-          xready = upto;
-        }
         r[0] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * off), 0, 16));
         if (isz)
           r[1] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(4 * (off + 2 * H)), 0, 16));
@@ -470,29 +478,21 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     // fused dy: `yready` slices are known complete; a step past them refreshes all 64 slice counters
     // ahead at once (one round trip), so the poll is rare once the producers are ahead
     int yready = 0;
-    auto dy_ready = [&](int q) {
-      const int need = q / a.xq.tpt;
-      unsigned spins = 0;
-      while (need >= yready) {
-        const int sl = yready + lane;
-        const unsigned long long nr = __ballot(!(sl >= a.xq.nslices || xproj_ready(a.xq, dir, sl)));
-        const int upto = nr ? yready + (int)__builtin_ctzll(nr) : yready + 64;
-        if (upto <= need && spin_give_up(spins, a.abort_word)) break;
-        yready = upto;
-      }
-    };
     auto issue = [&](int q, float4 (&r)[5]) {  // loads of processing step q
 #pragma unroll
       for (int v = 0; v < 5; ++v) r[v] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!lv || q >= L) return;
+      if (q >= L) return;
+      // this step's dy slice must be complete (written through by the producers); polled by all lanes,
+      // also those of padding rows or frames, which load no dy
+      if (a.fused) xproj_wait(a.xq, dir, q / a.xq.tpt, yready, lane, a.abort_word);
+      if (!lv) return;
       const int t = g.reverse ? q : L - 1 - q;
       const long row = (long)bl * L + t;
       const float* sv = g.sv + row * 5 * H + u;
 #pragma unroll
       for (int v = 0; v < 4; ++v) r[v] = *reinterpret_cast<const float4*>(sv + v * H);
       if (t >= lenl) return;
-      if (a.fused) {  // this step's dy slice must be complete (written through by the producers)
-        dy_ready(q);
+      if (a.fused) {
         r[4] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
                                               dyr, (int)(4 * (row * g.lddy + u)), 0, 16));
       } else {
