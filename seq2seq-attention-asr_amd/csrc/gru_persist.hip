@@ -76,6 +76,7 @@ struct XProj {
   unsigned* done;   // [nd][nslices] finished column tiles
 };
 constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
+constexpr int kXpDepth = 4;             // producer K-tiles in flight (register ring)
 
 struct PArgs {
   XProj xq;
@@ -138,28 +139,33 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
                      : q.W + (long)(d * H3 + ct * 64 + r) * q.ldw;
     }
     const int kq = 4 * (tid & 7);
-    floatx4 ra[2], rb[2];
-    auto gload = [&](int k0) {
+    // K-tiles are loaded kXpDepth ahead into a register ring: a producer owns its CU with one wave per
+    // SIMD, so one tile of MFMA work (~0.4 us) cannot cover an HBM load; the ring keeps kXpDepth tiles'
+    // loads in flight.  Out-of-range A rows load row 0 of x (a valid address) and select zero after the
+    // load, so no load is predicated.
+    floatx4 ra[kXpDepth][2], rb[kXpDepth][2];
+    auto gload = [&](floatx4 (&xa)[2], floatx4 (&xb)[2], int k0) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        ra[j] = aval[j] ? *reinterpret_cast<const floatx4*>(arow[j] + k0 + kq) : floatx4{0.f, 0.f, 0.f, 0.f};
-        rb[j] = q.nn ? *reinterpret_cast<const floatx4*>(brow[j] + (long)k0 * q.ldw)
+        const floatx4 v = *reinterpret_cast<const floatx4*>(arow[j] + k0 + kq);
+        xa[j] = aval[j] ? v : floatx4{0.f, 0.f, 0.f, 0.f};
+        xb[j] = q.nn ? *reinterpret_cast<const floatx4*>(brow[j] + (long)k0 * q.ldw)
                      : *reinterpret_cast<const floatx4*>(brow[j] + k0 + kq);
       }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](const floatx4 (&xa)[2], const floatx4 (&xb)[2], int buf) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int f = tid + 256 * j;
-        *reinterpret_cast<floatx4*>(As[buf] + (f >> 3) * LDK + 4 * (f & 7)) = ra[j];
+        *reinterpret_cast<floatx4*>(As[buf] + (f >> 3) * LDK + 4 * (f & 7)) = xa[j];
         if (q.nn) {
           float* pb = Bs[buf] + (4 * (f >> 5)) * LDK + (f & 31);
-          pb[0] = rb[j][0];
-          pb[LDK] = rb[j][1];
-          pb[2 * LDK] = rb[j][2];
-          pb[3 * LDK] = rb[j][3];
+          pb[0] = xb[j][0];
+          pb[LDK] = xb[j][1];
+          pb[2 * LDK] = xb[j][2];
+          pb[3 * LDK] = xb[j][3];
         } else {
-          *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = rb[j];
+          *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = xb[j];
         }
       }
     };
@@ -169,32 +175,39 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
     const int nk = q.K / 32;
     const bool act = tid < 256;  // a backward block's 5th (row loader) wave only joins the barriers
     if (act) {
-      gload(0);
-      lstore(0);
+#pragma unroll
+      for (int i = 0; i < kXpDepth; ++i)
+        if (i < nk) gload(ra[i], rb[i], 32 * i);
+      lstore(ra[0], rb[0], 0);
     }
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {  // gemm_f32's double-buffered 64x64 main loop, same MFMA order
-      const int buf = kt & 1;
-      const bool more = kt + 1 < nk;
-      if (!act) {
+    // gemm_f32's double-buffered 64x64 main loop, same MFMA order; unrolled by the ring depth so every
+    // ring slot index is a constant.  Iteration kt: slot kt % D (tile kt, already in LDS) reloads tile
+    // kt + D, the MFMAs run on LDS buffer kt & 1, slot (kt + 1) % D goes to the other buffer.
+    for (int kt0 = 0; kt0 < nk; kt0 += kXpDepth) {
+#pragma unroll
+      for (int j = 0; j < kXpDepth; ++j) {
+        const int kt = kt0 + j;
+        if (kt >= nk) break;
+        const int buf = j & 1;  // kXpDepth is even
+        if (act) {
+          if (kt + kXpDepth < nk) gload(ra[j], rb[j], 32 * (kt + kXpDepth));
+          floatx4 av[4], bv[4];
+          const float* pa = As[buf] + (wy * 32 + li) * LDK + 16 * lk;
+          const float* pb = Bs[buf] + (wx * 32 + li) * LDK + 16 * lk;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            av[c] = *reinterpret_cast<const floatx4*>(pa + 4 * c);
+            bv[c] = *reinterpret_cast<const floatx4*>(pb + 4 * c);
+          }
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
+          if (kt + 1 < nk) lstore(ra[(j + 1) % kXpDepth], rb[(j + 1) % kXpDepth], buf ^ 1);
+        }
         __syncthreads();
-        continue;
       }
-      if (more) gload((kt + 1) * 32);
-      floatx4 av[4], bv[4];
-      const float* pa = As[buf] + (wy * 32 + li) * LDK + 16 * lk;
-      const float* pb = Bs[buf] + (wx * 32 + li) * LDK + 16 * lk;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        av[c] = *reinterpret_cast<const floatx4*>(pa + 4 * c);
-        bv[c] = *reinterpret_cast<const floatx4*>(pb + 4 * c);
-      }
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
-      if (more) lstore(buf ^ 1);
-      __syncthreads();
     }
     // epilogue: write-through stores of the valid rows, drain, one counter add per tile
     const int col = d * H3 + ct * 64 + wx * 32 + li;
