@@ -70,10 +70,25 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
 int attn_bwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
              const void* saved, const float* dlogp, float* dh, int accumulate_dh, const AttnGrads& G, float scale,
              void* scratch, size_t scratch_bytes);
-// split form used by the model step (wgrad may run on a side stream after core)
+// The two terms of the XCD-local path's dh (after its loop): dh[b, l, :] = sum_t alpha[b, t, l] dc[b, t, :]
+// (alpha (B, T, L), dc (B, T, A)) + dVh[b, l, :] V (dVh (B, L, Sc), V (Sc, A)).
+struct AttnDhTerms {
+  const float* alpha = nullptr;
+  const float* dc = nullptr;
+  const float* dvh = nullptr;
+  const float* V = nullptr;
+  int B = 0, L = 0, T = 0, A = 0, Sc = 0;
+  GemmWs gws;  // split-K workspace for attn_dh_gemms
+};
+// dh = the two terms, as GEMMs (alpha^T dc per utterance, then -- after dvh_ready when given -- dh += dVh V)
+int attn_dh_gemms(hipStream_t st, const AttnDhTerms& t, float* dh, int accumulate_dh, hipEvent_t dvh_ready = nullptr);
+// split form used by the model step (wgrad may run on a side stream after core).  defer_dh (optional):
+// when the XCD-local path runs and dh is not accumulated, dh is NOT computed; its terms are returned there
+// (defer_dh->dvh != nullptr) for the caller to fuse into the encoder's BPTT launch.
 int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                   const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
-                  size_t scratch_bytes, hipStream_t side = nullptr, hipEvent_t* ev = nullptr);
+                  size_t scratch_bytes, hipStream_t side = nullptr, hipEvent_t* ev = nullptr,
+                  AttnDhTerms* defer_dh = nullptr);
 int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)

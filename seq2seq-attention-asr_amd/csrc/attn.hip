@@ -1341,9 +1341,29 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   return 0;
 }
 
+int attn_dh_gemms(hipStream_t st, const AttnDhTerms& t, float* dh, int accumulate_dh, hipEvent_t dvh_ready) {
+  const int B = t.B, L = t.L, T = t.T, A = t.A;
+  const GemmWs gws = t.gws;
+  // dh_l (+)= sum_t alpha_{t,l} dc_t  (one GEMM per utterance: alpha_b^T (L x T) . dc_b (T x A))
+  for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
+    GemmProblem pr[kMaxGemmBatch];
+    const int nb = std::min(kMaxGemmBatch, B - b0);
+    for (int i = 0; i < nb; ++i) {
+      const long b = b0 + i;
+      pr[i] = GemmProblem{t.alpha + b * T * L, t.dc + b * T * A, dh + b * L * A, nullptr, L, A, A, L, A, T,
+                          1.f, accumulate_dh ? 1.f : 0.f};
+    }
+    S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
+  }
+  if (dvh_ready) S2S_CHECK_HIP(hipStreamWaitEvent(st, dvh_ready, 0));
+  // dh += dVh V   (Vh = h V^T)
+  return gemm1(st, false, false, B * L, A, t.Sc, 1.f, t.dvh, t.Sc, t.V, A, 1.f, dh, A, nullptr, gws);
+}
+
 int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P,
                   const void* saved, const float* dlogp, float* dh, int accumulate_dh, void* scratch,
-                  size_t scratch_bytes, hipStream_t side, hipEvent_t* ev) {
+                  size_t scratch_bytes, hipStream_t side, hipEvent_t* ev, AttnDhTerms* defer_dh) {
+  if (defer_dh) *defer_dh = AttnDhTerms{};
   S2S_TRY(attn_check_dims(d));
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
@@ -1423,18 +1443,13 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       S2S_CHECK_HIP(hipGetLastError());
     }
     if (side) S2S_CHECK_HIP(hipEventRecord(ev[4], side));
-    // dh_l (+)= sum_t alpha_{t,l} dc_t  (one GEMM per utterance: alpha_b^T (L x T) . dc_b (T x A))
-    for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
-      GemmProblem pr[kMaxGemmBatch];
-      const int nb = std::min(kMaxGemmBatch, B - b0);
-      for (int i = 0; i < nb; ++i) {
-        const long b = b0 + i;
-        pr[i] = GemmProblem{k.ALPHA + b * T * L, x.DCS + b * T * A, dh + b * L * A, nullptr, L, A, A, L, A, T,
-                            1.f, accumulate_dh ? 1.f : 0.f};
-      }
-      S2S_TRY(gemm_f32(st, pr, nb, true, false, gws));
+    const AttnDhTerms terms{k.ALPHA, x.DCS, k.DVH, P.V, B, L, T, A, Sc, gws};
+    if (defer_dh && !accumulate_dh) {  // the caller fuses both terms into the encoder BPTT launch
+      if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[4], 0));
+      *defer_dh = terms;
+      return 0;
     }
-    if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[4], 0));
+    return attn_dh_gemms(st, terms, dh, accumulate_dh, side ? ev[4] : nullptr);
   } else if (pb.fn) {
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);

@@ -288,6 +288,7 @@ int wgrad_fork_mode() {
   }();
   return m;
 }
+int g_fuse_dh = 1;  // s2s_debug_fuse_dh(0) (diagnostic): the decoder's dh by GEMMs in front of the top BPTT
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
 // seed_dev: the context's dropout seed word when a captured step reads its seed from the device (the
 // host writes it before each replay), else null (the seed is d->dropout_seed)
@@ -391,8 +392,11 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // ---- decoder backward -> dh
   float* dYcur = w.dY0;
   float* dYnext = w.dY1;
+  // the decoder's dh (context term + dVh V) is produced by the top layer's BPTT launch itself when it can
+  // (gru_layer_dy_fused), otherwise by GEMMs in front of it
+  AttnDhTerms dht{};
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
-                        w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr));
+                        w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr, g_fuse_dh ? &dht : nullptr));
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
   S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
   S2S_TRY(mark_bucket(bev, 0, split ? side : st));
@@ -425,6 +429,26 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     // this layer's dX is the dy of the layer below: produced inside that layer's BPTT launch (or by one
     // GEMM in front of it), so the critical path has no GEMM between two BPTT launches
     gr.dx = nullptr;
+    if (l == nl - 1 && dht.dvh) {  // dy = dh = sum_t alpha dc + dVh V, in-launch
+      gr.ydA = dht.dvh;
+      gr.yldA = dht.Sc;
+      gr.yK = dht.Sc;
+      gr.yN = dht.A;
+      gr.yWx = dht.V;
+      gr.yldw = dht.A;
+      gr.yalpha = dht.alpha;
+      gr.ydc = dht.dc;
+      gr.yT = dht.T;
+      if (dht.A != 2 * H || !gru_layer_dy_fused(io, gr)) {
+        gr = GruLayerGrad{};
+        for (int dd = 0; dd < 2; ++dd) {
+          for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
+          gr.dy[dd] = dYcur + dd * H;
+        }
+        gr.lddy = 2L * H;
+        S2S_TRY(attn_dh_gemms(st, dht, dYcur, 0));
+      }
+    }
     if (l + 1 < nl) {
       const GruLayerIO up = layer_io(l + 1);
       gr.ydA = w.dA[l + 1];
@@ -1188,3 +1212,4 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
   s2s::set_gemm_precision(s2s::kGemmF32);
   return rc;
 }
+extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }

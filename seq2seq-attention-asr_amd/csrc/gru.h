@@ -39,6 +39,11 @@ struct GruLayerGrad {
   int yK, yN;
   const float* yWx;
   long yldw;
+  // optional with ydA (the top layer, whose dy is the decoder's dh; fused launch only): dy also gets
+  // sum_t yalpha[b, t, l] ydc[b, t, :] (yalpha (B, yT, L), ydc (B, yT, lddy)) -- then ydA . yWx is dVh V
+  const float* yalpha = nullptr;
+  const float* ydc = nullptr;
+  int yT = 0;
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
@@ -55,6 +60,8 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
                        size_t scratch_bytes);
 int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws);
 float* gru_layer_dA(const GruLayerIO& io, void* scratch);
+// gru_layer_bwd_core will produce gr's dy (ydA . yWx) inside its persistent BPTT launch
+bool gru_layer_dy_fused(const GruLayerIO& io, const GruLayerGrad& gr);
 // the x-weights (3 ndir H, Kx) rows of a packed layer (gru_layers_pack) and their row stride Kx
 const float* gru_layer_packed_wx(const GruLayerIO& io, long* ldw);
 

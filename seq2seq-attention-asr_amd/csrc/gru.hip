@@ -442,8 +442,8 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   a.H = H;
   a.len = io.len;
   const bool persist = use_persistent(nd, B, H);
-  const bool yfuse = gr.ydA && persist && (nd == 1 || gr.dy[1] == gr.dy[0] + H) &&
-                     gru_persist_fused_dy(nd, B, H, gr.yK, gr.yldw, gr.lddy);
+  const bool yfuse = gru_layer_dy_fused(io, gr);
+  S2S_REQUIRE(!gr.yalpha || yfuse, "gru: the dh context term is only produced inside the fused BPTT launch");
   if (gr.ydA && !yfuse) {  // the layer above's dX as one GEMM in front of the BPTT (same order as in-launch)
     GemmProblem p{gr.ydA, gr.yWx, const_cast<float*>(gr.dy[0]), nullptr, gr.yldA, gr.yldw, gr.lddy, B * L, gr.yN,
                   gr.yK, 1.f, 0.f};
@@ -455,6 +455,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     f.len = io.len;
     if (yfuse) {
       f.ydA = gr.ydA; f.yldA = gr.yldA; f.yK = gr.yK; f.yWx = gr.yWx; f.yldw = gr.yldw;
+      f.yalpha = gr.yalpha; f.ydc = gr.ydc; f.yT = gr.yT;
     }
     f.ndir = nd; f.B = B; f.L = L; f.H = H; f.lddy = gr.lddy; f.ldA = ldA;
     for (int d = 0; d < nd; ++d) {
@@ -483,6 +484,12 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     S2S_TRY(gemm_f32(st, &p, 1, false, false, layer_gemm_ws(scratch, nd, B, L, D, H)));
   }
   return 0;
+}
+
+bool gru_layer_dy_fused(const GruLayerIO& io, const GruLayerGrad& gr) {
+  const int nd = io.ndir, B = io.B, H = io.H;
+  return gr.ydA && use_persistent(nd, B, H) && (nd == 1 || gr.dy[1] == gr.dy[0] + H) &&
+         gru_persist_fused_dy(nd, B, H, gr.yK, gr.yldw, gr.lddy);
 }
 
 const float* gru_layer_packed_wx(const GruLayerIO& io, long* ldw) {

@@ -41,6 +41,10 @@ struct GruPersistBwd {
   int yK = 0;
   const float* yWx = nullptr;
   long yldw = 0;
+  // optional: dy += sum_t yalpha[b, t, l] ydc[b, t, :] (the decoder's context term of dh; row stride lddy)
+  const float* yalpha = nullptr;
+  const float* ydc = nullptr;
+  int yT = 0;
 };
 
 bool gru_persist_supported(int ndir, int B, int H);

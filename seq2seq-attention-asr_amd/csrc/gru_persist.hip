@@ -74,9 +74,13 @@ struct XProj {
   int tpt;          // steps per slice (64 / B)
   int nslices, ntn, nwork;
   unsigned* done;   // [nd][nslices] finished column tiles
+  // optional (the top layer's dy = the decoder's dh): xp += sum_t alpha[b, t, l] dc[b, t, col], alpha
+  // (B, T, L), dc (B, T, ldxp) -- the context term, beside the MFMA's dVh V
+  const float* alpha;
+  const float* dc;
+  int T;
 };
 constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
-constexpr int kXpDepth = 4;             // producer K-tiles in flight (register ring)
 
 struct PArgs {
   XProj xq;
@@ -89,6 +93,7 @@ struct PArgs {
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
+  unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
 };
 
 // diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
@@ -99,6 +104,8 @@ struct PArgs {
       a.stamps[((long)lw * a.L + s) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
 unsigned long long* g_gru_stamps[2] = {nullptr, nullptr};
+unsigned long long* g_gru_pstamps[2] = {nullptr, nullptr};
+constexpr int kProdStampItems = 32;
 
 // cross-wave sum + abort agreement at the same barrier
 __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds, bool ok, floatx4 acc, int wave,
@@ -111,109 +118,184 @@ __device__ __forceinline__ float reduce_or_abort(SkinnyRed& red, int* abort_lds,
 
 // ------------------------------------------------------------------------------ fused x-projection
 // producer p of nprod takes work items p, p + nprod, ... (a static round-robin in consumption order:
-// uniform loop bounds, no shared work counter)
+// uniform loop bounds, no shared work counter).  NN: W is (K, ldw) read row-contiguous (the backward's
+// dy); D: K-tiles in flight, a divisor of K / 32 (xproj_depth).
+// K-tiles are loaded D ahead into a register ring: a producer owns its CU with one wave per SIMD, so one
+// tile of MFMA work (~0.4 us) cannot cover an HBM load.  The main loop is branch-free (a steady part that
+// loads, stores and multiplies every iteration, then a D-iteration drain), so the compiler's vmcnt waits
+// count exactly the loads of the tile being stored.  Out-of-range tile rows load row 0 of x (valid, finite
+// data) as they are: a GEMM's output row depends on its own A row only, and those rows are never stored
+// (zeroing them with a select made the compiler hoist every ring slot's select, i.e. wait for every load).
+template <bool NN, int D>
 __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p, int nprod) {
   const XProj& q = a.xq;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nk = q.K / 32;
+  if (tid >= 256) {  // a 320-thread block's 5th (row loader) wave: only the producer's barriers
+    const int nb = nk + 2 + (q.alpha ? 1 : 0);
+    for (int w = p; w < q.nwork; w += nprod)
+      for (int i = 0; i < nb; ++i) __syncthreads();
+    return;
+  }
   const int wy = wave >> 1, wx = wave & 1, li = lane & 31, lk = lane >> 5;
   const int B = a.B, L = a.L, H3 = q.ncd, nd = q.nslices > 0 ? q.nwork / (q.nslices * q.ntn) : 1;
   constexpr int LDK = 36;
   float* As[2] = {lds, lds + 64 * LDK};
   float* Bs[2] = {lds + 128 * LDK, lds + 192 * LDK};
-  for (int w = p; w < q.nwork; w += nprod) {
+  int item = 0;
+  for (int w = p; w < q.nwork; w += nprod, ++item) {
+    if (a.pstamps && tid == 0 && item < kProdStampItems)
+      a.pstamps[((long)p * kProdStampItems + item) * 2] = __builtin_amdgcn_s_memrealtime();
     const int sl = w / (nd * q.ntn), rem = w - sl * nd * q.ntn, d = rem / q.ntn, ct = rem - d * q.ntn;
     const int rev = a.d[d].reverse ^ q.flip;
-    // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows (nn: B columns 4 (f / 32) ..
+    // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows (NN: B columns 4 (f / 32) ..
     // + 3 of k row f % 32, gemm_f32's row-contiguous loader)
     const float* arow[2];
-    bool aval[2];
     const float* brow[2];
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int r = (tid >> 3) + 32 * j, jt = r / B, b = r - jt * B, s = sl * q.tpt + jt;
-      aval[j] = jt < q.tpt && s < L;
+      const bool aval = jt < q.tpt && s < L;
       const int t = rev ? L - 1 - s : s;
-      arow[j] = q.x + (aval[j] ? ((long)b * L + t) * q.ldx : 0);
+      arow[j] = q.x + (aval ? ((long)b * L + t) * q.ldx : 0);
       const int f = tid + 256 * j;
-      brow[j] = q.nn ? q.W + (long)(f & 31) * q.ldw + d * H3 + ct * 64 + 4 * (f >> 5)
-                     : q.W + (long)(d * H3 + ct * 64 + r) * q.ldw;
+      brow[j] = NN ? q.W + (long)(f & 31) * q.ldw + d * H3 + ct * 64 + 4 * (f >> 5)
+                   : q.W + (long)(d * H3 + ct * 64 + r) * q.ldw;
     }
     const int kq = 4 * (tid & 7);
-    // K-tiles are loaded kXpDepth ahead into a register ring: a producer owns its CU with one wave per
-    // SIMD, so one tile of MFMA work (~0.4 us) cannot cover an HBM load; the ring keeps kXpDepth tiles'
-    // loads in flight.  Out-of-range A rows load row 0 of x (a valid address) and select zero after the
-    // load, so no load is predicated.
-    floatx4 ra[kXpDepth][2], rb[kXpDepth][2];
-    auto gload = [&](floatx4 (&xa)[2], floatx4 (&xb)[2], int k0) {
+    const long bstep = NN ? 32 * q.ldw : 32;  // B advance per K-tile
+    floatx4 ra[D][2], rb[D][2];
+    auto gload = [&](floatx4 (&xa)[2], floatx4 (&xb)[2], int kt) {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const floatx4 v = *reinterpret_cast<const floatx4*>(arow[j] + k0 + kq);
-        xa[j] = aval[j] ? v : floatx4{0.f, 0.f, 0.f, 0.f};
-        xb[j] = q.nn ? *reinterpret_cast<const floatx4*>(brow[j] + (long)k0 * q.ldw)
-                     : *reinterpret_cast<const floatx4*>(brow[j] + k0 + kq);
+        xa[j] = *reinterpret_cast<const floatx4*>(arow[j] + 32 * kt + kq);
+        xb[j] = *reinterpret_cast<const floatx4*>(brow[j] + kt * bstep + (NN ? 0 : kq));
       }
     };
     auto lstore = [&](const floatx4 (&xa)[2], const floatx4 (&xb)[2], int buf) {
+      float* as = As[0] + buf * (64 * LDK);
+      float* bs = Bs[0] + buf * (64 * LDK);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int f = tid + 256 * j;
-        *reinterpret_cast<floatx4*>(As[buf] + (f >> 3) * LDK + 4 * (f & 7)) = xa[j];
-        if (q.nn) {
-          float* pb = Bs[buf] + (4 * (f >> 5)) * LDK + (f & 31);
+        *reinterpret_cast<floatx4*>(as + (f >> 3) * LDK + 4 * (f & 7)) = xa[j];
+        if (NN) {
+          float* pb = bs + (4 * (f >> 5)) * LDK + (f & 31);
           pb[0] = xb[j][0];
           pb[LDK] = xb[j][1];
           pb[2 * LDK] = xb[j][2];
           pb[3 * LDK] = xb[j][3];
         } else {
-          *reinterpret_cast<floatx4*>(Bs[buf] + (f >> 3) * LDK + 4 * (f & 7)) = xb[j];
+          *reinterpret_cast<floatx4*>(bs + (f >> 3) * LDK + 4 * (f & 7)) = xb[j];
         }
       }
     };
     floatx16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.f;
-    const int nk = q.K / 32;
-    const bool act = tid < 256;  // a backward block's 5th (row loader) wave only joins the barriers
-    if (act) {
+    // gemm_f32's double-buffered 64x64 main loop, same MFMA order
+    // the MFMAs of one K-tile with `mid` (the next tile's LDS store) issued between its two halves, so the
+    // LDS writes and their wait overlap the second half's MFMAs (sched_barrier pins the placement)
+    auto mma = [&](int buf, auto&& mid) {
+      floatx4 av[4], bv[4];
+      const float* pa = As[0] + buf * (64 * LDK) + (wy * 32 + li) * LDK + 16 * lk;
+      const float* pb = Bs[0] + buf * (64 * LDK) + (wx * 32 + li) * LDK + 16 * lk;
 #pragma unroll
-      for (int i = 0; i < kXpDepth; ++i)
-        if (i < nk) gload(ra[i], rb[i], 32 * i);
-      lstore(ra[0], rb[0], 0);
-    }
+      for (int c = 0; c < 4; ++c) {
+        av[c] = *reinterpret_cast<const floatx4*>(pa + 4 * c);
+        bv[c] = *reinterpret_cast<const floatx4*>(pb + 4 * c);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      mid();
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int c = 2; c < 4; ++c)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
+    };
+#pragma unroll
+    for (int i = 0; i < D; ++i) gload(ra[i], rb[i], i);
+    lstore(ra[0], rb[0], 0);
     __syncthreads();
-    // gemm_f32's double-buffered 64x64 main loop, same MFMA order; unrolled by the ring depth so every
-    // ring slot index is a constant.  Iteration kt: slot kt % D (tile kt, already in LDS) reloads tile
-    // kt + D, the MFMAs run on LDS buffer kt & 1, slot (kt + 1) % D goes to the other buffer.
-    for (int kt0 = 0; kt0 < nk; kt0 += kXpDepth) {
+    // steady part: iteration kt (slot kt % D holds tile kt, already in LDS) reloads that slot with tile
+    // kt + D, multiplies LDS buffer kt & 1 and stores slot (kt + 1) % D into the other buffer
+    for (int kt0 = 0; kt0 < nk - D; kt0 += D) {
 #pragma unroll
-      for (int j = 0; j < kXpDepth; ++j) {
+      for (int j = 0; j < D; ++j) {
         const int kt = kt0 + j;
-        if (kt >= nk) break;
-        const int buf = j & 1;  // kXpDepth is even
-        if (act) {
-          if (kt + kXpDepth < nk) gload(ra[j], rb[j], 32 * (kt + kXpDepth));
-          floatx4 av[4], bv[4];
-          const float* pa = As[buf] + (wy * 32 + li) * LDK + 16 * lk;
-          const float* pb = Bs[buf] + (wx * 32 + li) * LDK + 16 * lk;
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            av[c] = *reinterpret_cast<const floatx4*>(pa + 4 * c);
-            bv[c] = *reinterpret_cast<const floatx4*>(pb + 4 * c);
-          }
-#pragma unroll
-          for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
-          if (kt + 1 < nk) lstore(ra[(j + 1) % kXpDepth], rb[(j + 1) % kXpDepth], buf ^ 1);
-        }
+        gload(ra[j], rb[j], kt + D);
+        mma(kt & 1, [&] { lstore(ra[(j + 1) % D], rb[(j + 1) % D], (kt + 1) & 1); });
         __syncthreads();
       }
     }
-    // epilogue: write-through stores of the valid rows, drain, one counter add per tile
+    // drain: the last D tiles are all loaded
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const int kt = nk - D + j;
+      mma(kt & 1, [&] {
+        if (j + 1 < D) lstore(ra[(j + 1) % D], rb[(j + 1) % D], (kt + 1) & 1);
+      });
+      __syncthreads();
+    }
     const int col = d * H3 + ct * 64 + wx * 32 + li;
+    if (q.alpha) {
+      // the decoder's context term of dh: ctx[row][c] = sum_t alpha[b, t, l] dc[b, t, c] in a fixed t order,
+      // computed with its own mapping (4 rows x 4 consecutive columns per thread: float4 dc loads, 4 steps
+      // of loads in flight) into the (now free) LDS tile area, then added to the MFMA outputs.  Rows outside
+      // the tile read utterance 0, frame 0 and are not stored.
+      float* ctxl = lds;  // [64][68]
+      const int c4 = 4 * (tid & 15), r0 = 4 * (tid >> 4);
+      long arow_[4], drow_[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int tr = r0 + i, jt = tr / B, s = sl * q.tpt + jt;
+        const bool v = jt < q.tpt && s < L;
+        const int b = v ? tr - jt * B : 0, l = v ? (rev ? L - 1 - s : s) : 0;
+        arow_[i] = (long)b * q.T * L + l;
+        drow_[i] = (long)b * q.T * q.ldxp + d * H3 + ct * 64 + c4;
+      }
+      floatx4 cx[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) cx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
+      int tt = 0;
+      for (; tt + 4 <= q.T; tt += 4) {
+        float av[4][4];
+        floatx4 dv[4][4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            av[u][i] = q.alpha[arow_[i] + (long)(tt + u) * L];
+            dv[u][i] = *reinterpret_cast<const floatx4*>(q.dc + drow_[i] + (long)(tt + u) * q.ldxp);
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) cx[i][e] += av[u][i] * dv[u][i][e];
+      }
+      for (; tt < q.T; ++tt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float av = q.alpha[arow_[i] + (long)tt * L];
+          const floatx4 dv = *reinterpret_cast<const floatx4*>(q.dc + drow_[i] + (long)tt * q.ldxp);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) cx[i][e] += av * dv[e];
+        }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<floatx4*>(ctxl + (r0 + i) * 68 + c4) = cx[i];
+      __syncthreads();  // (a 320-thread block's 5th wave matches it in its barrier loop)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += ctxl[(wy * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk) * 68 + wx * 32 + li];
+    }
+    // epilogue: write-through stores of the valid rows, drain, one counter add per tile
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if (!act) break;
       const int tr = wy * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk, jt = tr / B, b = tr - jt * B, s = sl * q.tpt + jt;
       if (jt < q.tpt && s < L) {
         const int t = rev ? L - 1 - s : s;
@@ -224,7 +306,19 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(q.done + d * q.nslices + sl, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (a.pstamps && tid == 0 && item < kProdStampItems)
+      a.pstamps[((long)p * kProdStampItems + item) * 2 + 1] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// the producer with the deepest ring that divides K / 32
+template <bool NN>
+__device__ __forceinline__ void xproj_produce_any(const PArgs& a, float* lds, int p, int nprod) {
+  const int nk = a.xq.K / 32;
+  if (nk % 4 == 0) xproj_produce<NN, 4>(a, lds, p, nprod);
+  else if (nk % 3 == 0) xproj_produce<NN, 3>(a, lds, p, nprod);
+  else if (nk % 2 == 0) xproj_produce<NN, 2>(a, lds, p, nprod);
+  else xproj_produce<NN, 1>(a, lds, p, nprod);
 }
 
 // consumer side: is slice `sl` of direction d complete?  (one sc1 load)
@@ -271,7 +365,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: x-projection producer (or idle)
     if (a.fused) {
       const int gch = 8 * ((a.nchains + 7) / 8);
-      xproj_produce(a, xlds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
+      xproj_produce_any<false>(a, xlds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
     }
     return;
   }
@@ -460,7 +554,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: dy producer (or idle)
     if (a.fused) {
       const int gch = 8 * ((a.nchains + 7) / 8);
-      xproj_produce(a, ylds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
+      xproj_produce_any<true>(a, ylds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
     }
     return;
   }
@@ -471,6 +565,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const int lw = dir * a.nwg + mt * ncol + c;  // logical workgroup id (stamps)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
+  if (a.stamps && tid == 0) a.stamps[((long)lw * L + L - 1) * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // entry
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const bool loader = wave == 4;
@@ -481,6 +576,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   }
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
+  if (a.stamps && tid == 0) a.stamps[((long)lw * L + L - 1) * 8 + 7] = __builtin_amdgcn_s_memrealtime();  // census done
 
   if (loader) {
     // lane l: utterance b0 + (l >> 2) of the tile, units c * 16 + 4 (l & 3) .. + 3
@@ -755,6 +851,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[0];
+  a.pstamps = g_gru_pstamps[0];
   if (f.x) {  // fused x-projection by the grid's spare slots
     XProj& q = a.xq;
     q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.ldw = f.Kx; q.nn = 0; q.ncd = 3 * f.H; q.flip = 0;
@@ -786,6 +883,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.stamps = g_gru_stamps[1];
+  a.pstamps = g_gru_pstamps[1];
   if (b.ydA) {  // fused dy (the layer above's dX) by the grid's spare slots
     XProj& q = a.xq;
     q.x = b.ydA; q.ldx = b.yldA; q.K = b.yK; q.W = b.yWx; q.ldw = b.yldw; q.nn = 1; q.ncd = b.H; q.flip = 1;
@@ -795,6 +893,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     q.ntn = b.H / 64;
     q.nwork = q.nslices * b.ndir * q.ntn;
     q.done = xcount;
+    q.alpha = b.yalpha; q.dc = b.ydc; q.T = b.yT;
     a.fused = 1;
   }
   S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
@@ -816,4 +915,9 @@ extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);
+}
+// diagnostic: producer item stamps [producer][32][2] of the next fused persistent launches (nullptr: off)
+extern "C" void s2s_debug_gru_prod_stamps(void* fwd, void* bwd) {
+  s2s::g_gru_pstamps[0] = static_cast<unsigned long long*>(fwd);
+  s2s::g_gru_pstamps[1] = static_cast<unsigned long long*>(bwd);
 }
