@@ -19,6 +19,8 @@
 //     loaded before the wait so their latency hides under it;
 //   * every wait is bounded: on timeout a wave raises the launch's abort word, every waiting
 //     wave sees it within 64 polls, all workgroups leave at their next barrier.
+#include <algorithm>
+
 #include "gru.h"
 #include "gru_persist.h"
 #include "handoff.h"
@@ -72,14 +74,45 @@ struct XProj {
   float* xp;
   long ldxp;
   int tpt;          // steps per slice (64 / B)
-  int nslices, ntn, nwork;
+  int nslices, ntn, nwork, nd;
   unsigned* done;   // [nd][nslices] finished column tiles
   // optional (the top layer's dy = the decoder's dh): xp += sum_t alpha[b, t, l] dc[b, t, col], alpha
   // (B, T, L), dc (B, T, ldxp) -- the context term, beside the MFMA's dVh V
   const float* alpha;
   const float* dc;
   int T;
+  // split-K start (backward): slices [0, sA) are cut into PA K-parts, [sA, sB) into PB, the rest whole, so
+  // the first slices the recurrence needs are ready after a fraction of a tile's K loop; a split item's parts
+  // write partial tiles to `slab` ([item][PA][16][256]) and the last part to finish (icnt[item]) sums them in
+  // part order and publishes the tile.  nwork counts units (parts).
+  int sA, sB, PA, PB;
+  float* slab;
+  unsigned* icnt;
 };
+constexpr int kXpMaxSplitItems = 64;
+
+// work unit u of the producers' round-robin: slice, direction, column tile, K-part of P, split item (-1: whole)
+struct XUnit {
+  int sl, d, ct, part, P, item;
+};
+__device__ __forceinline__ XUnit xunit(const XProj& q, int nd, int u) {
+  const int per = nd * q.ntn, nA = q.sA * per * q.PA, nB = (q.sB - q.sA) * per * q.PB;
+  XUnit x;
+  int rem;
+  if (u < nA) {
+    const int i = u / q.PA;
+    x.P = q.PA; x.part = u - i * q.PA; x.item = i; x.sl = i / per; rem = i - x.sl * per;
+  } else if (u < nA + nB) {
+    const int v = u - nA, i = v / q.PB;
+    x.P = q.PB; x.part = v - i * q.PB; x.item = q.sA * per + i; x.sl = q.sA + i / per; rem = i % per;
+  } else {
+    const int v = u - nA - nB;
+    x.P = 1; x.part = 0; x.item = -1; x.sl = q.sB + v / per; rem = v % per;
+  }
+  x.d = rem / q.ntn;
+  x.ct = rem - x.d * q.ntn;
+  return x;
+}
 constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
 
 struct PArgs {
@@ -131,14 +164,25 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
   const XProj& q = a.xq;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nk = q.K / 32;
+  __shared__ int last_part;  // split item: this block's part was the last to finish
+  const int nd = q.nd;
   if (tid >= 256) {  // a 320-thread block's 5th (row loader) wave: only the producer's barriers
-    const int nb = nk + 2 + (q.alpha ? 1 : 0);
-    for (int w = p; w < q.nwork; w += nprod)
+    for (int w = p; w < q.nwork; w += nprod) {
+      const XUnit x = xunit(q, nd, w);
+      const int nb = 1 + nk / x.P + (q.alpha ? 1 : 0);
       for (int i = 0; i < nb; ++i) __syncthreads();
+      if (x.P == 1) {
+        __syncthreads();
+      } else {
+        __syncthreads();
+        __syncthreads();
+        if (last_part) __syncthreads();
+      }
+    }
     return;
   }
   const int wy = wave >> 1, wx = wave & 1, li = lane & 31, lk = lane >> 5;
-  const int B = a.B, L = a.L, H3 = q.ncd, nd = q.nslices > 0 ? q.nwork / (q.nslices * q.ntn) : 1;
+  const int B = a.B, L = a.L, H3 = q.ncd;
   constexpr int LDK = 36;
   float* As[2] = {lds, lds + 64 * LDK};
   float* Bs[2] = {lds + 128 * LDK, lds + 192 * LDK};
@@ -146,7 +190,9 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
   for (int w = p; w < q.nwork; w += nprod, ++item) {
     if (a.pstamps && tid == 0 && item < kProdStampItems)
       a.pstamps[((long)p * kProdStampItems + item) * 2] = __builtin_amdgcn_s_memrealtime();
-    const int sl = w / (nd * q.ntn), rem = w - sl * nd * q.ntn, d = rem / q.ntn, ct = rem - d * q.ntn;
+    const XUnit xu = xunit(q, nd, w);
+    const int sl = xu.sl, d = xu.d, ct = xu.ct;
+    const int nkp = nk / xu.P, kb = xu.part * nkp;  // this unit's K-tiles [kb, kb + nkp)
     const int rev = a.d[d].reverse ^ q.flip;
     // this thread's two A rows (tile rows tid/8 and 32 + tid/8) and B rows (NN: B columns 4 (f / 32) ..
     // + 3 of k row f % 32, gemm_f32's row-contiguous loader)
@@ -218,16 +264,16 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
         for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[c][e], bv[c][e], acc, 0, 0, 0);
     };
 #pragma unroll
-    for (int i = 0; i < D; ++i) gload(ra[i], rb[i], i);
+    for (int i = 0; i < D; ++i) gload(ra[i], rb[i], kb + i);
     lstore(ra[0], rb[0], 0);
     __syncthreads();
     // steady part: iteration kt (slot kt % D holds tile kt, already in LDS) reloads that slot with tile
     // kt + D, multiplies LDS buffer kt & 1 and stores slot (kt + 1) % D into the other buffer
-    for (int kt0 = 0; kt0 < nk - D; kt0 += D) {
+    for (int kt0 = 0; kt0 < nkp - D; kt0 += D) {
 #pragma unroll
       for (int j = 0; j < D; ++j) {
         const int kt = kt0 + j;
-        gload(ra[j], rb[j], kt + D);
+        gload(ra[j], rb[j], kb + kt + D);
         mma(kt & 1, [&] { lstore(ra[(j + 1) % D], rb[(j + 1) % D], (kt + 1) & 1); });
         __syncthreads();
       }
@@ -235,7 +281,7 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
     // drain: the last D tiles are all loaded
 #pragma unroll
     for (int j = 0; j < D; ++j) {
-      const int kt = nk - D + j;
+      const int kt = nkp - D + j;
       mma(kt & 1, [&] {
         if (j + 1 < D) lstore(ra[(j + 1) % D], rb[(j + 1) % D], (kt + 1) & 1);
       });
@@ -261,8 +307,10 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
       floatx4 cx[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) cx[i] = floatx4{0.f, 0.f, 0.f, 0.f};
-      int tt = 0;
-      for (; tt + 4 <= q.T; tt += 4) {
+      // a split item's parts take consecutive ranges of t
+      const int te = ((xu.part + 1) * q.T) / xu.P;
+      int tt = (xu.part * q.T) / xu.P;
+      for (; tt + 4 <= te; tt += 4) {
         float av[4][4];
         floatx4 dv[4][4];
 #pragma unroll
@@ -279,7 +327,7 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
 #pragma unroll
             for (int e = 0; e < 4; ++e) cx[i][e] += av[u][i] * dv[u][i][e];
       }
-      for (; tt < q.T; ++tt)
+      for (; tt < te; ++tt)
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float av = q.alpha[arow_[i] + (long)tt * L];
@@ -292,6 +340,45 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
       __syncthreads();  // (a 320-thread block's 5th wave matches it in its barrier loop)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[r] += ctxl[(wy * 32 + (r & 3) + 8 * (r >> 2) + 4 * lk) * 68 + wx * 32 + li];
+    }
+    if (xu.P > 1) {
+      // split item: publish this part's partial tile (write-through 16-byte stores, each thread's 16 values
+      // contiguous); the last part to finish sums all parts in part order
+      typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+      const __amdgpu_buffer_rsrc_t srs = rsrc_of(q.slab);
+      const int ibase = (xu.item * q.PA) * 16384 + tid * 64;  // byte offset of part 0, this thread
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        __builtin_amdgcn_raw_buffer_store_b128(
+            __builtin_bit_cast(u32x4, floatx4{acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]}), srs,
+            ibase + xu.part * 16384 + 16 * i, 0, 16);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        last_part = __hip_atomic_fetch_add(q.icnt + xu.item, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                    (unsigned)(xu.P - 1);
+      __syncthreads();
+      if (!last_part) {
+        if (a.pstamps && tid == 0 && item < kProdStampItems)
+          a.pstamps[((long)p * kProdStampItems + item) * 2 + 1] = __builtin_amdgcn_s_memrealtime();
+        continue;
+      }
+      floatx4 pv[4][4];  // [part][quad], all loads in flight together (sc1: written by other XCDs)
+#pragma unroll
+      for (int pp = 0; pp < 4; ++pp)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          pv[pp][i] = pp < xu.P ? __builtin_bit_cast(floatx4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                                  srs, ibase + pp * 16384 + 16 * i, 0, 16))
+                                : floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v = pv[0][i][e] + pv[1][i][e];
+          if (xu.P > 2) v = (v + pv[2][i][e]) + pv[3][i][e];
+          acc[4 * i + e] = v;
+        }
     }
     // epilogue: write-through stores of the valid rows, drain, one counter add per tile
 #pragma unroll
@@ -314,7 +401,7 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
 // the producer with the deepest ring that divides K / 32
 template <bool NN>
 __device__ __forceinline__ void xproj_produce_any(const PArgs& a, float* lds, int p, int nprod) {
-  const int nk = a.xq.K / 32;
+  const int nk = a.xq.K / 32;  // (a split start needs nk / PA % 4 == 0: xproj_split)
   if (nk % 4 == 0) xproj_produce<NN, 4>(a, lds, p, nprod);
   else if (nk % 3 == 0) xproj_produce<NN, 3>(a, lds, p, nprod);
   else if (nk % 2 == 0) xproj_produce<NN, 2>(a, lds, p, nprod);
@@ -788,6 +875,7 @@ bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx) {
   return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
 }
 
+int g_xp_split = 1;  // s2s_debug_gru_xp_split(0) (diagnostic): no split-K start of the fused dy producers
 int g_fuse_dy = 1;  // s2s_debug_gru_fused_dy(0) (diagnostic): the dX GEMM in front of the BPTT instead
 
 bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy) {
@@ -808,14 +896,30 @@ static size_t census_bytes(int B, int H) { return 4 * (size_t)(2 * ((B + 15) / 1
 
 // header | tagged granules | census | x-projection counters (zeroed by sync_prep every launch) |
 // sentinel rows (re-armed in-kernel)
-static size_t xcount_words(int L) { return 2 * (size_t)L; }
+// slice counters [2][L] and split-item counters [kXpMaxSplitItems]
+static size_t xcount_words(int L) { return 2 * (size_t)L + kXpMaxSplitItems; }
 static size_t prep_bytes(int B, int L, int H) {
   return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H) + 4 * xcount_words(L);
 }
 static size_t sent_offset(int B, int L, int H) { return (prep_bytes(B, L, H) + 255) / 256 * 256; }
+static size_t slab_offset(int B, int L, int H) { return sent_offset(B, L, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H; }
+constexpr size_t kXpSlabBytes = (size_t)kXpMaxSplitItems * 4 * 4096 * sizeof(float);  // PA <= 4
 
-size_t gru_persist_sync_bytes(int B, int L, int H) {
-  return sent_offset(B, L, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H;
+size_t gru_persist_sync_bytes(int B, int L, int H) { return slab_offset(B, L, H) + kXpSlabBytes; }
+
+// split-K start of a fused producer grid (XProj::sA ..): the first round of units is the first slices cut
+// into 4 K-parts, the second the next slices into 2, so the recurrence's first slices come after a quarter
+// / half of a tile's K loop; only when every part keeps the 4-deep ring (nk / 4 % 4 == 0)
+static void xproj_split(XProj& q, int nd, int nprod) {
+  q.sA = q.sB = 0;
+  q.PA = q.PB = 1;
+  const int nk = q.K / 32, per = nd * q.ntn;
+  if (!g_xp_split || nk % 16 != 0 || per <= 0) return;
+  const int sA = std::max(1, nprod / (per * 4));
+  const int sB = std::min(q.nslices, sA + std::max(1, nprod / (per * 2)));
+  if (sB > q.nslices || sB * per > kXpMaxSplitItems || sA >= sB) return;
+  q.sA = sA; q.sB = sB; q.PA = 4; q.PB = 2;
+  q.nwork = (sA * 4 + (sB - sA) * 2 + (q.nslices - sB)) * per;
 }
 
 static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_word, granule_t* (&g)[2][3],
@@ -859,8 +963,10 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     q.tpt = 64 / f.B;
     q.nslices = (f.L + q.tpt - 1) / q.tpt;
     q.ntn = 3 * f.H / 64;
+    q.nd = f.ndir;
     q.nwork = q.nslices * f.ndir * q.ntn;
     q.done = xcount;
+    q.sA = q.sB = 0; q.PA = q.PB = 1;
     a.fused = 1;
   }
   S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
@@ -891,9 +997,14 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     q.tpt = 64 / b.B;
     q.nslices = (b.L + q.tpt - 1) / q.tpt;
     q.ntn = b.H / 64;
+    q.nd = b.ndir;
     q.nwork = q.nslices * b.ndir * q.ntn;
     q.done = xcount;
     q.alpha = b.yalpha; q.dc = b.ydc; q.T = b.yT;
+    q.icnt = xcount + 2 * b.L;
+    q.slab = reinterpret_cast<float*>(static_cast<char*>(sync) + slab_offset(b.B, b.L, b.H));
+    const int gch = 8 * ((a.nchains + 7) / 8);
+    xproj_split(q, b.ndir, (gch - a.nchains) * a.nmem);
     a.fused = 1;
   }
   S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
@@ -912,6 +1023,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
 extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
 extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
+extern "C" void s2s_debug_gru_xp_split(int on) { s2s::g_xp_split = on; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);

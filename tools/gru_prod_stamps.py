@@ -39,6 +39,8 @@ def main():
     model = s2s_amd.ChorowskiBaseline(cfg, graph=False)
     x = torch.randn(B, L, D, device="cuda")
     lab = torch.randint(0, cfg.outputDepth, (B, 40), device="cuda", dtype=torch.int32)
+    if os.environ.get("S2S_XP_SPLIT") == "0":
+        _lib.lib.s2s_debug_gru_xp_split(0)
     model.step(x, lab)  # warm-up (first-launch costs)
     torch.cuda.synchronize()
     st_fn(sf.data_ptr(), sb.data_ptr())
@@ -56,8 +58,19 @@ def main():
           f"first step starts {tbp[:, 0, 0].min() - t0:.1f} .. {tbp[:, 0, 0].max() - t0:.1f}, "
           f"last step ends {tbp[:, -1, 5].max() - t0:.1f}")
     tpt = 64 // B
-    nwork = ((L + tpt - 1) // tpt) * ndir * (H // 64)
-    print(f"  ({nl} encoder layer(s); the stamped launch is layer 1's)")
+    nslices = (L + tpt - 1) // tpt
+    per_s = ndir * (H // 64)
+    # the producers' work units (gru_persist.hip xunit / xproj_split): slice of each unit
+    K = 3 * ndir * H if nl > 1 else cfg.scoreDepth
+    split = os.environ.get("S2S_XP_SPLIT", "1") != "0" and (K // 32) % 16 == 0
+    sA = max(1, nprod_b // (per_s * 4)) if split else 0
+    sB = min(nslices, sA + max(1, nprod_b // (per_s * 2))) if split else 0
+    unit_slice = [i // per_s for i in range(sA * per_s) for _ in range(4)]
+    unit_slice += [sA + i // per_s for i in range((sB - sA) * per_s) for _ in range(2)]
+    unit_slice += [sB + i // per_s for i in range((nslices - sB) * per_s)]
+    nwork = len(unit_slice)
+    print(f"  ({nl} encoder layer(s); the stamped launch is layer 1's; split start: slices < {sA} in 4 K-parts, "
+          f"< {sB} in 2)")
     per = (nwork + nprod_b - 1) // nprod_b
     used = min(per, ITEMS)
     st, en = prod[:, :used, 0], prod[:, :used, 1]
@@ -67,14 +80,13 @@ def main():
           f"{st[:, 0].max() - t0:.1f}, end {en[:, 0].min() - t0:.1f} .. {en[:, 0].max() - t0:.1f}; "
           f"item duration mean {dur.mean():.1f} (min {dur.min():.1f}, max {dur.max():.1f}); last item end "
           f"{en[valid].max() - t0:.1f}")
-    nd_ntn = ndir * (H // 64)
     ready = {}
     for p in range(nprod_b):
         for i in range(used):
             w = p + i * nprod_b
             if w >= nwork or en[p, i] == 0:
                 continue
-            sl = w // nd_ntn
+            sl = unit_slice[w]
             ready[sl] = max(ready.get(sl, 0.0), en[p, i] - t0)
     print("  slice: ready / consumer step start (slice 0 .. 9, 15, 31)")
     for sl in list(range(10)) + [15, 31]:
