@@ -439,6 +439,17 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
 
 // C = alpha * (sum of the split slabs in slice order) (+ bias) + beta * C; blockIdx.y = problem.
 // Four consecutive columns per thread (float4) when rows allow it.
+template <int S>
+__device__ __forceinline__ floatx4 slab_sum(const float* part, long mn, long e) {
+  floatx4 v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const floatx4*>(part + s * mn + e);
+  floatx4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < S; ++s) sum += v[s];
+  return sum;
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
   const GemmTile& q = Lc.q[blockIdx.y];
   if (q.part == nullptr) return;
@@ -451,7 +462,16 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
   if (vec) {
     for (long e = 4 * (blockIdx.x * 256L + threadIdx.x); e < mn; e += 4L * gridDim.x * 256) {
       floatx4 sum = {0.f, 0.f, 0.f, 0.f};
-      for (int s = 0; s < q.splits; ++s) sum += *reinterpret_cast<const floatx4*>(q.part + s * mn + e);
+      // every slab's load in flight before the first add (a runtime-bounded loop issued them one by
+      // one behind each add); the sum order is the slice order either way
+      switch (q.splits) {
+        case 2: sum = slab_sum<2>(q.part, mn, e); break;
+        case 3: sum = slab_sum<3>(q.part, mn, e); break;
+        case 4: sum = slab_sum<4>(q.part, mn, e); break;
+        case 8: sum = slab_sum<8>(q.part, mn, e); break;
+        default:
+          for (int s = 0; s < q.splits; ++s) sum += *reinterpret_cast<const floatx4*>(q.part + s * mn + e);
+      }
       const int row = (int)(e / N), col = (int)(e % N);
       floatx4 v = alpha * sum;
       if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
