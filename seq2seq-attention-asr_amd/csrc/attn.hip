@@ -89,6 +89,12 @@ struct XArgs {
   float* XWHT;  // (S, S)    Wh[:, :S]^T                               (saved)
   float* XZRT;  // (S, 2S)   [Wz[:, :S]; Wr[:, :S]]^T                   (saved)
   float* XWST;  // (S, Sc)   Ws^T                                      (saved)
+  // prologue operand re-layouts (dec_xcd_pack_ops) so its GEMMs batch as NN problems (fwd scratch)
+  float* PWDYT;  // (S, S)   Wd[:, S:]^T
+  float* PWDCT;  // (S, S)   Wd[:, :S]^T
+  float* PWCT;   // (A, S)   Wc^T
+  float* PWXDT;  // (S, 3S)  WXD^T
+  float* WDCT;   // (A, S)   (Wd_c Wc)^T
   // granule buffers, [2 slots][...]
   granule_t *gS, *gWS, *gPM, *gPL, *gPC, *gC, *gQ;     // forward (inside fsync)
   granule_t *gDGZ, *gDGR, *gDGH, *gDC, *gPDWS, *gDWS;  // backward (inside bsync)
@@ -180,6 +186,11 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* PC = f.take<float>(B * NCH * A);
   float* U = f.take<float>(BT * Mk);
   float* WDC = f.take<float>(S * A);
+  float* PWDYT = f.take<float>(S * S);
+  float* PWDCT = f.take<float>(S * S);
+  float* PWCT = f.take<float>(A * S);
+  float* PWXDT = f.take<float>(S * 3 * S);
+  float* WDCT = f.take<float>(A * S);
   float* KX = f.take<float>(BT * 3 * S);
   float* KD = f.take<float>(BT * S);
   float* BKD = f.take<float>(S);
@@ -279,6 +290,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   if (x) {
     x->WX = WX; x->WXT = WXT; x->WXD = WXD; x->WDC = WDC; x->KX = KX; x->KD = KD; x->BKD = BKD; x->DE = DE;
     x->DCS = DC; x->VBAR = VBAR; x->XWHT = XWHT; x->XZRT = XZRT; x->XWST = XWST;
+    x->PWDYT = PWDYT; x->PWDCT = PWDCT; x->PWCT = PWCT; x->PWXDT = PWXDT; x->WDCT = WDCT;
     x->gS = xgS; x->gWS = xgWS; x->gPM = xgPM; x->gPL = xgPL; x->gPC = xgPC; x->gC = xgC; x->gQ = xgQ;
     x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
     x->fcensus = fcensus; x->bcensus = bcensus;
@@ -1218,18 +1230,26 @@ static int launch_xcd(const XPlan& xp, bool fwd, hipStream_t st, AttnK& k, XArgs
 static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const GemmWs& gws) {
   WgradPrecision wp;  // the weight folds Wx' = W_d Wd_c Wc are reused by every step: fp32
   const int S = d.S, A = d.A, rows = d.B * d.T;
-  // On the side stream beside the encoder its kernels run only in the gaps the persistent GRU launches
-  // leave: the re-layouts and y_in in one launch, then BKD, then the GEMM chain.
+  // On the side stream beside the encoder its kernels run only where the persistent GRU launches leave
+  // room -- and a kernel with a workgroup dealt to an XCD the layer's chains fill waits for the layer to
+  // end -- so the chain is kept to 4 launches: the re-layouts (incl. the transposed operands below) and
+  // y_in, BKD, then two batched NN GEMM launches (done by the end of encoder layer 2; the transposes and
+  // the separate NT launches of the earlier chain left its last GEMM after layer 3, in front of the decoder)
   hipLaunchKernelGGL(dec_xcd_pack_ops, dim3(1024), dim3(256), 0, st, k, x);
   hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);  // BKD = Wd_c bc + bd
   S2S_CHECK_HIP(hipGetLastError());
-  // WDC = Wd_c Wc (S x A); WX = WXD WDC (3S x A); WXT = WX^T
-  S2S_TRY(gemm1(st, false, false, S, A, S, 1.f, k.P.Wd, 2L * S, k.P.Wc, A, 0.f, x.WDC, A, nullptr, gws));
-  S2S_TRY(gemm1(st, false, false, 3 * S, A, S, 1.f, x.WXD, S, x.WDC, A, 0.f, x.WX, A, nullptr, gws));
-  S2S_TRY(transpose_f32(st, x.WX, A, 3 * S, A, x.WXT, 3L * S));
-  // KD = y_in Wd_y^T + BKD; KX = KD WXD^T
-  S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
-  S2S_TRY(gemm1(st, false, true, rows, 3 * S, S, 1.f, x.KD, S, x.WXD, S, 0.f, x.KX, 3L * S, nullptr, gws));
+  // WDC = Wd_c Wc (S x A), WDCT = WDC^T = Wc^T Wd_c^T (A x S), KD = y_in Wd_y^T + BKD (B*T x S)
+  const GemmProblem pa[3] = {
+      GemmProblem{k.P.Wd, k.P.Wc, x.WDC, nullptr, 2L * S, A, A, S, A, S, 1.f, 0.f},
+      GemmProblem{x.PWCT, x.PWDCT, x.WDCT, nullptr, S, S, S, A, S, S, 1.f, 0.f},
+      GemmProblem{k.CY + S, x.PWDYT, x.KD, x.BKD, 2L * S, S, S, rows, S, S, 1.f, 0.f}};
+  S2S_TRY(gemm_f32(st, pa, 3, false, false, gws));
+  // WX = WXD WDC (3S x A), WXT = WX^T = WDC^T WXD^T (A x 3S), KX = KD WXD^T (B*T x 3S)
+  const GemmProblem pb[3] = {
+      GemmProblem{x.WXD, x.WDC, x.WX, nullptr, S, A, A, 3 * S, A, S, 1.f, 0.f},
+      GemmProblem{x.WDCT, x.PWXDT, x.WXT, nullptr, S, 3L * S, 3L * S, A, 3 * S, S, 1.f, 0.f},
+      GemmProblem{x.KD, x.PWXDT, x.KX, nullptr, S, 3L * S, 3L * S, rows, 3 * S, S, 1.f, 0.f}};
+  S2S_TRY(gemm_f32(st, pb, 3, false, false, gws));
   return 0;
 }
 
