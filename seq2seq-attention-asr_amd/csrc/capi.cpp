@@ -194,6 +194,7 @@ struct ModelWs {
   size_t scratch_bytes;
   float *dlogp, *nll, *logp, *dY0, *dY1;
   GemmWs gws_side;  // split-K slabs of the encoder weight-gradient GEMMs (may run on the side stream)
+  char* gsync[2];   // the persistent GRU launches' sync regions, alternating (gru_layer_preps_next)
   float* xpad;      // (B*L, Dp) zero-padded copy of the input when inputFrameSize % 32 != 0, else null
   int Dp;
   size_t total;
@@ -226,6 +227,12 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
   w.dY0 = bp.take<float>(B * L * 2 * hmax);
   w.dY1 = bp.take<float>(B * L * 2 * hmax);
   w.gws_side = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
+  {
+    size_t sb = 0;
+    for (auto& ld : enc_layers(d)) sb = std::max(sb, gru_persist_sync_bytes(d->B, d->L, ld.H));
+    w.gsync[0] = bp.take<char>(sb);
+    w.gsync[1] = bp.take<char>(sb);
+  }
   w.Dp = (d->inputFrameSize + 31) / 32 * 32;
   w.xpad = d->inputFrameSize % 32 != 0 ? bp.take<float>(B * L * w.Dp) : nullptr;
   w.total = bp.off + 256;
@@ -288,6 +295,7 @@ int wgrad_fork_mode() {
   }();
   return m;
 }
+int g_sync_handover = 1;  // s2s_debug_sync_handover(0) (diagnostic): a sync_prep in front of every GRU launch
 int g_fuse_dh = 1;  // s2s_debug_fuse_dh(0) (diagnostic): the decoder's dh by GEMMs in front of the top BPTT
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
 // seed_dev: the context's dropout seed word when a captured step reads its seed from the device (the
@@ -376,8 +384,27 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
     if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
   }
+  // the persistent GRU launches of the step (forward layers 1..nl, then backward nl..1) alternate between
+  // two sync regions; a launch with spare slots prepares the next launch's region itself, so only the
+  // first launch has a sync_prep in front of it
+  int glaunch = 0;
+  bool gprepared = false;
+  auto hand_over = [&](GruLayerIO& io, bool fwd, const GruLayerIO* next) {
+    if (!g_sync_handover) return;
+    io.sync = w.gsync[glaunch & 1];
+    io.sync_prepared = gprepared ? 1 : 0;
+    io.sync_next = next ? w.gsync[(glaunch + 1) & 1] : nullptr;
+    io.sync_next_prep = next ? gru_layer_sync_prep_bytes(*next) : 0;
+    gprepared = next != nullptr && gru_layer_preps_next(io, fwd);
+    ++glaunch;
+  };
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
-  for (int l = 0; l < nl; ++l) S2S_TRY(gru_layer_fwd(st, layer_io(l), w.scratch, w.scratch_bytes));
+  for (int l = 0; l < nl; ++l) {
+    GruLayerIO io = layer_io(l);
+    const GruLayerIO next = layer_io(l + 1 < nl ? l + 1 : nl - 1);
+    hand_over(io, true, &next);
+    S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
+  }
   // ---- attention decoder forward
   if (split && pmode == 0) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
@@ -419,7 +446,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   };
   for (int l = nl - 1; l >= 0; --l) {
     const int H = layers[l].H;
-    const GruLayerIO io = layer_io(l);
+    GruLayerIO io = layer_io(l);
+    const GruLayerIO next = layer_io(l > 0 ? l - 1 : 0);
+    hand_over(io, false, l > 0 ? &next : nullptr);
     GruLayerGrad gr{};
     for (int dd = 0; dd < 2; ++dd) {
       for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
@@ -1213,3 +1242,4 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
   return rc;
 }
 extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }
+extern "C" void s2s_debug_sync_handover(int on) { g_sync_handover = on; }

@@ -21,6 +21,14 @@ struct GruLayerIO {
   // recurrence is h_t = m_t GRU(h_{t-1}, x_t), m_t = 1[t < len_b]: outputs are 0 on the padding frames and
   // the reverse direction starts at each utterance's own last frame (RNN.lua:142-145 on the utterance alone)
   const int* len = nullptr;
+  // optional sync-region hand-over of the persistent launches (model step): use `sync` (>=
+  // gru_persist_sync_bytes) instead of the scratch's; sync_prepared = the launch before prepared it;
+  // sync_next / sync_next_prep: this launch prepares that region for the next one (when it can:
+  // gru_layer_preps_next)
+  void* sync = nullptr;
+  int sync_prepared = 0;
+  void* sync_next = nullptr;
+  size_t sync_next_prep = 0;
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]
@@ -60,6 +68,9 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
                        size_t scratch_bytes);
 int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, const float* dA, GemmWs ws);
 float* gru_layer_dA(const GruLayerIO& io, void* scratch);
+// the layer's persistent launch (forward or backward) would prepare io.sync_next for the next launch
+bool gru_layer_preps_next(const GruLayerIO& io, bool fwd);
+size_t gru_layer_sync_prep_bytes(const GruLayerIO& io);
 // gru_layer_bwd_core will produce gr's dy (ydA . yWx) inside its persistent BPTT launch
 bool gru_layer_dy_fused(const GruLayerIO& io, const GruLayerGrad& gr);
 // the x-weights (3 ndir H, Kx) rows of a packed layer (gru_layers_pack) and their row stride Kx

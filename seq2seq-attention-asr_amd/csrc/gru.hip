@@ -348,6 +348,7 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   float* Wx = bp.take<float>(3L * nd * H * ((D + 31) / 32 * 32));
   float* xp = bp.take<float>((long)B * L * 3 * nd * H);
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, L, H));
+  if (io.sync) sync = static_cast<char*>(io.sync);
   if (io.packed) {
     const PackView v = pack_view(io.packed, nd, H);
     for (int d = 0; d < nd; ++d) {
@@ -385,6 +386,11 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
       f.xp[d] = xp + 3L * d * H; f.Uzr[d] = Uzr[d]; f.Uh[d] = Uh[d]; f.y[d] = io.y[d]; f.sv[d] = io.saved[d];
       f.reverse[d] = io.reverse[d];
     }
+    f.prepared = io.sync ? io.sync_prepared : 0;
+    if (io.sync_next && gru_layer_preps_next(io, true)) {
+      f.next_sync = io.sync_next;
+      f.next_prep = io.sync_next_prep;
+    }
     return gru_persist_fwd(st, f, sync);
   }
   const dim3 g1(2 * H / 16, (B + 15) / 16, nd), g2(H / 16, (B + 15) / 16, nd);
@@ -420,6 +426,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   float* dA_int = bp.take<float>((long)B * L * 3 * nd * H);
   float* dA = dA_ext ? dA_ext : dA_int;
   char* sync = bp.take<char>(gru_persist_sync_bytes(B, L, H));
+  if (io.sync) sync = static_cast<char*>(io.sync);
   const long ldA = 3L * nd * H;
   if (io.packed) {
     const PackView v = pack_view(io.packed, nd, H);
@@ -463,6 +470,11 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
       f.reverse[d] = io.reverse[d];
     }
     f.prep_event = gr.prep_event;
+    f.prepared = io.sync ? io.sync_prepared : 0;
+    if (io.sync_next && gru_layer_preps_next(io, false)) {
+      f.next_sync = io.sync_next;
+      f.next_prep = io.sync_next_prep;
+    }
     S2S_TRY(gru_persist_bwd(st, f, sync));
   } else {
     ProfScope ps(st, "gru_bwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);
@@ -485,6 +497,11 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   }
   return 0;
 }
+
+bool gru_layer_preps_next(const GruLayerIO& io, bool fwd) {
+  return use_persistent(io.ndir, io.B, io.H) && gru_persist_can_prep_next(io.ndir, io.B, io.H, fwd);
+}
+size_t gru_layer_sync_prep_bytes(const GruLayerIO& io) { return gru_persist_prep_bytes(io.B, io.L, io.H); }
 
 bool gru_layer_dy_fused(const GruLayerIO& io, const GruLayerGrad& gr) {
   const int nd = io.ndir, B = io.B, H = io.H;

@@ -21,6 +21,12 @@ struct GruPersistFwd {
   float* sv[2];
   int reverse[2];
   const int* len = nullptr;  // (B) frames per utterance (null: all L)
+  // sync-region hand-over between consecutive persistent launches: prepared = the region was prepared by
+  // the launch before (no sync_prep in front of this one); next_sync / next_prep: this launch's spare slots
+  // prepare that region for the next launch (gru_persist_can_prep_next)
+  int prepared = 0;
+  void* next_sync = nullptr;
+  size_t next_prep = 0;
 };
 struct GruPersistBwd {
   int ndir, B, L, H;
@@ -45,6 +51,9 @@ struct GruPersistBwd {
   const float* yalpha = nullptr;
   const float* ydc = nullptr;
   int yT = 0;
+  int prepared = 0;  // as GruPersistFwd
+  void* next_sync = nullptr;
+  size_t next_prep = 0;
 };
 
 bool gru_persist_supported(int ndir, int B, int H);
@@ -55,6 +64,8 @@ bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx);
 // GEMMs run on a side stream
 void gru_persist_set_exclusive(int on);
 size_t gru_persist_sync_bytes(int B, int L, int H);
+size_t gru_persist_prep_bytes(int B, int L, int H);  // the part sync_prep (or a preparing launch) zeroes
+bool gru_persist_can_prep_next(int ndir, int B, int H, bool fwd);
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync);
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync);
 

@@ -125,6 +125,10 @@ struct PArgs {
   unsigned* abort_word;
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
+  // the next persistent GRU launch's sync region (other than this one's), prepared by this launch's spare
+  // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0)
+  char* next_sync;
+  size_t next_prep;
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
 };
@@ -429,6 +433,26 @@ __device__ __forceinline__ void xproj_wait(const XProj& q, int d, int need, int&
   }
 }
 
+// spare slot sp of nsp: its share of preparing the next launch's sync region (sync_prep's work; the region
+// is not in use -- the launch before this one used it -- and the writes are visible when this launch ends)
+__device__ __forceinline__ void prep_next_sync(const PArgs& a, int sp, int nsp) {
+  if (!a.next_sync) return;
+  if (sp == 0 && threadIdx.x == 0) {
+    unsigned* hdr = reinterpret_cast<unsigned*>(a.next_sync);
+    const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const size_t n16 = (a.next_prep - 256) / 16;
+  uint4* p = reinterpret_cast<uint4*>(a.next_sync + 256);
+  for (size_t i = (size_t)sp * blockDim.x + threadIdx.x; i < n16; i += (size_t)nsp * blockDim.x)
+    p[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (threadIdx.x == 0 && sp == 0 && (a.next_prep - 256) % 16) {  // a last partial 16-byte piece
+    unsigned* t = reinterpret_cast<unsigned*>(a.next_sync + 256 + n16 * 16);
+    for (size_t i = 0; i < ((a.next_prep - 256) % 16) / 4; ++i) t[i] = 0u;
+  }
+}
+
 // ------------------------------------------------------------------------------ forward
 // chain (dir, mt) has nmem = 2H/16 members c1 (chain_slot placement, handoff.h); z-column
 // workgroups (c1 < H/16) also own the candidate tile of the same units.
@@ -450,10 +474,10 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: x-projection producer (or idle)
-    if (a.fused) {
-      const int gch = 8 * ((a.nchains + 7) / 8);
-      xproj_produce_any<false>(a, xlds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
-    }
+    const int gch = 8 * ((a.nchains + 7) / 8);
+    const int sp = (cs.chain - a.nchains) * a.nmem + cs.member, nsp = (gch - a.nchains) * a.nmem;
+    prep_next_sync(a, sp, nsp);
+    if (a.fused) xproj_produce_any<false>(a, xlds, sp, nsp);
     return;
   }
   const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
@@ -639,10 +663,10 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: dy producer (or idle)
-    if (a.fused) {
-      const int gch = 8 * ((a.nchains + 7) / 8);
-      xproj_produce_any<true>(a, ylds, (cs.chain - a.nchains) * a.nmem + cs.member, (gch - a.nchains) * a.nmem);
-    }
+    const int gch = 8 * ((a.nchains + 7) / 8);
+    const int sp = (cs.chain - a.nchains) * a.nmem + cs.member, nsp = (gch - a.nchains) * a.nmem;
+    prep_next_sync(a, sp, nsp);
+    if (a.fused) xproj_produce_any<true>(a, ylds, sp, nsp);
     return;
   }
   const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
@@ -906,6 +930,11 @@ static size_t slab_offset(int B, int L, int H) { return sent_offset(B, L, H) + 2
 constexpr size_t kXpSlabBytes = (size_t)kXpMaxSplitItems * 4 * 4096 * sizeof(float);  // PA <= 4
 
 size_t gru_persist_sync_bytes(int B, int L, int H) { return slab_offset(B, L, H) + kXpSlabBytes; }
+size_t gru_persist_prep_bytes(int B, int L, int H) { return prep_bytes(B, L, H); }
+bool gru_persist_can_prep_next(int ndir, int B, int H, bool fwd) {
+  const int MT = (B + 15) / 16, nchains = ndir * MT, nmem = fwd ? 2 * H / 16 : H / 16;
+  return chain_grid(nchains, nmem) > nchains * nmem;  // spare slots exist
+}
 
 // split-K start of a fused producer grid (XProj::sA ..): the first round of units is the first slices cut
 // into 4 K-parts, the second the next slices into 2, so the recurrence's first slices come after a quarter
@@ -969,7 +998,11 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     q.sA = q.sB = 0; q.PA = q.PB = 1;
     a.fused = 1;
   }
-  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
+  if (f.next_sync) {
+    a.next_sync = static_cast<char*>(f.next_sync);
+    a.next_prep = f.next_prep;
+  }
+  if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
   return launch(st, a, f.ndir, true);
@@ -1007,7 +1040,11 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     xproj_split(q, b.ndir, (gch - a.nchains) * a.nmem);
     a.fused = 1;
   }
-  S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
+  if (b.next_sync) {
+    a.next_sync = static_cast<char*>(b.next_sync);
+    a.next_prep = b.next_prep;
+  }
+  if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
   // the recurrence's algorithmic work only (a fused dy's GEMM runs on the spare slots beside it)
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
