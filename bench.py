@@ -522,6 +522,11 @@ def main():
             r["traffic_detail"] = detail
             r["mfma_counters"] = mfma_of(pmc, r["kernel"], r["avg_launch_us"])
             r["latency_floor"] = latency_floor(r["kernel"], L, r["avg_launch_us"])
+            if r["kernel"].startswith("gru_"):
+                r["work"] = ("the launch's algorithmic flops: the recurrence (2 B L 3H^2 per direction) plus the "
+                             "GEMM its spare-slot producers compute inside the launch (forward: the x-projection; "
+                             "backward: dy = the layer above's dX, or for the top layer the decoder's dh = "
+                             "dVh V + sum_t alpha dc), averaged over the step's launches")
         # the decoder recurrences (the attention path): priced against HBM (the attention
         # re-streams Vh and h every step) and against their own hand-off latency floor
         out["roofline_decoder"] = []

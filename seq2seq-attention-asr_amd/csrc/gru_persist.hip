@@ -1003,7 +1003,9 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     a.next_prep = f.next_prep;
   }
   if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
-  ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H,
+  // algorithmic work of the launch: the recurrence, plus the x-projection GEMM when its spare slots compute it
+  const double xflops = f.x ? 2.0 * f.B * f.L * 3.0 * f.ndir * f.H * f.Kx : 0.0;
+  ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H + xflops,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
   return launch(st, a, f.ndir, true);
 }
@@ -1046,8 +1048,10 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   }
   if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
-  // the recurrence's algorithmic work only (a fused dy's GEMM runs on the spare slots beside it)
-  ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H,
+  // algorithmic work of the launch: the recurrence, plus the dy its spare slots compute (the layer above's
+  // dX GEMM, or the decoder's dh: dVh V and the context term sum_t alpha dc)
+  const double yflops = b.ydA ? 2.0 * b.B * b.L * (double)b.ndir * b.H * (b.yK + b.yT) : 0.0;
+  ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
   return launch(st, a, b.ndir, false);
 }
