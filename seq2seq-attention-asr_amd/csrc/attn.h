@@ -38,6 +38,9 @@ struct AttnDims {
   // dlogp is 0 there, the reference never runs them)
   const int* flen = nullptr;
   const int* tlen = nullptr;
+  // the XCD-local decoder's sync regions were prepared by attn_fwd_prologue (the model step runs it, and
+  // joins it, before the decoder): attn_fwd / attn_bwd_core then launch no sync_prep of their own
+  int syncs_in_prologue = 0;
 };
 int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)

@@ -1262,7 +1262,12 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
   carve(d, &k, (char*)saved, (char*)scratch, &x);
   k.P = P;
   k.labels = labels;
-  return dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch));
+  S2S_TRY(dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch)));
+  if (d.syncs_in_prologue) {  // both decoder launches' sync regions, off the decoder's critical path
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
+  }
+  return 0;
 }
 
 int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* labels, const AttnParams& P, float* logp,
@@ -1301,7 +1306,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
     }
     hipLaunchKernelGGL(dec_xcd_vbar, dim3((d.Sc + 63) / 64, B), dim3(256), 0, side ? side : st, k, x);
-    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
+    if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
       // per forward; flops = the step products + the attention contractions
@@ -1443,7 +1448,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
+    if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
       ProfScope ps(st, "dec_bwd_xcd", dec_flops(d, true), 8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));

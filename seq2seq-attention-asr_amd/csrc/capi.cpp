@@ -295,6 +295,7 @@ int wgrad_fork_mode() {
   }();
   return m;
 }
+int g_dec_sync_prologue = 1;  // s2s_debug_dec_sync_prologue(0) (diagnostic): decoder sync preps in place
 int g_sync_handover = 1;  // s2s_debug_sync_handover(0) (diagnostic): a sync_prep in front of every GRU launch
 int g_fuse_dh = 1;  // s2s_debug_fuse_dh(0) (diagnostic): the decoder's dh by GEMMs in front of the top BPTT
 int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
@@ -326,6 +327,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
   ad.dropout_seed_dev = seed_dev;
+  ad.syncs_in_prologue = g_dec_sync_prologue;  // attn_fwd_prologue runs (and is joined) before the decoder
   AttnParams ap;
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
@@ -1243,3 +1245,4 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
 }
 extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }
 extern "C" void s2s_debug_sync_handover(int on) { g_sync_handover = on; }
+extern "C" void s2s_debug_dec_sync_prologue(int on) { g_dec_sync_prologue = on; }
