@@ -376,16 +376,18 @@ def test_labelmask_input_equals_int_labels(s2s):
 
 # --------------------------------------------------------------------------- whole training step
 
-def _model_case(s2s, cfg_kw, B, L, T, seed=1234, graph=False):
+def _model_case(s2s, cfg_kw, B, L, T, seed=1234, graph=False, overlap=False):
     cfg_o = orc.ModelConfig(**cfg_kw)
-    model = s2s.ChorowskiBaseline(s2s.ModelConfig(**cfg_kw), graph=graph)
+    model = s2s.ChorowskiBaseline(s2s.ModelConfig(**cfg_kw), graph=graph, overlap=overlap)
     P = orc.unflatten(model.params.cpu().double().numpy(), cfg_o)
     x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=seed, pad=min(10, L // 4), eos=min(23, cfg_o.outputDepth - 1))
     return cfg_o, model, P, x, labels
 
 
-def _check_step(model, cfg_o, P, x, labels, stream=None):
-    nll, logp = model.step(cu(x), cu(labels, torch.int32), stream=stream)
+def _check_step(model, cfg_o, P, x, labels, stream=None, nll=None, logp=None):
+    """One step (or the given step outputs nll / logp) against the float64 oracle."""
+    if logp is None:
+        nll, logp = model.step(cu(x), cu(labels, torch.int32), stream=stream)
     torch.cuda.synchronize()
     nll_ref, G, lref, enc = orc.training_step(x, labels, P, cfg_o)
     assert_rel(logp.cpu().numpy(), lref, "logp")
@@ -422,6 +424,22 @@ def test_model_step_chorowski_config2(s2s):
     """BASELINE config 2 at full size: B=32, L=128, T=40, F=123, 3x BiGRU(256), Sc=512, O=62."""
     cfg_o, model, P, x, labels = _model_case(s2s, {}, 32, 128, 40)
     _check_step(model, cfg_o, P, x, labels)
+
+
+def test_model_step_config2_dims_b45_graph(s2s):
+    """Config-2 model at B=45 under graph replay with the side stream, as the bench runs it: three 16-row
+    tiles (the last ragged), 6 of the 8 chain slots used, so the persistent launches' spare slots are 2
+    chains wide -- one-step x-projection / dy / dh slices with 45 of 64 producer rows valid, the split-K
+    start with 32 producers, the sync-region hand-over -- against the float64 oracle."""
+    cfg_o, model, P, x, labels = _model_case(s2s, {}, 45, 64, 20, seed=5, graph=True, overlap=True)
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    xs, ls = cu(x), cu(labels, torch.int32)
+    with torch.cuda.stream(st):
+        for _ in range(2):  # capture, then a replay
+            nll, logp = model.step(xs, ls, stream=st)
+    st.synchronize()
+    _check_step(model, cfg_o, P, x, labels, nll=nll, logp=logp)
 
 
 def test_model_step_librispeech_shape(s2s):
