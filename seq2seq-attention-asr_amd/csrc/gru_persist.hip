@@ -68,9 +68,9 @@ struct XProj {
   const float* x;
   long ldx;
   int K;            // padded input width (% 32 == 0): x and W hold K readable columns
-  const float* W;   // nn = 0: (nd*ncd, ldw) x-weights, direction d's rows [ncd d, ncd (d+1)); nn = 1: (K, ldw)
+  const float* W;   // NT (forward): (nd*ncd, ldw) x-weights, direction d's rows [ncd d, ncd (d+1)); NN: (K, ldw)
   long ldw;
-  int nn, ncd, flip;
+  int ncd, flip;  // (the W layout is the producer's NN template argument: forward NT, backward NN)
   float* xp;
   long ldxp;
   int tpt;          // steps per slice (64 / B)
@@ -987,7 +987,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.pstamps = g_gru_pstamps[0];
   if (f.x) {  // fused x-projection by the grid's spare slots
     XProj& q = a.xq;
-    q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.ldw = f.Kx; q.nn = 0; q.ncd = 3 * f.H; q.flip = 0;
+    q.x = f.x; q.ldx = f.ldx; q.K = f.Kx; q.W = f.Wx; q.ldw = f.Kx; q.ncd = 3 * f.H; q.flip = 0;
     q.xp = const_cast<float*>(f.xp[0]); q.ldxp = f.ldxp;
     q.tpt = 64 / f.B;
     q.nslices = (f.L + q.tpt - 1) / q.tpt;
@@ -1027,7 +1027,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.pstamps = g_gru_pstamps[1];
   if (b.ydA) {  // fused dy (the layer above's dX) by the grid's spare slots
     XProj& q = a.xq;
-    q.x = b.ydA; q.ldx = b.yldA; q.K = b.yK; q.W = b.yWx; q.ldw = b.yldw; q.nn = 1; q.ncd = b.H; q.flip = 1;
+    q.x = b.ydA; q.ldx = b.yldA; q.K = b.yK; q.W = b.yWx; q.ldw = b.yldw; q.ncd = b.H; q.flip = 1;
     q.xp = const_cast<float*>(b.dy[0]); q.ldxp = b.lddy;
     q.tpt = 64 / b.B;
     q.nslices = (b.L + q.tpt - 1) / q.tpt;
