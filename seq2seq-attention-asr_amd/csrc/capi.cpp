@@ -295,6 +295,7 @@ int wgrad_fork_mode() {
   }();
   return m;
 }
+int g_defer_pack = 1;  // s2s_debug_defer_pack(0) (diagnostic): every layer packed in front of layer 1
 int g_dec_sync_prologue = 1;  // s2s_debug_dec_sync_prologue(0) (diagnostic): decoder sync preps in place
 int g_sync_handover = 1;  // s2s_debug_sync_handover(0) (diagnostic): a sync_prep in front of every GRU launch
 int g_fuse_dh = 1;  // s2s_debug_fuse_dh(0) (diagnostic): the decoder's dh by GEMMs in front of the top BPTT
@@ -369,10 +370,15 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // and labels: layer 1 on the critical path, the rest beside layer 1's recurrence when split
   // weight packing for every layer and both passes: one launch on the critical path (~10 us); the
   // decoder's parameter folds (params and labels only) beside the encoder when split
+  // (when layer 1's persistent forward has spare slots, only what it reads is packed here; its spare slots
+  // pack the rest -- the backward transposes and the later layers -- while it runs)
+  GruPackJobs deferred{};
+  bool defer_pack = false;
   {
     std::vector<GruLayerIO> ios;
     for (int l = 0; l < nl; ++l) ios.push_back(layer_io(l));
-    S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl));
+    defer_pack = g_defer_pack && 2 * nl <= kMaxPackJobs && gru_layer_preps_next(ios[0], true);
+    S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
   }
   // decoder parameter folds + dlogp = -labelmask (params and labels only). Mode 0: on the side
   // stream, joined before the decoder (the persistent GRU launches hold every CU, so it runs in the
@@ -405,6 +411,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     GruLayerIO io = layer_io(l);
     const GruLayerIO next = layer_io(l + 1 < nl ? l + 1 : nl - 1);
     hand_over(io, true, &next);
+    if (l == 0 && defer_pack) io.pack_jobs = &deferred;
     S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
   }
   // ---- attention decoder forward
@@ -1246,3 +1253,4 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
 extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }
 extern "C" void s2s_debug_sync_handover(int on) { g_sync_handover = on; }
 extern "C" void s2s_debug_dec_sync_prologue(int on) { g_dec_sync_prologue = on; }
+extern "C" void s2s_debug_defer_pack(int on) { g_defer_pack = on; }

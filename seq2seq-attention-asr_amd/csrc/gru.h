@@ -3,6 +3,8 @@
 
 namespace s2s {
 
+struct GruPackJobs;  // gru_persist.h
+
 // One GRU layer, 1 or 2 directions sharing the same input x (the bidirectional
 // encoder layer of timit/model_chorowski_baseline.lua:22-32 runs both in each launch).
 struct GruLayerIO {
@@ -29,6 +31,8 @@ struct GruLayerIO {
   int sync_prepared = 0;
   void* sync_next = nullptr;
   size_t sync_next_prep = 0;
+  // forward only: weight packing (gru_layers_pack's deferred jobs) done by this launch's spare slots
+  const GruPackJobs* pack_jobs = nullptr;
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]
@@ -59,7 +63,10 @@ size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
 // x-projection rows), packed once per step so the forward and backward launches skip it.
 size_t gru_layer_pack_bytes(int ndir, int D, int H);
 int gru_layer_pack(hipStream_t st, const GruLayerIO& io, float* packed);
-int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers);  // one launch
+// one launch; defer (optional): pack only layer 1's forward layouts now and append the rest (layer 1's
+// backward transposes, every later layer) to *defer for layer 1's persistent forward (GruLayerIO::pack_jobs)
+int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers,
+                    GruPackJobs* defer = nullptr);
 int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes);
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes);
 // split form used by the model step: core = weight packing + BPTT + dx (critical path), writing the

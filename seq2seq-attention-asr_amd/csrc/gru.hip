@@ -180,37 +180,10 @@ __global__ __launch_bounds__(256) void gru_bwd_p2(GruBwdArgs a) {
   gru_gate_grads(g, B, L, H, b, tn, k, dhprev, a.len);
 }
 
-// Pack W{z,r,h} (H, H+D) into kernel layouts.
-//   Uzr (2H,H), Uh (H,H), UhT (H,H), UzrT (H,2H), Wx rows [z;r;h] (3H, D) at Wx + xrow0*D
-struct PackArgs {
-  const float* W[3];
-  float *Uzr, *Uh, *UhT, *UzrT, *Wx;
-  int H, D, Kx;  // Wx rows have stride Kx >= D, columns [D, Kx) zero
-};
+// Pack W{z,r,h} (H, H+D) into kernel layouts (gru_pack_elems).
+using PackArgs = GruPackJob;
 __device__ __forceinline__ void pack_body(const PackArgs& p) {
-  const int H = p.H, D = p.D, HD = H + D, Kx = p.Kx;
-  const long nU = 3L * H * H, nX = 3L * H * Kx;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nU + nX; i += (long)gridDim.x * blockDim.x) {
-    if (i < nU) {
-      const int g = (int)(i / ((long)H * H));
-      const int rem = (int)(i - (long)g * H * H);
-      const int n = rem / H, k = rem - n * H;
-      const float w = p.W[g][(long)n * HD + k];
-      if (g < 2) {
-        if (p.Uzr) p.Uzr[(long)(g * H + n) * H + k] = w;
-        if (p.UzrT) p.UzrT[(long)k * 2 * H + g * H + n] = w;
-      } else {
-        if (p.Uh) p.Uh[(long)n * H + k] = w;
-        if (p.UhT) p.UhT[(long)k * H + n] = w;
-      }
-    } else if (p.Wx) {
-      const long j = i - nU;
-      const int g = (int)(j / ((long)H * Kx));
-      const long rem = j - (long)g * H * Kx;
-      const int n = (int)(rem / Kx), c = (int)(rem - (long)n * Kx);
-      p.Wx[(long)(g * H + n) * Kx + c] = c < D ? p.W[g][(long)n * HD + H + c] : 0.f;
-    }
-  }
+  gru_pack_elems(p, blockIdx.x * (long)blockDim.x + threadIdx.x, (long)gridDim.x * blockDim.x);
 }
 __global__ void gru_pack(PackArgs p) { pack_body(p); }
 // several layer-directions in one launch (blockIdx.y = which)
@@ -277,7 +250,7 @@ static PackView pack_view(const float* pk, int nd, int H) {
   v.Wx = pk;
   return v;
 }
-int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers) {
+int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer) {
   PackBatch b{};
   int n = 0;
   long most = 0;
@@ -298,10 +271,20 @@ int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed,
     S2S_REQUIRE(Kx <= (D + 31) / 32 * 32, "gru: Dx must be <= round_up(D, 32)");
     const PackView v = pack_view(packed[l], nd, H);
     for (int d = 0; d < nd; ++d) {
+      PackArgs job{{io.W[d][0], io.W[d][1], io.W[d][2]}, const_cast<float*>(v.Uzr[d]),
+                   const_cast<float*>(v.Uh[d]), const_cast<float*>(v.UhT[d]), const_cast<float*>(v.UzrT[d]),
+                   const_cast<float*>(v.Wx) + 3L * d * H * Kx, H, D, Kx};
+      if (defer) {  // now: only what layer 1's forward reads; the rest goes to that launch's spare slots
+        PackArgs later = job;
+        later.Uzr = later.Uh = later.Wx = nullptr;
+        if (l > 0) later = job;
+        else job.UhT = job.UzrT = nullptr;
+        S2S_REQUIRE(defer->n < kMaxPackJobs, "gru: too many deferred pack jobs");
+        defer->j[defer->n++] = later;
+        if (l > 0) continue;
+      }
       if (n == kMaxPack) S2S_TRY(flush());
-      b.p[n++] = PackArgs{{io.W[d][0], io.W[d][1], io.W[d][2]}, const_cast<float*>(v.Uzr[d]),
-                          const_cast<float*>(v.Uh[d]), const_cast<float*>(v.UhT[d]), const_cast<float*>(v.UzrT[d]),
-                          const_cast<float*>(v.Wx) + 3L * d * H * Kx, H, D, Kx};
+      b.p[n++] = job;
       most = std::max(most, 3L * H * (H + Kx));
     }
   }
@@ -375,6 +358,8 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
   a.L = L;
   a.H = H;
   a.len = io.len;
+  S2S_REQUIRE(!io.pack_jobs || gru_layer_preps_next(io, true),
+              "gru: deferred weight packing needs a persistent forward with spare slots");
   if (use_persistent(nd, B, H)) {
     GruPersistFwd f{};
     f.len = io.len;
@@ -391,6 +376,7 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
       f.next_sync = io.sync_next;
       f.next_prep = io.sync_next_prep;
     }
+    f.pack = io.pack_jobs;
     return gru_persist_fwd(st, f, sync);
   }
   const dim3 g1(2 * H / 16, (B + 15) / 16, nd), g2(H / 16, (B + 15) / 16, nd);

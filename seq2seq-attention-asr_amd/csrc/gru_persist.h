@@ -3,6 +3,45 @@
 
 namespace s2s {
 
+// Packing one layer-direction's W{z,r,h} (H, H+D) into the kernel layouts (gru_layers_pack): Uzr (2H,H),
+// Uh (H,H), UhT (H,H), UzrT (H,2H), Wx rows [z;r;h] (3H, Kx; columns [D, Kx) zero); a null target is skipped
+struct GruPackJob {
+  const float* W[3];
+  float *Uzr, *Uh, *UhT, *UzrT, *Wx;
+  int H, D, Kx;
+};
+constexpr int kMaxPackJobs = 8;
+struct GruPackJobs {
+  GruPackJob j[kMaxPackJobs];
+  int n;
+};
+// element range [i0, ...) with stride of one job (the gru_pack kernels and the persistent forward's spare slots)
+__device__ __forceinline__ void gru_pack_elems(const GruPackJob& p, long i0, long stride) {
+  const int H = p.H, D = p.D, HD = H + D, Kx = p.Kx;
+  const long nU = 3L * H * H, nX = p.Wx ? 3L * H * Kx : 0;
+  for (long i = i0; i < nU + nX; i += stride) {
+    if (i < nU) {
+      const int g = (int)(i / ((long)H * H));
+      const int rem = (int)(i - (long)g * H * H);
+      const int n = rem / H, k = rem - n * H;
+      const float w = p.W[g][(long)n * HD + k];
+      if (g < 2) {
+        if (p.Uzr) p.Uzr[(long)(g * H + n) * H + k] = w;
+        if (p.UzrT) p.UzrT[(long)k * 2 * H + g * H + n] = w;
+      } else {
+        if (p.Uh) p.Uh[(long)n * H + k] = w;
+        if (p.UhT) p.UhT[(long)k * H + n] = w;
+      }
+    } else {
+      const long j = i - nU;
+      const int g = (int)(j / ((long)H * Kx));
+      const long rem = j - (long)g * H * Kx;
+      const int n = (int)(rem / Kx), c = (int)(rem - (long)n * Kx);
+      p.Wx[(long)(g * H + n) * Kx + c] = c < D ? p.W[g][(long)n * HD + H + c] : 0.f;
+    }
+  }
+}
+
 struct GruPersistFwd {
   int ndir, B, L, H;
   // fused x-projection (gru_persist_fused_xproj): x (B*L, ldx) with Kx readable columns and the
@@ -27,6 +66,8 @@ struct GruPersistFwd {
   int prepared = 0;
   void* next_sync = nullptr;
   size_t next_prep = 0;
+  // weight packing deferred to this launch's spare slots (the layouts later launches read), or null
+  const GruPackJobs* pack = nullptr;
 };
 struct GruPersistBwd {
   int ndir, B, L, H;

@@ -129,6 +129,7 @@ struct PArgs {
   // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0)
   char* next_sync;
   size_t next_prep;
+  GruPackJobs pack;  // weight packing for later launches, done by the forward's spare slots (pack.n = 0: none)
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
 };
@@ -478,6 +479,8 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     const int sp = (cs.chain - a.nchains) * a.nmem + cs.member, nsp = (gch - a.nchains) * a.nmem;
     prep_next_sync(a, sp, nsp);
     if (a.fused) xproj_produce_any<false>(a, xlds, sp, nsp);
+    for (int j = 0; j < a.pack.n; ++j)  // after the x-projections: the chains wait for those, not for this
+      gru_pack_elems(a.pack.j[j], (long)sp * blockDim.x + threadIdx.x, (long)nsp * blockDim.x);
     return;
   }
   const int dir = cs.chain / a.MT, mt = cs.chain % a.MT;
@@ -1002,6 +1005,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     a.next_sync = static_cast<char*>(f.next_sync);
     a.next_prep = f.next_prep;
   }
+  if (f.pack) a.pack = *f.pack;
   if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
   // algorithmic work of the launch: the recurrence, plus the x-projection GEMM when its spare slots compute it
   const double xflops = f.x ? 2.0 * f.B * f.L * 3.0 * f.ndir * f.H * f.Kx : 0.0;
