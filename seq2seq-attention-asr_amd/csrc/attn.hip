@@ -1287,8 +1287,9 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   // Vh = h V^T  (TemporalConvolutionZeroBias(A, Sc, 1), Attention.lua:44)
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
-  hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   const XPlan xp = dec_xcd_plan(d);
+  // s_0 = 0: the XCD-local path's prologue (dec_xcd_pack_ops) writes it
+  if (!xp.var) hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   const int pgrid = kDecWG * ((B + 15) / 16);
   const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pf = pvar ? pick_dec_fwd(pvar, d, pgrid) : PersistLaunch{};
@@ -1299,13 +1300,6 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    // VBAR (the backward's dws reference point) needs only Vh: beside the decoder loop when a side
-    // stream is given (joined by attn_bwd_core through ev[2])
-    if (side) {
-      S2S_CHECK_HIP(hipEventRecord(ev[0], st));
-      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
-    }
-    hipLaunchKernelGGL(dec_xcd_vbar, dim3((d.Sc + 63) / 64, B), dim3(256), 0, side ? side : st, k, x);
     if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
       // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
@@ -1313,13 +1307,14 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       ProfScope ps(st, "dec_fwd_xcd", dec_flops(d, false), 4.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
       S2S_TRY(launch_xcd(xp, true, st, k, x));
     }
-    // alpha / MonotonicAlignment indicators from the saved scores: only the backward (and alpha())
-    // read them, so beside the MLP head when split
+    // alpha / MonotonicAlignment indicators from the saved scores and VBAR (the backward's dws reference
+    // point) from Vh, in one launch: only the backward (and alpha()) read them, so beside the MLP head
+    // when split (joined by attn_bwd_core through ev[2])
     if (side) {
       S2S_CHECK_HIP(hipEventRecord(ev[1], st));
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1], 0));
     }
-    hipLaunchKernelGGL(dec_alpha_ind, dim3(T, B), dim3(256), 0, side ? side : st, k);
+    hipLaunchKernelGGL(dec_xcd_alpha_vbar, dim3(T * B + ((d.Sc + 63) / 64) * B), dim3(256), 0, side ? side : st, k, x);
     if (side) S2S_CHECK_HIP(hipEventRecord(ev[2], side));
     S2S_CHECK_HIP(hipGetLastError());
   } else if (pf.fn) {
