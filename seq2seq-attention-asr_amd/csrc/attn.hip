@@ -637,10 +637,10 @@ __global__ void dec_init_fwd(AttnK k) {
 }
 
 // MLP head (per row b*T+t, one wave each): maxout (first max wins), Linear(M,O), LogSoftMax.
-__global__ __launch_bounds__(256) void dec_mlp_head(AttnK k, int rows) {
+__device__ __forceinline__ void mlp_head_body(const AttnK& k, int rows, int blk) {
   extern __shared__ float sm[];  // 4 * M
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int r = blockIdx.x * 4 + wave;
+  const int r = blk * 4 + wave;
   const int M = k.M, Kw = k.K, O = k.O;
   float* mv = sm + wave * M;
   if (r < rows) {
@@ -678,6 +678,7 @@ __global__ __launch_bounds__(256) void dec_mlp_head(AttnK k, int rows) {
     if (k.logp) k.logp[(long)r * O + n] = v;
   }
 }
+__global__ __launch_bounds__(256) void dec_mlp_head(AttnK k, int rows) { mlp_head_body(k, rows, blockIdx.x); }
 
 // ------------------------------------------------------------------ backward kernels
 
@@ -1208,6 +1209,7 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
 }
 
 static int g_dec_allow_local = 1;
+static int g_merge_alpha_head = 1;  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
 
 template <int S, int A, int SC>
 static int launch_xcd_t(bool fwd, int res, hipStream_t st, AttnK& k, XArgs& x) {
@@ -1288,6 +1290,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
   const XPlan xp = dec_xcd_plan(d);
+  const bool merge_head = xp.var && !side && !d.ext && g_merge_alpha_head;  // dec_xcd_alpha_vbar_head
   // s_0 = 0: the XCD-local path's prologue (dec_xcd_pack_ops) writes it
   if (!xp.var) hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   const int pgrid = kDecWG * ((B + 15) / 16);
@@ -1314,9 +1317,14 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       S2S_CHECK_HIP(hipEventRecord(ev[1], st));
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1], 0));
     }
-    hipLaunchKernelGGL(dec_xcd_alpha_vbar, dim3(T * B + ((d.Sc + 63) / 64) * B), dim3(256), 0, side ? side : st, k, x);
-    if (side) S2S_CHECK_HIP(hipEventRecord(ev[2], side));
-    S2S_CHECK_HIP(hipGetLastError());
+    // (on the main stream, the MLP head's launch below runs them: one launch fewer between the decoder and
+    // its backward)
+    if (!merge_head) {
+      hipLaunchKernelGGL(dec_xcd_alpha_vbar, dim3(T * B + ((d.Sc + 63) / 64) * B), dim3(256), 0, side ? side : st, k,
+                         x);
+      if (side) S2S_CHECK_HIP(hipEventRecord(ev[2], side));
+      S2S_CHECK_HIP(hipGetLastError());
+    }
   } else if (pf.fn) {
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
     {
@@ -1356,7 +1364,11 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   }
   S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
                 (long)d.M * d.K, P.bm, gws));
-  hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
+  if (merge_head)
+    hipLaunchKernelGGL(dec_xcd_alpha_vbar_head, dim3(T * B + ((d.Sc + 63) / 64) * B + (rows + 3) / 4), dim3(256),
+                       4 * d.M * sizeof(float), st, k, x, rows);
+  else
+    hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }
@@ -2035,6 +2047,7 @@ int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* 
 // dec_xcd.inc (tools/xdec_stamps.py, tools/xdec_substamps.py); nullptr turns it off.
 // diagnostic: 0 forces write-through (sc1) hand-offs in every XCD-local decoder chain
 extern "C" void s2s_debug_dec_local(int allow) { s2s::g_dec_allow_local = allow; }
+extern "C" void s2s_debug_merge_alpha_head(int on) { s2s::g_merge_alpha_head = on; }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);
