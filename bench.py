@@ -459,6 +459,8 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         elapsed = time.perf_counter() - t0
+    # a persistent launch that timed out would have produced invalid gradients: fail instead of reporting
+    model.ctx.check_status(stream)
     if world > 1:
         t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

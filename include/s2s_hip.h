@@ -18,6 +18,10 @@
  *   - gradients ACCUMULATE (dW += scale * ...), as Torch's accGradParameters; zero them
  *     yourself (zeroGradParameters) or pass S2S_ZERO_GRADS to the model step;
  *   - calls return 0 on success, nonzero on error, never abort; s2s_last_error() has the text;
+ *   - the persistent (whole-sequence) launches hand data between workgroups with bounded waits: a wait
+ *     that times out makes the launch give up and sets the context's failure status (host-visible, no
+ *     device sync needed); every later compute call of that context then returns nonzero until
+ *     s2s_ctx_status(..., clear = 1) has reported it (RNN.lua:8-9 / Attention.lua:316 error() semantics);
  *   - `stream` is a hipStream_t (NULL = legacy default stream); calls are asynchronous on it
  *     and allocate nothing (scratch/saved buffers come from the caller, sized by the *_bytes
  *     queries);
@@ -66,6 +70,16 @@ int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
 #define S2S_PREC_BF16_ALL 2
 int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
 int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
+/* Failure status of the context's persistent launches, after synchronising `stream` (and the context's
+ * side stream): 0, or a bitwise OR of
+ *   S2S_STATUS_HANDOFF_TIMEOUT: a hand-off wait of a persistent launch exceeded its spin limit -- that
+ *     launch's outputs / gradients (and everything computed from them) are invalid;
+ *   S2S_STATUS_ABORTED_REGION: a persistent launch found its sync region already aborted and returned at
+ *     once (a preparing launch failed, or the s2s_debug_inject_abort test knob).
+ * clear = 1 resets it (compute calls fail while it is nonzero). */
+#define S2S_STATUS_HANDOFF_TIMEOUT 1
+#define S2S_STATUS_ABORTED_REGION 2
+int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear);
 
 /* ---------------------------------------------------------------- GRU layer
  * nn.RNN(nn.GRU(D, H), reverse)  (RNN.lua:120-201, GRU.lua:16-51, Recurrent.lua:104-151).

@@ -41,6 +41,9 @@ struct AttnDims {
   // the XCD-local decoder's sync regions were prepared by attn_fwd_prologue (the model step runs it, and
   // joins it, before the decoder): attn_fwd / attn_bwd_core then launch no sync_prep of their own
   int syncs_in_prologue = 0;
+  // the calling context's status words (handoff.h): a persistent decoder launch that times out or starts on
+  // an aborted region sets them (s2s_ctx_status); null = not reported
+  unsigned* status = nullptr;
 };
 int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)

@@ -1129,7 +1129,7 @@ const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved) {
 
 // S2S_DEC_MODE=step forces the per-step launch path (A/B and fallback); default: the persistent
 // decoder kernels whenever the shape has an instantiation.
-static unsigned long long* g_dec_stamps[2] = {nullptr, nullptr};
+static std::atomic<unsigned long long*> g_dec_stamps[2] = {{nullptr}, {nullptr}};
 
 static int dec_persist_variant(const AttnDims& d) {
   const char* m = std::getenv("S2S_DEC_MODE");
@@ -1208,8 +1208,8 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
   return 0;
 }
 
-static int g_dec_allow_local = 1;
-static int g_merge_alpha_head = 1;  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
+static std::atomic<int> g_dec_allow_local{1};
+static std::atomic<int> g_merge_alpha_head{1};  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
 
 template <int S, int A, int SC>
 static int launch_xcd_t(bool fwd, int res, hipStream_t st, AttnK& k, XArgs& x) {
@@ -1266,8 +1266,8 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
   k.labels = labels;
   S2S_TRY(dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch)));
   if (d.syncs_in_prologue) {  // both decoder launches' sync regions, off the decoder's critical path
-    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
-    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
   }
   return 0;
 }
@@ -1303,7 +1303,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
+    if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
     {
       // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
       // per forward; flops = the step products + the attention contractions
@@ -1326,7 +1326,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       S2S_CHECK_HIP(hipGetLastError());
     }
   } else if (pf.fn) {
-    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
     {
       ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
       S2S_TRY(launch_persist(pf, pgrid, st, k));
@@ -1455,7 +1455,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
+    if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
       ProfScope ps(st, "dec_bwd_xcd", dec_flops(d, true), 8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
@@ -1483,7 +1483,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     }
     return attn_dh_gemms(st, terms, dh, accumulate_dh, side ? ev[4] : nullptr);
   } else if (pb.fn) {
-    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
     S2S_TRY(launch_persist(pb, pgrid, st, k));
     S2S_CHECK_HIP(hipGetLastError());

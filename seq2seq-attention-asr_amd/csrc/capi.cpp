@@ -112,13 +112,28 @@ struct s2s_ctx {
   unsigned long long graph_clock = 0;
   long captures = 0, replays = 0;
   ncclComm_t comm = nullptr;
+  // failure status of the context's persistent launches (handoff.h: [0] a hand-off wait timed out, [1] a
+  // launch started on an aborted region): host-coherent memory the kernels write, so every call can check
+  // it without a device sync; s2s_ctx_status reads it after a stream sync and clears it
+  unsigned* status_host = nullptr;
+  unsigned* status_dev = nullptr;
 };
 
 namespace {
 
-// every compute entry point starts here: the device, and the context's GEMM precision for this call
+// every compute entry point starts here: the device, the context's GEMM precision for this call, and the
+// context's failure status -- a persistent launch of an earlier call that timed out left wrong results, so
+// every later call fails until the caller has seen it (s2s_ctx_status with clear = 1); Torch's error()
 int set_device(s2s_ctx* ctx) {
   S2S_REQUIRE(ctx != nullptr, "null context");
+  if (ctx->status_host) {
+    const unsigned t = __atomic_load_n(ctx->status_host, __ATOMIC_ACQUIRE);
+    const unsigned a = __atomic_load_n(ctx->status_host + 1, __ATOMIC_ACQUIRE);
+    S2S_REQUIRE(t == 0u && a == 0u,
+                std::string("a persistent launch of an earlier call failed (") +
+                    (t ? "hand-off wait timed out" : "launch started on an aborted sync region") +
+                    "): its outputs and gradients are invalid; s2s_ctx_status(ctx, stream, &st, 1) clears it");
+  }
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
   set_gemm_precision(ctx->precision == S2S_PREC_FP32 ? kGemmF32 : kGemmBf16);
   set_wgrad_bf16(ctx->precision == S2S_PREC_BF16_ALL);
@@ -295,18 +310,20 @@ int wgrad_fork_mode() {
   }();
   return m;
 }
-int g_defer_pack = 1;  // s2s_debug_defer_pack(0) (diagnostic): every layer packed in front of layer 1
-int g_dec_sync_prologue = 1;  // s2s_debug_dec_sync_prologue(0) (diagnostic): decoder sync preps in place
-int g_sync_handover = 1;  // s2s_debug_sync_handover(0) (diagnostic): a sync_prep in front of every GRU launch
-int g_fuse_dh = 1;  // s2s_debug_fuse_dh(0) (diagnostic): the decoder's dh by GEMMs in front of the top BPTT
-int g_dec_side = 0;  // decoder's vbar / alpha / dVh on the side stream (measured: no gain, cross-stream edges)
+// process-wide diagnostic knobs (s2s_debug_*, not in the C ABI header; A/B tools and tests only), read when a
+// call issues its launches; no per-step state lives in globals (exclusive-CU mode, precision and the failure
+// status are per call / per context)
+std::atomic<int> g_defer_pack{1};  // s2s_debug_defer_pack(0): every layer packed in front of layer 1
+std::atomic<int> g_dec_sync_prologue{1};  // s2s_debug_dec_sync_prologue(0): decoder sync preps in place
+std::atomic<int> g_sync_handover{1};  // s2s_debug_sync_handover(0): a sync_prep in front of every GRU launch
+std::atomic<int> g_fuse_dh{1};  // s2s_debug_fuse_dh(0): the decoder's dh by GEMMs in front of the top BPTT
+std::atomic<int> g_dec_side{0};  // decoder's vbar / alpha / dVh on the side stream (measured: no gain)
 // seed_dev: the context's dropout seed word when a captured step reads its seed from the device (the
 // host writes it before each replay), else null (the seed is d->dropout_seed)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
                     const float* params, float* grads, const float* x, const int* labels, float scale, int flags,
-                    float* logp, float* nll, void* workspace, const unsigned long long* seed_dev) {
+                    float* logp, float* nll, void* workspace, const unsigned long long* seed_dev, unsigned* status) {
   const bool split = side != nullptr;
-  gru_persist_set_exclusive(split ? 1 : 0);
   ModelWs w = model_ws(d, workspace);
   const std::vector<LayerDims> layers = enc_layers(d);
   const std::vector<long> sizes = param_sizes(d);
@@ -328,7 +345,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
   ad.dropout_seed_dev = seed_dev;
-  ad.syncs_in_prologue = g_dec_sync_prologue;  // attn_fwd_prologue runs (and is joined) before the decoder
+  ad.syncs_in_prologue = g_dec_sync_prologue;
+  ad.status = status;  // attn_fwd_prologue runs (and is joined) before the decoder
   AttnParams ap;
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
@@ -363,6 +381,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     io.ldy = 2L * H;
     io.packed = w.pack[l];
     io.len = d->frame_lengths;
+    // the persistent launches reserve their CU while the weight-gradient GEMMs run on the side stream
+    io.excl = split ? 1 : 0;
+    io.status = status;
     return io;
   };
   if (w.xpad) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
@@ -607,6 +628,14 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
   S2S_CHECK_HIP(hipSetDevice(device));
   auto* c = new s2s_ctx();
   c->device = device;
+  if (hipHostMalloc(reinterpret_cast<void**>(&c->status_host), 64, hipHostMallocMapped | hipHostMallocCoherent) !=
+          hipSuccess ||
+      hipHostGetDevicePointer(reinterpret_cast<void**>(&c->status_dev), c->status_host, 0) != hipSuccess) {
+    if (c->status_host) (void)hipHostFree(c->status_host);
+    delete c;
+    S2S_REQUIRE(false, "ctx: host-coherent status word allocation failed");
+  }
+  std::memset(c->status_host, 0, 64);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
   for (auto& e : c->ev)
     if (c->side && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
@@ -629,12 +658,27 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   for (auto& e : ctx->bev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
+  if (ctx->status_host) (void)hipHostFree(ctx->status_host);
   delete ctx;
 }
 
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags) {
   S2S_REQUIRE(ctx != nullptr, "null context");
   ctx->flags = flags;
+  return 0;
+}
+
+int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear) {
+  S2S_REQUIRE(ctx != nullptr && status != nullptr, "null argument");
+  S2S_CHECK_HIP(hipSetDevice(ctx->device));
+  S2S_CHECK_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+  *status = (__atomic_load_n(ctx->status_host, __ATOMIC_ACQUIRE) ? S2S_STATUS_HANDOFF_TIMEOUT : 0) |
+            (__atomic_load_n(ctx->status_host + 1, __ATOMIC_ACQUIRE) ? S2S_STATUS_ABORTED_REGION : 0);
+  if (clear) {
+    __atomic_store_n(ctx->status_host, 0u, __ATOMIC_RELEASE);
+    __atomic_store_n(ctx->status_host + 1, 0u, __ATOMIC_RELEASE);
+  }
   return 0;
 }
 
@@ -681,6 +725,7 @@ int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
   S2S_REQUIRE(y != nullptr, "gru: null y");
   for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "gru: null y");
   S2S_REQUIRE(ldy >= H, "gru: ldy < H");
+  io.status = ctx->status_dev;
   return gru_layer_fwd(static_cast<hipStream_t>(stream), io, scratch, scratch_bytes);
 }
 
@@ -706,6 +751,7 @@ int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
   gr.lddx = lddx;
   gr.dx_accumulate = dx_accumulate;
   gr.scale = scale;
+  io.status = ctx->status_dev;
   return gru_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
 }
 
@@ -793,7 +839,9 @@ int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
     pp[i] = params[i];
     S2S_REQUIRE(pp[i] != nullptr || attn_param_optional(d, i), "attn: null parameter");
   }
-  return attn_fwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, logp, saved, scratch, scratch_bytes);
+  AttnDims ad = to_attn(d);
+  ad.status = ctx->status_dev;
+  return attn_fwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, logp, saved, scratch, scratch_bytes);
 }
 
 int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
@@ -810,8 +858,10 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
     gp[i] = grads[i];
     S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || attn_param_optional(d, i), "attn: null parameter/grad");
   }
-  return attn_bwd(static_cast<hipStream_t>(stream), to_attn(d), h, labels, ap, saved, dlogp, dh, dh_accumulate, ag,
-                  scale, scratch, scratch_bytes);
+  AttnDims ad = to_attn(d);
+  ad.status = ctx->status_dev;
+  return attn_bwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, saved, dlogp, dh, dh_accumulate, ag, scale,
+                  scratch, scratch_bytes);
 }
 
 size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength) {
@@ -1051,7 +1101,7 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
   }
   if (!(ctx->flags & S2S_CTX_GRAPH) || st == nullptr)
     return model_step_impl(st, (st && (ctx->flags & S2S_CTX_OVERLAP)) ? ctx->side : nullptr, ctx->ev, bev, d,
-                           params, grads, x, labels, scale, flags, logp, nll, workspace, nullptr);
+                           params, grads, x, labels, scale, flags, logp, nll, workspace, nullptr, ctx->status_dev);
   // In-kernel dropout draws from a new seed every step: the replayed graph reads it from the context's
   // device word, written before each replay, so the seed is not part of the graph key.  Injected masks
   // (or no dropout) leave the seed unread: it is not part of the key either.
@@ -1081,7 +1131,7 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
     S2S_CHECK_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
     const int rc = model_step_impl(st, (ctx->flags & S2S_CTX_OVERLAP) ? ctx->side : nullptr, ctx->ev, bev, d,
                                    params, grads, x, labels, scale, flags, logp, nll, workspace,
-                                   dev_seed ? ctx->seed_dev : nullptr);
+                                   dev_seed ? ctx->seed_dev : nullptr, ctx->status_dev);
     hipGraph_t g = nullptr;
     const hipError_t ec = hipStreamEndCapture(st, &g);
     if (rc != 0) {
@@ -1251,6 +1301,23 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
   return rc;
 }
 extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }
+// test knob: the next n sync_preps (any context) start their region aborted, so the persistent launch behind
+// each reports S2S_STATUS_ABORTED_REGION and returns at once (tests/test_gpu_status.py)
+static std::atomic<int> g_inject_abort{0};
+// test probe: one wave of a persistent-style launch that waits for a value nobody writes (region: >= 768 bytes
+// of device memory); the context's status must then read S2S_STATUS_HANDOFF_TIMEOUT
+extern "C" int s2s_debug_handoff_timeout(s2s_ctx* ctx, s2s_stream_t stream, void* region) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(region != nullptr, "null region");
+  return handoff_timeout_probe_launch(static_cast<hipStream_t>(stream), region, ctx->status_dev);
+}
+extern "C" void s2s_debug_inject_abort(int n) { g_inject_abort = n; }
+int s2s::inject_abort_take() {
+  int v = g_inject_abort.load(std::memory_order_relaxed);
+  while (v > 0 && !g_inject_abort.compare_exchange_weak(v, v - 1)) {
+  }
+  return v > 0 ? 1 : 0;
+}
 extern "C" void s2s_debug_sync_handover(int on) { g_sync_handover = on; }
 extern "C" void s2s_debug_dec_sync_prologue(int on) { g_dec_sync_prologue = on; }
 extern "C" void s2s_debug_defer_pack(int on) { g_defer_pack = on; }

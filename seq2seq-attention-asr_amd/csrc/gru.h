@@ -33,6 +33,11 @@ struct GruLayerIO {
   size_t sync_next_prep = 0;
   // forward only: weight packing (gru_layers_pack's deferred jobs) done by this launch's spare slots
   const GruPackJobs* pack_jobs = nullptr;
+  // the persistent launches reserve their CU (unused dynamic LDS) so side-stream GEMMs only take idle CUs
+  int excl = 0;
+  // the calling context's status words (handoff.h): a persistent launch that times out or starts on an
+  // aborted region sets them (s2s_ctx_status); null = not reported
+  unsigned* status = nullptr;
 };
 struct GruLayerGrad {
   const float* dy[2];  // dy[d][(b*L+t)*lddy + j]

@@ -377,6 +377,8 @@ int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t sc
       f.next_prep = io.sync_next_prep;
     }
     f.pack = io.pack_jobs;
+    f.excl = io.excl;
+    f.status = io.status;
     return gru_persist_fwd(st, f, sync);
   }
   const dim3 g1(2 * H / 16, (B + 15) / 16, nd), g2(H / 16, (B + 15) / 16, nd);
@@ -461,6 +463,8 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
       f.next_sync = io.sync_next;
       f.next_prep = io.sync_next_prep;
     }
+    f.excl = io.excl;
+    f.status = io.status;
     S2S_TRY(gru_persist_bwd(st, f, sync));
   } else {
     ProfScope ps(st, "gru_bwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);

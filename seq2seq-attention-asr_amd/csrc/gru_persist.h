@@ -68,6 +68,8 @@ struct GruPersistFwd {
   size_t next_prep = 0;
   // weight packing deferred to this launch's spare slots (the layouts later launches read), or null
   const GruPackJobs* pack = nullptr;
+  int excl = 0;                // reserve the CU (kExclLds) beside side-stream GEMMs
+  unsigned* status = nullptr;  // the context's status words (handoff.h), or null
 };
 struct GruPersistBwd {
   int ndir, B, L, H;
@@ -95,19 +97,20 @@ struct GruPersistBwd {
   int prepared = 0;  // as GruPersistFwd
   void* next_sync = nullptr;
   size_t next_prep = 0;
+  int excl = 0;
+  unsigned* status = nullptr;
 };
 
 bool gru_persist_supported(int ndir, int B, int H);
 // the backward's spare slots can produce its dy (the dX GEMM of the layer above) in-launch
 bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy);
 bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx);
-// 1 = persistent GRU launches reserve their CU (see kExclLds); set around a step whose weight-gradient
-// GEMMs run on a side stream
-void gru_persist_set_exclusive(int on);
 size_t gru_persist_sync_bytes(int B, int L, int H);
 size_t gru_persist_prep_bytes(int B, int L, int H);  // the part sync_prep (or a preparing launch) zeroes
 bool gru_persist_can_prep_next(int ndir, int B, int H, bool fwd);
 int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync);
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync);
+// test probe of the hand-off timeout path (sync: >= 768 bytes of device memory)
+int handoff_timeout_probe_launch(hipStream_t st, void* sync, unsigned* status);
 
 }  // namespace s2s

@@ -126,9 +126,11 @@ struct PArgs {
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
   // the next persistent GRU launch's sync region (other than this one's), prepared by this launch's spare
-  // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0)
+  // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0,
+  // status pointer)
   char* next_sync;
   size_t next_prep;
+  unsigned* status;  // the context's status words (written into the next region's header), or null
   GruPackJobs pack;  // weight packing for later launches, done by the forward's spare slots (pack.n = 0: none)
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
@@ -141,8 +143,8 @@ struct PArgs {
     if (a.stamps && threadIdx.x == 0)                                                      \
       a.stamps[((long)lw * a.L + s) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
   } while (0)
-unsigned long long* g_gru_stamps[2] = {nullptr, nullptr};
-unsigned long long* g_gru_pstamps[2] = {nullptr, nullptr};
+std::atomic<unsigned long long*> g_gru_stamps[2] = {{nullptr}, {nullptr}};
+std::atomic<unsigned long long*> g_gru_pstamps[2] = {{nullptr}, {nullptr}};
 constexpr int kProdStampItems = 32;
 
 // cross-wave sum + abort agreement at the same barrier
@@ -442,6 +444,7 @@ __device__ __forceinline__ void prep_next_sync(const PArgs& a, int sp, int nsp) 
     unsigned* hdr = reinterpret_cast<unsigned*>(a.next_sync);
     const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    write_status_ptr(hdr, a.status);
     __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const size_t n16 = (a.next_prep - 256) / 16;
@@ -468,7 +471,7 @@ template <int NC>  // NC = H / 64
 __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
-  __shared__ unsigned tb_lds;
+  __shared__ unsigned tb_lds[2];
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
   __shared__ __attribute__((aligned(16))) float xring[kRowRing][2][256];  // [step % ring][gate | candidate][thread]
   extern __shared__ __attribute__((aligned(16))) float xlds[];  // producer tiles (fused x-projection)
@@ -492,7 +495,8 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
-  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  const unsigned tb = launch_tagbase(a.abort_word, tb_lds);
+  if (launch_aborted(tb_lds)) return;  // status reported; nothing handed off yet
   // z tiles publish h, r tiles q
   const bool loader = wave == 4;
   if (!loader)
@@ -660,7 +664,7 @@ template <int NC>
 __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
-  __shared__ unsigned tb_lds;
+  __shared__ unsigned tb_lds[2];
   __shared__ __attribute__((aligned(16))) float rowq[kRowRing][5][256];  // [step % ring][z r hh hp dy][thread]
   extern __shared__ __attribute__((aligned(16))) float ylds[];  // producer tiles (fused dy)
   const int H = a.H, B = a.B, L = a.L;
@@ -681,7 +685,8 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (a.stamps && tid == 0) a.stamps[((long)lw * L + L - 1) * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // entry
   if (tid == 0) abort_lds = 0;
-  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
+  const unsigned tb = launch_tagbase(a.abort_word, tb_lds);
+  if (launch_aborted(tb_lds)) return;  // status reported; nothing handed off yet
   const bool loader = wave == 4;
   if (!loader) {
     rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
@@ -855,16 +860,14 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 // each persistent workgroup reserves kExclLds bytes of dynamic LDS it never touches, so no GEMM
 // workgroup (37 KB of LDS) can share its CU; the GEMMs fill the CUs the recurrence leaves idle.
 constexpr int kExclLds = 124 * 1024;
-int g_excl = 0;
 
-int g_allow_local = 1;
+std::atomic<int> g_allow_local{1};
 
 template <int NC>
-int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
-  (void)ndir;
+int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
   const dim3 grid(chain_grid(a.nchains, a.nmem));
   // exclusive only while one chain per XCD fits one workgroup per CU (32 CUs per XCD)
-  const bool excl = g_excl && a.nchains <= 8 && a.nmem <= 32;
+  const bool excl = excl_req && a.nchains <= 8 && a.nmem <= 32;
   const unsigned shm = excl ? kExclLds : (a.fused ? kXpLds : 0);
   if (fwd) {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
@@ -879,12 +882,12 @@ int launch_nc(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
   return 0;
 }
 
-int launch(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
+int launch(hipStream_t st, const PArgs& a, bool excl, bool fwd) {
   switch (a.H / 64) {
-    case 1: return launch_nc<1>(st, a, ndir, fwd);
-    case 2: return launch_nc<2>(st, a, ndir, fwd);
-    case 4: return launch_nc<4>(st, a, ndir, fwd);
-    case 8: return launch_nc<8>(st, a, ndir, fwd);
+    case 1: return launch_nc<1>(st, a, excl, fwd);
+    case 2: return launch_nc<2>(st, a, excl, fwd);
+    case 4: return launch_nc<4>(st, a, excl, fwd);
+    case 8: return launch_nc<8>(st, a, excl, fwd);
   }
   set_error("gru persistent: unsupported H");
   return 2;
@@ -892,9 +895,7 @@ int launch(hipStream_t st, const PArgs& a, int ndir, bool fwd) {
 
 }  // namespace
 
-void gru_persist_set_exclusive(int on) { g_excl = on; }
-
-int g_fuse_xproj = 1;  // S2S_GRU_FUSED_XPROJ=0 (diagnostic) keeps the separate x-projection GEMM
+std::atomic<int> g_fuse_xproj{1};  // S2S_GRU_FUSED_XPROJ=0 (diagnostic) keeps the separate x-projection GEMM
 
 bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx) {
   if (!g_fuse_xproj || B > 64 || Kx % 32 != 0 || H % 64 != 0) return false;
@@ -902,8 +903,8 @@ bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx) {
   return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
 }
 
-int g_xp_split = 1;  // s2s_debug_gru_xp_split(0) (diagnostic): no split-K start of the fused dy producers
-int g_fuse_dy = 1;  // s2s_debug_gru_fused_dy(0) (diagnostic): the dX GEMM in front of the BPTT instead
+std::atomic<int> g_xp_split{1};  // s2s_debug_gru_xp_split(0) (diagnostic): no split-K start of the fused dy producers
+std::atomic<int> g_fuse_dy{1};  // s2s_debug_gru_fused_dy(0) (diagnostic): the dX GEMM in front of the BPTT instead
 
 bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy) {
   if (!g_fuse_xproj || !g_fuse_dy || B > 64 || K % 32 != 0 || H % 64 != 0 || ldw % 4 != 0 || lddy < (long)ndir * H) return false;
@@ -1006,12 +1007,13 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     a.next_prep = f.next_prep;
   }
   if (f.pack) a.pack = *f.pack;
-  if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H)));
+  a.status = f.status;
+  if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H), f.status));
   // algorithmic work of the launch: the recurrence, plus the x-projection GEMM when its spare slots compute it
   const double xflops = f.x ? 2.0 * f.B * f.L * 3.0 * f.ndir * f.H * f.Kx : 0.0;
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H + xflops,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
-  return launch(st, a, f.ndir, true);
+  return launch(st, a, f.excl != 0, true);
 }
 
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
@@ -1050,14 +1052,35 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     a.next_sync = static_cast<char*>(b.next_sync);
     a.next_prep = b.next_prep;
   }
-  if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H)));
+  a.status = b.status;
+  if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H), b.status));
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
   // algorithmic work of the launch: the recurrence, plus the dy its spare slots compute (the layer above's
   // dX GEMM, or the decoder's dh: dVh V and the context term sum_t alpha dc)
   const double yflops = b.ydA ? 2.0 * b.B * b.L * (double)b.ndir * b.H * (b.yK + b.yT) : 0.0;
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
-  return launch(st, a, b.ndir, false);
+  return launch(st, a, b.excl != 0, false);
+}
+
+// Test probe of the timeout path (s2s_debug_handoff_timeout): one wave waits for a granule nobody writes,
+// in a region prepared by sync_prep, with a short spin limit -- it must give up, raise the abort word and
+// report S2S_STATUS_HANDOFF_TIMEOUT through the region's status pointer, exactly as a stalled launch does.
+__global__ __launch_bounds__(64) void handoff_timeout_probe(char* sync) {
+  unsigned* hdr = reinterpret_cast<unsigned*>(sync);
+  const granule_t* g = reinterpret_cast<const granule_t*>(sync + 256);
+  unsigned spins = 0;
+  while (true) {
+    const granule_t x = __hip_atomic_load(g + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__all((unsigned)(x >> 32) == 0xfffffffeu)) break;  // never: the region is zeroed
+    if (spin_give_up(spins, hdr, 4096u)) break;
+  }
+}
+int handoff_timeout_probe_launch(hipStream_t st, void* sync, unsigned* status) {
+  S2S_TRY(launch_sync_prep(st, sync, 256 + 64 * sizeof(granule_t), status));
+  hipLaunchKernelGGL(handoff_timeout_probe, dim3(1), dim3(64), 0, st, static_cast<char*>(sync));
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
 }
 
 }  // namespace s2s

@@ -3,7 +3,9 @@
 // {value, tag} stored write-through (sc1); consumers re-read the granules they need with sc1
 // loads until every tag equals the expected epoch.  Buffers are zeroed (memset node) before each
 // launch; epochs are 1-based step counters within the launch.  Every wait is bounded: on timeout
-// (or when another wave already gave up) the abort word is raised and the wait returns false.
+// (or when another wave already gave up) the abort word is raised, the owning context's status word
+// is set (host-visible: s2s_ctx_status, and every later call of the context fails) and the wait
+// returns false.
 #pragma once
 #include "s2s_common.h"
 
@@ -76,11 +78,34 @@ __device__ __forceinline__ float peek_granule(const granule_t* g) {
   return __uint_as_float((unsigned)__hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-__device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_word) {
+// ---- sync-region header (256 bytes in front of every persistent launch's hand-off region)
+//   u32 word 0: abort word (0 = running; raised by the first wave that gives up a wait)
+//   u32 word 16 (byte 64): launch epoch (tags = (epoch << 16) + step)
+//   u64 at byte 128: the owning context's status words (host-visible, s2s_ctx_status), or 0
+// Both sync_prep and a preparing launch (prep_next_sync) write the status pointer, so every persistent
+// launch of a context reports a failure there: status[0] = 1 after a wait exceeded its spin limit,
+// status[1] = 1 after a launch found its region already aborted at start (it then returns at once).
+constexpr int kEpochWord = 16;      // u32 index of the epoch in the sync header
+constexpr int kStatusPtrWord = 32;  // u32 index of the u64 status pointer (byte 128)
+constexpr int kStatusTimeout = 0, kStatusAbortedRegion = 1;
+__device__ __forceinline__ void report_status(const unsigned* hdr, int which) {
+  const unsigned long long sp = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(hdr + kStatusPtrWord),
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (sp) __hip_atomic_store(reinterpret_cast<unsigned*>(sp) + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void write_status_ptr(unsigned* hdr, unsigned* status) {
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(hdr + kStatusPtrWord),
+                     (unsigned long long)reinterpret_cast<uintptr_t>(status), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// abort_word is the sync header's word 0
+__device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_word, unsigned limit = kSpinLimit) {
   ++spins;
   if ((spins & 63u) == 0) {
-    if (spins > kSpinLimit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+    if (spins > limit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
       __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      report_status(abort_word, kStatusTimeout);
       return true;
     }
   }
@@ -93,43 +118,52 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
 // left at the same addresses (same steps, so the same step tags) can never satisfy a wait, even if
 // a cache still holds them (measured: without epochs a repeated decoder launch with new weights
 // consumed the previous launch's values).  sync_prep (one launch replacing the memset) zeroes the
-// granule region past the 256-byte header and, in block 0, draws the epoch from a device counter
-// and resets the abort word -- both with memory-side atomics; every workgroup reads the epoch with
-// a memory-side atomic too (launch_tagbase).
-constexpr int kEpochWord = 16;  // u32 index of the epoch in the sync header (byte 64; abort word at 0)
+// granule region past the 256-byte header and, in block 0, draws the epoch from a device counter,
+// resets the abort word (or raises it: the s2s_debug_inject_abort test knob) and stores the status
+// pointer -- with memory-side atomics; every workgroup reads the epoch with a memory-side atomic too
+// (launch_tagbase).
 static __device__ unsigned g_s2s_epoch_ctr;
-static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes) {
+static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes, unsigned* status, unsigned abort0) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     unsigned* hdr = reinterpret_cast<unsigned*>(sync);
     const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    write_status_ptr(hdr, status);
+    __hip_atomic_exchange(hdr, abort0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const size_t n16 = (bytes - 256) / 16;
   uint4* p = reinterpret_cast<uint4*>(sync + 256);
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
     p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
-inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes) {
+// status: the context's status words (AttnDims::status / GruLayerIO::status), or null
+inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes, unsigned* status) {
   // bytes - 256 is a multiple of 8 (granules) and of 4 (census words); round the tail up is not
   // allowed, so clear the last partial 16-byte piece with the memset only when present
   const size_t n16 = (bytes - 256) / 16;
   int blocks = (int)std::min<size_t>(1024, (n16 + 255) / 256);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes);
+  hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes, status,
+                     inject_abort_take() ? 2u : 0u);
   if ((bytes - 256) % 16)
     S2S_CHECK_HIP(hipMemsetAsync(static_cast<char*>(sync) + 256 + n16 * 16, 0, (bytes - 256) % 16, st));
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }
-// tag base of this launch (all threads call; one barrier)
+// tag base of this launch (all threads call; one barrier).  lds[2]: lds[1] != 0 when the region was
+// already aborted when the launch started (a failed preparer, or the injected test abort): the status
+// is reported here and the caller returns at once (launch_aborted), before its first hand-off.
 __device__ __forceinline__ unsigned launch_tagbase(const unsigned* sync_hdr, unsigned* lds) {
-  if (threadIdx.x == 0)
-    *lds = __hip_atomic_fetch_add(const_cast<unsigned*>(sync_hdr) + kEpochWord, 0u, __ATOMIC_RELAXED,
-                                  __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    lds[0] = __hip_atomic_fetch_add(const_cast<unsigned*>(sync_hdr) + kEpochWord, 0u, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_AGENT);
+    lds[1] = __hip_atomic_load(sync_hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lds[1]) report_status(sync_hdr, kStatusAbortedRegion);
+  }
   __syncthreads();
-  return (*lds & 0xffffu) << 16;
+  return (lds[0] & 0xffffu) << 16;
 }
+__device__ __forceinline__ bool launch_aborted(const unsigned* lds) { return lds[1] != 0u; }
 
 // ---- XCD-local chains
 // A chain = the workgroups that hand data to each other (independent of other chains).  Launches

@@ -2,11 +2,15 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <string>
 
 namespace s2s {
+
+// test knob (s2s_debug_inject_abort, capi.cpp): 1 when this sync_prep starts its region aborted
+int inject_abort_take();
 
 // ---------------------------------------------------------------- errors
 // C-ABI calls never abort: they record a message and return nonzero

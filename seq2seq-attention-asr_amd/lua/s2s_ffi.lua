@@ -22,6 +22,7 @@ int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
 int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
 int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
 int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
+int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear);
 size_t s2s_gru_saved_bytes(int B, int L, int H);
 size_t s2s_gru_scratch_bytes(int ndir, int B, int L, int D, int H);
 int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved, const int* lengths, void* scratch, size_t scratch_bytes);
@@ -99,6 +100,8 @@ M.S2S_CTX_OVERLAP = 2
 M.S2S_PREC_FP32 = 0
 M.S2S_PREC_BF16_GEMM = 1
 M.S2S_PREC_BF16_ALL = 2
+M.S2S_STATUS_HANDOFF_TIMEOUT = 1
+M.S2S_STATUS_ABORTED_REGION = 2
 M.S2S_ATTN_NPARAMS = 17
 M.S2S_ATTN_NPARAMS_HYBRID = 20
 M.S2S_ATTN_NPARAMS_LSTM = 36
@@ -117,6 +120,19 @@ function M.context(device, flags)
    M.check(C.s2s_ctx_create(device or 0, out))
    if flags then M.check(C.s2s_ctx_set_flags(out[0], flags)) end
    return ffi.gc(out[0], C.s2s_ctx_destroy)
+end
+
+-- failure status of the context's persistent launches (after syncing `stream`); clear defaults to true.
+-- Call it at the trainer's sync points (gradients:norm(), timit/timit.lua:298): a nonzero status means the
+-- step's results are invalid, raised as the reference's error() would (RNN.lua:8-9).
+function M.ctx_status(ctx, stream, clear)
+   local st = ffi.new('int[1]')
+   M.check(C.s2s_ctx_status(ctx, stream, st, (clear == false) and 0 or 1))
+   return st[0]
+end
+function M.check_status(ctx, stream)
+   local st = M.ctx_status(ctx, stream, true)
+   if st ~= 0 then error('s2s: persistent launch failed (status ' .. st .. '): results since the last check are invalid') end
 end
 
 -- device pointer of a contiguous CudaTensor (nil -> NULL)

@@ -48,6 +48,7 @@ SIGNATURES = [
     ("s2s_ctx_set_graph_cache", c_int, [c_void_p, c_int]),
     ("s2s_ctx_set_precision", c_int, [c_void_p, c_int]),
     ("s2s_ctx_graph_stats", c_int, [c_void_p, P(c_long), P(c_long), P(c_int)]),
+    ("s2s_ctx_status", c_int, [c_void_p, c_void_p, P(c_int), c_int]),
     ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_gru_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int]),
     ("s2s_gru_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p, c_long,
@@ -150,6 +151,8 @@ S2S_UNIQUE_ID_BYTES = 128
 S2S_PREC_FP32 = 0
 S2S_PREC_BF16_GEMM = 1
 S2S_PREC_BF16_ALL = 2
+S2S_STATUS_HANDOFF_TIMEOUT = 1
+S2S_STATUS_ABORTED_REGION = 2
 
 
 class S2SError(RuntimeError):

@@ -41,6 +41,21 @@ class Context:
         """How many captured steps (one per shape / buffer set) the context keeps (default 8)."""
         check(lib.s2s_ctx_set_graph_cache(self.handle, int(capacity)))
 
+    def status(self, stream=None, clear=True):
+        """Failure status of this context's persistent launches (s2s_ctx_status), after synchronising `stream`
+        (default: the current stream): 0, or S2S_STATUS_HANDOFF_TIMEOUT | S2S_STATUS_ABORTED_REGION.  While it
+        is nonzero every compute call of the context raises S2SError; clear=True resets it."""
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        v = ctypes.c_int()
+        check(lib.s2s_ctx_status(self.handle, st, ctypes.byref(v), 1 if clear else 0))
+        return v.value
+
+    def check_status(self, stream=None):
+        """Raise S2SError when a persistent launch of this context failed since the last check (and clear it)."""
+        v = self.status(stream, clear=True)
+        if v:
+            raise _lib.S2SError(f"persistent launch failure (status {v}): the results since the last check are invalid")
+
     def graph_stats(self):
         """-> (graphs captured, replays launched, graphs cached) of this context."""
         c, r, n = ctypes.c_long(), ctypes.c_long(), ctypes.c_int()
