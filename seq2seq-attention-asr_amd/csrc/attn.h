@@ -41,9 +41,6 @@ struct AttnDims {
   // the XCD-local decoder's sync regions were prepared by attn_fwd_prologue (the model step runs it, and
   // joins it, before the decoder): attn_fwd / attn_bwd_core then launch no sync_prep of their own
   int syncs_in_prologue = 0;
-  // the calling context's status words (handoff.h): a persistent decoder launch that times out or starts on
-  // an aborted region sets them (s2s_ctx_status); null = not reported
-  unsigned* status = nullptr;
 };
 int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)
@@ -99,6 +96,9 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
+// the sync-region headers the decoder launches of d's path use (both null for the per-step path); returns
+// how many (0 or 2) -- the caller harvests their failure words after the call (handoff.h)
+int attn_sync_regions(const AttnDims& d, void* saved, void* scratch, void** fwd, void** bwd);
 const float* attn_saved_mlp_input(const AttnDims& d, const void* saved);
 const float* attn_saved_mono_ind(const AttnDims& d, const void* saved);
 const float* attn_saved_ws(const AttnDims& d, const void* saved);  // ws_t rows (B, T, Sc)

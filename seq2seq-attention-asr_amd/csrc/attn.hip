@@ -62,6 +62,9 @@ struct AttnK {
   granule_t *gZ, *gR, *gH, *gDD, *gDCY, *gDC, *gPDWS, *gDWS;           // backward
   char *fsync, *bsync;
   size_t fsync_bytes, bsync_bytes;
+  // the regions' 256-byte headers (abort word, epoch, sticky failure bits), kept apart from the overlapping
+  // forward / backward working sets: the forward region's header must survive the backward for the harvest
+  char *fhdr, *bhdr;
   unsigned long long* stamps;  // diagnostic phase stamps (nullptr = off)
   float* dh;
   long lddh;
@@ -296,6 +299,11 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     x->fcensus = fcensus; x->bcensus = bcensus;
     x->sS = xsS; x->sQ = xsQ; x->sC = xsC;
     x->sDGZ = xsDGZ; x->sDGR = xsDGR; x->sDGH = xsDGH; x->sDC = xsDC; x->sDWS = xsDWS;
+  }
+  if (k && scratch) {  // headers behind the GEMM slabs (attn_scratch_bytes)
+    const size_t hoff = ((std::max(f.off + 256, g.off + 256) + 255) & ~size_t(255)) + sizeof(float) * kGemmWsFloats;
+    k->fhdr = scratch + hoff;
+    k->bhdr = scratch + hoff + 256;
   }
   return Layout{sv.off + 256, f.off + 256, g.off + 256};
 }
@@ -1092,7 +1100,8 @@ static size_t attn_ws_offset(const AttnDims& d) {
   Layout l = carve(d, nullptr, nullptr, nullptr);
   return ((l.fwd > l.bwd ? l.fwd : l.bwd) + 255) & ~size_t(255);
 }
-size_t attn_scratch_bytes(const AttnDims& d) { return attn_ws_offset(d) + sizeof(float) * kGemmWsFloats; }
+// + the two sync-region headers (carve: fhdr, bhdr)
+size_t attn_scratch_bytes(const AttnDims& d) { return attn_ws_offset(d) + sizeof(float) * kGemmWsFloats + 512; }
 static GemmWs attn_gemm_ws(const AttnDims& d, void* scratch) {
   return GemmWs{reinterpret_cast<float*>(static_cast<char*>(scratch) + attn_ws_offset(d)), kGemmWsFloats};
 }
@@ -1255,6 +1264,18 @@ static int dec_xcd_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const X
   return 0;
 }
 
+// the decoder launches of d's path hand off through the fsync / bsync regions of `scratch` (the XCD-local or
+// the persistent kernels; the per-step path has none): their headers, for the caller's harvest
+int attn_sync_regions(const AttnDims& d, void* saved, void* scratch, void** fwd, void** bwd) {
+  *fwd = *bwd = nullptr;
+  if (!dec_xcd_plan(d).var && !dec_persist_variant(d)) return 0;
+  AttnK k{};
+  carve(d, &k, static_cast<char*>(saved), static_cast<char*>(scratch));
+  *fwd = k.fhdr;
+  *bwd = k.bhdr;
+  return 2;
+}
+
 int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, const AttnParams& P, void* saved,
                       void* scratch) {
   const XPlan xp = dec_xcd_plan(d);
@@ -1266,8 +1287,8 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
   k.labels = labels;
   S2S_TRY(dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch)));
   if (d.syncs_in_prologue) {  // both decoder launches' sync regions, off the decoder's critical path
-    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
-    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, nullptr, k.fhdr));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, nullptr, k.bhdr));
   }
   return 0;
 }
@@ -1303,7 +1324,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
+    if (!(d.syncs_in_prologue && prologue_done)) S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, nullptr, k.fhdr));
     {
       // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
       // per forward; flops = the step products + the attention contractions
@@ -1326,7 +1347,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       S2S_CHECK_HIP(hipGetLastError());
     }
   } else if (pf.fn) {
-    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, d.status));
+    S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, nullptr, k.fhdr));
     {
       ProfScope ps(st, "dec_fwd_persist", 0.0, 0.0);
       S2S_TRY(launch_persist(pf, pgrid, st, k));
@@ -1455,7 +1476,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     x.XLC = xp.XLC;
     x.NCH = xp.NCH;
     x.allow_local = g_dec_allow_local;
-    if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
+    if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, nullptr, k.bhdr));
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
       ProfScope ps(st, "dec_bwd_xcd", dec_flops(d, true), 8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
@@ -1483,7 +1504,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     }
     return attn_dh_gemms(st, terms, dh, accumulate_dh, side ? ev[4] : nullptr);
   } else if (pb.fn) {
-    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, d.status));
+    S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, nullptr, k.bhdr));
     ProfScope ps(st, "dec_bwd_persist", 0.0, 0.0);
     S2S_TRY(launch_persist(pb, pgrid, st, k));
     S2S_CHECK_HIP(hipGetLastError());

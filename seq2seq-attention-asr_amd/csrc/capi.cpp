@@ -15,6 +15,7 @@
 #include "attn.h"
 #include "frontend.h"
 #include "gru_persist.h"
+#include "handoff.h"
 #include "gru.h"
 #include "lstm.h"
 #include "s2s_common.h"
@@ -345,8 +346,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
   ad.dropout_seed_dev = seed_dev;
-  ad.syncs_in_prologue = g_dec_sync_prologue;
-  ad.status = status;  // attn_fwd_prologue runs (and is joined) before the decoder
+  ad.syncs_in_prologue = g_dec_sync_prologue;  // attn_fwd_prologue runs (and is joined) before the decoder
   AttnParams ap;
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
@@ -383,8 +383,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     io.len = d->frame_lengths;
     // the persistent launches reserve their CU while the weight-gradient GEMMs run on the side stream
     io.excl = split ? 1 : 0;
-    io.status = status;
-    return io;
+    return io;  // io.status stays null: the step harvests every sync region once, at its end
   };
   if (w.xpad) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
   // weight packing for every layer (both passes) and the decoder's parameter folds need only params
@@ -418,8 +417,10 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // first launch has a sync_prep in front of it
   int glaunch = 0;
   bool gprepared = false;
+  bool gused[2] = {false, false};  // a persistent launch of this step used the region (harvested at the end)
   auto hand_over = [&](GruLayerIO& io, bool fwd, const GruLayerIO* next) {
     if (!g_sync_handover) return;
+    if (gru_layer_persistent(io)) gused[glaunch & 1] = true;
     io.sync = w.gsync[glaunch & 1];
     io.sync_prepared = gprepared ? 1 : 0;
     io.sync_next = next ? w.gsync[(glaunch + 1) & 1] : nullptr;
@@ -427,6 +428,14 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     gprepared = next != nullptr && gru_layer_preps_next(io, fwd);
     ++glaunch;
   };
+  // the region headers hold failure words: the first persistent launch's sync_prep clears the other region's
+  // header too (sync_prep `clear`); when layer 1 runs per-step kernels, clear both here instead
+  if (g_sync_handover && !gru_layer_persistent(layer_io(0))) {
+    bool later = false;
+    for (int l = 1; l < nl; ++l) later = later || gru_layer_persistent(layer_io(l));
+    if (later)
+      for (int r = 0; r < 2; ++r) S2S_CHECK_HIP(hipMemsetAsync(w.gsync[r], 0, 256, st));
+  }
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   for (int l = 0; l < nl; ++l) {
     GruLayerIO io = layer_io(l);
@@ -539,6 +548,16 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     dYcur = dYnext;
     dYnext = tmp;
   }
+  // failure words of every sync region the step's persistent launches used -> the context's status (handoff.h),
+  // on the main stream after the last BPTT (beside the side stream's weight-gradient tail)
+  if (status) {
+    void* regions[4];
+    int nr = 0;
+    for (int r = 0; r < 2; ++r)
+      if (gused[r]) regions[nr++] = w.gsync[r];
+    nr += attn_sync_regions(ad, w.attn_saved, w.attn_scratch, &regions[nr], &regions[nr + 1]);
+    S2S_TRY(launch_sync_harvest(st, regions, nr, status));
+  }
   if (split) {  // join: the step ends when the side stream's gradient GEMMs are done
     S2S_CHECK_HIP(hipEventRecord(ev[15], side));
     S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[15], 0));
@@ -635,7 +654,7 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
     delete c;
     S2S_REQUIRE(false, "ctx: host-coherent status word allocation failed");
   }
-  std::memset(c->status_host, 0, 64);
+  if (c->status_host) std::memset(c->status_host, 0, 64);
   if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
   for (auto& e : c->ev)
     if (c->side && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
@@ -673,12 +692,12 @@ int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear) {
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
   S2S_CHECK_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+  *status = 0;
+  if (!ctx->status_host) return 0;
   *status = (__atomic_load_n(ctx->status_host, __ATOMIC_ACQUIRE) ? S2S_STATUS_HANDOFF_TIMEOUT : 0) |
             (__atomic_load_n(ctx->status_host + 1, __ATOMIC_ACQUIRE) ? S2S_STATUS_ABORTED_REGION : 0);
-  if (clear) {
-    __atomic_store_n(ctx->status_host, 0u, __ATOMIC_RELEASE);
-    __atomic_store_n(ctx->status_host + 1, 0u, __ATOMIC_RELEASE);
-  }
+  if (clear)
+    for (int i = 0; i < 16; ++i) __atomic_store_n(ctx->status_host + i, 0u, __ATOMIC_RELEASE);
   return 0;
 }
 
@@ -829,6 +848,13 @@ const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_dropout_mask(to_attn(d), saved) : nullptr;
 }
 
+// the decoder's persistent launch of this call (which = 0 forward, 1 backward) -> the context's status
+static int harvest_attn(s2s_ctx* ctx, s2s_stream_t stream, const AttnDims& ad, void* saved, void* scratch, int which) {
+  void* r[2];
+  if (attn_sync_regions(ad, saved, scratch, &r[0], &r[1]) == 0) return 0;
+  return launch_sync_harvest(static_cast<hipStream_t>(stream), &r[which], 1, ctx->status_dev);
+}
+
 int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
                  const float* const* params, float* logp, void* saved, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
@@ -839,9 +865,9 @@ int s2s_attn_fwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
     pp[i] = params[i];
     S2S_REQUIRE(pp[i] != nullptr || attn_param_optional(d, i), "attn: null parameter");
   }
-  AttnDims ad = to_attn(d);
-  ad.status = ctx->status_dev;
-  return attn_fwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, logp, saved, scratch, scratch_bytes);
+  const AttnDims ad = to_attn(d);
+  S2S_TRY(attn_fwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, logp, saved, scratch, scratch_bytes));
+  return harvest_attn(ctx, stream, ad, saved, scratch, 0);
 }
 
 int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const int* labels,
@@ -858,10 +884,10 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
     gp[i] = grads[i];
     S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || attn_param_optional(d, i), "attn: null parameter/grad");
   }
-  AttnDims ad = to_attn(d);
-  ad.status = ctx->status_dev;
-  return attn_bwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, saved, dlogp, dh, dh_accumulate, ag, scale,
-                  scratch, scratch_bytes);
+  const AttnDims ad = to_attn(d);
+  S2S_TRY(attn_bwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, saved, dlogp, dh, dh_accumulate, ag, scale,
+                   scratch, scratch_bytes));
+  return harvest_attn(ctx, stream, ad, const_cast<void*>(saved), scratch, 1);
 }
 
 size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength) {
@@ -1215,6 +1241,12 @@ int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n) {
   return optim_state_reset(static_cast<hipStream_t>(stream), state, n);
 }
 
+int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n, unsigned t) {
+  S2S_TRY(set_device(ctx));
+  S2S_REQUIRE(state && n > 0, "optim: null state");
+  return optim_set_noise_step(static_cast<hipStream_t>(stream), state, n, t);
+}
+
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
                             float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
   S2S_TRY(set_device(ctx));
@@ -1304,6 +1336,13 @@ extern "C" void s2s_debug_fuse_dh(int on) { g_fuse_dh = on; }
 // test knob: the next n sync_preps (any context) start their region aborted, so the persistent launch behind
 // each reports S2S_STATUS_ABORTED_REGION and returns at once (tests/test_gpu_status.py)
 static std::atomic<int> g_inject_abort{0};
+// diagnostic: the context's 16 status words ([0] timeout, [1] aborted region, [4 + i] raw failure bits of the
+// last harvest's region i) -- tools/status_diag.py
+extern "C" int s2s_debug_status_words(s2s_ctx* ctx, unsigned* out16) {
+  S2S_REQUIRE(ctx && out16, "null argument");
+  for (int i = 0; i < 16; ++i) out16[i] = ctx->status_host ? __atomic_load_n(ctx->status_host + i, __ATOMIC_ACQUIRE) : 0u;
+  return 0;
+}
 // test probe: one wave of a persistent-style launch that waits for a value nobody writes (region: >= 768 bytes
 // of device memory); the context's status must then read S2S_STATUS_HANDOFF_TIMEOUT
 extern "C" int s2s_debug_handoff_timeout(s2s_ctx* ctx, s2s_stream_t stream, void* region) {

@@ -35,8 +35,8 @@ struct GruLayerIO {
   const GruPackJobs* pack_jobs = nullptr;
   // the persistent launches reserve their CU (unused dynamic LDS) so side-stream GEMMs only take idle CUs
   int excl = 0;
-  // the calling context's status words (handoff.h): a persistent launch that times out or starts on an
-  // aborted region sets them (s2s_ctx_status); null = not reported
+  // the calling context's status words (handoff.h): the layer's persistent launch is followed by a harvest of
+  // its sync region into them (s2s_ctx_status); null = no harvest (the model step harvests once at its end)
   unsigned* status = nullptr;
 };
 struct GruLayerGrad {
@@ -64,6 +64,8 @@ struct GruLayerGrad {
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
+// the layer's recurrences run as persistent launches (sync regions, hand-offs) rather than per-step kernels
+bool gru_layer_persistent(const GruLayerIO& io);
 // Every kernel layout of one layer's weights (recurrent Uzr/Uh and their transposes, the padded
 // x-projection rows), packed once per step so the forward and backward launches skip it.
 size_t gru_layer_pack_bytes(int ndir, int D, int H);

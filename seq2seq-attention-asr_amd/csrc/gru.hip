@@ -214,6 +214,8 @@ static bool use_persistent(int nd, int B, int H) {
   return gru_persist_supported(nd, B, H);
 }
 
+bool gru_layer_persistent(const GruLayerIO& io) { return use_persistent(io.ndir, io.B, io.H); }
+
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H) {
   Bump bp{nullptr, 0, 0};
   for (int d = 0; d < ndir; ++d) {

@@ -69,7 +69,7 @@ struct GruPersistFwd {
   // weight packing deferred to this launch's spare slots (the layouts later launches read), or null
   const GruPackJobs* pack = nullptr;
   int excl = 0;                // reserve the CU (kExclLds) beside side-stream GEMMs
-  unsigned* status = nullptr;  // the context's status words (handoff.h), or null
+  unsigned* status = nullptr;  // harvest this launch's failure words into these status words (null: the caller does)
 };
 struct GruPersistBwd {
   int ndir, B, L, H;

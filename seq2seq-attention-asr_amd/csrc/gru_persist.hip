@@ -126,11 +126,9 @@ struct PArgs {
   unsigned* census;      // [nchains][nmem] XCC ids (chain_is_local)
   const int* len;        // (B) frames per utterance (null: all L): h_t = 0 for t >= len_b
   // the next persistent GRU launch's sync region (other than this one's), prepared by this launch's spare
-  // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0,
-  // status pointer)
+  // slots -- what sync_prep would do in front of that launch (zero [256, next_prep), fresh epoch, abort 0)
   char* next_sync;
   size_t next_prep;
-  unsigned* status;  // the context's status words (written into the next region's header), or null
   GruPackJobs pack;  // weight packing for later launches, done by the forward's spare slots (pack.n = 0: none)
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
@@ -444,8 +442,7 @@ __device__ __forceinline__ void prep_next_sync(const PArgs& a, int sp, int nsp) 
     unsigned* hdr = reinterpret_cast<unsigned*>(a.next_sync);
     const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    write_status_ptr(hdr, a.status);
-    __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    rearm_abort_word(hdr);  // the previous launch's failure stays in the sticky bits until the harvest
   }
   const size_t n16 = (a.next_prep - 256) / 16;
   uint4* p = reinterpret_cast<uint4*>(a.next_sync + 256);
@@ -471,7 +468,7 @@ template <int NC>  // NC = H / 64
 __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
-  __shared__ unsigned tb_lds[2];
+  __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
   __shared__ __attribute__((aligned(16))) float xring[kRowRing][2][256];  // [step % ring][gate | candidate][thread]
   extern __shared__ __attribute__((aligned(16))) float xlds[];  // producer tiles (fused x-projection)
@@ -495,8 +492,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16;
   if (tid == 0) abort_lds = 0;
-  const unsigned tb = launch_tagbase(a.abort_word, tb_lds);
-  if (launch_aborted(tb_lds)) return;  // status reported; nothing handed off yet
+  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   // z tiles publish h, r tiles q
   const bool loader = wave == 4;
   if (!loader)
@@ -664,7 +660,7 @@ template <int NC>
 __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
   __shared__ int abort_lds, local_lds;
-  __shared__ unsigned tb_lds[2];
+  __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float rowq[kRowRing][5][256];  // [step % ring][z r hh hp dy][thread]
   extern __shared__ __attribute__((aligned(16))) float ylds[];  // producer tiles (fused dy)
   const int H = a.H, B = a.B, L = a.L;
@@ -685,8 +681,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const int b0 = mt * 16;
   if (a.stamps && tid == 0) a.stamps[((long)lw * L + L - 1) * 8 + 6] = __builtin_amdgcn_s_memrealtime();  // entry
   if (tid == 0) abort_lds = 0;
-  const unsigned tb = launch_tagbase(a.abort_word, tb_lds);
-  if (launch_aborted(tb_lds)) return;  // status reported; nothing handed off yet
+  const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const bool loader = wave == 4;
   if (!loader) {
     rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
@@ -1007,13 +1002,14 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
     a.next_prep = f.next_prep;
   }
   if (f.pack) a.pack = *f.pack;
-  a.status = f.status;
-  if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H), f.status));
+  if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H), a.next_sync));
   // algorithmic work of the launch: the recurrence, plus the x-projection GEMM when its spare slots compute it
   const double xflops = f.x ? 2.0 * f.B * f.L * 3.0 * f.ndir * f.H * f.Kx : 0.0;
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H + xflops,
                4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
-  return launch(st, a, f.excl != 0, true);
+  S2S_TRY(launch(st, a, f.excl != 0, true));
+  void* r[1] = {sync};
+  return launch_sync_harvest(st, r, 1, f.status);
 }
 
 int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
@@ -1052,20 +1048,21 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     a.next_sync = static_cast<char*>(b.next_sync);
     a.next_prep = b.next_prep;
   }
-  a.status = b.status;
-  if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H), b.status));
+  if (!b.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(b.B, b.L, b.H), a.next_sync));
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
   // algorithmic work of the launch: the recurrence, plus the dy its spare slots compute (the layer above's
   // dX GEMM, or the decoder's dh: dVh V and the context term sum_t alpha dc)
   const double yflops = b.ydA ? 2.0 * b.B * b.L * (double)b.ndir * b.H * (b.yK + b.yT) : 0.0;
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops,
                4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
-  return launch(st, a, b.excl != 0, false);
+  S2S_TRY(launch(st, a, b.excl != 0, false));
+  void* r[1] = {sync};
+  return launch_sync_harvest(st, r, 1, b.status);
 }
 
 // Test probe of the timeout path (s2s_debug_handoff_timeout): one wave waits for a granule nobody writes,
-// in a region prepared by sync_prep, with a short spin limit -- it must give up, raise the abort word and
-// report S2S_STATUS_HANDOFF_TIMEOUT through the region's status pointer, exactly as a stalled launch does.
+// in a region prepared by sync_prep, with a short spin limit -- it must give up and raise the abort word,
+// which the harvest behind it reports as S2S_STATUS_HANDOFF_TIMEOUT, exactly as for a stalled launch.
 __global__ __launch_bounds__(64) void handoff_timeout_probe(char* sync) {
   unsigned* hdr = reinterpret_cast<unsigned*>(sync);
   const granule_t* g = reinterpret_cast<const granule_t*>(sync + 256);
@@ -1077,10 +1074,11 @@ __global__ __launch_bounds__(64) void handoff_timeout_probe(char* sync) {
   }
 }
 int handoff_timeout_probe_launch(hipStream_t st, void* sync, unsigned* status) {
-  S2S_TRY(launch_sync_prep(st, sync, 256 + 64 * sizeof(granule_t), status));
+  S2S_TRY(launch_sync_prep(st, sync, 256 + 64 * sizeof(granule_t)));
   hipLaunchKernelGGL(handoff_timeout_probe, dim3(1), dim3(64), 0, st, static_cast<char*>(sync));
   S2S_CHECK_HIP(hipGetLastError());
-  return 0;
+  void* r[1] = {sync};
+  return launch_sync_harvest(st, r, 1, status);
 }
 
 }  // namespace s2s

@@ -3,9 +3,8 @@
 // {value, tag} stored write-through (sc1); consumers re-read the granules they need with sc1
 // loads until every tag equals the expected epoch.  Buffers are zeroed (memset node) before each
 // launch; epochs are 1-based step counters within the launch.  Every wait is bounded: on timeout
-// (or when another wave already gave up) the abort word is raised, the owning context's status word
-// is set (host-visible: s2s_ctx_status, and every later call of the context fails) and the wait
-// returns false.
+// (or when another wave already gave up) the abort word is raised and the wait returns false; the
+// call's harvest launch reports it to the owning context (s2s_ctx_status; every later call fails).
 #pragma once
 #include "s2s_common.h"
 
@@ -79,25 +78,18 @@ __device__ __forceinline__ float peek_granule(const granule_t* g) {
 }
 
 // ---- sync-region header (256 bytes in front of every persistent launch's hand-off region)
-//   u32 word 0: abort word (0 = running; raised by the first wave that gives up a wait)
+//   u32 word 0: abort word (0 = running; 1 = a wave gave up a wait; 2 = started aborted: the
+//               s2s_debug_inject_abort test knob)
 //   u32 word 16 (byte 64): launch epoch (tags = (epoch << 16) + step)
-//   u64 at byte 128: the owning context's status words (host-visible, s2s_ctx_status), or 0
-// Both sync_prep and a preparing launch (prep_next_sync) write the status pointer, so every persistent
-// launch of a context reports a failure there: status[0] = 1 after a wait exceeded its spin limit,
-// status[1] = 1 after a launch found its region already aborted at start (it then returns at once).
-constexpr int kEpochWord = 16;      // u32 index of the epoch in the sync header
-constexpr int kStatusPtrWord = 32;  // u32 index of the u64 status pointer (byte 128)
-constexpr int kStatusTimeout = 0, kStatusAbortedRegion = 1;
-__device__ __forceinline__ void report_status(const unsigned* hdr, int which) {
-  const unsigned long long sp = __hip_atomic_load(reinterpret_cast<const unsigned long long*>(hdr + kStatusPtrWord),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (sp) __hip_atomic_store(reinterpret_cast<unsigned*>(sp) + which, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-__device__ __forceinline__ void write_status_ptr(unsigned* hdr, unsigned* status) {
-  __hip_atomic_store(reinterpret_cast<unsigned long long*>(hdr + kStatusPtrWord),
-                     (unsigned long long)reinterpret_cast<uintptr_t>(status), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-}
+//   u32 word 48 (byte 192): sticky failure bits of the region's earlier launches since the last harvest: a
+//               launch that prepares the region for the next one (prep_next_sync) ORs the abort word into it
+//               before resetting the abort word
+// The failure is reported OFF the hand-off path: a harvest launch at the end of every call (sync_harvest,
+// stream-ordered after the call's persistent launches) ORs each region's abort word and sticky bits into the
+// owning context's host-visible status words and clears them.  (Reporting from inside the waits, even on the
+// give-up path only, changed the waits' code generation: +0.19 ms per config-2 step, same-box A/B.)
+constexpr int kEpochWord = 16;   // u32 index of the epoch in the sync header
+constexpr int kStickyWord = 48;  // u32 index of the sticky failure bits
 
 // abort_word is the sync header's word 0
 __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_word, unsigned limit = kSpinLimit) {
@@ -105,7 +97,6 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
   if ((spins & 63u) == 0) {
     if (spins > limit || __hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
       __hip_atomic_store(abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      report_status(abort_word, kStatusTimeout);
       return true;
     }
   }
@@ -119,16 +110,22 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
 // a cache still holds them (measured: without epochs a repeated decoder launch with new weights
 // consumed the previous launch's values).  sync_prep (one launch replacing the memset) zeroes the
 // granule region past the 256-byte header and, in block 0, draws the epoch from a device counter,
-// resets the abort word (or raises it: the s2s_debug_inject_abort test knob) and stores the status
-// pointer -- with memory-side atomics; every workgroup reads the epoch with a memory-side atomic too
-// (launch_tagbase).
+// resets the abort word (or raises it: the s2s_debug_inject_abort test knob) and the sticky bits (the
+// previous call's harvest has reported them) -- with memory-side atomics; every workgroup reads the epoch
+// with a memory-side atomic too (launch_tagbase).
 static __device__ unsigned g_s2s_epoch_ctr;
-static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes, unsigned* status, unsigned abort0) {
+static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes, unsigned abort0, char* clear,
+                                                         char* hdr_at) {
   if (blockIdx.x == 0 && threadIdx.x == 0) {
-    unsigned* hdr = reinterpret_cast<unsigned*>(sync);
+    if (clear) {  // the other (idle) region of a hand-over pair: its words may still be uninitialised memory
+      unsigned* c = reinterpret_cast<unsigned*>(clear);
+      __hip_atomic_exchange(c + kStickyWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_exchange(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    unsigned* hdr = reinterpret_cast<unsigned*>(hdr_at ? hdr_at : sync);
     const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
     __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    write_status_ptr(hdr, status);
+    __hip_atomic_exchange(hdr + kStickyWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_exchange(hdr, abort0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   const size_t n16 = (bytes - 256) / 16;
@@ -136,34 +133,65 @@ static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n16; i += (size_t)gridDim.x * blockDim.x)
     p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
-// status: the context's status words (AttnDims::status / GruLayerIO::status), or null
-inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes, unsigned* status) {
+// clear (optional): the header of the region the launch behind this prep will prepare for the next launch
+// (prep_next_sync folds that region's abort word into its sticky bits, which must not be stale memory);
+// hdr (optional): the region's header lives there instead of at `sync` (whose first 256 bytes are then unused)
+inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes, void* clear = nullptr, void* hdr = nullptr) {
   // bytes - 256 is a multiple of 8 (granules) and of 4 (census words); round the tail up is not
   // allowed, so clear the last partial 16-byte piece with the memset only when present
   const size_t n16 = (bytes - 256) / 16;
   int blocks = (int)std::min<size_t>(1024, (n16 + 255) / 256);
   if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes, status,
-                     inject_abort_take() ? 2u : 0u);
+  hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes,
+                     inject_abort_take() ? 2u : 0u, static_cast<char*>(clear), static_cast<char*>(hdr));
   if ((bytes - 256) % 16)
     S2S_CHECK_HIP(hipMemsetAsync(static_cast<char*>(sync) + 256 + n16 * 16, 0, (bytes - 256) % 16, st));
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }
-// tag base of this launch (all threads call; one barrier).  lds[2]: lds[1] != 0 when the region was
-// already aborted when the launch started (a failed preparer, or the injected test abort): the status
-// is reported here and the caller returns at once (launch_aborted), before its first hand-off.
-__device__ __forceinline__ unsigned launch_tagbase(const unsigned* sync_hdr, unsigned* lds) {
-  if (threadIdx.x == 0) {
-    lds[0] = __hip_atomic_fetch_add(const_cast<unsigned*>(sync_hdr) + kEpochWord, 0u, __ATOMIC_RELAXED,
-                                    __HIP_MEMORY_SCOPE_AGENT);
-    lds[1] = __hip_atomic_load(sync_hdr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lds[1]) report_status(sync_hdr, kStatusAbortedRegion);
-  }
-  __syncthreads();
-  return (lds[0] & 0xffffu) << 16;
+// a launch that prepares `hdr`'s region for the next launch: keep its previous launch's failure (sticky)
+__device__ __forceinline__ void rearm_abort_word(unsigned* hdr) {
+  const unsigned old = __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (old) __hip_atomic_fetch_or(hdr + kStickyWord, old, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool launch_aborted(const unsigned* lds) { return lds[1] != 0u; }
+// harvest: region i's abort word | sticky bits -> the context's status words ([0] a wait timed out, [1] a
+// launch started on an aborted region), then cleared.  One thread per region.
+constexpr int kMaxHarvest = 8;
+struct HarvestArgs {
+  char* region[kMaxHarvest];
+  int n;
+  unsigned* status;
+};
+static __global__ __launch_bounds__(64) void sync_harvest(HarvestArgs h) {
+  const int i = threadIdx.x;
+  if (i >= h.n) return;
+  unsigned* hdr = reinterpret_cast<unsigned*>(h.region[i]);
+  const unsigned v = __hip_atomic_exchange(hdr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) |
+                     __hip_atomic_exchange(hdr + kStickyWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (v) __hip_atomic_store(h.status + 4 + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);  // diagnostic: raw bits
+  if (v & 1u) __hip_atomic_store(h.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (v & 2u) __hip_atomic_store(h.status + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// status null: nothing reported (no launch)
+inline int launch_sync_harvest(hipStream_t st, void* const* regions, int n, unsigned* status) {
+  if (!status || n <= 0) return 0;
+  HarvestArgs h{};
+  S2S_REQUIRE(n <= kMaxHarvest, "harvest: too many regions");
+  for (int i = 0; i < n; ++i) h.region[i] = static_cast<char*>(regions[i]);
+  h.n = n;
+  h.status = status;
+  hipLaunchKernelGGL(sync_harvest, dim3(1), dim3(64), 0, st, h);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+// tag base of this launch (all threads call; one barrier)
+__device__ __forceinline__ unsigned launch_tagbase(const unsigned* sync_hdr, unsigned* lds) {
+  if (threadIdx.x == 0)
+    *lds = __hip_atomic_fetch_add(const_cast<unsigned*>(sync_hdr) + kEpochWord, 0u, __ATOMIC_RELAXED,
+                                  __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  return (*lds & 0xffffu) << 16;
+}
 
 // ---- XCD-local chains
 // A chain = the workgroups that hand data to each other (independent of other chains).  Launches

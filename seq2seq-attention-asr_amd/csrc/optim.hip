@@ -182,6 +182,14 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
   return 0;
 }
 
+// the gradient-noise counter t (gradnoise.t, timit.lua:312) of a state: a resumed trainer sets it from its
+// checkpointed table; stream-ordered, no sync (the next step increments it before drawing)
+int optim_set_noise_step(hipStream_t st, void* state, size_t n, unsigned t) {
+  const OptState s = carve_state(state, n);
+  S2S_CHECK_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.scal + 3), (int)t, 1, st));
+  return 0;
+}
+
 // zero paramVariance / accDelta (optim.adadelta's lazily created state) and the noise counter t
 int optim_state_reset(hipStream_t st, void* state, size_t n) {
   S2S_CHECK_HIP(hipMemsetAsync(state, 0, optim_state_bytes(n), st));

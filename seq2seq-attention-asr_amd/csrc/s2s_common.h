@@ -194,6 +194,7 @@ struct Bump {
 
 // ---------------------------------------------------------------- optimizer (optim.hip)
 size_t optim_state_bytes(size_t n);
+int optim_set_noise_step(hipStream_t st, void* state, size_t n, unsigned t);
 int optim_state_reset(hipStream_t st, void* state, size_t n);
 struct OptimConfig {
   float rho, eps, maxnorm, weightDecay, colnorm_max, gradnoise_eta, gradnoise_gamma;

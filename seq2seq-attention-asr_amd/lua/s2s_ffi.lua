@@ -81,6 +81,7 @@ const void* s2s_model_attn_saved(const s2s_model_dims* d, const void* workspace)
 typedef struct { float rho, eps, maxnorm, weightDecay, colnorm_max; float gradnoise_eta, gradnoise_gamma; unsigned long long gradnoise_seed; } s2s_optim_config;
 size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);
+int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n, unsigned t);
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params, float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
 int s2s_model_weight_matrices(const s2s_model_dims* d, long* mats);
 int s2s_prof_enable(int on);
@@ -290,7 +291,13 @@ end
 -- the trainer's post-backward block (timit/timit.lua:292-347): clip, L2, optim.adadelta, column-norm
 -- constraint, on the flat parameters / gradients; state is a CudaByteTensor kept across steps
 -- (zeroed on first use, as optim.adadelta's paramVariance / accDelta start at 0).
-function M.adadelta_step(ctx, stream, d, opt, params, grads, state, gradnorm)
+-- gradnoise: the trainer's table {eta, gamma, t} (timit.lua:185-189; restored from model.gradnoise on a
+-- resume, timit.lua:92), passed explicitly.  nil means the exp configs' {eta = 0} (no noise) -- NOT the
+-- trainer's own fallback eta = 1e-3 (timit.lua:185-189), which a caller must pass in to get it.  With eta ~= 0
+-- the device counter is set to gradnoise.t before the step and the table's t is advanced as the reference
+-- does (timit.lua:312), so a resumed run continues the noise schedule; gradnoise.seed (default 0x5EED) keys
+-- the counter-based normals and must be equal on every data-parallel rank.
+function M.adadelta_step(ctx, stream, d, opt, params, grads, state, gradnorm, gradnoise)
    local n = params:nElement()
    if not M._mats or M._mats_d ~= d then
       local nm = C.s2s_model_weight_matrices(d, nil)
@@ -307,9 +314,13 @@ function M.adadelta_step(ctx, stream, d, opt, params, grads, state, gradnorm)
    cfg.rho, cfg.eps = opt.rho or 0.95, opt.eps or 1e-8
    cfg.maxnorm, cfg.weightDecay = opt.maxnorm or 1e20, opt.weightDecay or 0
    cfg.colnorm_max = opt.colnormconstr and (opt.colnorm_max or 1) or 0
-   local gn = opt.gradnoise or {}   -- the trainer's gradnoise = {eta, gamma, t} (timit.lua:185-189)
+   local gn = gradnoise or {eta = 0, gamma = 0.55, t = 0}
    cfg.gradnoise_eta, cfg.gradnoise_gamma = gn.eta or 0, gn.gamma or 0.55
    cfg.gradnoise_seed = gn.seed or 0x5EED
+   if cfg.gradnoise_eta ~= 0 then
+      M.check(C.s2s_optim_set_noise_step(ctx, stream, vptr(state), n, gn.t or 0))
+      gn.t = (gn.t or 0) + 1
+   end
    M.check(C.s2s_optim_adadelta_step(ctx, stream, cfg, dptr(params), dptr(grads), n, vptr(state), M._mats,
                                      M._nmats, gradnorm and dptr(gradnorm) or nil))
 end

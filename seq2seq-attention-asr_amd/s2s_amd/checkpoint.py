@@ -49,12 +49,23 @@ def load_flat(path):
 
 def save(path, model, optimizer=None, meta=None):
     """torch.save(paths.concat(savedir, 'model.t7'), model) for a ChorowskiBaseline (+ its Adadelta).
-    The step counter and dropout seed base travel in the metadata, so a resumed run continues the
-    dropout mask sequence instead of replaying it from step 1."""
+    The step counter and the user seed travel in the metadata, so a resumed run continues the dropout
+    mask sequence instead of replaying it from step 1.  The per-rank seed base is NOT saved: every
+    data-parallel rank loads the same file and re-derives its own base from (seed, rank)."""
     meta = dict(meta or {})
     meta.setdefault("steps", int(getattr(model, "_steps", 0)))
-    meta.setdefault("dropout_seed_base", str(int(getattr(model, "dropout_seed_base", 0))))
+    meta.setdefault("seed", str(int(getattr(model, "seed", 0))))
     save_flat(path, model.cfg, model.params, optimizer.state if optimizer is not None else None, meta)
+
+
+def seed_base_for(meta, rank, default):
+    """The loading rank's dropout seed base: _mix64(user seed, rank), so replicas resumed from one file keep
+    drawing independent nn.Dropout masks (the base mixes in the rank, model.py).  A checkpoint without the
+    user seed leaves `default` (the model's own base) in place."""
+    from .model import _mix64
+    if "seed" not in meta:
+        return default
+    return _mix64(int(meta["seed"]), int(rank))
 
 
 def load(path, model=None, optimizer=None):
@@ -69,8 +80,10 @@ def load(path, model=None, optimizer=None):
     model.params.copy_(params.to(model.params.device))
     if "steps" in meta:
         model._steps = int(meta["steps"])
-    if "dropout_seed_base" in meta:
-        model.dropout_seed_base = int(meta["dropout_seed_base"])
+    from .model import _dist_rank
+    if "seed" in meta:
+        model.seed = int(meta["seed"])
+    model.dropout_seed_base = seed_base_for(meta, _dist_rank(), model.dropout_seed_base)
     if optimizer is not None:
         if state is None or state.numel() != optimizer.state.numel():
             raise ValueError("checkpoint holds no matching optimizer state")

@@ -150,6 +150,7 @@ class ChorowskiBaseline:
         self._steps = 0
         # default dropout seeds: a per-step counter mixed with the init seed and the data-parallel rank,
         # so replicas draw independent nn.Dropout masks (the reference draws a fresh mask per forward)
+        self.seed = int(seed)
         self.dropout_seed_base = _mix64(seed, _dist_rank())
         self._check_layout()
 
@@ -218,7 +219,21 @@ class ChorowskiBaseline:
         that dist.allreduce_buckets waits on.
         frame_lengths / label_lengths: (B,) frames and labels per utterance of a padded variable-length
         batch (each in [1, L] / [1, T]): the step then equals the reference's per-utterance loop over the
-        unpadded utterances (timit/timit.lua:239-295); logp rows past T_b are padding."""
+        unpadded utterances (timit/timit.lua:239-295); logp rows past T_b are padding.
+        stream: the step runs there; it first waits for the caller's current stream (inputs and an injected
+        mask written there are complete), and every host-side tensor op of the step (mask / lengths copies
+        into the model-owned buffers) is issued on it too.  Outputs are ready on `stream`."""
+        if stream is not None and stream != torch.cuda.current_stream(self.device):
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):
+                return self._step(x, labels, scale, zero_grads, normalizeNLL, logp, nll, stream, dropout_seed,
+                                  dropout_mask, bucket_events, frame_lengths, label_lengths)
+        return self._step(x, labels, scale, zero_grads, normalizeNLL, logp, nll, stream, dropout_seed, dropout_mask,
+                          bucket_events, frame_lengths, label_lengths)
+
+    def _step(self, x, labels, scale, zero_grads, normalizeNLL, logp, nll, stream, dropout_seed, dropout_mask,
+              bucket_events, frame_lengths, label_lengths):
+        # every torch op here runs on the step's stream (step() entered its context when it differs)
         if x.dim() == 2:
             x = x[None]
         if labels.dim() == 1:
@@ -268,12 +283,8 @@ class ChorowskiBaseline:
                 buf = torch.empty((2, B), dtype=torch.int32, device=self.device)
                 self._lenbufs[B] = buf
             host = torch.stack([fl, tl]).pin_memory()
-            if stream is not None:
-                with torch.cuda.stream(stream):
-                    buf.copy_(host, non_blocking=True)
-            else:
-                buf.copy_(host, non_blocking=True)
-            self._len_host = host  # kept alive until the copy has run
+            buf.copy_(host, non_blocking=True)  # on the step's stream; the caching host allocator keeps
+            self._len_host = host                # the pinned source alive until the copy has run
             d.frame_lengths = buf[0].data_ptr()
             d.label_lengths = buf[1].data_ptr()
         flags = (_lib.S2S_ZERO_GRADS if zero_grads else 0) | (_lib.S2S_NORMALIZE_NLL if normalizeNLL else 0)
@@ -295,6 +306,10 @@ class ChorowskiBaseline:
         Returns nll (B,) in input order and the per-utterance logp list ((T_i, O) each)."""
         if len(xs) != len(labels) or not xs:
             raise ValueError("step_ragged needs one label sequence per utterance")
+        if stream is not None and stream != torch.cuda.current_stream(self.device):
+            stream.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(stream):  # padding, the steps and the output clones all on `stream`
+                return self.step_ragged(xs, labels, max_batch, normalizeNLL, stream)
         B = len(xs)
         scale = 1.0 / B if B > 1 else 1.0
         nll = torch.empty(B, device=self.device, dtype=torch.float32)

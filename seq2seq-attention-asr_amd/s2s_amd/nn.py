@@ -46,6 +46,8 @@ class Context:
         (default: the current stream): 0, or S2S_STATUS_HANDOFF_TIMEOUT | S2S_STATUS_ABORTED_REGION.  While it
         is nonzero every compute call of the context raises S2SError; clear=True resets it."""
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        if not hasattr(lib, "s2s_ctx_status"):  # an older A/B build (S2S_HIP_LIB) has no status words
+            return 0
         v = ctypes.c_int()
         check(lib.s2s_ctx_status(self.handle, st, ctypes.byref(v), 1 if clear else 0))
         return v.value

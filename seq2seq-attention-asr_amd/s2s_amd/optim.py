@@ -58,6 +58,11 @@ class Adadelta:
         self.gradnorm = torch.zeros(1, dtype=torch.float32, device=params.device)
         self.ctx = get_context(params.device.index)
 
+    def set_noise_step(self, t, stream=None):
+        """gradnoise.t of a resumed run (timit/timit.lua:92, 312): the next step draws with t + 1."""
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        check(lib.s2s_optim_set_noise_step(self.ctx.handle, st, dptr(self.state), self.n, int(t)))
+
     def step(self, stream=None):
         """One update; self.gradnorm holds ||g|| before clipping (timit.lua:297 gradnorms)."""
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()

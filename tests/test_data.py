@@ -141,6 +141,20 @@ def test_step_ragged_equals_per_utterance_loop():
     assert np.abs(g - gref).max() / np.abs(gref).max() < 1e-4
 
 
+def test_checkpoint_seed_base_is_per_rank():
+    """Every data-parallel rank loads the same checkpoint: each must re-derive its own dropout seed base from
+    the saved user seed and its rank (the ranks' masks stay independent after a resume), and the same rank
+    must get back the base it had before saving."""
+    from s2s_amd import checkpoint
+    from s2s_amd.model import _mix64
+    meta = {"steps": 5, "seed": "1234"}
+    b0 = checkpoint.seed_base_for(meta, 0, default=-1)
+    b1 = checkpoint.seed_base_for(meta, 1, default=-1)
+    assert b0 != b1
+    assert b0 == _mix64(1234, 0) and b1 == _mix64(1234, 1)
+    assert checkpoint.seed_base_for({"steps": 5}, 1, default=42) == 42  # older file: keep the model's own
+
+
 @pytest.mark.gpu
 def test_checkpoint_restores_model_and_optimizer(tmp_path):
     if not torch.cuda.is_available():
@@ -161,8 +175,9 @@ def test_checkpoint_restores_model_and_optimizer(tmp_path):
     opt2 = optim.Adadelta(m2, colnormconstr=True)
     _, meta = checkpoint.load(p, m2, opt2)
     assert meta["epoch"] == 1
-    # the step counter and dropout seed base travel too (a resumed run continues the mask sequence)
-    assert m2._steps == m._steps == 1 and m2.dropout_seed_base == m.dropout_seed_base
+    # the step counter and user seed travel too (a resumed run continues the mask sequence); the same
+    # rank re-derives the same seed base
+    assert m2._steps == m._steps == 1 and m2.dropout_seed_base == m.dropout_seed_base and m2.seed == 1
     assert torch.equal(m2.params, m.params) and torch.equal(opt2.state, opt.state)
     # the restored pair continues identically
     for mm, oo in ((m, opt), (m2, opt2)):

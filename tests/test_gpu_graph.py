@@ -161,3 +161,29 @@ def test_decoder_accessors_after_model_step(s2s):
     close(ws[:, :, 0], cache["ws"], "Ws")
     assert torch.equal(ws[:, :, 7], ws[:, :, 0])
     close(model.decoder_Vh(), cache["Vh"], "Vh.output")
+
+
+def test_graph_step_on_explicit_stream_outside_its_context(s2s):
+    """step(..., stream=st) called while the CURRENT stream is another one (the advisor's round-2 case): the
+    injected dropout mask and the lengths are written into the model-owned buffers on `st`, after `st` has
+    waited for the current stream that produced them, so each replay reads its own step's mask -- equal
+    bitwise to an eager model stepping on the current stream."""
+    cfg = s2s.ModelConfig(**KW, dropout=0.5)
+    gm = s2s.ChorowskiBaseline(cfg, graph=True, overlap=True)
+    ref = s2s.ChorowskiBaseline(cfg)
+    ref.params.copy_(gm.params)
+    S, A = cfg.stateDepth, cfg.annotationDepth
+    st = torch.cuda.Stream()
+    x, lab = _inputs(3, 16, 5, 11)
+    g = torch.Generator(device="cuda").manual_seed(5)
+    for i in range(5):
+        mask = (torch.rand(3, 5, S + A, device="cuda", generator=g) > 0.5).float() * 2.0  # current stream
+        nll, logp = gm.step(x, lab, stream=st, dropout_mask=mask, frame_lengths=[16, 12 + i, 9],
+                            label_lengths=[5, 4, 3])
+        torch.cuda.current_stream().wait_stream(st)
+        got = (nll.clone(), logp.clone(), gm.grads.clone())
+        n2, l2 = ref.step(x, lab, dropout_mask=mask, frame_lengths=[16, 12 + i, 9], label_lengths=[5, 4, 3])
+        torch.cuda.synchronize()
+        assert torch.equal(got[1], l2) and torch.equal(got[0], n2), i
+        assert torch.equal(got[2], ref.grads), i
+    assert gm.ctx.graph_stats()[0] == 1  # one capture: mask and lengths live in stable model-owned buffers

@@ -623,6 +623,31 @@ def test_optimizer_step_matches_oracle(s2s, maxnorm, wd, colnorm, eta):
             assert np.linalg.norm(xs[off:off + r * c].reshape(r, c), axis=1).max() <= 1.0 + 1e-5
 
 
+def test_optimizer_noise_counter_resumes(s2s):
+    """A resumed trainer restores gradnoise = {eta, gamma, t} (timit/timit.lua:92) and continues the schedule
+    (t += 1, :312): s2s_optim_set_noise_step(t) on a fresh state draws the next step's noise with t + 1, the
+    oracle's state["gradnoise_t"] = t."""
+    cfg = s2s.ModelConfig()
+    n = sum(int(np.prod(s)) for _, s in s2s.param_shapes(cfg))
+    rng = np.random.default_rng(5)
+    x = (rng.standard_normal(n) * 0.08).astype(np.float32)
+    xg = cu(x)
+    gg = torch.empty_like(xg)
+    opt = s2s.optim.Adadelta(params=xg, grads=gg, rho=0.95, eps=1e-8, gradnoise_eta=1e-3, gradnoise_seed=7)
+    opt.set_noise_step(41)
+    xr, st = x.astype(np.float64), {"gradnoise_t": 41}
+    for it in range(2):
+        g = (rng.standard_normal(n) * 1e-3).astype(np.float32)
+        gg.copy_(cu(g))
+        opt.step()
+        gr = g.astype(np.float64)
+        orc.optimizer_step(xr, gr, st, 0.95, 1e-8, gradnoise_eta=1e-3, gradnoise_seed=7)
+        torch.cuda.synchronize()
+        assert_rel(gg.cpu().numpy(), gr, f"g[{it}]", 1e-5)
+        assert_rel(xg.cpu().numpy(), xr, f"x[{it}]", 1e-5)
+    assert st["gradnoise_t"] == 43
+
+
 @pytest.mark.parametrize("K,maxlen", [(1, 8), (5, 12)])
 def test_beam_search_matches_oracle(s2s, K, maxlen):
     """decoder:BeamSearch (Attention.lua:332-438) on the device for a batch of
