@@ -196,6 +196,10 @@ const float* s2s_attn_vh(const s2s_attn_dims* d, const void* saved);
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 /* (B, T, S+A) dropout multipliers of the last forward inside `saved` (NULL when dropout == 0) */
 const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
+/* (B, T, mlpDepth) int32 Maxout decisions of the last forward inside `saved`: which unit i < maxoutWindow of
+ * group j won (first maximum, TemporalMaxPooling; Maxout.lua:14-18) -- the discrete decision the backward
+ * routes each gradient row by (the fused Chorowski decoder_mlp only) */
+const int* s2s_attn_maxout_argmax(const s2s_attn_dims* d, const void* saved);
 
 /* decoder:BeamSearch(annotations, eos, K, maxseqlength) (Attention.lua:332-438; timit/timit.lua:401) for
  * B utterances at once, in evaluate() mode: h (B, L, A); eos and the output tokens 0-based; out (B, ldo),

@@ -342,7 +342,7 @@ def hybrid_features(alpha_prev: Array, P: Dict[str, Array], kW: int):
 
 
 def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfig",
-                  dropout_mask: Optional[Array] = None):
+                  dropout_mask: Optional[Array] = None, maxout_idx: Optional[Array] = None):
     """nn.Attention:updateOutput (Attention.lua:305-322) = decoder gModule
     {h, labelmask} -> RNNAttention over T steps (RNNAttention.lua:144-185).
 
@@ -362,7 +362,9 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
       y_in = Wy y + by; c_in = Wc c + bc; d = Wd [c_in; y_in] + bd   (:149-151)
       s = GRU(d, s_prev)         decoder_recurrent (model_chorowski_baseline.lua:48-51)
       logp = LogSoftMax(Wo Maxout([s; c]) + bo)   decoder_mlp (:53-59, Maxout.lua:14-18)
-    Vh = h V^T once per utterance (TCZB(A, Sc, 1), Attention.lua:43-47,202)."""
+    Vh = h V^T once per utterance (TCZB(A, Sc, 1), Attention.lua:43-47,202).
+    maxout_idx (B, T, M) ints (optional): take these Maxout winners instead of the argmax -- to compare an
+    implementation under ITS OWN discrete decisions (a reduced-precision run flips near ties)."""
     B, L, A = h.shape
     T = labels.shape[1]
     S, Sc, O, M, k = cfg.stateDepth, cfg.scoreDepth, cfg.outputDepth, cfg.mlpDepth, cfg.maxoutWindow
@@ -421,7 +423,7 @@ def attention_fwd(h: Array, labels: Array, P: Dict[str, Array], cfg: "ModelConfi
             v = v * dropout_mask[:, t]
         u = v @ P["Wm"].T + P["bm"]
         ug = u.reshape(B, M, k)
-        am = np.argmax(ug, axis=2)                                 # first max wins
+        am = np.argmax(ug, axis=2) if maxout_idx is None else np.asarray(maxout_idx[:, t], np.int64)  # first max wins
         m = np.take_along_axis(ug, am[..., None], 2)[..., 0]
         o = m @ P["Wo"].T + P["bo"]
         logp = log_softmax(o, 1)
@@ -671,7 +673,8 @@ def unflatten(flat: Array, cfg: ModelConfig) -> Dict[str, Array]:
 
 
 def training_step(x: Array, labels: Array, P: Dict[str, Array], cfg: ModelConfig,
-                  normalizeNLL: bool = True, dropout_mask: Optional[Array] = None):
+                  normalizeNLL: bool = True, dropout_mask: Optional[Array] = None,
+                  maxout_idx: Optional[Array] = None):
     """timit/timit.lua:240-295 for one optimizer step's gradient, B utterances of
     equal length: per utterance logp = fwd({X, onehot(Y)}) (:262-265);
     nll_b = -sum(onehot * logp) [/T] (:268-272, reporting only); dlogp = -onehot (:278);
@@ -681,7 +684,7 @@ def training_step(x: Array, labels: Array, P: Dict[str, Array], cfg: ModelConfig
     T = labels.shape[1]
     O = cfg.outputDepth
     enc, ecache = encoder_fwd(x, P, cfg.numLayers)
-    logp, acache = attention_fwd(enc, labels, P, cfg, dropout_mask)
+    logp, acache = attention_fwd(enc, labels, P, cfg, dropout_mask, maxout_idx)
     onehot = np.zeros((B, T, O), x.dtype)
     np.put_along_axis(onehot, labels[..., None], 1.0, axis=2)
     nll_b = -(onehot * logp).sum((1, 2))

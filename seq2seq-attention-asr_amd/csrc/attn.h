@@ -96,6 +96,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
                    const void* saved, const AttnGrads& G, float scale, void* scratch);
 // alpha (B, T, L) view into the saved buffer (Attention:alpha(), Attention.lua:241-243)
 const float* attn_saved_alpha(const AttnDims& d, const void* saved);
+const int* attn_saved_maxout_argmax(const AttnDims& d, const void* saved);
 // the sync-region headers the decoder launches of d's path use (both null for the per-step path); returns
 // how many (0 or 2) -- the caller harvests their failure words after the call (handoff.h)
 int attn_sync_regions(const AttnDims& d, void* saved, void* scratch, void** fwd, void** bwd);

@@ -1130,6 +1130,11 @@ const float* attn_saved_mono_ind(const AttnDims& d, const void* saved) {
   carve(d, &k, (char*)saved, nullptr);
   return k.IND;
 }
+const int* attn_saved_maxout_argmax(const AttnDims& d, const void* saved) {
+  AttnK k{};
+  carve(d, &k, (char*)saved, nullptr);
+  return k.AM;
+}
 const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved) {
   AttnK k{};
   carve(d, &k, (char*)saved, nullptr);

@@ -844,6 +844,9 @@ const float* s2s_attn_vh(const s2s_attn_dims* d, const void* saved) {
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_mono_ind(to_attn(d), saved) : nullptr;
 }
+const int* s2s_attn_maxout_argmax(const s2s_attn_dims* d, const void* saved) {
+  return d && saved ? attn_saved_maxout_argmax(to_attn(d), saved) : nullptr;
+}
 const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved) {
   return d && saved ? attn_saved_dropout_mask(to_attn(d), saved) : nullptr;
 }

@@ -42,6 +42,7 @@ const float* s2s_attn_ws(const s2s_attn_dims* d, const void* saved);
 const float* s2s_attn_vh(const s2s_attn_dims* d, const void* saved);
 const float* s2s_attn_mono_ind(const s2s_attn_dims* d, const void* saved);
 const float* s2s_attn_dropout_mask(const s2s_attn_dims* d, const void* saved);
+const int* s2s_attn_maxout_argmax(const s2s_attn_dims* d, const void* saved);
 size_t s2s_attn_beam_workspace_bytes(const s2s_attn_dims* d, int K, int maxseqlength);
 int s2s_attn_beam_search(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const float* const* params, int eos, int K, int maxseqlength, int* out, int ldo, int* out_len, float* out_score, void* workspace, size_t workspace_bytes);
 int s2s_attn_beam_init(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, const float* h, const float* const* params, int eos, int K, int maxseqlength, void* workspace, size_t workspace_bytes);

@@ -72,6 +72,7 @@ SIGNATURES = [
     ("s2s_attn_alpha", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mlp_input", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_mono_ind", c_void_p, [P(s2s_attn_dims), c_void_p]),
+    ("s2s_attn_maxout_argmax", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_ws", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_attn_vh", c_void_p, [P(s2s_attn_dims), c_void_p]),
     ("s2s_model_attn_dims", c_int, [P(s2s_model_dims), P(s2s_attn_dims)]),

@@ -41,7 +41,8 @@ def allreduce_buckets(grads: torch.Tensor, buckets, wait=None, comm_stream=None)
     under hipGraph replay), and bucket i's all-reduce is issued from comm_stream -- so it runs on
     RCCL while the BPTT of the encoder layers below is still in flight.  The caller's current stream
     then waits for every bucket (the optimizer reads the summed gradient).  Sums are elementwise,
-    so the result equals one all-reduce of the flat buffer."""
+    so the result equals one all-reduce of the flat buffer.  On CPU tensors (gloo) wait(i, None) is called
+    before bucket i's all-reduce is issued (tests drive the bucket order with it)."""
     if world() == 1:
         return grads
     works = []
@@ -55,7 +56,9 @@ def allreduce_buckets(grads: torch.Tensor, buckets, wait=None, comm_stream=None)
                 comm_stream.wait_stream(cur)
             with torch.cuda.stream(comm_stream):
                 works.append(dist.all_reduce(view, async_op=True))
-        else:
+        else:  # CPU tensors (gloo): wait(i, None) is the host-side "bucket i is final" hook
+            if wait is not None:
+                wait(i, None)
             works.append(dist.all_reduce(view, async_op=True))
     for w in works:
         w.wait()

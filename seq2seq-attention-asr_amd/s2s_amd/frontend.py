@@ -44,6 +44,7 @@ class TemporalConvolution(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         x = input if input.dim() == 3 else input.unsqueeze(0)
         if x.dim() != 3 or x.shape[2] != self.inputFrameSize:
             raise S2SArgumentError("TemporalConvolution: input must be (L, inputFrameSize) or (B, L, inputFrameSize)")
@@ -77,6 +78,7 @@ class TemporalMaxPooling(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         x = input if input.dim() == 3 else input.unsqueeze(0)
         B, L, D = x.shape
         Lo = (L - self.kW) // self.dW + 1
@@ -103,6 +105,7 @@ class ReLU(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         self.output = torch.empty_like(input)
         check(lib.s2s_relu_fwd(_ctx(input), stream_ptr(), input.numel(), dptr(input), dptr(self.output)))
         return self.output
@@ -156,6 +159,7 @@ class LogSoftMax(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         n = input.shape[-1]
         self.output = torch.empty_like(input)
         check(lib.s2s_logsoftmax_fwd(_ctx(input), stream_ptr(), input.numel() // n, n, dptr(input),
@@ -195,6 +199,7 @@ class SpatialConvolutionMM(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         x = input if input.dim() == 4 else input.unsqueeze(0)
         B, C, H, W = self._dims(x)
         y = torch.empty((B, self.nOutputPlane, H - self.kH + 1, W - self.kW + 1), device=x.device,
@@ -235,6 +240,7 @@ class SpatialMaxPooling(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         x = input if input.dim() == 4 else input.unsqueeze(0)
         B, C, H, W = x.shape
         Ho, Wo = (H - self.kH) // self.dH + 1, (W - self.kW) // self.dW + 1
@@ -267,6 +273,7 @@ class Transpose2(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         if input.dim() not in (3, 4):
             raise S2SArgumentError("inconsistent tensor size")  # Transpose2.lua:29
         x = input if input.dim() == 4 else input.unsqueeze(0)

@@ -107,7 +107,10 @@ def grad_buckets(cfg: ModelConfig):
     d = _lib.s2s_model_dims(1, 1, 1, c.inputFrameSize, c.hiddenFrameSize, c.outputFrameSize, c.numLayers,
                             c.scoreDepth, c.stateDepth, c.outputDepth, c.mlpDepth, c.maxoutWindow, c.penalty, 0.0)
     out = []
-    for i in range(lib.s2s_model_bucket_count(ctypes.byref(d))):
+    nb = lib.s2s_model_bucket_count(ctypes.byref(d))
+    if nb < 0:
+        check(1)  # the dims are not a model the library runs (s2s_last_error says why)
+    for i in range(nb):
         off, n = ctypes.c_size_t(), ctypes.c_size_t()
         check(lib.s2s_model_bucket(ctypes.byref(d), i, ctypes.byref(off), ctypes.byref(n)))
         out.append((off.value, n.value))
@@ -367,6 +370,12 @@ class ChorowskiBaseline:
         ad, sv = self._attn()
         return saved_view(self._wsbuf, lib.s2s_attn_vh(ctypes.byref(ad), ctypes.c_void_p(sv)),
                           (ad.B, ad.L, ad.scoreDepth))
+
+    def decoder_maxout_argmax(self):
+        """(B, T, mlpDepth) int32 Maxout decisions of the last step's decoder (which unit of each group won)."""
+        ad, sv = self._attn()
+        return saved_view(self._wsbuf, lib.s2s_attn_maxout_argmax(ctypes.byref(ad), ctypes.c_void_p(sv)),
+                          (ad.B, ad.T, ad.mlpDepth), torch.int32)
 
     def dropout_mask_used(self):
         """(B, T, S+A) nn.Dropout multipliers of the last step (None without dropout)."""

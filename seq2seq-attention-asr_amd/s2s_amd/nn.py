@@ -159,6 +159,17 @@ class Module:
     def evaluate(self):
         self.train = False
 
+    def _check_params(self, x):
+        """every parameter / gradient buffer must be a contiguous float32 tensor on x's device: the kernels take
+        raw device pointers, and a host tensor's pointer would fault on the GPU (call .cuda() first)"""
+        ws, gs = self.parameters()
+        for i, t in enumerate(ws + gs):
+            if t is None:
+                continue
+            if not (t.is_cuda and t.device == x.device and t.dtype == torch.float32 and t.is_contiguous()):
+                raise S2SArgumentError(f"{type(self).__name__}: parameter {i} must be a contiguous float32 tensor on "
+                                       f"{x.device} (is {t.device}, {t.dtype}); call .cuda() first")
+
     def cuda(self, device=None):
         dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
         ws, gs = self.parameters()
@@ -266,6 +277,7 @@ class _GruSeq(Module):
 
     def updateOutput(self, input):
         _require_cuda_f32(input, "input")
+        self._check_params(input)
         B, L, D = self._shape(input)
         H, nd = self.dimoutput, len(self.cells)
         if D != self.cells[0].diminput:
@@ -562,6 +574,7 @@ class Attention(Module):
         if h.dim() not in (2, 3):
             raise S2SArgumentError("x must be 2d or 3d")  # Attention.lua:316
         _require_cuda_f32(h, "h")
+        self._check_params(h)
         lab = self.labels_from(y, self.outputDepth)
         if lab.dim() == 1:
             lab = lab[None]
@@ -688,6 +701,13 @@ class Attention(Module):
         n = d.B * d.T
         return self._saved[off:off + 4 * n].view(torch.float32).view(d.B, d.T)
 
+    def maxout_argmax(self):
+        """(B, T, mlpDepth) int32: which unit of each Maxout group won in the last forward (first maximum,
+        Maxout.lua:14-18) -- the discrete decision its backward routes each gradient row by."""
+        d = self._d
+        return saved_view(self._saved, lib.s2s_attn_maxout_argmax(ctypes.byref(d), dptr(self._saved)),
+                          (d.B, d.T, d.mlpDepth), torch.int32)
+
     def alpha(self):
         """Attention:alpha() (Attention.lua:241-243): (B, T, L) attention weights of the last forward."""
         d = self._d
@@ -715,15 +735,15 @@ class Attention(Module):
         return vh[..., :self.scoreDepth]
 
 
-def saved_view(buf, p, shape):
-    """float32 view of `shape` at device address p inside the byte buffer `buf`."""
+def saved_view(buf, p, shape, dtype=torch.float32):
+    """`dtype` (4-byte) view of `shape` at device address p inside the byte buffer `buf`."""
     if not p:
         raise S2SArgumentError("no such tensor in the saved buffer")
     off = p - buf.data_ptr()
     n = math.prod(shape)
     if off < 0 or off + 4 * n > buf.numel():
         raise S2SArgumentError("saved-buffer view out of range")
-    return buf[off:off + 4 * n].view(torch.float32).view(*shape)
+    return buf[off:off + 4 * n].view(dtype).view(*shape)
 
 
 def nll_seed(logp, labels, normalize=False, label_lengths=None):

@@ -22,8 +22,12 @@ def _free_port():
     return p
 
 
-def _cfg():
+def _cfg(abi=False):
+    """abi: dims the C ABI accepts (hidden / state sizes multiples of 16), for the real bucket layout"""
     from oracle import s2s_oracle as orc
+    if abi:
+        return orc.ModelConfig(inputFrameSize=6, hiddenFrameSize=16, outputFrameSize=16, scoreDepth=16,
+                               stateDepth=16, outputDepth=7, mlpDepth=3, maxoutWindow=2, numLayers=2)
     return orc.ModelConfig(inputFrameSize=6, hiddenFrameSize=4, outputFrameSize=4, scoreDepth=5, stateDepth=4,
                            outputDepth=7, mlpDepth=3, maxoutWindow=2, numLayers=2)
 
@@ -40,7 +44,7 @@ def _worker(rank, world, port, B, out_path, buckets):
         "s2s_dist", os.path.join(ROOT, "seq2seq-attention-asr_amd", "s2s_amd", "dist.py"))
     sd = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(sd)
-    cfg = _cfg()
+    cfg = _cfg(buckets == "events")
     P = orc.init_params(cfg, seed=5)
     x, labels = orc.synthetic_batch(cfg, B * world, 6, 4, seed=9, pad=1, eos=2)
     xs, ls = x[rank * B:(rank + 1) * B], labels[rank * B:(rank + 1) * B]
@@ -62,6 +66,28 @@ def _worker(rank, world, port, B, out_path, buckets):
         assert cover[0][0] == 0 and sum(n for _, n in mb) == flat.numel()
         assert all(o + n == o2 for (o, n), (o2, _) in zip(cover, cover[1:]))
         sd.allreduce_buckets(flat, mb)
+    elif buckets == "events":
+        # the real bucket layout from the C ABI (s2s_model_bucket) and the step's "bucket i final" hook: the
+        # buffer holds garbage until wait(i) finalises bucket i (as the step's event does on the GPU), so a
+        # bucket reduced before its wait -- or a wrong layout -- corrupts the sum
+        import s2s_amd
+        mcfg = s2s_amd.ModelConfig(**{f: getattr(cfg, f) for f in (
+            "inputFrameSize", "hiddenFrameSize", "outputFrameSize", "scoreDepth", "stateDepth", "outputDepth",
+            "mlpDepth", "maxoutWindow", "numLayers")})
+        mb = s2s_amd.model.grad_buckets(mcfg)
+        final = flat.clone()
+        flat.fill_(float("nan"))
+        order = []
+
+        def wait(i, stream):
+            assert stream is None
+            off, n = mb[i]
+            flat[off:off + n] = final[off:off + n]
+            order.append(i)
+        sd.allreduce_buckets(flat, mb, wait=wait)
+        assert order == list(range(cfg.numLayers + 1)), order
+        # decoder first, then encoder layers top-down: bucket 0 starts where the encoder ends
+        assert mb[0][0] + mb[0][1] == flat.numel() and mb[-1][0] == 0
     else:
         sd.allreduce_gradients(flat, bucket_elems=buckets)
     if rank == 0:
@@ -70,14 +96,14 @@ def _worker(rank, world, port, B, out_path, buckets):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("buckets", [0, 37, "model"])
+@pytest.mark.parametrize("buckets", [0, 37, "model", "events"])
 def test_dp_allreduce_equals_global_batch(tmp_path, buckets):
     from oracle import s2s_oracle as orc
     world, B = 2, 2
     out = str(tmp_path / "g.npy")
     mp.start_processes(_worker, args=(world, _free_port(), B, out, buckets), nprocs=world, start_method="spawn")
     got = np.load(out)
-    cfg = _cfg()
+    cfg = _cfg(buckets == "events")
     P = orc.init_params(cfg, seed=5)
     x, labels = orc.synthetic_batch(cfg, B * world, 6, 4, seed=9, pad=1, eos=2)
     _, G, _, _ = orc.training_step(x, labels, P, cfg)

@@ -53,6 +53,16 @@ def test_oracle_tconv_matches_torch(B, L, Din, Dout, kW):
         assert_rel(g, r.detach().numpy(), n, 1e-12)
 
 
+def test_oracle_sconv_notebook_known_answer():
+    """Attention.ipynb cell 2 (the "Vh" cell): SpatialConvolutionMM(1, scoreDepth=4, kW=annotationDepth=5, kH=1)
+    with every parameter filled with 1 (p:fill(1)), on ones(1, L=10, 5) -> a (4, 10, 1) output of 6s (5 ones
+    + bias 1).  Pins the (out, in*kH*kW) weight / bias layout of the SpatialConvolutionMM restatement."""
+    Wt = np.ones((4, 1 * 1 * 5))
+    y = fo.sconv_fwd(np.ones((1, 1, 10, 5)), Wt, np.ones(4), kH=1, kW=5)
+    assert y.shape == (1, 4, 10, 1)
+    np.testing.assert_array_equal(y, np.full((1, 4, 10, 1), 6.0))
+
+
 def test_oracle_tmaxpool_matches_torch():
     rng = np.random.default_rng(3)
     x = rng.standard_normal((2, 13, 5))
@@ -232,6 +242,19 @@ def test_sconv_matches_oracle(fe, B, C, H, W, O, k, relu):
     assert_rel(_np(dx), dxr, "dx")
     assert_rel(_np(m.gradWeight), 0.5 + 2.0 * dWr, "dW")
     assert_rel(_np(m.gradBias), 2.0 * dbr, "db")
+
+
+@pytest.mark.gpu
+def test_sconv_notebook_known_answer_on_gpu(fe):
+    """Attention.ipynb cell 2 on the HIP SpatialConvolutionMM: every parameter 1, input ones(1, 10, 5) (3-D, one
+    image), kW = 5, kH = 1 -> (4, 10, 1) of 6s, exactly."""
+    conv = fe.SpatialConvolutionMM(1, 4, 5, 1).cuda()
+    conv.weight.fill_(1.0)
+    conv.bias.fill_(1.0)
+    y = conv.forward(torch.ones(1, 10, 5, device="cuda"))
+    torch.cuda.synchronize()
+    assert tuple(y.shape) == (4, 10, 1)
+    assert torch.equal(y.cpu(), torch.full((4, 10, 1), 6.0))
 
 
 @pytest.mark.gpu
@@ -839,3 +862,16 @@ def test_beam_search_keeps_K_hypotheses_from_the_first_step(fe, K):
     h = rng.standard_normal((B, L, A)) * 1.5
     for maxlen in (1, 2, 3, 5, 8):
         _check_beam(att, h, P, cfg, eos, K, maxlen)
+
+
+@pytest.mark.gpu
+def test_host_parameters_are_refused_not_launched(fe):
+    """A module whose parameters are still host tensors (no .cuda()) must raise before any launch: the kernels
+    take raw device pointers and a host pointer would fault on the GPU."""
+    import s2s_amd
+    conv = fe.SpatialConvolutionMM(1, 4, 5, 1)
+    with pytest.raises(s2s_amd.nn.S2SArgumentError, match="cuda"):
+        conv.forward(torch.ones(1, 10, 5, device="cuda"))
+    rnn = s2s_amd.RNN(s2s_amd.GRU(8, 16))
+    with pytest.raises(s2s_amd.nn.S2SArgumentError, match="cuda"):
+        rnn.forward(torch.ones(2, 5, 8, device="cuda"))

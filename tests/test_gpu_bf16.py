@@ -102,6 +102,67 @@ def test_model_step_bf16_config3_dims(lib, prec):
     assert errs["logp"] > 1e-6  # bf16 really ran (fp32 reaches ~2e-7 here)
 
 
+# With the Maxout decisions pinned (the oracle runs under the GPU's own winners, s2s_attn_maxout_argmax) the
+# discrete flips are gone and what is left is bf16 operand rounding (unit roundoff 2^-9 = 2e-3 per operand) carried
+# through the recurrences: the bars below are that, not the 0.2 of the unpinned comparison above.
+BF16_PINNED_LOGP_RTOL = 1e-3
+BF16_PINNED_GRAD_RTOL = 1e-2
+
+
+@pytest.mark.parametrize("B,fused", [(64, False), (16, True)])
+@pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
+def test_model_step_bf16_config3_decisions_pinned(lib, B, fused, prec):
+    """BASELINE config 3 as benched (model_chorowski_baseline_dropout.lua:56, bf16 MFMA): B = 64 -- the BiGRU
+    launches fill the chip, so the x-projections and dX run as separate bf16 GEMMs (asserted from the live kernel
+    profile: the persistent launches carry only the recurrence's flops) -- and B = 16, where the persistent
+    launches' spare slots compute them in fp32.  Reduced L / T for the float64 oracle, injected
+    dropout masks; the oracle runs under the GPU's own Maxout decisions (Maxout.lua:14-18), so every tensor is
+    held to the operand-rounding bar."""
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    from s2s_amd import profile as prof
+    cfg_o = orc.ModelConfig()
+    model = s2s_amd.ChorowskiBaseline(s2s_amd.ModelConfig(dropout=0.5), precision=prec)
+    P = orc.unflatten(model.params.cpu().double().numpy(), cfg_o)
+    L, T = 40, 12
+    x, labels = orc.synthetic_batch(cfg_o, B, L, T, seed=B, pad=10, eos=23)
+    rng = np.random.default_rng(B + 1)
+    mask = (rng.random((B, T, cfg_o.stateDepth + 2 * cfg_o.outputFrameSize)) >= 0.5) / 0.5
+    xs = torch.tensor(x, dtype=torch.float32, device="cuda")
+    ls = torch.tensor(labels, dtype=torch.int32, device="cuda")
+    ms = torch.tensor(mask, dtype=torch.float32, device="cuda")
+    lib.check(lib.lib.s2s_prof_enable(1))
+    try:
+        prof.collect()
+        nll, logp = model.step(xs, ls, dropout_mask=ms)
+        torch.cuda.synchronize()
+        agg = prof.collect()
+    finally:
+        lib.lib.s2s_prof_enable(0)
+    H = cfg_o.hiddenFrameSize
+    rec = 2.0 * 2 * B * L * 3 * H * H  # both directions' recurrence of one layer
+    fwd = agg["gru_fwd_persist"]
+    assert fwd["launches"] == 3
+    assert "gemm_bf16" in agg, sorted(agg)  # bf16 GEMMs ran
+    per = fwd["flops"] / fwd["launches"]
+    if fused:
+        assert per > 1.5 * rec, (per, rec)  # the x-projections were computed inside the launches
+    else:
+        assert abs(per - rec) <= 1e-6 * rec, (per, rec)  # recurrence only: x-projections by separate GEMMs
+        assert agg["gru_bwd_persist"]["flops"] / agg["gru_bwd_persist"]["launches"] <= 1.0001 * rec  # dX too
+    am = model.decoder_maxout_argmax().cpu().numpy()
+    assert am.shape == (B, T, cfg_o.mlpDepth) and am.min() >= 0 and am.max() < cfg_o.maxoutWindow
+    _, G, lref, _ = orc.training_step(x, labels, P, cfg_o, dropout_mask=mask, maxout_idx=am)
+    errs = {"logp": _rel(logp.cpu().numpy(), lref)}
+    Gg = orc.unflatten(model.grads.cpu().double().numpy(), cfg_o)
+    errs.update({"grad " + k: _rel(Gg[k], G[k]) for k in G})
+    print(f"config 3 B={B} {prec} rel L2 errs (Maxout decisions pinned):", {k: f"{v:.1e}" for k, v in errs.items()})
+    bad = {k: f"{v:.2e}" for k, v in errs.items()
+           if not v <= (BF16_PINNED_LOGP_RTOL if k == "logp" else BF16_PINNED_GRAD_RTOL)}
+    assert not bad, bad
+    assert errs["logp"] > 1e-6  # bf16 really ran (fp32 reaches ~2e-7 here)
+
+
 @pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
 def test_vgg_model_step_bf16_config5(lib, prec):
     """BASELINE config 5 (librispeech/model_vgg.lua, bf16): full width (1x1 layers 2048), B = 1, L = 256,

@@ -315,3 +315,23 @@ def test_gradient_noise_draws_and_schedule():
         orc.optimizer_step(x, g, st, gradnoise_eta=1e-3, gradnoise_gamma=0.55, gradnoise_seed=3)
         np.testing.assert_allclose(g, orc.gradient_noise(n, 3, t) * (1e-3 / (1 + t) ** 0.55) ** 0.5, rtol=1e-12)
     assert st["gradnoise_t"] == 2
+
+
+def test_forced_maxout_decisions():
+    """training_step(maxout_idx=...) runs the step under given Maxout winners: its own argmax reproduces the
+    free run exactly, and a different winner changes m (and logp) accordingly."""
+    cfg = orc.ModelConfig(inputFrameSize=6, hiddenFrameSize=4, outputFrameSize=4, scoreDepth=5, stateDepth=4,
+                          outputDepth=5, mlpDepth=3, maxoutWindow=3, numLayers=1)
+    P = orc.init_params(cfg, seed=3)
+    x, labels = orc.synthetic_batch(cfg, 2, 7, 4, seed=1, pad=1, eos=2)
+    enc, _ = orc.encoder_fwd(x, P, cfg.numLayers)
+    lp, cache = orc.attention_fwd(enc, labels, P, cfg)
+    am = cache["argmax"]
+    nll, G, lp2, _ = orc.training_step(x, labels, P, cfg, maxout_idx=am)
+    nll0, G0, lp0, _ = orc.training_step(x, labels, P, cfg)
+    assert np.array_equal(lp2, lp0) and nll == nll0
+    assert all(np.array_equal(G[k], G0[k]) for k in G)
+    other = (am + 1) % cfg.maxoutWindow
+    _, c2 = orc.attention_fwd(enc, labels, P, cfg, maxout_idx=other)
+    u = c2["u"].reshape(2, 4, cfg.mlpDepth, cfg.maxoutWindow)
+    np.testing.assert_array_equal(c2["m"], np.take_along_axis(u, other[..., None], 3)[..., 0])
