@@ -136,11 +136,46 @@ struct PArgs {
 
 // diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
 // end and p2 sweep start / done / end; forward p1 sub-phases: 6 = MFMA issued, 7 = reduced
+// S2S_GRU_DIAG=1 (a diagnostic build, tools/ab_variant.sh): 16 slots per (workgroup, step), slots 8.. hold the
+// poll passes of each sweep and the da_z sweep's end (tools/gru_stamps.py --diag); production builds keep 8
+#ifndef S2S_GRU_DIAG
+#define S2S_GRU_DIAG 0
+#endif
+constexpr int kStampSlots = S2S_GRU_DIAG ? 16 : 8;
 #define GRU_STAMP(ph)                                                                      \
   do {                                                                                     \
     if (a.stamps && threadIdx.x == 0)                                                      \
-      a.stamps[((long)lw * a.L + s) * 8 + (ph)] = __builtin_amdgcn_s_memrealtime();          \
+      a.stamps[((long)lw * a.L + s) * kStampSlots + (ph)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define GRU_STAMP_V(ph, v)                                                                 \
+  do {                                                                                     \
+    if (a.stamps && threadIdx.x == 0) a.stamps[((long)lw * a.L + s) * kStampSlots + (ph)] = (v); \
+  } while (0)
+#if S2S_GRU_DIAG
+// sweep_sent_tile counting its poll passes (diagnostic builds only)
+template <int NC>
+__device__ __forceinline__ bool sweep_sent_n(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
+                                             int wave, int lane, unsigned* abort_word, unsigned& n) {
+  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  unsigned spins = 0;
+  while (true) {
+    ++n;
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const long off = lo + 4L * 256 * (wave + 4 * i);
+      const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+      ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+      a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+#define SWEEP_SENT(slot_, ...) sweep_sent_n<NC>(__VA_ARGS__, npoll[slot_])
+#else
+#define SWEEP_SENT(slot_, ...) sweep_sent_tile<NC>(__VA_ARGS__)
+#endif
 std::atomic<unsigned long long*> g_gru_stamps[2] = {{nullptr}, {nullptr}};
 std::atomic<unsigned long long*> g_gru_pstamps[2] = {{nullptr}, {nullptr}};
 constexpr int kProdStampItems = 32;
@@ -495,8 +530,9 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   // z tiles publish h, r tiles q
   const bool loader = wave == 4;
-  if (!loader)
-    rearm_rect(isz ? g.s0 : g.s1, (long)B * H, L, H, b0, min(16, B - b0), isz ? c1 * 16 : c1 * 16 - H, 16);
+  if (!loader)  // this member's 1-KB tile of every (tile-major) slot
+    rearm_rect((isz ? g.s0 : g.s1) + (long)mt * 16 * H + (long)(isz ? c1 : c1 - H / 16) * 256, (long)a.MT * 16 * H, L,
+               16, 0, 16, 0, 16);
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
@@ -551,6 +587,8 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 
   const __amdgpu_buffer_rsrc_t hg = rsrc_of(g.g0), qg = rsrc_of(g.g1), hs = rsrc_of(g.s0), qs = rsrc_of(g.s1);
   const long slot = (long)B * H;  // granules per slot
+  const long slotS = (long)a.MT * 16 * H, tileS = (long)mt * 16 * H;  // tile-major sentinel slot, this row tile
+  const int rowt = min(b0 + (lane & 15), B - 1) - b0;
   const int br = min(b0 + (lane & 15), B - 1);
   const int ob = b0 + (tid >> 4), on = c1 * 16 + (tid & 15);  // this thread's output
   const bool live = ob < B;
@@ -572,9 +610,15 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(0);
     if (s > 0) {
       float4 av[NC];
-      if (loc) ok = sweep_sent<NC>(av, hs, 4 * ((s - 1) * slot + (long)br * H), wave, lane, a.abort_word);
+#if S2S_GRU_DIAG
+      unsigned npoll[1] = {0};
+#endif
+      if (loc) ok = SWEEP_SENT(0, av, hs, 4 * ((s - 1) * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
       GRU_STAMP(1);
+#if S2S_GRU_DIAG
+      GRU_STAMP_V(8, npoll[0]);
+#endif
       acc = mfma_chunks<NC>(av, w1);
       // r tiles: the swept operand already holds h_{t-1} of this tile's 16 units (chunk it of
       // wave wt); park it in LDS for the q = r * h epilogue (read after the reduce barrier)
@@ -601,7 +645,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
         const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
         const float q = gate * hp;
         if (loc) {  // critical first
-          if (live) put_sent(g.s1 + s * slot + (long)ob * H + j, q);
+          if (live) put_sent(g.s1 + s * slotS + tile_off(ob, j, H), q);
         } else {
           put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live);
         }
@@ -620,9 +664,15 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     GRU_STAMP(3);
     if (s > 0) {
       float4 av[NC];
-      if (loc) ok = sweep_sent<NC>(av, qs, 4 * (s * slot + (long)br * H), wave, lane, a.abort_word);
+#if S2S_GRU_DIAG
+      unsigned npoll[1] = {0};
+#endif
+      if (loc) ok = SWEEP_SENT(0, av, qs, 4 * (s * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
       GRU_STAMP(4);
+#if S2S_GRU_DIAG
+      GRU_STAMP_V(9, npoll[0]);
+#endif
       acc = mfma_chunks<NC>(av, w2);
     }
     sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
@@ -633,7 +683,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
       if (t >= lenb) hreg = 0.f;
       if (loc) {  // first
-        if (live) put_sent(g.s0 + s * slot + (long)ob * H + on, hreg);
+        if (live) put_sent(g.s0 + s * slotS + tile_off(ob, on, H), hreg);
       } else {
         put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live);
       }
@@ -683,10 +733,11 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const bool loader = wave == 4;
-  if (!loader) {
-    rearm_rect(g.s0, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
-    rearm_rect(g.s1, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
-    rearm_rect(g.s2, (long)B * H, L, H, b0, min(16, B - b0), c * 16, 16);
+  if (!loader) {  // this member's 1-KB tile of every (tile-major) slot
+    const long tt = (long)mt * 16 * H + (long)c * 256, st = (long)a.MT * 16 * H;
+    rearm_rect(g.s0 + tt, st, L, 16, 0, 16, 0, 16);
+    rearm_rect(g.s1 + tt, st, L, 16, 0, 16, 0, 16);
+    rearm_rect(g.s2 + tt, st, L, 16, 0, 16, 0, 16);
   }
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
@@ -751,6 +802,8 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const __amdgpu_buffer_rsrc_t zs = rsrc_of(g.s0), rs_ = rsrc_of(g.s1), hs = rsrc_of(g.s2);
   const long slot = (long)B * H;
   const int br = min(b0 + (lane & 15), B - 1);
+  const long slotS = (long)a.MT * 16 * H, tileS = (long)mt * 16 * H;  // tile-major sentinel slot, this row tile
+  const int rowt = br - b0;
   const int ob = b0 + (tid >> 4), ok_ = c * 16 + (tid & 15);
   const bool live = ob < B;
   const int lenb = (a.len && live) ? a.len[ob] : L;  // masked frames: dL/dh_t = 0 (forward h_t = 0)
@@ -772,7 +825,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     const float daz = dh * (v.hh - v.hp) * (v.z * (1.0f - v.z));
     const float dah = (dh * v.z) * (1.0f - v.hh * v.hh);
     if (loc) {
-      const long off = pn * slot + (long)ob * H + ok_;
+      const long off = pn * slotS + tile_off(ob, ok_, H);
       if (pub) {
         put_sent(g.s2 + off, dah);  // da_h gates the next p1: first
         put_sent(g.s0 + off, daz);
@@ -802,14 +855,20 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     // ---- p1: dq = Uh^T da_h -> da_r, partial dh_{t-1}
     float4 av[NC];
     GRU_STAMP(0);
-    bool ok = loc ? sweep_sent<NC>(av, hs, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word)
+#if S2S_GRU_DIAG
+    unsigned npoll[3] = {0, 0, 0};
+#endif
+    bool ok = loc ? SWEEP_SENT(0, av, hs, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word)
                   : sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
     GRU_STAMP(1);
+#if S2S_GRU_DIAG
+    GRU_STAMP_V(8, npoll[0]);
+#endif
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
     if (loc) {
-      if (live) put_sent(g.s1 + p * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
+      if (live) put_sent(g.s1 + p * slotS + tile_off(ob, ok_, H), (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
     } else {
       put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)), tag, live);
     }
@@ -829,8 +888,15 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       // merged poll of both rows re-reads da_z while waiting for da_r (measured slower)
       float4 az[NC], ar[NC];
       if (loc) {
-        ok = sweep_sent<NC>(az, zs, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word);
-        ok = ok && sweep_sent<NC>(ar, rs_, 4 * (p * slot + (long)br * H), wave, lane, a.abort_word);
+        ok = SWEEP_SENT(1, az, zs, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word);
+#if S2S_GRU_DIAG
+        GRU_STAMP(10);  // the da_z sweep (published a whole phase earlier) is done
+#endif
+        ok = ok && SWEEP_SENT(2, ar, rs_, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word);
+#if S2S_GRU_DIAG
+        GRU_STAMP_V(9, npoll[1]);
+        GRU_STAMP_V(11, npoll[2]);
+#endif
       } else {
         ok = sweep_skinny<NC>(az, zg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
         ok = ok && sweep_skinny<NC>(ar, rg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
@@ -925,7 +991,11 @@ static size_t prep_bytes(int B, int L, int H) {
   return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H) + 4 * xcount_words(L);
 }
 static size_t sent_offset(int B, int L, int H) { return (prep_bytes(B, L, H) + 255) / 256 * 256; }
-static size_t slab_offset(int B, int L, int H) { return sent_offset(B, L, H) + 2 * 3 * sizeof(float) * (size_t)L * B * H; }
+// sentinel rows are tile-major: 16 rows per row tile (handoff.h tile_off)
+static size_t sent_rows(int B) { return (size_t)(B + 15) / 16 * 16; }
+static size_t slab_offset(int B, int L, int H) {
+  return sent_offset(B, L, H) + 2 * 3 * sizeof(float) * (size_t)L * sent_rows(B) * H;
+}
 constexpr size_t kXpSlabBytes = (size_t)kXpMaxSplitItems * 4 * 4096 * sizeof(float);  // PA <= 4
 
 size_t gru_persist_sync_bytes(int B, int L, int H) { return slab_offset(B, L, H) + kXpSlabBytes; }
@@ -965,7 +1035,7 @@ static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_wor
   for (int d = 0; d < 2; ++d)
     for (int k = 0; k < 3; ++k) {
       sv[d][k] = q;
-      q += (long)L * B * H;
+      q += (long)L * sent_rows(B) * H;
     }
 }
 

@@ -290,6 +290,35 @@ __device__ __forceinline__ bool sweep_sent(float4 (&a)[NC], __amdgpu_buffer_rsrc
   }
 }
 
+// Tile-major sentinel slots: a slot is [row tile][H / 16 column tiles][16 rows][16 columns] (row tiles of 16
+// utterances), so the 16 x 16 tile one chain member publishes per step is 1 KB contiguous -- every 128-B line has
+// one writer -- and chunk i of a sweeping wave (columns wave * 16 + 64 i .. + 15 = column tile wave + 4 i) is
+// one wave instruction over that 1-KB tile instead of 64 B of each of 16 rows.  Measured (tools/sweepbench.hip:
+// 16 members, H = 256, one seam per step): 1.18-1.20 -> 1.00-1.04 us per seam.
+__device__ __forceinline__ long tile_off(int row, int col, int H) {
+  return (long)(row >> 4) * 16 * H + (long)(col >> 4) * 256 + (row & 15) * 16 + (col & 15);
+}
+// sweep_sent's operand layout over a tile-major slot: tbase = byte offset of the slot's row tile, rowt = this
+// lane's row within it
+template <int NC>
+__device__ __forceinline__ bool sweep_sent_tile(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
+                                                int wave, int lane, unsigned* abort_word) {
+  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  unsigned spins = 0;
+  while (true) {
+    bool ok = true;
+#pragma unroll
+    for (int i = 0; i < NC; ++i) {
+      const long off = lo + 4L * 256 * (wave + 4 * i);
+      const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
+      ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+      a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+    }
+    if (__all(ok)) return true;
+    if (spin_give_up(spins, abort_word)) return false;
+  }
+}
+
 // sweep_skinny_rows over sentinel rows: all R * NC loads of a pass issued before any check
 template <int NC, int R>
 __device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],

@@ -4,7 +4,10 @@ s_memrealtime stamps (100 MHz).  Run on a GPU box:  python tools/gru_stamps.py [
 Per step of one chain (direction, 16-row tile):
   forward   h_{t-1} -> [z|r] (p1, 2H/16 workgroups)  ->  q = r*h -> hh, h_t (p2, H/16 workgroups)
   backward  da_h -> dq, da_r (p1, H/16)  ->  [da_z; da_r] -> dh_{t-1}, gates (p2, H/16)
-hand-off = consumer sweep done - last producer's phase end; compute = phase end - sweep done."""
+hand-off = consumer sweep done - last producer's phase end; compute = phase end - sweep done.
+S2S_GRU_DIAG=1 with a diagnostic build (tools/ab_variant.sh diag "-DS2S_GRU_DIAG=1", S2S_HIP_LIB=...): 16 stamp slots;
+each seam is split into the producers' publication skew, the consumers' poll passes and the sweep of data that is
+already there (the backward's da_z sweep)."""
 import ctypes
 import os
 import sys
@@ -38,6 +41,30 @@ def analyse(name, st, nwg, ndir, ntile, prod1, cons1, prod2, cons2):
           f"+ compute2 {r[4]:.2f}")
 
 
+def seams(name, st, nwg, ndir, ntile, specs):
+    """specs: (label, producers, producer stamp slot, producer step offset, consumers, start slot, done slot,
+    polls slot).  Per seam and step: producers' publication spread (last - first), consumer start relative to
+    the last publication (negative: the consumer was already polling), done - last publication, poll passes."""
+    L = st.shape[1]
+    for label, prod, pslot, poff, cons, s0, s1, pc in specs:
+        sk, st0, dn, pol, sw = [], [], [], [], []
+        for d in range(ndir):
+            for m in range(ntile):
+                base = d * nwg + m * (nwg // ntile)
+                c = st[base:base + nwg // ntile]
+                for s in range(2, L):
+                    pub = c[prod, s + poff, pslot]
+                    last, first = pub.max(), pub.min()
+                    sk.append(last - first)
+                    st0.append(c[cons, s, s0].mean() - last)
+                    dn.append(c[cons, s, s1].mean() - last)
+                    sw.append(c[cons, s, s1].mean() - c[cons, s, s0].mean())
+                    pol.append(c[cons, s, pc].mean() * 100.0)  # stamps were scaled by 0.01
+        print(f"  {name} {label}: publication spread {np.mean(sk):.2f} us; consumers start {np.mean(st0):+.2f} us "
+              f"from the last publication, done {np.mean(dn):+.2f} us after it (sweep {np.mean(sw):.2f} us, "
+              f"{np.mean(pol):.1f} poll passes)")
+
+
 def main():
     B, L, H = (int(a) for a in sys.argv[1:4]) if len(sys.argv) > 3 else (32, 128, 256)
     # S2S_GRU_LAYERS=2: the stamped backward is the lower layer's, whose dy (the upper layer's dX) the
@@ -47,8 +74,9 @@ def main():
     ndir = 2
     ntile = (B + 15) // 16
     nf, nb = ndir * (2 * H // 16) * ntile, ndir * (H // 16) * ntile
-    sf = torch.zeros(nf * L * 8, dtype=torch.int64, device="cuda")
-    sb = torch.zeros(nb * L * 8, dtype=torch.int64, device="cuda")
+    K = 16 if os.environ.get("S2S_GRU_DIAG") == "1" else 8
+    sf = torch.zeros(nf * L * K, dtype=torch.int64, device="cuda")
+    sb = torch.zeros(nb * L * K, dtype=torch.int64, device="cuda")
     fn = _lib.lib.s2s_debug_gru_stamps
     fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     x = torch.randn(B, L, D, device="cuda")
@@ -63,8 +91,8 @@ def main():
     model.step(x, lab)
     torch.cuda.synchronize()
     fn(None, None)
-    tf = sf.cpu().numpy().reshape(nf, L, 8).astype(np.float64) * 0.01
-    tb = sb.cpu().numpy().reshape(nb, L, 8).astype(np.float64) * 0.01
+    tf = sf.cpu().numpy().reshape(nf, L, K).astype(np.float64) * 0.01
+    tb = sb.cpu().numpy().reshape(nb, L, K).astype(np.float64) * 0.01
     z = list(range(H // 16))
     zr = list(range(2 * H // 16))
     r = list(range(H // 16, 2 * H // 16))
@@ -84,6 +112,15 @@ def main():
                                                                     for i in range(4)) + " us")
     print(f"  backward: first step starts at +0, step 8 at {tbp[:, 8, 0].mean() - t0:.1f} us, last step ends at "
           f"{tbp[:, -1, 5].max() - t0:.1f} us")
+    if K == 16:
+        print("seam decomposition (diagnostic build):")
+        seams("forward", tf, nf // ndir, ndir, ntile, [
+            ("h   -> [z|r]", z, 5, -1, zr, 0, 1, 8),
+            ("q   -> hh   ", r, 2, 0, z, 3, 4, 9)])
+        seams("backward", tbp, nb // ndir, ndir, ntile, [
+            ("da_h -> dq  ", allc, 5, -1, allc, 0, 1, 8),
+            ("da_z (ready)", allc, 5, -1, allc, 3, 10, 9),
+            ("da_r -> dh  ", allc, 2, 0, allc, 10, 4, 11)])
 
 
 if __name__ == "__main__":
