@@ -529,13 +529,17 @@ def main():
                              "GEMM its spare-slot producers compute inside the launch (forward: the x-projection; "
                              "backward: dy = the layer above's dX, or for the top layer the decoder's dh = "
                              "dVh V + sum_t alpha dc), averaged over the step's launches")
-        # the decoder recurrences (the attention path): priced against HBM (the attention
-        # re-streams Vh and h every step) and against their own hand-off latency floor
+        # the decoder recurrences (the attention path): priced against their own hand-off latency floor; the
+        # HBM rate is the counters' bytes (the attention operands themselves stay in LDS, profile.py)
         out["roofline_decoder"] = []
         for e in dec:
             t, detail = traffic_of(pmc, e["kernel"])
             e["traffic"] = round(t) if t is not None else None
             e["traffic_detail"] = detail
+            if t is not None:
+                gbs = t / (e["avg_launch_us"] * 1e-6) / 1e9
+                e["hbm"] = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                            "frac": round(gbs / PEAK_HBM_GBS, 4), "source": "PMC traffic / live launch time"}
             e["mfma_counters"] = mfma_of(pmc, e["kernel"], e["avg_launch_us"])
             e["latency_floor"] = latency_floor(e["kernel"], T, e["avg_launch_us"])
             out["roofline_decoder"].append(e)

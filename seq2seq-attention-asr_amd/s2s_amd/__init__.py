@@ -9,5 +9,5 @@ from ._lib import S2SError, lib  # noqa: F401  (fails loudly when the HIP librar
 from .nn import (GRU, LSTM, RNN, BiRNN, Attention, MaxoutMLP, nll_seed, Context, get_context, precision)  # noqa: F401
 from .model import ModelConfig, ChorowskiBaseline, param_shapes  # noqa: F401
 from . import optim  # noqa: F401
-from . import frontend, data, checkpoint  # noqa: F401
+from . import frontend, data, checkpoint, train_utils  # noqa: F401
 from .frontend import ConvBiLSTMEncoder, VGGEncoder, VGGAttentionModel, ConvBiLSTMAttentionModel  # noqa: F401

@@ -1,0 +1,55 @@
+"""TrainUtils.orthogonalize / orthogonalizeGraph (TrainUtils.lua:5-26, 137-188) on the flat layout.
+
+The reference applies `orthogonalize` to every weight-bearing leaf module of the autoencoder after
+`reset(init_std)` when `opt.orthogonalize` is set (librispeech/exp0_scriptchecker.lua:49-52,
+timit/exp_logmel7_chorowski_normNLL_colnorm.lua:39).  Per module: `w = [weight | bias]` (bias as one
+more column when the module has one), Q of a Householder QR of w (of w^T when w has fewer rows than
+columns, then transposed back), and the module's weight / bias take Q's columns.  Init-time host code,
+outside the timed step; the QR runs where the parameters live (LAPACK geqrf / orgqr, the algorithm
+Torch7's torch.qr calls, so Q's column signs follow the same convention).
+"""
+import torch
+
+from .model import param_shapes
+
+
+def orthogonalize(weight, bias=None):
+    """TrainUtils.lua:5-26 on one module, in place.  weight (rows, cols), bias (rows,) or None."""
+    w = weight if bias is None else torch.cat([weight, bias.reshape(-1, 1)], 1)
+    w = w.double()
+    if w.shape[0] < w.shape[1]:
+        q = torch.linalg.qr(w.t(), mode="reduced")[0].t()
+    else:
+        q = torch.linalg.qr(w, mode="reduced")[0]
+    weight.copy_(q[:, :weight.shape[1]])
+    if bias is not None:
+        bias.copy_(q[:, weight.shape[1]])
+    return weight, bias
+
+
+def modules(cfg):
+    """(weight name, bias name or None) of every leaf module of the Chorowski autoencoder that holds a
+    weight, in the flat layout's naming (model.param_shapes).  The encoder's GRU gates are
+    LinearZeroBias (weight only, GRU.lua:22-25).  V and we are TemporalConvolutionZeroBias: a bias
+    that updateOutput re-zeroes (TemporalConvolutionZeroBias.lua:13-38) and the flat layout drops; a
+    zero bias column changes neither Q's weight columns (QR is column-sequential) nor, in the wide
+    case, Q^T's first columns (its row of w^T is zero, so Q's matching row is zero), so both are
+    orthogonalized as weight-only modules.  Ws / Wy / Wc / Wd / Wm / Wo are nn.Linear (weight + bias);
+    the decoder GRU's gates are LinearZeroBias."""
+    names = [n for n, _ in param_shapes(cfg)]
+    out = []
+    for n in names:
+        if n.startswith("enc") or n.startswith("dec.") or n in ("V", "we"):
+            out.append((n, None))
+    for w, b in (("Ws", "bs"), ("Wy", "by"), ("Wc", "bc"), ("Wd", "bd"), ("Wm", "bm"), ("Wo", "bo")):
+        out.append((w, b))
+    return out
+
+
+@torch.no_grad()
+def orthogonalize_model(model):
+    """TrainUtils.orthogonalizeGraph(model.autoencoder) on a ChorowskiBaseline's flat parameters."""
+    v = model.views()
+    for w, b in modules(model.cfg):
+        orthogonalize(v[w], v[b] if b is not None else None)
+    return model
