@@ -250,8 +250,9 @@ def cpu_vgg_baseline(L, T, seconds_budget):
 
 def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
     """BASELINE config 5: librispeech/model_vgg.lua training step (VGG encoder -> attention decoder with the
-    two-Maxout decoder_mlp -> loss seed -> backward), B = 16 utterances of 1024 frames per GPU, eager
-    launches (the host-side Sequential of the front-end), all-reduce of every gradient when N > 1."""
+    two-Maxout decoder_mlp -> loss seed -> backward), B = 16 utterances of 1024 frames per GPU, the whole
+    step (gradient zeroing included) replayed from one captured HIP graph (VGGAttentionModel.graph_step;
+    --no-graph: eager launches of the host-side Sequential), all-reduce of every gradient when N > 1."""
     kw, B, L, T = CONFIGS[args.config]
     g = torch.Generator().manual_seed(1234 + rank)
     model = s2s_amd.VGGAttentionModel(kw["inputFrameSize"], outputFrameSize=512, hidden=2048,
@@ -264,8 +265,11 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
     grads = model.parameters()[1]
 
     def step():
-        model.zeroGradParameters()
-        model.step(x, labels)
+        if args.no_graph:
+            model.zeroGradParameters()
+            model.step(x, labels)
+        else:
+            model.graph_step(x, labels)
         if world > 1:  # one flat all-reduce per gradient tensor list (RCCL)
             for gt in grads:
                 dist.all_reduce(gt)
@@ -300,14 +304,15 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
            "config": {"workload": f"{CONFIG_DESC[args.config][0]}: {args.config}", "model": CONFIG_DESC[args.config][1],
                       "global_batch": B * world, "utterances_per_gpu": B, "seq_len": L, "label_len": T,
                       "feat_dim": kw["inputFrameSize"], "annotation_frames": (L - 8) // 2,
-                      "parallelism": f"dp{world}", "launch": "eager"}}
+                      "parallelism": f"dp{world}", "launch": "eager" if args.no_graph else "hipGraph replay"}}
     if rank == 0 and not args.no_kernel_timing:
         from s2s_amd import _lib
         from s2s_amd import profile as s2s_profile
         _lib.check(_lib.lib.s2s_prof_enable(1))
         s2s_profile.collect()
-        for _ in range(2):
-            step()
+        for _ in range(2):  # eager: the library brackets each launch with events
+            model.zeroGradParameters()
+            model.step(x, labels)
         torch.cuda.synchronize()
         agg = s2s_profile.collect()
         _lib.lib.s2s_prof_enable(0)

@@ -7,6 +7,12 @@ fallback (the CPU oracle under oracle/ is test infrastructure only).
 import ctypes
 import os
 
+# torch first: it loads the HIP runtime it was built with, and libs2s_hip.so then binds to that same
+# (already loaded) libamdhip64.  Loading the library first pulls /opt/rocm/lib's runtime in ahead of
+# torch's, and the second runtime of the process then finds no device (seen when build() and smoke()
+# ran in one process).
+import torch  # noqa: F401
+
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # S2S_HIP_LIB overrides the in-tree library (same-box A/B comparisons of two builds)
 LIB_PATH = os.environ.get("S2S_HIP_LIB") or os.path.join(_HERE, "libs2s_hip.so")

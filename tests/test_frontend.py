@@ -535,6 +535,38 @@ def test_vgg_attention_model_step_matches_oracle(fe):
     _assert_grads(pairs)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("prec", ["fp32", "bf16-all"])
+def test_vgg_graph_step_equals_eager(fe, prec):
+    """VGGAttentionModel.graph_step (the config-5 bench's captured step) is bitwise the eager
+    zeroGradParameters() + step(), also after the inputs are refilled in place (new data, one capture)."""
+    import s2s_amd
+    rng = np.random.default_rng(4)
+    B, L, Fq, T, O = 2, 40, 40, 6, 29
+
+    def make():
+        return s2s_amd.VGGAttentionModel(Fq, outputFrameSize=128, hidden=128, scoreDepth=128, stateDepth=64,
+                                         outputDepth=O, mlpDepth=8, generator=torch.Generator().manual_seed(3),
+                                         precision=prec).cuda()
+
+    eager, graphed = make(), make()
+    x = cu(rng.standard_normal((B, 3, L, Fq)) * 10)
+    labels = cu(np.append(rng.integers(0, O - 1, (B, T - 1)), np.full((B, 1), O - 1), axis=1), torch.int32)
+    xg, lg = x.clone(), labels.clone()
+    for it in range(3):
+        if it == 2:  # new data in the captured buffers
+            x.copy_(cu(rng.standard_normal((B, 3, L, Fq)) * 10))
+            xg.copy_(x)
+        eager.zeroGradParameters()
+        nll_e, logp_e = eager.step(x, labels)
+        nll_g, logp_g = graphed.graph_step(xg, lg)
+        torch.cuda.synchronize()
+        assert torch.equal(logp_e, logp_g) and torch.equal(nll_e, nll_g), it
+        for i, (ge, gg) in enumerate(zip(eager.parameters()[1], graphed.parameters()[1])):
+            assert torch.equal(ge, gg), (it, i)
+    assert len(graphed._graphs) == 1
+
+
 # --------------------------------------------------------------------------- LSTM decoder (conv + BiLSTM model)
 
 def _lstm_dec_case(rng, S, A, Sc, O, hybrid, mlp_kind):
