@@ -393,6 +393,8 @@ int tmaxpool_bwd(hipStream_t st, int B, int L, int D, int kW, int dW, const int*
 }
 
 // ------------------------------------------------------------------ SpatialConvolutionMM
+// s2s_debug_sconv_wgrad_implicit(0): the bf16 weight gradient through the im2col panel and the bf16 GEMM (A/B, tests)
+std::atomic<int> g_sconv_wgrad_implicit{1};
 // scratch: split-K slabs | im2col panel (K, B N) | dcol (K, B N) | dyt (Cout, B N); under bf16 the implicit
 // forward / input gradient keep their re-laid-out weights (Cin Cout kH kW) in the panel / dcol region
 static size_t sconv_dcol_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW) {
@@ -460,15 +462,21 @@ int sconv_bwd(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, in
     hipLaunchKernelGGL(rowsum_final_kernel, dim3((Cout + 255) / 256), dim3(256), 0, st, part, Cout, scale, 1.f, db);
     S2S_CHECK_HIP(hipGetLastError());
   }
-  // bf16 forward / input gradient are implicit GEMMs (no panels); the weight gradient keeps the panel
+  // bf16 forward / input gradient are implicit GEMMs (no panels)
   const bool implicit = gemm_precision() == kGemmBf16 && kH == kW && (kW == 3 || kW == 1);
   if (dW) {
-    if (!col_from_fwd || implicit)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
-      launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
-    S2S_CHECK_HIP(hipGetLastError());
-    // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
-    WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
-    S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
+    WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM, bf16 under S2S_PREC_BF16_ALL
+    const size_t region = sconv_dcol_bytes(B, Cin, H, W, Cout, kH, kW);
+    if (gemm_precision() == kGemmBf16 && implicit && Cin % 64 == 0 && g_sconv_wgrad_implicit) {
+      // implicit bf16 weight gradient: the channels-last copy of x in the panel region, split partials in dcol's
+      S2S_TRY(sconv_wgrad_implicit(st, B, Cin, H, W, Cout, kH, kW, x, dyt, dW, scale, col, region, dcol, region));
+    } else {
+      if (!col_from_fwd || implicit)  // else: the forward's im2col panel is still in scratch (same x, same scratch)
+        launch_im2col(st, x, B, Cin, H, W, kH, kW, Ho, Wo, col);
+      S2S_CHECK_HIP(hipGetLastError());
+      // gradWeight (Cout, K) += scale * dyt (Cout, B*N) col^T
+      S2S_TRY(gemm1(st, false, true, Cout, K, (int)BN, scale, dyt, BN, col, BN, 1.f, dW, K, nullptr, ws_of(scratch)));
+    }
   }
   if (dx && implicit)  // dx = transposed convolution of dyt, the re-laid-out weights in the dcol region
     return sconv_dx_implicit(st, B, Cin, H, W, Cout, kH, kW, Wt, dyt, dx, dx_accumulate, dcol);
@@ -545,3 +553,5 @@ int logsoftmax_bwd(hipStream_t st, long rows, int n, const float* y, const float
 }
 
 }  // namespace s2s
+
+extern "C" void s2s_debug_sconv_wgrad_implicit(int on) { s2s::g_sconv_wgrad_implicit = on; }

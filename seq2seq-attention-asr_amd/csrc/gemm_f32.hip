@@ -872,4 +872,58 @@ int sconv_dx_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, in
   return conv_launch(st, true, c, Wt, scratch, "conv_dx_bf16");
 }
 
+// weight gradient on the channels-last bf16 copy of x (conv_wgrad_bf16_kernel): xh in xh_scratch, the split-K
+// partial tiles in slab (both scratch regions the im2col path would have used for its panels)
+size_t sconv_wgrad_slab_floats(int B, int Cin, int H, int W, int Cout, int kH, int kW, int* S_out, long* chunk_out) {
+  const long BN = (long)B * (H - kH + 1) * (W - kW + 1);
+  const int kk = kH * kW, tiles = ((Cout + kConvBM - 1) / kConvBM) * (kk * Cin / kConvBN);
+  const long ktiles = (BN + HBK - 1) / HBK;
+  // ~2048 workgroups, at least 8 K-tiles per chunk
+  long S = std::max(1L, std::min(ktiles / 8, (2048L + tiles - 1) / tiles));
+  const long chunk = (ktiles + S - 1) / S * HBK;
+  S = (BN + chunk - 1) / chunk;
+  if (S_out) *S_out = (int)S;
+  if (chunk_out) *chunk_out = chunk;
+  return (size_t)S * Cout * kk * Cin;
+}
+int sconv_wgrad_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, const float* x,
+                         const float* dyt, float* dW, float scale, void* xh_scratch, size_t xh_bytes, float* slab,
+                         size_t slab_bytes) {
+  WgradArgs c{};
+  c.g = ConvGeom{B, Cin, H, W, Cout, kH, kW, H - kH + 1, W - kW + 1};
+  const int kk = kH * kW;
+  S2S_REQUIRE(Cin % kConvBN == 0 && Cout > 0 && B > 0, "conv wgrad: implicit bf16 path needs Cin % 64 == 0");
+  const long P = (long)H * W;
+  c.xhlen = (long)B * P * Cin;
+  S2S_REQUIRE(2 * c.xhlen < (1L << 31) - 4096, "conv wgrad: input too large for 32-bit byte offsets");
+  S2S_REQUIRE(xh_bytes >= 2 * (size_t)c.xhlen, "conv wgrad: scratch too small");
+  int S;
+  long chunk;
+  const size_t nslab = sconv_wgrad_slab_floats(B, Cin, H, W, Cout, kH, kW, &S, &chunk);
+  S2S_REQUIRE(sizeof(float) * nslab <= slab_bytes, "conv wgrad: slab scratch too small");
+  __bf16* xh = static_cast<__bf16*>(xh_scratch);
+  hipLaunchKernelGGL(nchw_to_nhwc_bf16, dim3((unsigned)((P + 63) / 64), Cin / 64, B), dim3(256), 0, st, x, nullptr, Cin,
+                     (int)P, xh);
+  c.dyt = dyt;
+  c.BN = (long)B * c.g.Ho * c.g.Wo;
+  c.xh = xh;
+  c.slab = slab;
+  c.tiles_m = (Cout + kConvBM - 1) / kConvBM;
+  c.tiles_n = kk * Cin / kConvBN;
+  c.S = S;
+  c.chunk = chunk;
+  c.nblocks = c.tiles_m * c.tiles_n * S;
+  {
+    ProfScope ps(st, "conv_wgrad_bf16", 2.0 * Cout * (double)kk * Cin * c.BN,
+                 4.0 * (double)Cout * c.BN + 2.0 * c.xhlen + 4.0 * nslab);
+    hipLaunchKernelGGL(conv_wgrad_bf16_kernel, dim3((unsigned)((c.nblocks + 7) / 8 * 8)), dim3(256), 0, st, c);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
+  const long n = (long)Cout * Cin * kk;
+  hipLaunchKernelGGL(conv_wgrad_reduce, dim3((unsigned)std::min<long>(1024, (n + 255) / 256)), dim3(256), 0, st, slab,
+                     S, Cout, Cin, kk, scale, dW);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace s2s

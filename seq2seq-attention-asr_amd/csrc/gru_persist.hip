@@ -130,6 +130,9 @@ struct PArgs {
   char* next_sync;
   size_t next_prep;
   GruPackJobs pack;  // weight packing for later launches, done by the forward's spare slots (pack.n = 0: none)
+  // sentinel slots in use per role: kSentRing (a ring, re-armed by the loader wave two steps after every
+  // consumer has read a slot) or 0 (one slot per step, all re-armed at launch start; s2s_debug_gru_ring(0))
+  int ring;
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
 };
@@ -498,6 +501,30 @@ __device__ __forceinline__ void prep_next_sync(const PArgs& a, int sp, int nsp) 
 // z-column blocks, [B] (p2 reduce); step q + 2's values are written between [A] of step q and [A] of
 // step q + 1, after which the recurrence waves read them.
 constexpr int kRowRing = 4;  // steps of loaded operands in flight (LDS ring)
+// Sentinel slot ring (XCD-local chains).  A slot of step s is consumed by every chain member within the
+// step after it was produced, and a member's sweep proves that every other member has finished with it:
+//   forward  h_s  (z tiles; read by all members in p1 of step s+1): once a member's p1 sweep of step s+2 is
+//            complete, every z member has published h_{s+1} (after reading h_s and, in p2 of s+1, every r
+//            member's q_{s+1}, itself published after that r member read h_s) -- re-arm at [A] of step s+2;
+//            q_s  (r tiles; read by z members in p2 of step s): the p1 sweep of step s+1 saw every z member's
+//            h_s, published after its p2 read of q_s -- re-arm at [A] of step s+1;
+//   backward da_h_p, da_z_p, da_r_p (read by all in p1 / p2 of step p): the p1 sweep of step p+1 saw every
+//            member's da_h_{p+1}, published after its p2 of step p -- re-arm at [A] of step p+1.
+// The re-arm of a member's own 1-KB tile is done by its loader wave between barriers and drained (vmcnt(0))
+// before the barrier after which the member publishes again, so every value a consumer sees from that member
+// later than the re-arm is ordered after it in the XCD's L2: with kSentRing = 4 the consumer of slot s + 4
+// has already taken a value the member published after re-arming slot s, and cannot mistake slot s's stale
+// value for step s + 4's.  Only kSentRing slots are live (a few KB per member instead of L KB), so the slots
+// stay in L2: the per-step slots were re-armed at launch start and written again per step, most of both
+// recurrences' HBM write traffic (profiles/r03/pmc_hbm.csv), and re-arming L slots delayed each launch's start.
+constexpr int kSentRing = 4;
+__device__ __forceinline__ int sent_slot(const PArgs& a, int s) { return a.ring ? (s & (a.ring - 1)) : s; }
+// re-arm this member's 1-KB tile of slot s of one tile-major sentinel role (the loader wave's 64 lanes)
+__device__ __forceinline__ void rearm_tile(float* role, const PArgs& a, int s, long tile, int lane) {
+  const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
+                                __uint_as_float(kSent));
+  *reinterpret_cast<float4*>(role + (long)sent_slot(a, s) * a.MT * 16 * a.H + tile + 4 * lane) = sv;
+}
 constexpr int kFwdThreads = 320;
 template <int NC>  // NC = H / 64
 __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
@@ -530,9 +557,9 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   // z tiles publish h, r tiles q
   const bool loader = wave == 4;
-  if (!loader)  // this member's 1-KB tile of every (tile-major) slot
-    rearm_rect((isz ? g.s0 : g.s1) + (long)mt * 16 * H + (long)(isz ? c1 : c1 - H / 16) * 256, (long)a.MT * 16 * H, L,
-               16, 0, 16, 0, 16);
+  const long mytile = (long)mt * 16 * H + (long)(isz ? c1 : c1 - H / 16) * 256;  // this member's tile in a slot
+  if (!loader)  // this member's 1-KB tile of every (tile-major) slot in use
+    rearm_rect((isz ? g.s0 : g.s1) + mytile, (long)a.MT * 16 * H, a.ring ? a.ring : L, 16, 0, 16, 0, 16);
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c1, a.allow_local != 0, a.abort_word, &local_lds, tb);
 
@@ -569,11 +596,17 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     put(1, rb);
     issue(2, ra);
     __syncthreads();  // [P]
+    const bool ring = a.ring && loc;
     for (int s = 0; s < L; ++s) {
+      if (ring) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last step's re-arms have landed
       __syncthreads();  // [A]
       if (abort_lds) return;
       put(s + 2, ra);   // loaded during the previous step
       issue(s + 3, ra);
+      if (ring) {  // slots every member has finished with (h_{s-2} of z tiles, q_{s-1} of r tiles)
+        if (isz && s >= 2) rearm_tile(g.s0, a, s - 2, mytile, lane);
+        if (!isz && s >= 1) rearm_tile(g.s1, a, s - 1, mytile, lane);
+      }
       if (!isz) continue;
       __syncthreads();  // [B]
       if (abort_lds) return;
@@ -613,7 +646,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
       unsigned npoll[1] = {0};
 #endif
-      if (loc) ok = SWEEP_SENT(0, av, hs, 4 * ((s - 1) * slotS + tileS), rowt, wave, lane, a.abort_word);
+      if (loc) ok = SWEEP_SENT(0, av, hs, 4 * (sent_slot(a, s - 1) * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
       GRU_STAMP(1);
 #if S2S_GRU_DIAG
@@ -645,7 +678,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
         const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
         const float q = gate * hp;
         if (loc) {  // critical first
-          if (live) put_sent(g.s1 + s * slotS + tile_off(ob, j, H), q);
+          if (live) put_sent(g.s1 + sent_slot(a, s) * slotS + tile_off(ob, j, H), q);
         } else {
           put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live);
         }
@@ -667,7 +700,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
       unsigned npoll[1] = {0};
 #endif
-      if (loc) ok = SWEEP_SENT(0, av, qs, 4 * (s * slotS + tileS), rowt, wave, lane, a.abort_word);
+      if (loc) ok = SWEEP_SENT(0, av, qs, 4 * (sent_slot(a, s) * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
       GRU_STAMP(4);
 #if S2S_GRU_DIAG
@@ -683,7 +716,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
       if (t >= lenb) hreg = 0.f;
       if (loc) {  // first
-        if (live) put_sent(g.s0 + s * slotS + tile_off(ob, on, H), hreg);
+        if (live) put_sent(g.s0 + sent_slot(a, s) * slotS + tile_off(ob, on, H), hreg);
       } else {
         put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live);
       }
@@ -733,11 +766,13 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const bool loader = wave == 4;
-  if (!loader) {  // this member's 1-KB tile of every (tile-major) slot
-    const long tt = (long)mt * 16 * H + (long)c * 256, st = (long)a.MT * 16 * H;
-    rearm_rect(g.s0 + tt, st, L, 16, 0, 16, 0, 16);
-    rearm_rect(g.s1 + tt, st, L, 16, 0, 16, 0, 16);
-    rearm_rect(g.s2 + tt, st, L, 16, 0, 16, 0, 16);
+  const long mytile = (long)mt * 16 * H + (long)c * 256;  // this member's tile in a slot
+  if (!loader) {  // this member's 1-KB tile of every (tile-major) slot in use
+    const long st = (long)a.MT * 16 * H;
+    const int ns = a.ring ? a.ring : L;
+    rearm_rect(g.s0 + mytile, st, ns, 16, 0, 16, 0, 16);
+    rearm_rect(g.s1 + mytile, st, ns, 16, 0, 16, 0, 16);
+    rearm_rect(g.s2 + mytile, st, ns, 16, 0, 16, 0, 16);
   }
   rearm_done();
   const bool loc = chain_is_local(a.census, cs.chain, a.nmem, c, a.allow_local != 0, a.abort_word, &local_lds, tb);
@@ -784,10 +819,17 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     put(1, rb);
     issue(2, ra);
     __syncthreads();  // [P]
+    const bool ring = a.ring && loc;
     for (int p = 0; p < L; ++p) {
       __syncthreads();  // [A]
       if (abort_lds) return;
       put(p + 2, ra);   // loaded during the previous step
+      if (ring && p >= 1) {  // step p-1's slots: every member has finished with them (header comment)
+        rearm_tile(g.s0, a, p - 1, mytile, lane);
+        rearm_tile(g.s1, a, p - 1, mytile, lane);
+        rearm_tile(g.s2, a, p - 1, mytile, lane);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before the member publishes step p+1
+      }
       __syncthreads();  // [B]
       if (abort_lds) return;
       issue(p + 3, ra);
@@ -825,7 +867,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     const float daz = dh * (v.hh - v.hp) * (v.z * (1.0f - v.z));
     const float dah = (dh * v.z) * (1.0f - v.hh * v.hh);
     if (loc) {
-      const long off = pn * slotS + tile_off(ob, ok_, H);
+      const long off = sent_slot(a, pn) * slotS + tile_off(ob, ok_, H);
       if (pub) {
         put_sent(g.s2 + off, dah);  // da_h gates the next p1: first
         put_sent(g.s0 + off, daz);
@@ -858,7 +900,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
     unsigned npoll[3] = {0, 0, 0};
 #endif
-    bool ok = loc ? SWEEP_SENT(0, av, hs, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word)
+    bool ok = loc ? SWEEP_SENT(0, av, hs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word)
                   : sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
     GRU_STAMP(1);
 #if S2S_GRU_DIAG
@@ -868,7 +910,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (aborted) return;
     if (loc) {
-      if (live) put_sent(g.s1 + p * slotS + tile_off(ob, ok_, H), (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
+      if (live) put_sent(g.s1 + sent_slot(a, p) * slotS + tile_off(ob, ok_, H), (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
     } else {
       put_granule_pair(g.g1, sl * slot + (long)ob * H + ok_, (dq * cur.hp) * (cur.r * (1.0f - cur.r)), tag, live);
     }
@@ -888,11 +930,11 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       // merged poll of both rows re-reads da_z while waiting for da_r (measured slower)
       float4 az[NC], ar[NC];
       if (loc) {
-        ok = SWEEP_SENT(1, az, zs, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word);
+        ok = SWEEP_SENT(1, az, zs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
 #if S2S_GRU_DIAG
         GRU_STAMP(10);  // the da_z sweep (published a whole phase earlier) is done
 #endif
-        ok = ok && SWEEP_SENT(2, ar, rs_, 4 * (p * slotS + tileS), rowt, wave, lane, a.abort_word);
+        ok = ok && SWEEP_SENT(2, ar, rs_, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
 #if S2S_GRU_DIAG
         GRU_STAMP_V(9, npoll[1]);
         GRU_STAMP_V(11, npoll[2]);
@@ -923,6 +965,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 constexpr int kExclLds = 124 * 1024;
 
 std::atomic<int> g_allow_local{1};
+std::atomic<int> g_sent_ring{kSentRing};  // s2s_debug_gru_ring(0): one sentinel slot per step (A/B)
 
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
@@ -1052,6 +1095,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.len = f.len;
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
+  a.ring = f.L > kSentRing ? (int)g_sent_ring : 0;
   a.stamps = g_gru_stamps[0];
   a.pstamps = g_gru_pstamps[0];
   if (f.x) {  // fused x-projection by the grid's spare slots
@@ -1095,6 +1139,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.len = b.len;
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
+  a.ring = b.L > kSentRing ? (int)g_sent_ring : 0;
   a.stamps = g_gru_stamps[1];
   a.pstamps = g_gru_pstamps[1];
   if (b.ydA) {  // fused dy (the layer above's dX) by the grid's spare slots
@@ -1160,6 +1205,8 @@ extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
 extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_xp_split(int on) { s2s::g_xp_split = on; }
+// diagnostic: 0 = one sentinel slot per step re-armed at launch start (the round-2 form), else the 4-slot ring
+extern "C" void s2s_debug_gru_ring(int on) { s2s::g_sent_ring = on ? s2s::kSentRing : 0; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);

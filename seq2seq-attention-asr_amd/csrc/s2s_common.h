@@ -139,6 +139,14 @@ int sconv_fwd_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, i
                        const float* Wt, const float* bias, float* y, void* scratch);
 int sconv_dx_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, const float* Wt,
                       const float* dyt, float* dx, int accumulate, void* scratch);
+// weight gradient dW (Cout, Cin kH kW) += scale * dyt (Cout, B Ho Wo) x col^T without the im2col panel (bf16
+// operands, fp32 accumulation; Cin % 64 == 0): xh_scratch takes the channels-last bf16 copy of x (2 B Cin H W
+// bytes), slab the split partial tiles (sconv_wgrad_slab_floats floats)
+size_t sconv_wgrad_slab_floats(int B, int Cin, int H, int W, int Cout, int kH, int kW, int* S_out = nullptr,
+                               long* chunk_out = nullptr);
+int sconv_wgrad_implicit(hipStream_t st, int B, int Cin, int H, int W, int Cout, int kH, int kW, const float* x,
+                         const float* dyt, float* dW, float scale, void* xh_scratch, size_t xh_bytes, float* slab,
+                         size_t slab_bytes);
 inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
                  const float* B, long ldb, float beta, float* C, long ldc, const float* bias = nullptr,
                  GemmWs ws = GemmWs{}) {

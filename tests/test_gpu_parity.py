@@ -523,23 +523,27 @@ def test_bucket_events_mark_final_gradients(s2s, graph):
         assert model.grads.abs().sum() > 0
 
 
-@pytest.mark.parametrize("local", [1, 0])
+@pytest.mark.parametrize("local,ring", [(1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("B,H", [(32, 256), (45, 128)])
-def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, B, H):
+def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, ring, B, H):
     """The persistent layer kernel (in-launch granule hand-offs; XCD-local L2-resident chains when
     local=1 and the census finds them on one XCD, write-through sc1 when local=0) must reproduce
     the per-step launch path bit for bit -- same arithmetic, same summation order -- over
-    repeated launches."""
+    repeated launches.  ring: the local chains' sentinel slots as the 4-slot ring re-armed in the loop
+    (1, the default) or one slot per step re-armed at launch start (0)."""
     import ctypes
     from s2s_amd import _lib
     fn = _lib.lib.s2s_debug_gru_local
     fn.argtypes = [ctypes.c_int]
+    fr = _lib.lib.s2s_debug_gru_ring
+    fr.argtypes = [ctypes.c_int]
     rng = np.random.default_rng(11)
     L, D = 40, 48
     x = cu(rng.standard_normal((B, L, D)))
     f, b = s2s.GRU(D, H), s2s.GRU(D, H)
     outs = {}
     fn(local)
+    fr(ring)
     for mode in ("step", "persistent"):
         monkeypatch.setenv("S2S_GRU_MODE", mode)
         mod = s2s.BiRNN(f, b).cuda()
@@ -553,6 +557,7 @@ def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local
         torch.cuda.synchronize()
         outs[mode] = res
     fn(1)
+    fr(1)
     for rep in range(3):
         ys, dxs, gs = outs["step"][rep]
         yp, dxp, gp = outs["persistent"][rep]
