@@ -232,3 +232,50 @@ def test_bf16_implicit_conv_exact_on_rounded_operands(lib, B, Cin, H, W, Cout, r
     dxref = np.einsum("bohwij,ocij->bchw", win(pad, (3, 3), axis=(2, 3)), Wr[:, :, ::-1, ::-1])
     err = np.abs(dx.cpu().numpy() - dxref).max() / np.abs(dxref).max()
     assert err <= 2e-5, ("dx", err)
+
+
+@pytest.mark.parametrize("implicit", [1, 0])
+@pytest.mark.parametrize("B,Cin,H,W,Cout,relu", [(2, 64, 17, 11, 64, False), (1, 128, 9, 13, 128, True),
+                                                   (2, 64, 40, 21, 128, True), (3, 5, 7, 6, 7, False),
+                                                   (16, 64, 70, 38, 64, True)])
+def test_bf16_conv_weight_gradient_exact_on_rounded_operands(lib, implicit, B, Cin, H, W, Cout, relu):
+    """SpatialConvolutionMM weight / bias gradient under bf16-all: Cin % 64 == 0 takes the implicit bf16 weight
+    gradient (conv_wgrad_bf16_kernel: channels-last gather, split pixel chunks summed in order; implicit=0 forces
+    the im2col panel + bf16 GEMM for comparison), other Cin the panel.  gradWeight (accumulated onto a nonzero
+    start, scale 0.5) equals the float64 product of the bf16-rounded ReLU-masked dy and input up to the fp32
+    accumulation order (<= 2e-5 max|ref|); ragged pixel chunks, two output-channel tiles, 9 / 18 column tiles."""
+    import s2s_amd
+    from s2s_amd import frontend as fe
+    from numpy.lib.stride_tricks import sliding_window_view as win
+    knob = lib.lib.s2s_debug_sconv_wgrad_implicit
+    knob.argtypes = [ctypes.c_int]
+    rng = np.random.default_rng(B * 100 + Cin + W)
+    conv = fe.SpatialConvolutionMM(Cin, Cout, 3, 3, relu=relu)
+    x = rng.standard_normal((B, Cin, H, W)).astype(np.float32)
+    Wt = (rng.standard_normal((Cout, Cin * 9)) * 0.2).astype(np.float32)
+    bias = (rng.standard_normal(Cout) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((B, Cout, H - 2, W - 2)).astype(np.float32)
+    gw0 = rng.standard_normal((Cout, Cin * 9)).astype(np.float32)
+    conv.weight = torch.tensor(Wt, device="cuda")
+    conv.bias = torch.tensor(bias, device="cuda")
+    conv.gradWeight = torch.tensor(gw0, device="cuda")
+    conv.gradBias = torch.zeros_like(conv.bias)
+    xg, dyg = torch.tensor(x, device="cuda"), torch.tensor(dy, device="cuda")
+    knob(implicit)
+    try:
+        with s2s_amd.precision("bf16-all"):
+            conv.forward(xg)
+            conv.backward(xg, dyg, 0.5)
+        torch.cuda.synchronize()
+    finally:
+        knob(1)
+    xr, Wr = bf16_round(x), bf16_round(Wt).reshape(Cout, Cin, 3, 3)
+    pre = np.einsum("bchwij,ocij->bohw", win(xr, (3, 3), axis=(2, 3)), Wr) + bias.astype(np.float64)[None, :, None, None]
+    dyt = dy.astype(np.float64) * (pre > 0) if relu else dy.astype(np.float64)
+    dyr = bf16_round(dyt.astype(np.float32))
+    gref = gw0 + 0.5 * np.einsum("bohw,bchwij->ocij", dyr, win(xr, (3, 3), axis=(2, 3))).reshape(Cout, Cin * 9)
+    err = np.abs(conv.gradWeight.cpu().numpy() - gref).max() / np.abs(gref - gw0).max()
+    assert err <= 2e-5, ("dW", err)
+    bref = 0.5 * dyt.sum(axis=(0, 2, 3))
+    err = np.abs(conv.gradBias.cpu().numpy() - bref).max() / np.abs(bref).max()
+    assert err <= 2e-5, ("db", err)
