@@ -118,6 +118,7 @@ struct s2s_ctx {
   // it without a device sync; s2s_ctx_status reads it after a stream sync and clears it
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
+  s2s::LtStage lt;  // bf16 operand copies of the hipBLASLt GEMMs (blaslt.cpp)
 };
 
 namespace {
@@ -138,6 +139,7 @@ int set_device(s2s_ctx* ctx) {
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
   set_gemm_precision(ctx->precision == S2S_PREC_FP32 ? kGemmF32 : kGemmBf16);
   set_wgrad_bf16(ctx->precision == S2S_PREC_BF16_ALL);
+  set_lt_stage(&ctx->lt);
   return 0;
 }
 
@@ -671,6 +673,7 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   for (auto& g : ctx->graphs) (void)drop_graph(ctx, g);
   ctx->graphs.clear();
   if (ctx->seed_dev) (void)hipFree(ctx->seed_dev);
+  s2s::lt_stage_free(&ctx->lt);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);

@@ -323,11 +323,29 @@ size_t tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW) {
   return kWsBytes + align256(sizeof(float) * (size_t)B * L * Dout) + align256(sizeof(float) * (size_t)B * L * kW * Din);
 }
 
+// A large plain GEMM of the front-end: on hipBLASLt under the bf16 modes (gemm_lt, blaslt.cpp), else gemm_f32.
+// Problems below ~1 GFLOP stay in-house (launch overhead, and they are not the front-end's time).
+static int big_gemm(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
+                    const float* Bm, long ldb, float beta, float* C, long ldc, const float* bias, int relu,
+                    GemmWs ws = GemmWs{}) {
+  GemmProblem q{A, Bm, C, bias, lda, ldb, ldc, M, N, K, alpha, beta};
+  q.relu = relu;
+  if (gemm_precision() == kGemmBf16 && 2.0 * M * (double)N * K >= 1e9) {
+    bool done = false;
+    S2S_TRY(gemm_lt(st, q, tA, tB, ws, &done));
+    if (done) return 0;
+  }
+  return gemm_f32(st, &q, 1, tA, tB, ws);
+}
+
 int tconv_fwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W,
               const float* b, float* y) {
   S2S_REQUIRE(B > 0 && Din > 0 && Dout > 0 && kW > 0, "TemporalConvolution: bad sizes");
   S2S_REQUIRE(L >= kW, "TemporalConvolution: input sequence smaller than kernel size");
   const int Lo = L - kW + 1;
+  // kW = 1 (nn.Linear, the VGG model's 1x1 layers): the utterances' rows are one (B L x Din) matrix -- one GEMM
+  if (kW == 1 && gemm_precision() == kGemmBf16)
+    return big_gemm(st, false, true, B * L, Dout, Din, 1.f, x, Din, W, Din, 0.f, y, Dout, b, relu);
   for (int b0 = 0; b0 < B; b0 += kMaxGemmBatch) {
     GemmProblem pr[kMaxGemmBatch];
     const int nb = std::min(kMaxGemmBatch, B - b0);
@@ -360,12 +378,12 @@ int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
   if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db, ws_of(scratch)));
   if (dW) {
     WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
-    S2S_TRY(gemm1(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
-                  nullptr, ws_of(scratch)));
+    S2S_TRY(big_gemm(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
+                     nullptr, 0, ws_of(scratch)));
   }
   if (dx) {
-    S2S_TRY(gemm1(st, false, false, B * L, kW * Din, Dout, 1.f, dyp, Dout, W, (long)kW * Din, 0.f, dU,
-                  (long)kW * Din));
+    S2S_TRY(big_gemm(st, false, false, B * L, kW * Din, Dout, 1.f, dyp, Dout, W, (long)kW * Din, 0.f, dU,
+                     (long)kW * Din, nullptr, 0));
     hipLaunchKernelGGL(tconv_gather_dx, dim3(grid1d((long)B * L * Din)), dim3(256), 0, st, dU, B, L, Din, kW,
                        dx_accumulate, dx);
     S2S_CHECK_HIP(hipGetLastError());

@@ -1,5 +1,6 @@
 // Shared internals of libs2s_hip.so (MI355X / gfx950 only).
 #pragma once
+#include <vector>
 #include <hip/hip_runtime.h>
 
 #include <atomic>
@@ -129,6 +130,20 @@ struct GemmWs {
 constexpr size_t kGemmWsFloats = size_t(8) << 20;  // 32 MiB
 // All problems of one call share transA/transB.
 int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB, GemmWs ws = GemmWs{});
+// One problem on hipBLASLt with bf16 operand rounding (HIPBLAS_COMPUTE_32F_FAST_16BF: fp32 in HBM, RNE bf16 in
+// the MFMA, fp32 accumulate and result; blaslt.cpp) -- the front-end's large plain GEMMs under the bf16 modes.
+// *done = false (nothing launched) when it does not apply (rbias / Mread / Nread, no algorithm, disabled by
+// s2s_debug_gemm_lt(0)); the caller then runs gemm_f32.
+// staging buffer for gemm_lt's bf16 operand copies, owned by a context (grown outside stream capture only)
+struct LtStage {
+  void* p = nullptr;
+  size_t n = 0;
+  std::vector<void*> old;
+};
+void set_lt_stage(LtStage* s);  // the calling thread's current context's buffer (set at every C-ABI entry)
+void lt_stage_free(LtStage* s);
+bool gemm_lt_enabled();
+int gemm_lt(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done);
 // Implicit-GEMM SpatialConvolutionMM on bf16 MFMA (conv_bf16.inc): no im2col panel.  Forward y (B, Cout, Ho,
 // Wo) = conv(x) + bias (per channel), ReLU when relu; input gradient dx (B, Cin, H, W) (+)= transposed
 // convolution of dyt (Cout, B Ho Wo) -- the ReLU-masked output gradient -- with W.  scratch:

@@ -279,3 +279,57 @@ def test_bf16_conv_weight_gradient_exact_on_rounded_operands(lib, implicit, B, C
     bref = 0.5 * dyt.sum(axis=(0, 2, 3))
     err = np.abs(conv.gradBias.cpu().numpy() - bref).max() / np.abs(bref).max()
     assert err <= 2e-5, ("db", err)
+
+
+@pytest.mark.parametrize("lt", [1, 0])
+@pytest.mark.parametrize("B,L,Din,Dout,relu", [(4, 508, 896, 2048, True), (3, 300, 2048, 512, False), (2, 50, 64, 40, True)])
+def test_bf16_linear_layer_exact_on_rounded_operands(lib, lt, B, L, Din, Dout, relu):
+    """TemporalConvolution(Din, Dout, 1) (+ReLU) -- the VGG model's 1x1 layers and nn.Linear -- under bf16-all: one
+    GEMM over the B L rows, on hipBLASLt when large (HIPBLAS_COMPUTE_32F_FAST_16BF; lt=0 forces the in-house bf16
+    kernel).  Forward, input gradient and weight / bias gradients equal float64 products of the RNE-bf16-rounded
+    operands up to fp32 accumulation order (<= 2e-5 of max|ref|), and two runs are bitwise equal."""
+    import s2s_amd
+    from s2s_amd import frontend as fe
+    knob = lib.lib.s2s_debug_gemm_lt
+    knob.argtypes = [ctypes.c_int]
+    rng = np.random.default_rng(B + L + Din)
+    m = fe.TemporalConvolution(Din, Dout, 1, relu=relu)
+    x = rng.standard_normal((B, L, Din)).astype(np.float32)
+    W = (rng.standard_normal((Dout, Din)) / np.sqrt(Din)).astype(np.float32)
+    b = (rng.standard_normal(Dout) * 0.1).astype(np.float32)
+    dy = rng.standard_normal((B, L, Dout)).astype(np.float32)
+    m.weight, m.bias = torch.tensor(W, device="cuda"), torch.tensor(b, device="cuda")
+    xg, dyg = torch.tensor(x, device="cuda"), torch.tensor(dy, device="cuda")
+    calls = lib.lib.s2s_debug_gemm_lt_calls
+    calls.restype = ctypes.c_long
+    last = lib.lib.s2s_debug_gemm_lt_last
+    n0 = calls()
+    outs = []
+    knob(lt)
+    try:
+        for _ in range(2):
+            m.gradWeight, m.gradBias = torch.zeros_like(m.weight), torch.zeros_like(m.bias)
+            with s2s_amd.precision("bf16-all"):
+                y = m.forward(xg).clone()
+                dx = m.backward(xg, dyg, 0.5).clone()
+            outs.append((y, dx, m.gradWeight.clone(), m.gradBias.clone()))
+        torch.cuda.synchronize()
+    finally:
+        knob(1)
+    for a, c in zip(outs[0], outs[1]):
+        assert torch.equal(a, c)
+    big = 2.0 * B * L * Din * Dout >= 1e9
+    assert (calls() - n0 == 6) == (bool(lt) and big), (calls() - n0, last())  # fwd, dx, dW per run
+    y, dx, gw, gb = (t.double().cpu().numpy() for t in outs[0])
+    xr, Wr = bf16_round(x).reshape(B * L, Din), bf16_round(W)
+    pre = xr @ Wr.T + b.astype(np.float64)
+    yref = np.maximum(pre, 0) if relu else pre
+    assert np.abs(y.reshape(B * L, Dout) - yref).max() / np.abs(yref).max() <= 2e-5
+    dyt = dy.reshape(B * L, Dout).astype(np.float64) * ((pre > 0) if relu else 1.0)
+    dyr = bf16_round(dyt.astype(np.float32))
+    dxref = dyr @ Wr
+    assert np.abs(dx.reshape(B * L, Din) - dxref).max() / np.abs(dxref).max() <= 2e-5
+    gref = 0.5 * dyr.T @ xr
+    assert np.abs(gw - gref).max() / np.abs(gref).max() <= 2e-5
+    bref = 0.5 * dyt.sum(0)
+    assert np.abs(gb - bref).max() / np.abs(bref).max() <= 2e-5
