@@ -164,7 +164,7 @@ bool gemm_lt_enabled() { return g_gemm_lt != 0; }
 
 int gemm_lt(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done) {
   *done = false;
-  if (!g_gemm_lt || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
+  if (!g_gemm_lt || !t_stage || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
   int dev = 0;
   S2S_CHECK_HIP(hipGetDevice(&dev));
   // C^T (N x M) = op(B)^T op(A)^T: A' = B's buffer, B' = A's buffer (see the header comment)

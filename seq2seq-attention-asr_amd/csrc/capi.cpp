@@ -1120,6 +1120,9 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
                    const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
                    void* workspace, size_t workspace_bytes) {
   S2S_TRY(set_device(ctx));
+  // the model step keeps its GEMMs in-house: it is captured into a HIP graph at its first call (graph mode), where
+  // hipBLASLt's plan creation and first kernel loads would happen inside the capture
+  set_lt_stage(nullptr);
   S2S_TRY(check_model_dims(d));
   S2S_REQUIRE(params && grads && x && labels && workspace, "model: null argument");
   S2S_REQUIRE(workspace_bytes >= model_ws(d, nullptr).total, "model: workspace too small");
