@@ -103,6 +103,52 @@ def cpu_worker(args):
 
 
 def cpu_baseline(kw, L, T, seconds_budget):
+    """CPU baseline on the host's cores (at most 16, the GPU box's share): the C restatement of the training step
+    (oracle/cpu_ref.c, fp32, reference semantics -- every utterance forwarded and back-propagated alone with
+    per-time-step matrix-vector products, timit/timit.lua:240-295 -- OpenMP over the minibatch's utterances);
+    the NumPy restatement in one process per core when the C library is not built."""
+    try:
+        return cpu_baseline_c(kw, L, T, seconds_budget)
+    except (OSError, FileNotFoundError):
+        return cpu_baseline_numpy(kw, L, T, seconds_budget)
+
+
+def cpu_baseline_c(kw, L, T, seconds_budget):
+    import numpy as np
+    from oracle import cpu_ref
+    from oracle import s2s_oracle as orc
+    cores = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    kw = dict(kw)
+    p = kw.pop("dropout", 0.0)
+    cfg = orc.ModelConfig(**kw)
+    flat = orc.flatten(orc.init_params(cfg, seed=1234, dtype=np.float32), cfg)
+    rng = np.random.default_rng(11)
+
+    def batch(n, seed):
+        x, lab = orc.synthetic_batch(cfg, n, L, T, seed=seed, dtype=np.float32)
+        m = None
+        if p > 0:  # nn.Dropout masks of the decoder MLP input, scaled by 1/(1-p)
+            m = ((rng.random((n, T, cfg.stateDepth + cfg.annotationDepth)) >= p) / (1.0 - p)).astype(np.float32)
+        return x, lab, m
+
+    x, lab, m = batch(cores, 1)
+    t = time.perf_counter()
+    cpu_ref.training_step(x, lab, flat, cfg, dropout_mask=m, threads=cores)  # one utterance per thread
+    t1 = time.perf_counter() - t
+    rounds = max(1, int(seconds_budget / max(t1, 1e-3)))
+    n = rounds * cores
+    x, lab, m = batch(n, 2)
+    t = time.perf_counter()
+    cpu_ref.training_step(x, lab, flat, cfg, dropout_mask=m, threads=cores)
+    wall = time.perf_counter() - t
+    return {"value": round(n * L / wall, 1), "unit": "frames/s", "cores": cores, "kind": "port",
+            "sample": f"one minibatch of {n} utterances (L={L}, T={T}, fp32) of the same model, each forwarded and "
+                      f"back-propagated alone (reference semantics, per-time-step matrix-vector products), "
+                      f"gradients summed: oracle/cpu_ref.c (C restatement of the Torch7 path, not Torch7), "
+                      f"OpenMP over the utterances on {cores} threads, {wall:.1f} s wall"}
+
+
+def cpu_baseline_numpy(kw, L, T, seconds_budget):
     """CPU restatement (oracle/, numpy fp32, per-utterance like timit/timit.lua:240-295) on the host's
     cores: one single-threaded worker process per core, each running whole utterances."""
     import multiprocessing as mp
