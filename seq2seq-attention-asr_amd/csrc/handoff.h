@@ -496,6 +496,49 @@ __device__ __forceinline__ floatx4 mfma_chunks(const float4 (&a)[NC], const floa
   return acc0 + acc1;
 }
 
+// mfma_chunks with the W fragments held in AGPRs, the accumulator half of gfx950's unified register file: an
+// MFMA may read its A / B operands from AGPRs (cdna_hip_programming.md §3), so a kernel that keeps 100+ floats of
+// weight fragments per lane for a whole launch leaves its 256 VGPRs to the code between the products -- the
+// decoder kernels' attention loops otherwise run on one or two free VGPRs, every tanh chain serialised.  The
+// same instruction sequence and accumulator split as mfma_chunks (bitwise-equal sums).  Inline asm, so its wait
+// states are explicit: s_nop 1 before each MFMA (a just-written VGPR / AGPR operand), the first product of each
+// accumulator takes C = 0 (no VALU-written C), and s_nop 11 after the chain before anything reads the
+// accumulators (8-pass XDL result -> reader), tied to them so the readers stay below it.
+template <int NC>
+__device__ __forceinline__ floatx4 mfma_chunks_aw(const float4 (&a)[NC], const float4 (&w)[NC]) {
+  floatx4 acc0, acc1;
+#define S2S_MFMA_AW0(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(acc) : "v"(x), "a"(y))
+#define S2S_MFMA_AW(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "a"(y))
+  static_assert(NC >= 1, "mfma_chunks_aw");
+  S2S_MFMA_AW0(acc0, a[0].x, w[0].x);
+  if (NC >= 2) S2S_MFMA_AW0(acc1, a[1].x, w[1].x);
+  else acc1 = floatx4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i + 1 < NC; i += 2) {
+    if (i > 0) {
+      S2S_MFMA_AW(acc0, a[i].x, w[i].x);
+      S2S_MFMA_AW(acc1, a[i + 1].x, w[i + 1].x);
+    }
+    S2S_MFMA_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA_AW(acc1, a[i + 1].y, w[i + 1].y);
+    S2S_MFMA_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA_AW(acc1, a[i + 1].z, w[i + 1].z);
+    S2S_MFMA_AW(acc0, a[i].w, w[i].w);
+    S2S_MFMA_AW(acc1, a[i + 1].w, w[i + 1].w);
+  }
+  if (NC & 1) {
+    constexpr int i = NC - 1;
+    if (NC > 1) S2S_MFMA_AW(acc0, a[i].x, w[i].x);
+    S2S_MFMA_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA_AW(acc0, a[i].w, w[i].w);
+  }
+#undef S2S_MFMA_AW0
+#undef S2S_MFMA_AW
+  asm volatile("s_nop 11" : "+v"(acc0), "+v"(acc1));
+  return acc0 + acc1;
+}
+
 // W operand fragments of one output-unit row (chunk i at wave*16 + 64 i), kept in VGPRs
 template <int NC>
 __device__ __forceinline__ void load_wfrag(float4 (&w)[NC], const float* row, int wave, int lane) {
