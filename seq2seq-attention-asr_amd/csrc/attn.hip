@@ -1438,10 +1438,10 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   const int rows = B * T, bt = (B + 15) / 16;
   const XPlan xp = dec_xcd_plan(d);
   // the XCD-local path's first dh writer is the alpha^T dc GEMM (beta 0 when not accumulating)
-  if (!accumulate_dh && !xp.var) S2S_CHECK_HIP(hipMemsetAsync(dh, 0, sizeof(float) * (size_t)B * L * A, st));
+  if (!accumulate_dh && !xp.var) S2S_TRY(zero_async(st, dh, sizeof(float) * (size_t)B * L * A));
   if (!xp.var) {  // the XCD-local path writes DVH / DWEACC whole after its loop
-    S2S_CHECK_HIP(hipMemsetAsync(k.DVH, 0, sizeof(float) * (size_t)B * L * Sc, st));
-    S2S_CHECK_HIP(hipMemsetAsync(k.DWEACC, 0, sizeof(float) * (size_t)B * k.NCH * Sc, st));
+    S2S_TRY(zero_async(st, k.DVH, sizeof(float) * (size_t)B * L * Sc));
+    S2S_TRY(zero_async(st, k.DWEACC, sizeof(float) * (size_t)B * k.NCH * Sc));
   }
   // packed transposes for the backward products
   if (d.lstm) S2S_TRY(transpose_f32(st, k.LW, 2L * S, 4 * S, 2 * S, k.GT, 4L * S));  // GT = LW^T
@@ -1516,8 +1516,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   } else {
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   if (d.hf > 0) {
-    S2S_CHECK_HIP(hipMemsetAsync(k.QA, 0, sizeof(float) * 2 * (size_t)B * L * d.hk, st));
-    S2S_CHECK_HIP(hipMemsetAsync(k.PDG, 0, sizeof(float) * (size_t)B * k.NCH * d.hk * Sc, st));
+    S2S_TRY(zero_async(st, k.QA, sizeof(float) * 2 * (size_t)B * L * d.hk));
+    S2S_TRY(zero_async(st, k.PDG, sizeof(float) * (size_t)B * k.NCH * d.hk * Sc));
   }
   ProfScope ps(st, "dec_bwd_steps", 0.0, 0.0);
   for (int t = T - 1; t >= 0; --t) {

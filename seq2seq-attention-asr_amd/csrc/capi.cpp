@@ -343,7 +343,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   const int pmode = prologue_mode();
   if (split) S2S_TRY(fork_to(st, side, ev[13]));
   if (flags & S2S_ZERO_GRADS)
-    S2S_CHECK_HIP(hipMemsetAsync(grads, 0, sizeof(float) * (size_t)off, split ? side : st));
+    S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
@@ -436,7 +436,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     bool later = false;
     for (int l = 1; l < nl; ++l) later = later || gru_layer_persistent(layer_io(l));
     if (later)
-      for (int r = 0; r < 2; ++r) S2S_CHECK_HIP(hipMemsetAsync(w.gsync[r], 0, 256, st));
+      for (int r = 0; r < 2; ++r) S2S_TRY(zero_async(st, w.gsync[r], 256));
   }
   // ---- encoder forward (3 x BiGRU, JoinTable(2,2) by strided writes)
   for (int l = 0; l < nl; ++l) {

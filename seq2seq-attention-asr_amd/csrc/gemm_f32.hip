@@ -579,6 +579,10 @@ __global__ void pad_cols_kernel(const float* __restrict__ src, long lds, float* 
   }
 }
 
+__global__ void fill_words_kernel(unsigned* __restrict__ dst, size_t n, unsigned v) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) dst[i] = v;
+}
+
 __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ dst, size_t n, float alpha,
                              float beta) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
@@ -793,6 +797,26 @@ int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alph
   hipLaunchKernelGGL(axpby_kernel, dim3((unsigned)blocks), dim3(256), 0, st, src, dst, n, alpha, beta);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
+}
+
+// Kernel fills instead of hipMemsetAsync / hipMemsetD32Async: measured on MI355X (ROCm 7.2), a memset
+// captured into a HIP graph together with the kernels around it did not clear its range on the second and
+// later replays (a captured LSTM fwd + bwd read the previous replay's carries: tools/diag_graph.py);
+// a fill kernel is an ordinary kernel node.
+int fill_u32_async(hipStream_t st, void* dst, unsigned value, size_t count) {
+  S2S_REQUIRE((reinterpret_cast<uintptr_t>(dst) & 3) == 0, "fill_u32_async: dst must be 4-byte aligned");
+  if (count == 0) return 0;
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 2048) blocks = 2048;
+  hipLaunchKernelGGL(fill_words_kernel, dim3((unsigned)blocks), dim3(256), 0, st, static_cast<unsigned*>(dst), count,
+                     value);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int zero_async(hipStream_t st, void* dst, size_t bytes) {
+  S2S_REQUIRE(bytes % 4 == 0, "zero_async: whole 4-byte words only");
+  return fill_u32_async(st, dst, 0u, bytes / 4);
 }
 
 // ------------------------------------------------------------------ implicit-GEMM convolutions (conv_bf16.inc)

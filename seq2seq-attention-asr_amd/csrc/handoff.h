@@ -138,14 +138,14 @@ static __global__ __launch_bounds__(256) void sync_prep(char* sync, size_t bytes
 // hdr (optional): the region's header lives there instead of at `sync` (whose first 256 bytes are then unused)
 inline int launch_sync_prep(hipStream_t st, void* sync, size_t bytes, void* clear = nullptr, void* hdr = nullptr) {
   // bytes - 256 is a multiple of 8 (granules) and of 4 (census words); round the tail up is not
-  // allowed, so clear the last partial 16-byte piece with the memset only when present
+  // allowed, so clear the last partial 16-byte piece with zero_async only when present
   const size_t n16 = (bytes - 256) / 16;
   int blocks = (int)std::min<size_t>(1024, (n16 + 255) / 256);
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(sync_prep, dim3(blocks), dim3(256), 0, st, static_cast<char*>(sync), bytes,
                      inject_abort_take() ? 2u : 0u, static_cast<char*>(clear), static_cast<char*>(hdr));
   if ((bytes - 256) % 16)
-    S2S_CHECK_HIP(hipMemsetAsync(static_cast<char*>(sync) + 256 + n16 * 16, 0, (bytes - 256) % 16, st));
+    S2S_TRY(zero_async(st, static_cast<char*>(sync) + 256 + n16 * 16, (bytes - 256) % 16));
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -351,8 +351,8 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
   for (int d = 0; d < nd; ++d) {
     S2S_TRY(launch_lstm_pack(st, io.W + d * np, H, D, io.peep, c.Wx4 + 4L * d * H * D, nullptr, c.Wb[d],
                              io.peep ? c.WocT[d] : nullptr));
-    S2S_CHECK_HIP(hipMemsetAsync(c.dhc[d], 0, sizeof(float) * (size_t)B * H, st));
-    S2S_CHECK_HIP(hipMemsetAsync(c.dcc[d], 0, sizeof(float) * (size_t)B * H, st));
+    S2S_TRY(zero_async(st, c.dhc[d], sizeof(float) * (size_t)B * H));
+    S2S_TRY(zero_async(st, c.dcc[d], sizeof(float) * (size_t)B * H));
     a.d[d] = LstmBwdDir{gr.dy[d], gr.lddy, io.saved[d], c.WocT[d], c.Wb[d], c.dA + 4L * d * H, ldA,
                         c.dhc[d], c.dcc[d], c.dcp[d], c.dcn[d], io.reverse[d]};
   }

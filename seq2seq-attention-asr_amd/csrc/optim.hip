@@ -186,13 +186,13 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
 // checkpointed table; stream-ordered, no sync (the next step increments it before drawing)
 int optim_set_noise_step(hipStream_t st, void* state, size_t n, unsigned t) {
   const OptState s = carve_state(state, n);
-  S2S_CHECK_HIP(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(s.scal + 3), (int)t, 1, st));
+  S2S_TRY(fill_u32_async(st, s.scal + 3, t, 1));
   return 0;
 }
 
 // zero paramVariance / accDelta (optim.adadelta's lazily created state) and the noise counter t
 int optim_state_reset(hipStream_t st, void* state, size_t n) {
-  S2S_CHECK_HIP(hipMemsetAsync(state, 0, optim_state_bytes(n), st));
+  S2S_TRY(zero_async(st, state, optim_state_bytes(n)));
   return 0;
 }
 

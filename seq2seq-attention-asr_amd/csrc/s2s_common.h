@@ -180,6 +180,10 @@ int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd,
 int transpose_f32(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd);
 // dst (rows x dcols, ld dcols) = src (rows x cols, ld lds) with columns [cols, dcols) zeroed
 int pad_cols_f32(hipStream_t st, const float* src, long lds, float* dst, int rows, int cols, int dcols);
+// dst[0, bytes) = 0 / count words = value, by a kernel launch: every clear of the library goes through these
+// (no hipMemsetAsync: its graph nodes did not replay reliably, gemm_f32.hip)
+int zero_async(hipStream_t st, void* dst, size_t bytes);
+int fill_u32_async(hipStream_t st, void* dst, unsigned value, size_t count);
 // dst[i] = alpha * src[i] + beta * dst[i]
 int axpby_f32(hipStream_t st, const float* src, float* dst, size_t n, float alpha, float beta);
 

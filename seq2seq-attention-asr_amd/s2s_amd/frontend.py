@@ -414,7 +414,42 @@ class VGGEncoder(Module):
         return self.gradInput
 
 
-class VGGAttentionModel(Module):
+class GraphStep:
+    """graph_step() for the host-side models (VGGAttentionModel, ConvBiLSTMAttentionModel): their step is a
+    sequence of module calls from Python (front-end Sequential, decoder, decoder_mlp, loss seed and every
+    backward), hundreds of launches -- the per-step decoder kernels of the conv + BiLSTM model alone launch a
+    handful per decoder step -- replayed from one captured HIP graph."""
+
+    def graph_step(self, x, labels, scale=None, normalizeNLL=False):
+        """zeroGradParameters() + step() replayed from a captured HIP graph: every launch of the host-side
+        step (front-end, decoder, decoder_mlp, loss seed and every backward) becomes one graph launch.  The
+        capture is keyed by the input / label buffers (pointers and shapes): refill x and labels in place to
+        train on new data.  The first call of a key runs one eager step
+        (which sizes every lazily grown buffer, so the capture allocates only from its graph pool), then
+        captures and replays; the returned (nll, logp) are the graph's own buffers, rewritten by every
+        replay.  grads = this step's gradient (the graph zeroes them first)."""
+        key = (x.data_ptr(), tuple(x.shape), labels.data_ptr(), tuple(labels.shape), scale, normalizeNLL)
+        graphs = self.__dict__.setdefault("_graphs", {})
+        g = graphs.get(key)
+        if g is None:
+            self.zeroGradParameters()
+            self.step(x, labels, scale, normalizeNLL)
+            cur = torch.cuda.current_stream(x.device)
+            cur.synchronize()
+            graph = torch.cuda.CUDAGraph()
+            side = torch.cuda.Stream(x.device)
+            side.wait_stream(cur)
+            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+                self.zeroGradParameters()
+                out = self.step(x, labels, scale, normalizeNLL)
+            cur.wait_stream(side)
+            graphs[key] = g = (graph, out)
+        g[0].replay()
+        return g[1]
+
+
+
+class VGGAttentionModel(GraphStep, Module):
     """librispeech/model_vgg.lua:loadmodel(opt) end to end: VGGEncoder -> nn.Attention(GRU(S, S),
     decoder_mlp = Maxout(S+A, M, 7) -> Linear(M, M) -> Maxout(M, M, 7) -> Linear(M, O) -> LogSoftMax
     (:71-77), scoreDepth, hybrid (off by default), S, A, O, monoAlignPenalty = true, penalty) with the
@@ -455,35 +490,7 @@ class VGGAttentionModel(Module):
             self.encoder.backward(x, dh, scale)
         return nll, logp
 
-    def graph_step(self, x, labels, scale=None, normalizeNLL=False):
-        """zeroGradParameters() + step() replayed from a captured HIP graph: the ~100 launches of the
-        host-side Sequential (conv stack, 1x1 layers, decoder, decoder_mlp, loss seed and every backward)
-        become one graph launch.  The capture is keyed by the input / label buffers (pointers and shapes):
-        refill x and labels in place to train on new data.  The first call of a key runs one eager step
-        (which sizes every lazily grown buffer, so the capture allocates only from its graph pool), then
-        captures and replays; the returned (nll, logp) are the graph's own buffers, rewritten by every
-        replay.  grads = this step's gradient (the graph zeroes them first)."""
-        key = (x.data_ptr(), tuple(x.shape), labels.data_ptr(), tuple(labels.shape), scale, normalizeNLL)
-        graphs = self.__dict__.setdefault("_graphs", {})
-        g = graphs.get(key)
-        if g is None:
-            self.zeroGradParameters()
-            self.step(x, labels, scale, normalizeNLL)
-            cur = torch.cuda.current_stream(x.device)
-            cur.synchronize()
-            graph = torch.cuda.CUDAGraph()
-            side = torch.cuda.Stream(x.device)
-            side.wait_stream(cur)
-            with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
-                self.zeroGradParameters()
-                out = self.step(x, labels, scale, normalizeNLL)
-            cur.wait_stream(side)
-            graphs[key] = g = (graph, out)
-        g[0].replay()
-        return g[1]
-
-
-class ConvBiLSTMAttentionModel(Module):
+class ConvBiLSTMAttentionModel(GraphStep, Module):
     """The conv + BiLSTM model timit/timit.lua builds when no model file is given (:106-145), end to end:
     ConvBiLSTMEncoder (3 x conv(k=3, 256) + ReLU + TemporalMaxPooling(2, 2), BiLSTM 2 x 128) ->
     nn.Attention(decoder_recurrent = LSTM(400, 400), decoder_mlp = Linear(400 + 256, 2*O) -> ReLU ->

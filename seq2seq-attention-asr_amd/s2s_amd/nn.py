@@ -8,6 +8,7 @@ SGD mode, Recurrent.lua:67-77); 3-D inputs are a batch of equal-length utterance
 """
 import contextlib
 import ctypes
+import os
 import math
 
 import torch
@@ -104,8 +105,14 @@ def dptr(t):
     return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
 
 
+_POISON = os.environ.get("S2S_POISON_SCRATCH") == "1"  # diagnostic: fill every scratch / saved buffer with NaN
+
+
 def _bytes(n, device):
-    return torch.empty(max(int(n), 1), dtype=torch.uint8, device=device)
+    t = torch.empty(max(int(n), 1), dtype=torch.uint8, device=device)
+    if _POISON:
+        t.fill_(0xFF)  # all-ones words: NaN in every float view -- a read before write shows up in the outputs
+    return t
 
 
 def _require_cuda_f32(t, name):

@@ -567,6 +567,73 @@ def test_vgg_graph_step_equals_eager(fe, prec):
     assert len(graphed._graphs) == 1
 
 
+@pytest.mark.gpu
+def test_conv_bilstm_graph_step_equals_eager(fe):
+    """ConvBiLSTMAttentionModel.graph_step (timit/timit.lua:106-145: LSTM decoder, hybrid attention, per-step
+    decoder kernels) is bitwise the eager zeroGradParameters() + step(), also with new data in the captured
+    buffers."""
+    import s2s_amd
+    rng = np.random.default_rng(8)
+    B, L, D, T, O = 3, 64, 20, 7, 11
+
+    def make():
+        return s2s_amd.ConvBiLSTMAttentionModel(D, numPhonemes=O, hiddenFrameSize=32, outputFrameSize=16, stateDepth=48,
+                                                scoreDepth=30, penalty=0.1, generator=torch.Generator().manual_seed(2)).cuda()
+
+    eager, graphed = make(), make()
+    x = cu(rng.standard_normal((B, L, D)))
+    labels = cu(rng.integers(0, O, (B, T)), torch.int32)
+    xg, lg = x.clone(), labels.clone()
+    for it in range(3):
+        if it == 2:
+            x.copy_(cu(rng.standard_normal((B, L, D))))
+            xg.copy_(x)
+        eager.zeroGradParameters()
+        nll_e, logp_e = eager.step(x, labels)
+        nll_g, logp_g = graphed.graph_step(xg, lg)
+        torch.cuda.synchronize()
+        assert torch.equal(logp_e, logp_g) and torch.equal(nll_e, nll_g), it
+        for i, (ge, gg) in enumerate(zip(eager.parameters()[1], graphed.parameters()[1])):
+            assert torch.equal(ge, gg), (it, i)
+
+
+@pytest.mark.gpu
+def test_lstm_fwd_bwd_one_graph_replays(fe):
+    """BiRNN(LSTM) forward + backward captured in ONE graph equals the eager pair on every replay (the backward's
+    carries used to be cleared by hipMemsetAsync, whose graph node left the previous replay's values in place from
+    the second replay on; the library clears with fill kernels now)."""
+    import s2s_amd
+    rng = np.random.default_rng(11)
+    B, L, D, H = 3, 6, 32, 16
+    x = cu(rng.standard_normal((B, L, D)))
+    gy = cu(rng.standard_normal((B, L, 2 * H)))
+
+    def make():
+        return s2s_amd.BiRNN(s2s_amd.LSTM(D, H, False, torch.Generator().manual_seed(1)),
+                             s2s_amd.LSTM(D, H, False, torch.Generator().manual_seed(2))).cuda()
+
+    def fn(m):
+        m.zeroGradParameters()
+        y = m.forward(x)
+        return y, m.backward(x, gy, 0.5)
+
+    eager, graphed = make(), make()
+    fn(graphed)
+    torch.cuda.synchronize()
+    graph, side = torch.cuda.CUDAGraph(), torch.cuda.Stream()
+    side.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
+        yg, dxg = fn(graphed)
+    torch.cuda.current_stream().wait_stream(side)
+    for it in range(3):
+        ye, dxe = fn(eager)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(ye, yg) and torch.equal(dxe, dxg), it
+        for i, (ge, gg) in enumerate(zip(eager.parameters()[1], graphed.parameters()[1])):
+            assert torch.equal(ge, gg), (it, i)
+
+
 # --------------------------------------------------------------------------- LSTM decoder (conv + BiLSTM model)
 
 def _lstm_dec_case(rng, S, A, Sc, O, hybrid, mlp_kind):

@@ -29,7 +29,8 @@ static float bf16r(float f) {
   return f;
 }
 
-static int run(hipblasLtHandle_t h, bool bf16in, int opA, int opB, int m, int n, int k, const char* tag) {
+static int run(hipblasLtHandle_t h, bool bf16in, int opA, int opB, int m, int n, int k, const char* tag,
+               bool f32compute = false) {
   std::mt19937 g(7);
   std::normal_distribution<float> nd;
   const int ra = opA ? k : m, ca = opA ? m : k, rb = opB ? n : k, cb = opB ? k : n;
@@ -54,7 +55,8 @@ static int run(hipblasLtHandle_t h, bool bf16in, int opA, int opB, int m, int n,
   }
   const hipDataType ti = bf16in ? HIP_R_16BF : HIP_R_32F;
   hipblasLtMatmulDesc_t desc;
-  CK(hipblasLtMatmulDescCreate(&desc, bf16in ? HIPBLAS_COMPUTE_32F : HIPBLAS_COMPUTE_32F_FAST_16BF, HIP_R_32F));
+  CK(hipblasLtMatmulDescCreate(&desc, (bf16in || f32compute) ? HIPBLAS_COMPUTE_32F : HIPBLAS_COMPUTE_32F_FAST_16BF,
+                                HIP_R_32F));
   hipblasOperation_t ta = opA ? HIPBLAS_OP_T : HIPBLAS_OP_N, tb = opB ? HIPBLAS_OP_T : HIPBLAS_OP_N;
   CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   CK(hipblasLtMatmulDescSetAttribute(desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
@@ -148,6 +150,13 @@ static void avail(hipblasLtHandle_t h, int opA, int opB, int m, int n, int k, in
 int main() {
   hipblasLtHandle_t h;
   CK(hipblasLtCreate(&h));
+  if (getenv("LT_F32")) {  // exact fp32 (HIPBLAS_COMPUTE_32F) at the config-2 step's critical-path shapes
+    run(h, false, 1, 0, 448, 1280, 768, "f32 MLP u = v Wm^T      (T,N)", true);
+    run(h, false, 1, 0, 512, 4096, 512, "f32 Vh = h V^T          (T,N)", true);
+    run(h, false, 0, 1, 384, 256, 4096, "f32 wgrad dW_g (N,T)        ", true);
+    run(h, false, 0, 0, 768, 1280, 448, "f32 dv = du Wm          (N,N)", true);
+    return 0;
+  }
   if (getenv("LT_AVAIL")) {
     for (int epi = 0; epi < 4; ++epi)
       for (size_t ws : {(size_t)0, (size_t)32 << 20}) {
