@@ -336,18 +336,24 @@ __global__ void dec_hyb_fold(AttnK k) {
   k.HCU[j] = c;
 }
 
-// UF of frame l for the 4 score columns of float4 c4; ap = alpha_{t-1} of the utterance (nullptr at t = 0)
-__device__ __forceinline__ float4 hyb_uf4(const AttnK& k, int c4, const float* ap, int l) {
+// alpha_{t-1} of frames ch*LC - pad_left .. ch*LC + LC - 1 + (kW - 1 - pad_left) into apl (0 outside [0, L) and
+// at t = 0): apl[lloc + i] is the tap-i input of chunk frame lloc.  All threads call it; ends on a barrier.
+__device__ __forceinline__ void hyb_stage_alpha(const AttnK& k, const float* ap, int ch, float* apl) {
+  const int pl = hyb_pad_left(k.hk), n = LC + k.hk - 1;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int m = ch * LC + i - pl;
+    apl[i] = (ap && m >= 0 && m < k.L) ? ap[m] : 0.f;
+  }
+  __syncthreads();
+}
+// UF of chunk frame lloc for the 4 score columns of float4 c4 (UF_{l,j} = HCU_j + sum_i HG_{j,i} apl[lloc + i]);
+// apl = the staged alpha_{t-1} halo, hg = the taps HGT ([kW][Sc], global or staged in LDS)
+__device__ __forceinline__ float4 hyb_uf4_lds(const AttnK& k, int c4, const float* apl, const float* hg, int lloc) {
   float4 u = reinterpret_cast<const float4*>(k.HCU)[c4];
-  if (ap) {
-    const int pl = hyb_pad_left(k.hk);
-    for (int i = 0; i < k.hk; ++i) {
-      const int m = l + i - pl;
-      if (m < 0 || m >= k.L) continue;
-      const float a = ap[m];
-      const float4 g = reinterpret_cast<const float4*>(k.HGT + (long)i * k.Sc)[c4];
-      u.x += g.x * a; u.y += g.y * a; u.z += g.z * a; u.w += g.w * a;
-    }
+  for (int i = 0; i < k.hk; ++i) {
+    const float a = apl[lloc + i];
+    const float4 g = reinterpret_cast<const float4*>(hg + (long)i * k.Sc)[c4];
+    u.x += g.x * a; u.y += g.y * a; u.z += g.z * a; u.w += g.w * a;
   }
   return u;
 }
@@ -407,12 +413,14 @@ __global__ __launch_bounds__(256) void dec_f1_ws(AttnK k) {
 __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
   __shared__ float sc[LC];
   __shared__ float pw[LC];
+  __shared__ float apl[LC + kMaxHybK];  // hybrid: alpha_{t-1} halo of the chunk (hyb_stage_alpha)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = blockIdx.x, b = blockIdx.y, t = k.t;
   const int L = k.L, Sc = k.Sc, A = k.A;
   const float* ws = k.WS + ((long)b * k.T + t) * Sc;
   const float* we = k.P.we;
   const float* ap = (k.hf > 0 && t > 0) ? k.ALPHA + ((long)b * k.T + t - 1) * L : nullptr;  // alpha_{t-1}
+  if (k.hf > 0) hyb_stage_alpha(k, ap, ch, apl);
   const int Lb = frames_of(k, b);
   for (int i = 0; i < 4; ++i) {
     const int li = wave * 4 + i, l = ch * LC + li;
@@ -425,7 +433,7 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
         const float4 e = reinterpret_cast<const float4*>(we)[c4];
         float4 z = make_float4(w.x + v.x, w.y + v.y, w.z + v.z, w.w + v.w);
         if (k.hf > 0) {  // Z = Ws + Vh + UF (Attention.lua:95)
-          const float4 u = hyb_uf4(k, c4, ap, l);
+          const float4 u = hyb_uf4_lds(k, c4, apl, k.HGT, li);
           z.x += u.x; z.y += u.y; z.z += u.z; z.w += u.w;
         }
         part += e.x * tanhf(z.x) + e.y * tanhf(z.y) + e.z * tanhf(z.z) + e.w * tanhf(z.w);
@@ -829,10 +837,14 @@ __global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
 //   dh_l += alpha_l dc;  dZ = de_l we (1 - tanh^2);  dVh_l += dZ;  partial dws, dwe
 //   HYB (hybrid attention): Z includes UF; d alpha_l also gets the carry from step t+1's location
 //   features (hyb_carry); q_{l,i} = sum_j dZ_lj HG_ji -> QA for step t-1; dG partials -> PDG
+//   HYB keeps this chunk's dZ rows in LDS (dynamic, LC x Sc floats) and forms q and the dG partials from them
+//   after the frame loop: per-lane register partials over every tap (kMaxHybK x 16 floats) spilled to scratch
+//   at one wave per SIMD (37.7 us per step at the conv + BiLSTM model's B = 32, Sc = 160; tools/ab_convlstm.py)
 template <bool HYB>
 __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   __shared__ float redv[4];
   __shared__ float pws[4][1024];
+  extern __shared__ float zl[];  // HYB: [LC][Sc] dZ rows of this chunk, then HGT [kW][Sc], then the alpha halo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = blockIdx.x, b = blockIdx.y, t = k.t;
   const int L = k.L, A = k.A, Sc = k.Sc, T = k.T;
@@ -859,18 +871,16 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   float dwsp[16], dwep[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) { dwsp[i] = 0.f; dwep[i] = 0.f; }
-  constexpr int HK = HYB ? kMaxHybK : 1;
-  float dgp[HK][16];  // dG partials: [tap i][column 4 c4 + e of this lane]
-  if (HYB) {
-#pragma unroll
-    for (int i = 0; i < HK; ++i)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) dgp[i][e] = 0.f;
-  }
   const float* ap = (HYB && t > 0) ? k.ALPHA + (row - 1) * L : nullptr;  // alpha_{t-1}
-  const int pl = HYB ? hyb_pad_left(k.hk) : 0;
+  const int lend = min(LC, L - ch * LC);  // frames of this chunk
+  float* hg = zl + (long)LC * Sc;         // HYB: the taps HGT, staged
+  float* apl = hg + (long)k.hk * Sc;      // HYB: alpha_{t-1} halo of the chunk
+  if (HYB) {
+    for (int i = tid; i < k.hk * Sc; i += 256) hg[i] = k.HGT[i];
+    hyb_stage_alpha(k, ap, ch, apl);
+  }
   for (int i4 = 0; i4 < 4; ++i4) {
-    const int l = ch * LC + wave * 4 + i4;
+    const int lloc = wave * 4 + i4, l = ch * LC + lloc;
     if (l >= L) break;
     const float* hl = k.h + ((long)b * L + l) * A;
     float dd = 0.f;
@@ -884,11 +894,6 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     const float dal = HYB ? dd + (lam * (float)(Lb - l) * (ind - indn) + hyb_carry(k, b, l))
                           : dd + lam * (float)(Lb - l) * (ind - indn);
     const float de = al * (dal - ssum);
-    float qv[HK];
-    if (HYB) {
-#pragma unroll
-      for (int i = 0; i < HK; ++i) qv[i] = 0.f;
-    }
     float* dhl = k.dh + ((long)b * L + l) * k.lddh;
     for (int a = lane; a < A; a += 64) dhl[a] += al * dc[a];
     const float* vh = k.Vh + ((long)b * L + l) * Sc;
@@ -903,37 +908,17 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
         float4 o = reinterpret_cast<float4*>(dvh)[c4];
         float4 zz = make_float4(w.x + v.x, w.y + v.y, w.z + v.z, w.w + v.w);
         if (HYB) {
-          const float4 u = hyb_uf4(k, c4, ap, l);
+          const float4 u = hyb_uf4_lds(k, c4, apl, hg, lloc);
           zz.x += u.x; zz.y += u.y; zz.z += u.z; zz.w += u.w;
         }
         const float th0 = tanhf(zz.x), th1 = tanhf(zz.y), th2 = tanhf(zz.z), th3 = tanhf(zz.w);
         const float z0 = de * e.x * (1.f - th0 * th0), z1 = de * e.y * (1.f - th1 * th1);
         const float z2 = de * e.z * (1.f - th2 * th2), z3 = de * e.w * (1.f - th3 * th3);
-        if (HYB) {
-#pragma unroll
-          for (int ii = 0; ii < HK; ++ii) {
-            if (ii >= k.hk) break;
-            const float4 g = reinterpret_cast<const float4*>(k.HGT + (long)ii * Sc)[c4];
-            qv[ii] += ((z0 * g.x + z1 * g.y) + z2 * g.z) + z3 * g.w;
-            const int m = l + ii - pl;
-            const float a = (ap && m >= 0 && m < L) ? ap[m] : 0.f;
-            dgp[ii][4 * i] += z0 * a; dgp[ii][4 * i + 1] += z1 * a;
-            dgp[ii][4 * i + 2] += z2 * a; dgp[ii][4 * i + 3] += z3 * a;
-          }
-        }
+        if (HYB) reinterpret_cast<float4*>(zl + (long)lloc * Sc)[c4] = make_float4(z0, z1, z2, z3);
         o.x += z0; o.y += z1; o.z += z2; o.w += z3;
         reinterpret_cast<float4*>(dvh)[c4] = o;
         dwsp[4 * i] += z0; dwsp[4 * i + 1] += z1; dwsp[4 * i + 2] += z2; dwsp[4 * i + 3] += z3;
         dwep[4 * i] += de * th0; dwep[4 * i + 1] += de * th1; dwep[4 * i + 2] += de * th2; dwep[4 * i + 3] += de * th3;
-      }
-    }
-    if (HYB) {  // q_{l,i} for d alpha_{t-1} (read by step t-1's kernel through hyb_carry)
-      float* qa = k.QA + ((long)(t & 1) * k.B + b) * L * k.hk + (long)l * k.hk;
-#pragma unroll
-      for (int ii = 0; ii < HK; ++ii) {
-        if (ii >= k.hk) break;
-        const float s = wave_sum(qv[ii]);
-        if (lane == 0) qa[ii] = s;
       }
     }
   }
@@ -958,20 +943,32 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
       if (pass == 0) pd[kk] = v; else pe[kk] += v;
     }
   }
-  if (HYB) {  // dG partials of this chunk, accumulated over the steps (PDG zeroed before the loop)
-    for (int ii = 0; ii < k.hk && ii < HK; ++ii) {
-      __syncthreads();
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c4 = lane + 64 * i;
-        if (c4 < Sc / 4) {
-          float* dst = &pws[wave][4 * c4];
-          dst[0] = dgp[ii][4 * i]; dst[1] = dgp[ii][4 * i + 1]; dst[2] = dgp[ii][4 * i + 2]; dst[3] = dgp[ii][4 * i + 3];
-        }
+  if (HYB) {  // (the passes above ended on a barrier after every zl store)
+    const int hk = k.hk;
+    // q_{l,i} = sum_j dZ_lj HG_ji for d alpha_{t-1} (read by step t-1's kernel through hyb_carry)
+    float* qa = k.QA + ((long)(t & 1) * k.B + b) * L * hk + (long)ch * LC * hk;
+    for (int p = wave; p < lend * hk; p += 4) {
+      const int lloc = p / hk, ii = p - lloc * hk;
+      const float4* z4 = reinterpret_cast<const float4*>(zl + (long)lloc * Sc);
+      const float4* g4 = reinterpret_cast<const float4*>(hg + (long)ii * Sc);
+      float q = 0.f;
+      for (int c4 = lane; c4 < Sc / 4; c4 += 64) {
+        const float4 z = z4[c4], g = g4[c4];
+        q += ((z.x * g.x + z.y * g.y) + z.z * g.z) + z.w * g.w;
       }
-      __syncthreads();
-      float* pg = k.PDG + (((long)b * k.NCH + ch) * k.hk + ii) * Sc;
-      for (int kk = tid; kk < Sc; kk += 256) pg[kk] += ((pws[0][kk] + pws[1][kk]) + pws[2][kk]) + pws[3][kk];
+      q = wave_sum(q);
+      if (lane == 0) qa[(long)lloc * hk + ii] = q;
+    }
+    // dG partials of this chunk, accumulated over the steps (PDG zeroed before the loop): sum_l dZ_lj
+    // alpha_{t-1}[l + i - pad_left] (no term at t = 0)
+    if (ap) {
+      float* pg = k.PDG + ((long)b * k.NCH + ch) * hk * Sc;
+      for (int e = tid; e < hk * Sc; e += 256) {
+        const int ii = e / Sc, kk = e - ii * Sc;
+        float g = 0.f;
+        for (int lloc = 0; lloc < lend; ++lloc) g += zl[(long)lloc * Sc + kk] * apl[lloc + ii];
+        pg[e] += g;
+      }
     }
   }
 }
@@ -1515,6 +1512,11 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_CHECK_HIP(hipGetLastError());
   } else {
   hipLaunchKernelGGL(dec_bwd_init, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
+  // dec_b6_attn<true>'s dZ rows, staged taps and alpha halo
+  const size_t b6_lds = d.hf > 0 ? sizeof(float) * ((LC + (size_t)d.hk) * Sc + LC + kMaxHybK) : 0;
+  if (b6_lds > 32 * 1024)
+    S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_b6_attn<true>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)b6_lds));
   if (d.hf > 0) {
     S2S_TRY(zero_async(st, k.QA, sizeof(float) * 2 * (size_t)B * L * d.hk));
     S2S_TRY(zero_async(st, k.PDG, sizeof(float) * (size_t)B * k.NCH * d.hk * Sc));
@@ -1530,7 +1532,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     }
     hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
-    if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), 0, st, k);
+    if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), b6_lds, st, k);
     else hipLaunchKernelGGL(dec_b6_attn<false>, dim3(k.NCH, B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b7_dws, dim3(B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
@@ -1594,15 +1596,19 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
     S2S_TRY(colsum_f32(st, k.DU, Mk, rows, Mk, scale, 1.f, G.bm, cws));
   }
   S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd, cws));
-  if (d.lstm)
+  if (d.lstm) {
+    ColsumOut outs[4];
     for (int q = 0; q < 4; ++q) {  // LSTM.lua:25-29: Linear(S,S)(x) + Linear(S,S)(h), both with bias
       S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S + S, 2L * S, G.lstm[4 * q], S, S, S, true));      // Wqx
       S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S, 2L * S, G.lstm[4 * q + 2], S, S, S, true));      // Wqh
-      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 1], cws));               // bqx
-      S2S_TRY(colsum_f32(st, k.DGA + q * S, 4L * S, rows, S, scale, 1.f, G.lstm[4 * q + 3], cws));               // bqh
+      outs[q] = ColsumOut{q * S, S, {G.lstm[4 * q + 1], G.lstm[4 * q + 3], nullptr}, 2};                   // bqx, bqh
     }
-  S2S_TRY(colsum_f32(st, k.DCY, 2L * S, rows, S, scale, 1.f, G.bc, cws));
-  S2S_TRY(colsum_f32(st, k.DCY + S, 2L * S, rows, S, scale, 1.f, G.by, cws));
+    S2S_TRY(colsum_scatter_f32(st, k.DGA, 4L * S, rows, 4 * S, scale, outs, 4, cws));
+  }
+  {
+    const ColsumOut outs[2] = {{0, S, {G.bc, nullptr, nullptr}, 1}, {S, S, {G.by, nullptr, nullptr}, 1}};
+    S2S_TRY(colsum_scatter_f32(st, k.DCY, 2L * S, rows, 2 * S, scale, outs, 2, cws));
+  }
   S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, scale, 1.f, G.bs, cws));
   S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we, cws));
   if (d.hf > 0) {  // hybrid features: dG (sum over utterances, chunks; steps summed in the loop), dcu = sum dws

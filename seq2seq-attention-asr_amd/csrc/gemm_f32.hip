@@ -544,6 +544,17 @@ __global__ void colsum_final_kernel(const float* __restrict__ part, int parts, i
   out[col] = (beta == 0.f ? 0.f : beta * out[col]) + alpha * t;
 }
 
+// colsum_scatter's second stage: output range e = blockIdx.y, columns col0 .. col0 + ncols of the parts, added
+// (alpha-scaled, the same expression as colsum_final_kernel with beta = 1) into each of its destinations
+__global__ void colsum_scatter_kernel(const float* __restrict__ part, int parts, int N, float alpha, ColsumOuts o) {
+  const ColsumOut& e = o.e[blockIdx.y];
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= e.ncols) return;
+  float t = 0.f;
+  for (int p = 0; p < parts; ++p) t += part[(long)p * N + e.col0 + j];
+  for (int q = 0; q < e.ndst; ++q) e.dst[q][j] = 1.f * e.dst[q][j] + alpha * t;
+}
+
 __global__ void copy2d_kernel(const float* __restrict__ src, long lds, float* __restrict__ dst, long ldd, int rows,
                               int cols, int accumulate) {
   const long n = (long)rows * cols;
@@ -760,6 +771,31 @@ int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alp
   } else {
     hipLaunchKernelGGL(colsum_kernel, dim3((N + 63) / 64), dim3(1024), 0, st, X, ldx, M, N, alpha, beta, out);
   }
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+int colsum_scatter_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, const ColsumOut* outs,
+                       int nouts, GemmWs ws) {
+  S2S_REQUIRE(nouts >= 0 && nouts <= kMaxColsumOuts, "colsum_scatter: too many output ranges");
+  if (N <= 0 || nouts == 0) return 0;
+  const int parts = std::min(kColParts, (M + 255) / 256);
+  if (!(ws.p && parts > 1 && ws.n >= (size_t)kColParts * N)) {  // colsum_f32's one-stage form per destination
+    for (int e = 0; e < nouts; ++e)
+      for (int q = 0; q < outs[e].ndst; ++q)
+        S2S_TRY(colsum_f32(st, X + outs[e].col0, ldx, M, outs[e].ncols, alpha, 1.f, outs[e].dst[q], ws));
+    return 0;
+  }
+  ColsumOuts o{};
+  int maxc = 0;
+  for (int e = 0; e < nouts; ++e) {
+    S2S_REQUIRE(outs[e].col0 >= 0 && outs[e].col0 + outs[e].ncols <= N && outs[e].ndst <= 3, "colsum_scatter: bad range");
+    o.e[e] = outs[e];
+    maxc = std::max(maxc, outs[e].ncols);
+  }
+  hipLaunchKernelGGL(colsum_part_kernel, dim3((N + 63) / 64, parts), dim3(256), 0, st, X, ldx, M, N, ws.p);
+  hipLaunchKernelGGL(colsum_scatter_kernel, dim3((maxc + 255) / 256, nouts), dim3(256), 0, st, ws.p, parts, N, alpha,
+                     o);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

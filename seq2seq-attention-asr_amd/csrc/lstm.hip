@@ -394,14 +394,20 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
     WgradPrecision wp;  // weight gradients: fp32 under S2S_PREC_BF16_GEMM
     S2S_TRY(gemm_f32(st, pr, n, true, false, c.ws));
   }
+  }
+  // every bias gradient (bqx = bqh = sum_rows da_q, + bqc with peepholes) of both directions: the column sums of
+  // dA in one pass
+  ColsumOut outs[8];
+  int no = 0;
+  for (int d = 0; d < nd; ++d) {
+    float* const* G = gr.dW + d * np;
     for (int q = 0; q < 4; ++q) {
-      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 1], c.ws));
-      S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[4 * q + 3], c.ws));
-      if (io.peep && q != 2)
-        S2S_TRY(colsum_f32(st, dAd + q * H, ldA, B * L, H, gr.scale, 1.f, G[kLstmParams + 2 * (q == 3 ? 2 : q) + 1],
-                           c.ws));
+      ColsumOut& o = outs[no++];
+      o = ColsumOut{(int)(4L * d * H + q * H), H, {G[4 * q + 1], G[4 * q + 3], nullptr}, 2};
+      if (io.peep && q != 2) o.dst[o.ndst++] = G[kLstmParams + 2 * (q == 3 ? 2 : q) + 1];
     }
   }
+  S2S_TRY(colsum_scatter_f32(st, c.dA, ldA, B * L, (int)ldA, gr.scale, outs, no, c.ws));
   return 0;
 }
 

@@ -175,6 +175,19 @@ inline int gemm1(hipStream_t st, bool tA, bool tB, int M, int N, int K, float al
 int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out,
                GemmWs ws = GemmWs{});
 // Strided 2-D copy (rows x cols) dst[r*ldd + c] = src[r*lds + c]  (+ optional accumulate).
+// Column sums of several column ranges of one matrix in two launches: out_e,q[j] += alpha * sum_rows X[:, col0_e + j]
+// for every destination q of range e (bitwise equal to colsum_f32(..., alpha, 1, dst) per range and destination)
+struct ColsumOut {
+  int col0, ncols;
+  float* dst[3];
+  int ndst;
+};
+constexpr int kMaxColsumOuts = 24;
+struct ColsumOuts {
+  ColsumOut e[kMaxColsumOuts];
+};
+int colsum_scatter_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, const ColsumOut* outs,
+                       int nouts, GemmWs ws);
 int copy2d_f32(hipStream_t st, const float* src, long lds, float* dst, long ldd, int rows, int cols, bool accumulate);
 // dst[c*ldd + r] = src[r*lds + c] for the rows x cols block
 int transpose_f32(hipStream_t st, const float* src, long lds, int rows, int cols, float* dst, long ldd);

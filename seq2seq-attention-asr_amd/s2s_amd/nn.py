@@ -150,8 +150,9 @@ class Module:
         return [], []
 
     def zeroGradParameters(self):
-        for g in self.parameters()[1]:
-            g.zero_()
+        gs = [g for g in self.parameters()[1] if g is not None]
+        if gs:
+            torch._foreach_zero_(gs)  # one multi-tensor launch (a model has 30-60 gradient tensors)
 
     def forward(self, input):
         return self.updateOutput(input)

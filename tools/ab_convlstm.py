@@ -26,9 +26,12 @@ def main():
     def graph():
         m_g.graph_step(x, labels)
 
-    res = {"eager": [], "graph": []}
-    for _ in range(3):
-        for name, fn in (("eager", eager), ("graph", graph)):
+    modes = (("eager", eager), ("graph", graph))
+    if os.environ.get("AB_ONLY"):  # one mode (profiling): AB_ONLY=eager|graph
+        modes = tuple(m for m in modes if m[0] == os.environ["AB_ONLY"])
+    res = {name: [] for name, _ in modes}
+    for _ in range(3 if len(modes) > 1 else 1):
+        for name, fn in modes:
             for _ in range(2):
                 fn()
             torch.cuda.synchronize()
