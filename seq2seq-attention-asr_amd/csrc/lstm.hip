@@ -96,6 +96,42 @@ __global__ void lstm_fwd_cell(LstmFwdArgs a) {
   }
 }
 
+// k1 + k2 in one launch (no peepholes): the 1024-thread workgroup computes all four gates of its 16 units -- four
+// skinny products in the same order as lstm_fwd_gates, one per four waves (skinny4_1024) -- then the cell update of
+// those units (bitwise equal to the two-launch form, one launch per step fewer)
+__global__ __launch_bounds__(1024) void lstm_fwd_step(LstmFwdArgs a) {
+  __shared__ SkinnyRed red[4];
+  const LstmFwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tp = g.reverse ? t + 1 : t - 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int j0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  const int br = min(b0 + (lane & 15), B - 1);
+  float s[4];
+  skinny4_1024(red, g.y + ((long)br * L + (step > 0 ? tp : t)) * g.ldy,
+               [&](int q) { return g.Wh[q] + (long)(j0 + (lane & 15)) * H; }, H, step == 0, s);
+  const int b = b0 + (tid >> 4), j = j0 + (tid & 15);
+  if (tid >= 256 || b >= B) return;
+  const long row = (long)b * L + t;
+  const float* xp = g.xp + row * g.ldxp;
+  float* sv = g.sv + row * SV_N * H;
+  const float gi = sigmoidf_(s[0] + xp[j]), gf = sigmoidf_(s[1] + xp[H + j]);
+  const float gg = tanhf(s[2] + xp[2 * H + j]), go = sigmoidf_(s[3] + xp[3 * H + j]);
+  sv[SV_I * H + j] = gi;
+  sv[SV_F * H + j] = gf;
+  sv[SV_G * H + j] = gg;
+  sv[SV_O * H + j] = go;
+  const float cp = step > 0 ? g.sv[((long)b * L + tp) * SV_N * H + SV_C * H + j] : 0.f;
+  sv[SV_HP * H + j] = step > 0 ? g.y[((long)b * L + tp) * g.ldy + j] : 0.f;
+  sv[SV_CP * H + j] = cp;
+  const float c = gf * cp + gi * gg;
+  sv[SV_C * H + j] = c;
+  const float tc = tanhf(c);
+  sv[SV_TC * H + j] = tc;
+  g.y[row * g.ldy + j] = go * tc;
+}
+
 // k3 (peepholes): o = sig(pre_o + Woc c'), h' = o * tanh(c')
 __global__ __launch_bounds__(256) void lstm_fwd_ogate(LstmFwdArgs a) {
   __shared__ SkinnyRed red;
@@ -205,6 +241,38 @@ __global__ __launch_bounds__(256) void lstm_bwd_carry(LstmBwdArgs a) {
   if (b >= B) return;
   if (cpart) g.dcc[b * H + n - H] = g.dcp[b * H + n - H] + s;
   else g.dhc[b * H + n] = s;
+}
+
+// b3 of step s + 1 and b1 of step s in one launch (no peepholes): the workgroup's 16 units get dL/dh_t from the
+// skinny product over the row the previous launch wrote (dc_t = dc_{t+1} * f, the dc half of b3 being zero
+// without peepholes), then their gate pre-activation gradients -- the same sums as lstm_bwd_carry +
+// lstm_bwd_elem, one launch per step.  At the first step of the sweep (first = 1) the carries are zero.
+__global__ __launch_bounds__(256) void lstm_bwd_step(LstmBwdArgs a, int first) {
+  __shared__ SkinnyRed red;
+  const LstmBwdDir& g = a.d[blockIdx.z];
+  const int B = a.B, L = a.L, H = a.H, step = a.step;
+  const int t = g.reverse ? L - 1 - step : step;
+  const int tn = g.reverse ? t - 1 : t + 1;  // the row of step + 1 (processed by the previous launch)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int j0 = blockIdx.x * 16, b0 = blockIdx.y * 16;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (!first) {
+    const int br = min(b0 + (lane & 15), B - 1);
+    acc = skinny_wave(g.dA + ((long)br * L + tn) * g.ldA, g.Wb + (long)(j0 + (lane & 15)) * 4 * H, 4 * H, wave, lane);
+  }
+  const float sh = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), j = j0 + (tid & 15);
+  if (b >= B) return;
+  const int idx = b * H + j;
+  const float dhc = first ? 0.f : sh;
+  const float dcc = first ? 0.f : g.dcp[idx] + 0.f;  // lstm_bwd_carry's dc column: dcp + (a zero product)
+  const long row = (long)b * L + t;
+  const float* sv = g.sv + row * SV_N * H;
+  const float o = sv[SV_O * H + j], tc = sv[SV_TC * H + j];
+  const float dh = g.dy[row * g.lddy + j] + dhc;
+  const float dc = dcc + dh * o * (1.0f - tc * tc);
+  g.dA[row * g.ldA + 3 * H + j] = (dh * tc) * (o * (1.0f - o));
+  lstm_cell_grads(g, H, row, b, j, dc);
 }
 
 // packs: Wx4 (4H, D) rows [Wix; Wfx; Wgx; Wox]; bias4 (4H) = bqx + bqh (+ bqc for i, f, o);
@@ -329,11 +397,16 @@ int lstm_layer_fwd(hipStream_t st, const LstmLayerIO& io, void* scratch, size_t 
   a.B = B; a.L = L; a.H = H; a.peep = io.peep;
   const dim3 gg(4 * H / 16, (B + 15) / 16, nd), gc((B * H + 255) / 256, nd), go(H / 16, (B + 15) / 16, nd);
   ProfScope ps(st, "lstm_fwd_steps", 2.0 * nd * B * L * 4.0 * H * H * (io.peep ? 1.75 : 1.0), 0.0);
+  const dim3 gs(H / 16, (B + 15) / 16, nd);
   for (int s = 0; s < L; ++s) {
     a.step = s;
-    hipLaunchKernelGGL(lstm_fwd_gates, gg, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(lstm_fwd_cell, gc, dim3(256), 0, st, a);
-    if (io.peep) hipLaunchKernelGGL(lstm_fwd_ogate, go, dim3(256), 0, st, a);
+    if (io.peep) {
+      hipLaunchKernelGGL(lstm_fwd_gates, gg, dim3(256), 0, st, a);
+      hipLaunchKernelGGL(lstm_fwd_cell, gc, dim3(256), 0, st, a);
+      hipLaunchKernelGGL(lstm_fwd_ogate, go, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL(lstm_fwd_step, gs, dim3(1024), 0, st, a);
+    }
   }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
@@ -351,8 +424,10 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
   for (int d = 0; d < nd; ++d) {
     S2S_TRY(launch_lstm_pack(st, io.W + d * np, H, D, io.peep, c.Wx4 + 4L * d * H * D, nullptr, c.Wb[d],
                              io.peep ? c.WocT[d] : nullptr));
-    S2S_TRY(zero_async(st, c.dhc[d], sizeof(float) * (size_t)B * H));
-    S2S_TRY(zero_async(st, c.dcc[d], sizeof(float) * (size_t)B * H));
+    if (io.peep) {  // (the fused step of the peephole-free form starts from zero carries itself)
+      S2S_TRY(zero_async(st, c.dhc[d], sizeof(float) * (size_t)B * H));
+      S2S_TRY(zero_async(st, c.dcc[d], sizeof(float) * (size_t)B * H));
+    }
     a.d[d] = LstmBwdDir{gr.dy[d], gr.lddy, io.saved[d], c.WocT[d], c.Wb[d], c.dA + 4L * d * H, ldA,
                         c.dhc[d], c.dcc[d], c.dcp[d], c.dcn[d], io.reverse[d]};
   }
@@ -360,11 +435,16 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
   const dim3 ge((B * H + 255) / 256, nd), gp(H / 16, (B + 15) / 16, nd), gb(2 * H / 16, (B + 15) / 16, nd);
   {
     ProfScope ps(st, "lstm_bwd_steps", 2.0 * nd * B * L * 4.0 * H * H * (io.peep ? 1.75 : 1.0), 0.0);
+    const dim3 gs(H / 16, (B + 15) / 16, nd);
     for (int s = L - 1; s >= 0; --s) {
       a.step = s;
-      hipLaunchKernelGGL(lstm_bwd_elem, ge, dim3(256), 0, st, a);
-      if (io.peep) hipLaunchKernelGGL(lstm_bwd_peep, gp, dim3(256), 0, st, a);
-      if (s > 0) hipLaunchKernelGGL(lstm_bwd_carry, gb, dim3(256), 0, st, a);
+      if (io.peep) {
+        hipLaunchKernelGGL(lstm_bwd_elem, ge, dim3(256), 0, st, a);
+        hipLaunchKernelGGL(lstm_bwd_peep, gp, dim3(256), 0, st, a);
+        if (s > 0) hipLaunchKernelGGL(lstm_bwd_carry, gb, dim3(256), 0, st, a);
+      } else {
+        hipLaunchKernelGGL(lstm_bwd_step, gs, dim3(256), 0, st, a, s == L - 1 ? 1 : 0);
+      }
     }
     S2S_CHECK_HIP(hipGetLastError());
   }

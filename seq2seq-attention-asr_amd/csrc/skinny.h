@@ -59,4 +59,24 @@ __device__ __forceinline__ float skinny_reduce(SkinnyRed& red, floatx4 acc, int 
   return ((red.v[0][i][j] + red.v[1][i][j]) + red.v[2][i][j]) + red.v[3][i][j];
 }
 
+// Four skinny products (gates q = 0..3 of the same 16 units) in one 1024-thread workgroup: waves 4q .. 4q + 3
+// split gate q's K exactly as skinny_wave's four waves do, so s[q] (returned to threads 0..255 for output
+// (tid>>4, tid&15)) is bitwise the skinny_reduce of that product -- four times the loads in flight per
+// workgroup of a four-launch (or four-product serial) form.  wrow(q) = this lane's weight row of gate q.
+template <typename WRow>
+__device__ __forceinline__ void skinny4_1024(SkinnyRed (&red)[4], const float* __restrict__ xrow, WRow wrow, int K,
+                                             bool zero, float (&s)[4]) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, q = wave >> 2, w4 = wave & 3;
+  floatx4 acc = {0.f, 0.f, 0.f, 0.f};
+  if (!zero) acc = skinny_wave(xrow, wrow(q), K, w4, lane);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[q].v[w4][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  if (tid < 256) {
+    const int i = tid >> 4, j = tid & 15;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) s[g] = ((red[g].v[0][i][j] + red[g].v[1][i][j]) + red[g].v[2][i][j]) + red[g].v[3][i][j];
+  }
+}
+
 }  // namespace s2s
