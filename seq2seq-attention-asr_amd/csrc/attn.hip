@@ -834,7 +834,8 @@ __global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
 // K6: fused attention backward for one 16-frame chunk.  grid (NCH, B)
 //   d alpha_l = dc . h_l + carry_l + gdiff_l      (MM bwd + MonotonicAlignment.lua:44-77)
 //   de_l = alpha_l (d alpha_l - sum_j alpha_j d alpha_j)   with sum = dc . c + sum alpha (carry + gdiff)
-//   dh_l += alpha_l dc;  dZ = de_l we (1 - tanh^2);  dVh_l += dZ;  partial dws, dwe
+//   dZ = de_l we (1 - tanh^2);  dVh_l += dZ;  partial dws, dwe  (dh_l = sum_t alpha_{t,l} dc_t is one GEMM per
+//   utterance after the loop, attn_dh_gemms: a read-modify-write of dh per frame and step cost 5.3 us of 28)
 //   HYB (hybrid attention): Z includes UF; d alpha_l also gets the carry from step t+1's location
 //   features (hyb_carry); q_{l,i} = sum_j dZ_lj HG_ji -> QA for step t-1; dG partials -> PDG
 //   HYB keeps this chunk's dZ rows in LDS (dynamic, LC x Sc floats) and forms q and the dG partials from them
@@ -894,8 +895,6 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     const float dal = HYB ? dd + (lam * (float)(Lb - l) * (ind - indn) + hyb_carry(k, b, l))
                           : dd + lam * (float)(Lb - l) * (ind - indn);
     const float de = al * (dal - ssum);
-    float* dhl = k.dh + ((long)b * L + l) * k.lddh;
-    for (int a = lane; a < A; a += 64) dhl[a] += al * dc[a];
     const float* vh = k.Vh + ((long)b * L + l) * Sc;
     float* dvh = k.DVH + ((long)b * L + l) * Sc;
 #pragma unroll
@@ -945,19 +944,25 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   }
   if (HYB) {  // (the passes above ended on a barrier after every zl store)
     const int hk = k.hk;
-    // q_{l,i} = sum_j dZ_lj HG_ji for d alpha_{t-1} (read by step t-1's kernel through hyb_carry)
+    // q_{l,i} = sum_j dZ_lj HG_ji for d alpha_{t-1} (read by step t-1's kernel through hyb_carry): four threads
+    // per (frame, tap) pair, float4 columns c4 = r, r + 4, ... then a 4-lane butterfly (a wave reduction per
+    // pair cost 6.5 us of the kernel's 28 at Sc = 160, kW = 5)
     float* qa = k.QA + ((long)(t & 1) * k.B + b) * L * hk + (long)ch * LC * hk;
-    for (int p = wave; p < lend * hk; p += 4) {
-      const int lloc = p / hk, ii = p - lloc * hk;
-      const float4* z4 = reinterpret_cast<const float4*>(zl + (long)lloc * Sc);
-      const float4* g4 = reinterpret_cast<const float4*>(hg + (long)ii * Sc);
+    for (int p0 = 0; p0 < lend * hk; p0 += 64) {
+      const int p = p0 + (tid >> 2), r = tid & 3;
       float q = 0.f;
-      for (int c4 = lane; c4 < Sc / 4; c4 += 64) {
-        const float4 z = z4[c4], g = g4[c4];
-        q += ((z.x * g.x + z.y * g.y) + z.z * g.z) + z.w * g.w;
+      if (p < lend * hk) {
+        const int lloc = p / hk, ii = p - lloc * hk;
+        const float4* z4 = reinterpret_cast<const float4*>(zl + (long)lloc * Sc);
+        const float4* g4 = reinterpret_cast<const float4*>(hg + (long)ii * Sc);
+        for (int c4 = r; c4 < Sc / 4; c4 += 4) {
+          const float4 z = z4[c4], g = g4[c4];
+          q += ((z.x * g.x + z.y * g.y) + z.z * g.z) + z.w * g.w;
+        }
       }
-      q = wave_sum(q);
-      if (lane == 0) qa[(long)lloc * hk + ii] = q;
+      q += __shfl_xor(q, 1, 64);
+      q += __shfl_xor(q, 2, 64);
+      if (p < lend * hk && r == 0) qa[p] = q;
     }
     // dG partials of this chunk, accumulated over the steps (PDG zeroed before the loop): sum_l dZ_lj
     // alpha_{t-1}[l + i - pad_left] (no term at t = 0)
@@ -973,23 +978,62 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   }
 }
 
-// K7: DWS[b][t] = sum over chunks (grid B)
-__global__ void dec_b7_dws(AttnK k) {
-  const int b = blockIdx.x, t = k.t, Sc = k.Sc, NCH = k.NCH;
-  for (int kk = threadIdx.x; kk < Sc; kk += blockDim.x) {
-    float s = 0.f;
-    for (int j = 0; j < NCH; ++j) s += k.PDWS[((long)b * NCH + j) * Sc + kk];
-    k.DWS[((long)b * k.T + t) * Sc + kk] = s;
+// skinny_wave over the chunk-summed dws row: operand chunk = sum_j PDWS[b][j][k..k+3] in chunk order from 0 (the
+// sum dec_b7_dws formed, bitwise); `store` (the workgroups of blockIdx.x == 0) also writes the summed row to DWS
+__device__ __forceinline__ float4 dws_chunk(const float* __restrict__ p, int nch, long stride, int off) {
+  float4 x = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = 0; j < nch; ++j) {
+    const float4 v = *reinterpret_cast<const float4*>(p + j * stride + off);
+    x.x += v.x; x.y += v.y; x.z += v.z; x.w += v.w;
   }
+  return x;
+}
+__device__ __forceinline__ floatx4 skinny_wave_dws(const float* __restrict__ prow, int nch, float* __restrict__ dws_row,
+                                                   bool store, const float* __restrict__ wrow, int K, int wave,
+                                                   int lane) {
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int kq = 4 * (lane >> 4);
+  int kc = wave * 16;
+  for (; kc + 64 < K; kc += 128) {
+    const float4 a0 = dws_chunk(prow, nch, K, kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    const float4 a1 = dws_chunk(prow, nch, K, kc + 64 + kq);
+    const float4 b1 = *reinterpret_cast<const float4*>(wrow + kc + 64 + kq);
+    if (store) {
+      *reinterpret_cast<float4*>(dws_row + kc + kq) = a0;
+      *reinterpret_cast<float4*>(dws_row + kc + 64 + kq) = a1;
+    }
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+  }
+  for (; kc < K; kc += 64) {
+    const float4 a0 = dws_chunk(prow, nch, K, kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    if (store) *reinterpret_cast<float4*>(dws_row + kc + kq) = a0;
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
 }
 
-// K8: ds_{t-1} = DSPF + Ws^T dws (N = S, K = Sc); then gate grads of step t-1
+// K7 + K8: dws_t = sum over the attention chunks' partials (-> DWS, the weight gradients' rows), ds_{t-1} = DSPF +
+// Ws^T dws (N = S, K = Sc); then the gate grads of step t-1.  (The chunk sum was its own launch, dec_b7_dws: one
+// launch per decoder step fewer.)
 __global__ __launch_bounds__(256) void dec_b8_ws(AttnK k) {
   __shared__ SkinnyRed red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
-  floatx4 acc = skinny_wave(k.DWS + ((long)brow(b0, lane, k.B) * k.T + t) * k.Sc,
-                            k.WsT + (long)(n0 + (lane & 15)) * k.Sc, k.Sc, wave, lane);
+  const int bl = b0 + (lane & 15), br = min(bl, k.B - 1);
+  floatx4 acc = skinny_wave_dws(k.PDWS + (long)br * k.NCH * k.Sc, k.NCH, k.DWS + ((long)br * k.T + t) * k.Sc,
+                                blockIdx.x == 0 && bl < k.B, k.WsT + (long)(n0 + (lane & 15)) * k.Sc, k.Sc, wave, lane);
   const float s = skinny_reduce(red, acc, wave, lane, tid);
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B || t == 0) return;
@@ -1435,7 +1479,10 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   const int rows = B * T, bt = (B + 15) / 16;
   const XPlan xp = dec_xcd_plan(d);
   // the XCD-local path's first dh writer is the alpha^T dc GEMM (beta 0 when not accumulating)
-  if (!accumulate_dh && !xp.var) S2S_TRY(zero_async(st, dh, sizeof(float) * (size_t)B * L * A));
+  const int pvar = xp.var ? 0 : dec_persist_variant(d);
+  // the persistent kernels accumulate dh in place (the XCD-local and the per-step paths write it by GEMMs after
+  // their loop, beta 0 when not accumulating)
+  if (!accumulate_dh && pvar) S2S_TRY(zero_async(st, dh, sizeof(float) * (size_t)B * L * A));
   if (!xp.var) {  // the XCD-local path writes DVH / DWEACC whole after its loop
     S2S_TRY(zero_async(st, k.DVH, sizeof(float) * (size_t)B * L * Sc));
     S2S_TRY(zero_async(st, k.DWEACC, sizeof(float) * (size_t)B * k.NCH * Sc));
@@ -1470,7 +1517,6 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_CHECK_HIP(hipGetLastError());
   }
   const int pgrid = kDecWG * ((B + 15) / 16);
-  const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pb = pvar ? pick_dec_bwd(pvar, d, pgrid) : PersistLaunch{};
   if (xp.var) {
     x.U = xp.U;
@@ -1534,10 +1580,11 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
     if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), b6_lds, st, k);
     else hipLaunchKernelGGL(dec_b6_attn<false>, dim3(k.NCH, B), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_b7_dws, dim3(B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
   S2S_CHECK_HIP(hipGetLastError());
+  // dh (+)= sum_t alpha_t^T dc_t (per utterance) + dVh V
+  return attn_dh_gemms(st, AttnDhTerms{k.ALPHA, k.DC, k.DVH, P.V, B, L, T, A, Sc, gws}, dh, accumulate_dh, nullptr);
   }
   // dh += dVh V   (Vh = h V^T)
   S2S_TRY(gemm1(st, false, false, B * L, A, Sc, 1.f, k.DVH, Sc, P.V, A, 1.f, dh, A, nullptr, gws));

@@ -570,7 +570,10 @@ def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local
 @pytest.mark.parametrize("B,L,T,A,Sc,S,O", [(32, 40, 12, 512, 512, 256, 62), (21, 50, 9, 128, 128, 64, 29)])
 def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B, L, T, A, Sc, S, O):
     """The persistent decoder kernels (granule hand-offs, 128 workgroups per 16-row tile) must
-    reproduce the per-step launch path bit for bit, forward and backward, over repeated launches."""
+    reproduce the per-step launch path bit for bit, forward and backward, over repeated launches -- except dh:
+    the per-step path forms dh = sum_t alpha_t^T dc_t + dVh V by GEMMs after its loop (a per-frame
+    read-modify-write in every step cost more than the GEMM), the persistent kernel accumulates it step by step,
+    so the two sum the same products in different orders (held to 1e-6 of max |dh|)."""
     rng = np.random.default_rng(3)
     att = s2s.Attention(s2s.GRU(S, S), s2s.MaxoutMLP(S + A, 8, 7, O), Sc, 10, 0, S, A, O, True, 0.2).cuda()
     h = cu(rng.standard_normal((B, L, A)) * 0.5)
@@ -591,6 +594,9 @@ def test_persistent_decoder_bitwise_equals_per_step_launches(s2s, monkeypatch, B
     names = ["logp", "alpha", "dh"] + ["d" + n for n in s2s.Attention.PARAM_NAMES]
     for rep in range(2):
         for name, a, b in zip(names, outs["step"][rep], outs["persist"][rep]):
+            if name == "dh":
+                assert (a - b).abs().max().item() <= 1e-6 * a.abs().max().item(), f"dh (rep {rep})"
+                continue
             assert torch.equal(a, b), f"{name} differs (rep {rep}): max |d| = {(a - b).abs().max().item():.3e}"
 
 
