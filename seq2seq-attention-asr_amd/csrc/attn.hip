@@ -560,6 +560,37 @@ __global__ __launch_bounds__(256) void dec_f5_d(AttnK k) {
   k.RHX[row * 2 * S + S + n] = d;
 }
 
+// ---- folded F4 + F5 of the per-step path (LSTM decoder / hybrid attention: the shapes the XCD-local kernels do
+// not serve).  d = Wd [Wc c + bc; y_in] + bd = WDC c + KD with WDC = Wd_c Wc (S x A) and KD = Wd_y y_in + Wd_c bc
+// + bd per row (teacher-forced y_in), both formed before the loop -- one launch per step instead of two.
+// y_in rows of every step: CY[:, S:] = by + Wy[:, y_{t-1}] (zeros_y at t = 0 or a negative label)
+__global__ void dec_fold_yin(AttnK k) {
+  const int S = k.S;
+  const long n = (long)k.B * k.T * S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const long row = i / S;
+    const int j = (int)(i - row * S), t = (int)(row % k.T);
+    float v = k.P.by[j];
+    if (t > 0 && k.labels[row - 1] >= 0) v += k.P.Wy[(long)j * k.O + k.labels[row - 1]];
+    k.CY[row * 2 * S + S + j] = v;
+  }
+}
+// F45: d = WDC c_t + KD_t (N = S, K = A) -> HX[:, S:] and RHX[:, S:]
+__global__ __launch_bounds__(256) void dec_f45_fold(AttnK k, const float* __restrict__ wdc, const float* __restrict__ kd) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S, A = k.A;
+  floatx4 acc = skinny_wave(k.C + ((long)brow(b0, lane, k.B) * k.T + t) * A, wdc + (long)(n0 + (lane & 15)) * A, A,
+                            wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  const float d = s + kd[row * S + n];
+  k.HX[row * 2 * S + S + n] = d;
+  k.RHX[row * 2 * S + S + n] = d;
+}
+
 // F6: [z|r] = sig(W{z,r} [s_{t-1}; d])  (N = 2S, K = 2S)
 __global__ __launch_bounds__(256) void dec_f6_gru1(AttnK k) {
   __shared__ SkinnyRed red;
@@ -824,6 +855,21 @@ __global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
   floatx4 acc = skinny_wave(k.DCY + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
                             k.WcT + (long)(n0 + (lane & 15)) * S, S, wave, lane);
+  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
+  if (b >= k.B) return;
+  const long row = (long)b * k.T + t;
+  k.DC[row * k.A + n] = k.DV[row * (S + k.A) + S + n] + s;
+}
+
+// K45 (folded, the per-step path's LSTM / hybrid shapes): dc = dv_c + WDC^T dd (N = A, K = S; wdct = WDC^T);
+// DCY = dd Wd for the weight gradients is one GEMM after the loop
+__global__ __launch_bounds__(256) void dec_b45_fold(AttnK k, const float* __restrict__ wdct) {
+  __shared__ SkinnyRed red;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
+  floatx4 acc = skinny_wave(k.DD + ((long)brow(b0, lane, k.B) * k.T + t) * S, wdct + (long)(n0 + (lane & 15)) * S, S,
+                            wave, lane);
   const float s = skinny_reduce(red, acc, wave, lane, tid);
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B) return;
@@ -1197,6 +1243,10 @@ static int dec_persist_variant(const AttnDims& d) {
   return 0;
 }
 
+// The per-step path folds F4 + F5 (and K4 + K5) for the shapes only it serves: the LSTM decoder and hybrid attention
+// (the GRU content-attention per-step path stays bitwise equal to the persistent kernels of attn_persist.inc)
+static bool dec_fold_f45(const AttnDims& d) { return d.lstm || d.hf > 0; }
+
 // algorithmic flops of one decoder recurrence launch (T P_step + T L (2 Sc + A) per utterance,
 // times 2; the backward does twice the forward's products)
 static double dec_flops(const AttnDims& d, bool bwd) {
@@ -1404,13 +1454,27 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   ProfScope ps(st, "dec_fwd_steps", 0.0, 0.0);
   if (d.hf > 0) hipLaunchKernelGGL(dec_hyb_fold, dim3((d.Sc + 255) / 256), dim3(256), 0, st, k);
   if (d.lstm) hipLaunchKernelGGL(dec_lstm_pack, dim3(256), dim3(256), 0, st, k);
+  const bool fold = dec_fold_f45(d);
+  const int A = d.A, rows = B * T;
+  if (fold) {  // y_in rows, BKD = Wd_c bc + bd, WDC = Wd_c Wc, KD = y_in Wd_y^T + BKD
+    WgradPrecision wp;  // the folds are reused by every step: fp32
+    hipLaunchKernelGGL(dec_fold_yin, dim3(512), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);
+    S2S_CHECK_HIP(hipGetLastError());
+    S2S_TRY(gemm1(st, false, false, S, A, S, 1.f, P.Wd, 2L * S, P.Wc, A, 0.f, x.WDC, A, nullptr, gws));
+    S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
+  }
   for (int t = 0; t < T; ++t) {
     k.t = t;
     hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f3_combine, dim3(B), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+    if (fold) {
+      hipLaunchKernelGGL(dec_f45_fold, dim3(S / 16, bt), dim3(256), 0, st, k, x.WDC, x.KD);
+    } else {
+      hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
+    }
     if (d.lstm) {
       hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_f7_lstm, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
@@ -1420,6 +1484,8 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     }
   }
   S2S_CHECK_HIP(hipGetLastError());
+  // c_in rows for the weight gradients (the folded steps never formed them): CY[:, :S] = C Wc^T + bc
+  if (fold) S2S_TRY(gemm1(st, false, true, rows, S, A, 1.f, k.C, A, P.Wc, A, 0.f, k.CY, 2L * S, P.bc, gws));
   }
   // decoder MLP over all B*T rows: U = [s; c] Wm^T + bm, then maxout / Linear / LogSoftMax
   if (d.ext) return 0;  // external decoder_mlp: the caller runs it on the saved VV rows
@@ -1498,11 +1564,19 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   // the h-half of Wh reaches ds_{t-1} through dq = Wh[:, :S]^T da_h (K2), not through GT
   hipLaunchKernelGGL(fill2d_kernel, dim3(64), dim3(256), 0, st, k.GT + 2 * S, 3L * S, S, S, 0.f);
   }
-  S2S_TRY(transpose_f32(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
-  S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
+  if (!dec_fold_f45(d)) {
+    S2S_TRY(transpose_f32(st, P.Wd, 2L * S, S, 2 * S, k.WdT, S));
+    S2S_TRY(transpose_f32(st, P.Wc, A, S, A, k.WcT, S));
+  }
   S2S_TRY(transpose_f32(st, P.Ws, S, Sc, S, k.WsT, Sc));
   }
   const GemmWs gws = attn_gemm_ws(d, scratch);
+  // folded K4 + K5 (per-step path, LSTM / hybrid shapes): WDC^T = Wc^T Wd_c^T (A x S) in WcT's place
+  const bool fold = !xp.var && !dec_persist_variant(d) && dec_fold_f45(d);
+  if (fold) {
+    WgradPrecision wp;
+    S2S_TRY(gemm1(st, true, true, A, S, S, 1.f, P.Wc, A, P.Wd, 2L * S, 0.f, k.WcT, S, nullptr, gws));
+  }
   if (d.ext) {  // external decoder_mlp: dlogp holds d[s_t; c_t] (B*T, S+A)
     S2S_TRY(copy2d_f32(st, dlogp, S + A, k.DV, S + A, rows, S + A, false));
   } else {
@@ -1576,13 +1650,19 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     }
-    hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
+    if (fold) {
+      hipLaunchKernelGGL(dec_b45_fold, dim3(A / 16, bt), dim3(256), 0, st, k, k.WcT);
+    } else {
+      hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
+    }
     if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), b6_lds, st, k);
     else hipLaunchKernelGGL(dec_b6_attn<false>, dim3(k.NCH, B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
   S2S_CHECK_HIP(hipGetLastError());
+  // [dc_in | dy_in] rows for the weight gradients (the folded steps never formed them): DCY = DD Wd
+  if (fold) S2S_TRY(gemm1(st, false, false, rows, 2 * S, S, 1.f, k.DD, S, P.Wd, 2L * S, 0.f, k.DCY, 2L * S, nullptr, gws));
   // dh (+)= sum_t alpha_t^T dc_t (per utterance) + dVh V
   return attn_dh_gemms(st, AttnDhTerms{k.ALPHA, k.DC, k.DVH, P.V, B, L, T, A, Sc, gws}, dh, accumulate_dh, nullptr);
   }
