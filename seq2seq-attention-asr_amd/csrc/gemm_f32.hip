@@ -450,6 +450,17 @@ __device__ __forceinline__ floatx4 slab_sum(const float* part, long mn, long e) 
   return sum;
 }
 
+template <int S>
+__device__ __forceinline__ float slab_sum1(const float* part, long mn, long e) {
+  float v[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) v[s] = part[s * mn + e];
+  float sum = 0.f;
+#pragma unroll
+  for (int s = 0; s < S; ++s) sum += v[s];
+  return sum;
+}
+
 __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
   const GemmTile& q = Lc.q[blockIdx.y];
   if (q.part == nullptr) return;
@@ -486,8 +497,17 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
     return;
   }
   for (long e = blockIdx.x * 256L + threadIdx.x; e < mn; e += (long)gridDim.x * 256) {
+    // every slab's load in flight before the first add, as in the float4 form (the scalar form serves outputs
+    // whose rows are not 16-byte multiples, e.g. the GRU weight gradients' [H | D] rows); slice order either way
     float sum = 0.f;
-    for (int s = 0; s < q.splits; ++s) sum += q.part[s * mn + e];
+    switch (q.splits) {
+      case 2: sum = slab_sum1<2>(q.part, mn, e); break;
+      case 3: sum = slab_sum1<3>(q.part, mn, e); break;
+      case 4: sum = slab_sum1<4>(q.part, mn, e); break;
+      case 8: sum = slab_sum1<8>(q.part, mn, e); break;
+      default:
+        for (int s = 0; s < q.splits; ++s) sum += q.part[s * mn + e];
+    }
     const int row = (int)(e / N), col = (int)(e % N);
     float v = alpha * sum;
     if (bias) v += bias[col];
