@@ -410,7 +410,11 @@ __global__ __launch_bounds__(256) void dec_f1_ws(AttnK k) {
 }
 
 // F2: scores + chunk-local softmax stats + partial context.  grid (NCH, B)
-__global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
+// WV waves per workgroup (LC / WV frames each): every frame's score is one wave's, so the wave count does not
+// change a bit of the results; the training loop runs 8 (half the serial frame chain of 4 x 4)
+template <int WV>
+__global__ __launch_bounds__(64 * WV) void dec_f2_attn(AttnK k) {
+  constexpr int FPW = LC / WV, NT = 64 * WV;
   __shared__ float sc[LC];
   __shared__ float pw[LC];
   __shared__ float apl[LC + kMaxHybK];  // hybrid: alpha_{t-1} halo of the chunk (hyb_stage_alpha)
@@ -422,8 +426,8 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
   const float* ap = (k.hf > 0 && t > 0) ? k.ALPHA + ((long)b * k.T + t - 1) * L : nullptr;  // alpha_{t-1}
   if (k.hf > 0) hyb_stage_alpha(k, ap, ch, apl);
   const int Lb = frames_of(k, b);
-  for (int i = 0; i < 4; ++i) {
-    const int li = wave * 4 + i, l = ch * LC + li;
+  for (int i = 0; i < FPW; ++i) {
+    const int li = wave * FPW + i, l = ch * LC + li;
     float part = 0.f;
     if (l < Lb) {
       const float* vh = k.Vh + ((long)b * L + l) * Sc;
@@ -460,12 +464,20 @@ __global__ __launch_bounds__(256) void dec_f2_attn(AttnK k) {
   }
   float* pc = k.PC + ((long)b * k.NCH + ch) * A;
   const int lend = min(LC, L - ch * LC);
-  for (int a4 = tid; a4 < A / 4; a4 += 256) {
+  for (int a4 = tid; a4 < A / 4; a4 += NT) {
+    // every frame's row load in flight before the first add; the sum runs in frame order (as before)
+    float4 hv[LC];
+#pragma unroll
+    for (int i = 0; i < LC; ++i)
+      hv[i] = i < lend ? reinterpret_cast<const float4*>(k.h + ((long)b * L + ch * LC + i) * A)[a4]
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
     float4 acc = {0.f, 0.f, 0.f, 0.f};
-    for (int i = 0; i < lend; ++i) {
-      const float4 hv = reinterpret_cast<const float4*>(k.h + ((long)b * L + ch * LC + i) * A)[a4];
-      const float p = pw[i];
-      acc.x += p * hv.x; acc.y += p * hv.y; acc.z += p * hv.z; acc.w += p * hv.w;
+#pragma unroll
+    for (int i = 0; i < LC; ++i) {
+      if (i < lend) {
+        const float p = pw[i];
+        acc.x += p * hv[i].x; acc.y += p * hv[i].y; acc.z += p * hv[i].z; acc.w += p * hv[i].w;
+      }
     }
     reinterpret_cast<float4*>(pc)[a4] = acc;
   }
@@ -888,9 +900,12 @@ __global__ __launch_bounds__(256) void dec_b45_fold(AttnK k, const float* __rest
 //   after the frame loop: per-lane register partials over every tap (kMaxHybK x 16 floats) spilled to scratch
 //   at one wave per SIMD (37.7 us per step at the conv + BiLSTM model's B = 32, Sc = 160; tools/ab_convlstm.py)
 template <bool HYB>
-__global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
-  __shared__ float redv[4];
-  __shared__ float pws[4][1024];
+__global__ __launch_bounds__(HYB ? 512 : 256) void dec_b6_attn(AttnK k) {
+  // HYB: 8 waves x 2 frames (the content-attention form keeps 4 x 4: it is bitwise equal to the persistent
+  // kernels of attn_persist.inc, and the wave count sets the order of the cross-wave sums)
+  constexpr int WV = HYB ? 8 : 4, FPW = LC / WV, NT = 64 * WV;
+  __shared__ float redv[WV];
+  __shared__ float pws[WV][1024];
   extern __shared__ float zl[];  // HYB: [LC][Sc] dZ rows of this chunk, then HGT [kW][Sc], then the alpha halo
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ch = blockIdx.x, b = blockIdx.y, t = k.t;
@@ -904,14 +919,16 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   const int Lb = frames_of(k, b);  // MonotonicAlignment's L (alpha = 0 past it)
   // sum_j alpha_j d alpha_j
   float part = 0.f;
-  for (int a = tid; a < A; a += 256) part += dc[a] * c[a];
-  for (int l = tid; l < L; l += 256)
+  for (int a = tid; a < A; a += NT) part += dc[a] * c[a];
+  for (int l = tid; l < L; l += NT)
     part += alpha[l] * (HYB ? lam * (float)(Lb - l) * (ind - indn) + hyb_carry(k, b, l)
                             : lam * (float)(Lb - l) * (ind - indn));
   part = wave_sum(part);
   if (lane == 0) redv[wave] = part;
   __syncthreads();
-  const float ssum = ((redv[0] + redv[1]) + redv[2]) + redv[3];
+  float ssum = redv[0];
+#pragma unroll
+  for (int w = 1; w < WV; ++w) ssum += redv[w];
   const float* ws = k.WS + row * Sc;
   const float* we = k.P.we;
   // Sc <= 1024 asserted on the host: each lane owns k = 4*(lane + 64 i)
@@ -923,11 +940,11 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
   float* hg = zl + (long)LC * Sc;         // HYB: the taps HGT, staged
   float* apl = hg + (long)k.hk * Sc;      // HYB: alpha_{t-1} halo of the chunk
   if (HYB) {
-    for (int i = tid; i < k.hk * Sc; i += 256) hg[i] = k.HGT[i];
+    for (int i = tid; i < k.hk * Sc; i += NT) hg[i] = k.HGT[i];
     hyb_stage_alpha(k, ap, ch, apl);
   }
-  for (int i4 = 0; i4 < 4; ++i4) {
-    const int lloc = wave * 4 + i4, l = ch * LC + lloc;
+  for (int i4 = 0; i4 < FPW; ++i4) {
+    const int lloc = wave * FPW + i4, l = ch * LC + lloc;
     if (l >= L) break;
     const float* hl = k.h + ((long)b * L + l) * A;
     float dd = 0.f;
@@ -983,8 +1000,10 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
       }
     }
     __syncthreads();
-    for (int kk = tid; kk < Sc; kk += 256) {
-      const float v = ((pws[0][kk] + pws[1][kk]) + pws[2][kk]) + pws[3][kk];
+    for (int kk = tid; kk < Sc; kk += NT) {
+      float v = pws[0][kk];
+#pragma unroll
+      for (int w = 1; w < WV; ++w) v += pws[w][kk];
       if (pass == 0) pd[kk] = v; else pe[kk] += v;
     }
   }
@@ -994,7 +1013,7 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     // per (frame, tap) pair, float4 columns c4 = r, r + 4, ... then a 4-lane butterfly (a wave reduction per
     // pair cost 6.5 us of the kernel's 28 at Sc = 160, kW = 5)
     float* qa = k.QA + ((long)(t & 1) * k.B + b) * L * hk + (long)ch * LC * hk;
-    for (int p0 = 0; p0 < lend * hk; p0 += 64) {
+    for (int p0 = 0; p0 < lend * hk; p0 += NT / 4) {
       const int p = p0 + (tid >> 2), r = tid & 3;
       float q = 0.f;
       if (p < lend * hk) {
@@ -1014,7 +1033,7 @@ __global__ __launch_bounds__(256) void dec_b6_attn(AttnK k) {
     // alpha_{t-1}[l + i - pad_left] (no term at t = 0)
     if (ap) {
       float* pg = k.PDG + ((long)b * k.NCH + ch) * hk * Sc;
-      for (int e = tid; e < hk * Sc; e += 256) {
+      for (int e = tid; e < hk * Sc; e += NT) {
         const int ii = e / Sc, kk = e - ii * Sc;
         float g = 0.f;
         for (int lloc = 0; lloc < lend; ++lloc) g += zl[(long)lloc * Sc + kk] * apl[lloc + ii];
@@ -1467,7 +1486,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   for (int t = 0; t < T; ++t) {
     k.t = t;
     hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
-    hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, B), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f2_attn<8>, dim3(k.NCH, B), dim3(512), 0, st, k);
     hipLaunchKernelGGL(dec_f3_combine, dim3(B), dim3(256), 0, st, k);
     if (fold) {
       hipLaunchKernelGGL(dec_f45_fold, dim3(S / 16, bt), dim3(256), 0, st, k, x.WDC, x.KD);
@@ -1656,7 +1675,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
     }
-    if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(256), b6_lds, st, k);
+    if (d.hf > 0) hipLaunchKernelGGL(dec_b6_attn<true>, dim3(k.NCH, B), dim3(512), b6_lds, st, k);
     else hipLaunchKernelGGL(dec_b6_attn<false>, dim3(k.NCH, B), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_b8_ws, dim3(S / 16, bt), dim3(256), 0, st, k);
   }
@@ -2098,7 +2117,7 @@ int attn_beam_step(hipStream_t st, const AttnDims& d, const AttnParams& P, int K
   const int R = d.B * K, S = d.S, bt = (R + 15) / 16, rows = 2 * R;
   hipLaunchKernelGGL(beam_prep, dim3(64), dim3(256), 0, st, k, v.q, count & 1);
   hipLaunchKernelGGL(dec_f1_ws, dim3(d.Sc / 16, bt), dim3(256), 0, st, k);
-  hipLaunchKernelGGL(dec_f2_attn, dim3(k.NCH, R), dim3(256), 0, st, k);
+  hipLaunchKernelGGL(dec_f2_attn<8>, dim3(k.NCH, R), dim3(512), 0, st, k);
   hipLaunchKernelGGL(dec_f3_combine, dim3(R), dim3(256), 0, st, k);
   hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
   hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
