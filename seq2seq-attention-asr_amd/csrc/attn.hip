@@ -588,13 +588,14 @@ __global__ void dec_fold_yin(AttnK k) {
   }
 }
 // F45: d = WDC c_t + KD_t (N = S, K = A) -> HX[:, S:] and RHX[:, S:]
-__global__ __launch_bounds__(256) void dec_f45_fold(AttnK k, const float* __restrict__ wdc, const float* __restrict__ kd) {
-  __shared__ SkinnyRed red;
+__global__ __launch_bounds__(512) void dec_f45_fold(AttnK k, const float* __restrict__ wdc, const float* __restrict__ kd) {
+  __shared__ SkinnyRed8 red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S, A = k.A;
-  floatx4 acc = skinny_wave(k.C + ((long)brow(b0, lane, k.B) * k.T + t) * A, wdc + (long)(n0 + (lane & 15)) * A, A,
+  floatx4 acc = skinny_wave8(k.C + ((long)brow(b0, lane, k.B) * k.T + t) * A, wdc + (long)(n0 + (lane & 15)) * A, A,
                             wave, lane);
-  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const float s = skinny_reduce8(red, acc, wave, lane, tid);
+  if (tid >= 256) return;
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B) return;
   const long row = (long)b * k.T + t;
@@ -657,13 +658,14 @@ __global__ void dec_lstm_pack(AttnK k) {
 }
 
 // F6 (LSTM): gate q of unit u = act(LW[q*S+u] . [s_{t-1}; d] + LB)  (N = 4S, K = 2S); act = sigmoid, g: tanh
-__global__ __launch_bounds__(256) void dec_f6_lstm(AttnK k) {
-  __shared__ SkinnyRed red;
+__global__ __launch_bounds__(512) void dec_f6_lstm(AttnK k) {
+  __shared__ SkinnyRed8 red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
-  floatx4 acc = skinny_wave(k.HX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
+  floatx4 acc = skinny_wave8(k.HX + ((long)brow(b0, lane, k.B) * k.T + t) * 2 * S,
                             k.LW + (long)(n0 + (lane & 15)) * 2 * S, 2 * S, wave, lane);
-  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const float s = skinny_reduce8(red, acc, wave, lane, tid);
+  if (tid >= 256) return;
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B) return;
   const long row = (long)b * k.T + t;
@@ -805,13 +807,14 @@ __global__ void dec_bwd_init(AttnK k) {
 }
 
 // K3 (LSTM): [ds_prev | dd] = LW^T dGA  (N = 2S, K = 4S; GT = LW^T)
-__global__ __launch_bounds__(256) void dec_b3_lstm(AttnK k) {
-  __shared__ SkinnyRed red;
+__global__ __launch_bounds__(512) void dec_b3_lstm(AttnK k) {
+  __shared__ SkinnyRed8 red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
-  floatx4 acc = skinny_wave(k.DGA + ((long)brow(b0, lane, k.B) * k.T + t) * 4 * S,
+  floatx4 acc = skinny_wave8(k.DGA + ((long)brow(b0, lane, k.B) * k.T + t) * 4 * S,
                             k.GT + (long)(n0 + (lane & 15)) * 4 * S, 4 * S, wave, lane);
-  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const float s = skinny_reduce8(red, acc, wave, lane, tid);
+  if (tid >= 256) return;
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B) return;
   if (n < S) k.DSPF[b * S + n] = s;
@@ -876,13 +879,14 @@ __global__ __launch_bounds__(256) void dec_b5_wc(AttnK k) {
 
 // K45 (folded, the per-step path's LSTM / hybrid shapes): dc = dv_c + WDC^T dd (N = A, K = S; wdct = WDC^T);
 // DCY = dd Wd for the weight gradients is one GEMM after the loop
-__global__ __launch_bounds__(256) void dec_b45_fold(AttnK k, const float* __restrict__ wdct) {
-  __shared__ SkinnyRed red;
+__global__ __launch_bounds__(512) void dec_b45_fold(AttnK k, const float* __restrict__ wdct) {
+  __shared__ SkinnyRed8 red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int n0 = blockIdx.x * 16, b0 = blockIdx.y * 16, t = k.t, S = k.S;
-  floatx4 acc = skinny_wave(k.DD + ((long)brow(b0, lane, k.B) * k.T + t) * S, wdct + (long)(n0 + (lane & 15)) * S, S,
+  floatx4 acc = skinny_wave8(k.DD + ((long)brow(b0, lane, k.B) * k.T + t) * S, wdct + (long)(n0 + (lane & 15)) * S, S,
                             wave, lane);
-  const float s = skinny_reduce(red, acc, wave, lane, tid);
+  const float s = skinny_reduce8(red, acc, wave, lane, tid);
+  if (tid >= 256) return;
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= k.B) return;
   const long row = (long)b * k.T + t;
@@ -1489,13 +1493,13 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     hipLaunchKernelGGL(dec_f2_attn<8>, dim3(k.NCH, B), dim3(512), 0, st, k);
     hipLaunchKernelGGL(dec_f3_combine, dim3(B), dim3(256), 0, st, k);
     if (fold) {
-      hipLaunchKernelGGL(dec_f45_fold, dim3(S / 16, bt), dim3(256), 0, st, k, x.WDC, x.KD);
+      hipLaunchKernelGGL(dec_f45_fold, dim3(S / 16, bt), dim3(512), 0, st, k, x.WDC, x.KD);
     } else {
       hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
     }
     if (d.lstm) {
-      hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(512), 0, st, k);
       hipLaunchKernelGGL(dec_f7_lstm, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
     } else {
       hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
@@ -1664,13 +1668,13 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   for (int t = T - 1; t >= 0; --t) {
     k.t = t;
     if (d.lstm) {
-      hipLaunchKernelGGL(dec_b3_lstm, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
+      hipLaunchKernelGGL(dec_b3_lstm, dim3(2 * S / 16, bt), dim3(512), 0, st, k);
     } else {
       hipLaunchKernelGGL(dec_b2_gru1, dim3(S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_b3_gru2, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     }
     if (fold) {
-      hipLaunchKernelGGL(dec_b45_fold, dim3(A / 16, bt), dim3(256), 0, st, k, k.WcT);
+      hipLaunchKernelGGL(dec_b45_fold, dim3(A / 16, bt), dim3(512), 0, st, k, k.WcT);
     } else {
       hipLaunchKernelGGL(dec_b4_wd, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_b5_wc, dim3(A / 16, bt), dim3(256), 0, st, k);
@@ -2122,7 +2126,7 @@ int attn_beam_step(hipStream_t st, const AttnDims& d, const AttnParams& P, int K
   hipLaunchKernelGGL(dec_f4_cin, dim3(S / 16, bt), dim3(256), 0, st, k);
   hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
   if (d.lstm) {
-    hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(256), 0, st, k);
+    hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(512), 0, st, k);
     hipLaunchKernelGGL(dec_f7_lstm, dim3((R * S + 255) / 256), dim3(256), 0, st, k);
   } else {
     hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);

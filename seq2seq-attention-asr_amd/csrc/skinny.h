@@ -59,6 +59,54 @@ __device__ __forceinline__ float skinny_reduce(SkinnyRed& red, floatx4 acc, int 
   return ((red.v[0][i][j] + red.v[1][i][j]) + red.v[2][i][j]) + red.v[3][i][j];
 }
 
+// 8-wave form (512-thread workgroup) for the per-step kernels whose K is long (the LSTM decoder's gate and carry
+// products, K = 2S / 4S): 16-wide chunks round-robin over 8 waves (stride 128), twice the loads in flight per
+// workgroup; the 8 partial tiles are summed in wave order (a different order from skinny_wave's 4).
+struct SkinnyRed8 {
+  float v[8][16][17];
+};
+__device__ __forceinline__ floatx4 skinny_wave8(const float* __restrict__ xrow, const float* __restrict__ wrow, int K,
+                                                int wave, int lane) {
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  const int kq = 4 * (lane >> 4);
+  int kc = wave * 16;
+  for (; kc + 128 < K; kc += 256) {
+    const float4 a0 = *reinterpret_cast<const float4*>(xrow + kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    const float4 a1 = *reinterpret_cast<const float4*>(xrow + kc + 128 + kq);
+    const float4 b1 = *reinterpret_cast<const float4*>(wrow + kc + 128 + kq);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.x, b1.x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.y, b1.y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.z, b1.z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a1.w, b1.w, acc1, 0, 0, 0);
+  }
+  for (; kc < K; kc += 128) {
+    const float4 a0 = *reinterpret_cast<const float4*>(xrow + kc + kq);
+    const float4 b0 = *reinterpret_cast<const float4*>(wrow + kc + kq);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.x, b0.x, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.y, b0.y, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.z, b0.z, acc0, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a0.w, b0.w, acc0, 0, 0, 0);
+  }
+  return acc0 + acc1;
+}
+// all 512 threads call it; threads 0..255 get output (tid>>4, tid&15), the others 0
+__device__ __forceinline__ float skinny_reduce8(SkinnyRed8& red, floatx4 acc, int wave, int lane, int tid) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red.v[wave][4 * (lane >> 4) + r][lane & 15] = acc[r];
+  __syncthreads();
+  if (tid >= 256) return 0.f;
+  const int i = tid >> 4, j = tid & 15;
+  float s = red.v[0][i][j];
+#pragma unroll
+  for (int w = 1; w < 8; ++w) s += red.v[w][i][j];
+  return s;
+}
+
 // Four skinny products (gates q = 0..3 of the same 16 units) in one 1024-thread workgroup: waves 4q .. 4q + 3
 // split gate q's K exactly as skinny_wave's four waves do, so s[q] (returned to threads 0..255 for output
 // (tid>>4, tid&15)) is bitwise the skinny_reduce of that product -- four times the loads in flight per
