@@ -246,9 +246,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_carry(LstmBwdArgs a) {
 // b3 of step s + 1 and b1 of step s in one launch (no peepholes): the workgroup's 16 units get dL/dh_t from the
 // skinny product over the row the previous launch wrote (dc_t = dc_{t+1} * f, the dc half of b3 being zero
 // without peepholes), then their gate pre-activation gradients -- the same sums as lstm_bwd_carry +
-// lstm_bwd_elem, one launch per step.  At the first step of the sweep (first = 1) the carries are zero.
-__global__ __launch_bounds__(256) void lstm_bwd_step(LstmBwdArgs a, int first) {
-  __shared__ SkinnyRed red;
+// lstm_bwd_elem, one launch per step (the product in 512-thread workgroups, skinny_wave8).  At the first step of
+// the sweep (first = 1) the carries are zero.
+__global__ __launch_bounds__(512) void lstm_bwd_step(LstmBwdArgs a, int first) {
+  __shared__ SkinnyRed8 red;
   const LstmBwdDir& g = a.d[blockIdx.z];
   const int B = a.B, L = a.L, H = a.H, step = a.step;
   const int t = g.reverse ? L - 1 - step : step;
@@ -258,9 +259,10 @@ __global__ __launch_bounds__(256) void lstm_bwd_step(LstmBwdArgs a, int first) {
   floatx4 acc = {0.f, 0.f, 0.f, 0.f};
   if (!first) {
     const int br = min(b0 + (lane & 15), B - 1);
-    acc = skinny_wave(g.dA + ((long)br * L + tn) * g.ldA, g.Wb + (long)(j0 + (lane & 15)) * 4 * H, 4 * H, wave, lane);
+    acc = skinny_wave8(g.dA + ((long)br * L + tn) * g.ldA, g.Wb + (long)(j0 + (lane & 15)) * 4 * H, 4 * H, wave, lane);
   }
-  const float sh = skinny_reduce(red, acc, wave, lane, tid);
+  const float sh = skinny_reduce8(red, acc, wave, lane, tid);
+  if (tid >= 256) return;
   const int b = b0 + (tid >> 4), j = j0 + (tid & 15);
   if (b >= B) return;
   const int idx = b * H + j;
@@ -443,7 +445,7 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
         hipLaunchKernelGGL(lstm_bwd_peep, gp, dim3(256), 0, st, a);
         if (s > 0) hipLaunchKernelGGL(lstm_bwd_carry, gb, dim3(256), 0, st, a);
       } else {
-        hipLaunchKernelGGL(lstm_bwd_step, gs, dim3(256), 0, st, a, s == L - 1 ? 1 : 0);
+        hipLaunchKernelGGL(lstm_bwd_step, gs, dim3(512), 0, st, a, s == L - 1 ? 1 : 0);
       }
     }
     S2S_CHECK_HIP(hipGetLastError());
