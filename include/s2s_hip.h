@@ -364,6 +364,10 @@ int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);
 /* set the state's gradient-noise counter to gradnoise.t (a resumed trainer's checkpointed table,
  * timit/timit.lua:92,312): the next step draws with t + 1 */
 int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n, unsigned t);
+/* If the context's failure status (s2s_ctx_status) is set when the update RUNS -- a persistent launch of an
+ * earlier step on this stream timed out, its gradients are invalid -- the update is skipped on the device
+ * (params, state and the noise counter untouched; *gradnorm is still written).  This covers calls already
+ * queued in program order behind the failed step; calls made after the host has seen it fail outright. */
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
                             float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
 /* the model's weight matrices (every module weight: encoder W_z/W_r/W_h, V, Ws, we, Wy, Wc, Wd, decoder

@@ -101,8 +101,11 @@ void* stage_acquire(hipStream_t st, size_t bytes) {
   return p;
 }
 
+// one handle per device, created once under its own lock (callers may or may not hold g_lt_mu)
+std::mutex g_lt_handle_mu;
 hipblasLtHandle_t handle_of(int dev) {
   if (dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lk(g_lt_handle_mu);
   if (!g_lt_handle[dev] && hipblasLtCreate(&g_lt_handle[dev]) != HIPBLAS_STATUS_SUCCESS) g_lt_handle[dev] = nullptr;
   return g_lt_handle[dev];
 }

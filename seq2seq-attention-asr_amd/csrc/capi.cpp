@@ -1263,7 +1263,9 @@ int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_c
   S2S_REQUIRE(cfg->rho >= 0.f && cfg->rho < 1.f && cfg->eps > 0.f && cfg->maxnorm > 0.f, "optim: bad config");
   const OptimConfig c{cfg->rho,           cfg->eps,           cfg->maxnorm,       cfg->weightDecay,
                       cfg->colnorm_max,   cfg->gradnoise_eta, cfg->gradnoise_gamma, cfg->gradnoise_seed};
-  return optim_adadelta_step(static_cast<hipStream_t>(stream), c, params, grads, n, state, mats, n_mats, gradnorm);
+  // device-side guard: the update is skipped if the context's failure status is set when it runs
+  return optim_adadelta_step(static_cast<hipStream_t>(stream), c, params, grads, n, state, mats, n_mats, gradnorm,
+                             ctx->status_dev);
 }
 
 int s2s_model_bucket_count(const s2s_model_dims* d) {

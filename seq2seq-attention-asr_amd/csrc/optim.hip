@@ -29,7 +29,8 @@ struct OptState {
   float* v;        // optim.adadelta paramVariance
   float* u;        // optim.adadelta accDelta
   float* partial;  // [kNormBlocks] sums of squares
-  float* scal;     // [0] ||g||, [1] clip factor, [2] noise sigma, [3] noise counter t (uint32 bits)
+  float* scal;     // [0] ||g||, [1] clip factor, [2] noise sigma, [3] noise counter t (uint32 bits),
+                   // [4] nonzero: skip this update (the context's failure status was set, see opt_finalize)
 };
 
 OptState carve_state(void* state, size_t n) {
@@ -71,8 +72,13 @@ __device__ __forceinline__ float noise_normal(unsigned long long key, size_t i) 
   return sqrtf(-2.f * logf(u1)) * cosf(6.28318530717958647692f * u2);
 }
 
+// status: the context's failure words (handoff.h; host-coherent, written by the step's harvest kernel earlier
+// on this stream).  A set word means a persistent launch of an earlier step timed out and its gradients are
+// invalid: the whole update is skipped on the device (parameters, state and noise counter untouched), so calls
+// already queued in program order behind the failed step cannot apply them before the host gate sees it.
 __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb, float maxnorm, float eta,
-                                                    float gamma, float* scal, float* gradnorm_out) {
+                                                    float gamma, float* scal, float* gradnorm_out,
+                                                    const unsigned* status) {
   __shared__ float red[4];
   float s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
@@ -80,7 +86,12 @@ __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
+    const bool skip = status && ((__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) |
+                                  __hip_atomic_load(status + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u);
+    scal[4] = skip ? 1.f : 0.f;
     const float gn = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
+    if (gradnorm_out) *gradnorm_out = gn;
+    if (skip) return;
     scal[0] = gn;
     scal[1] = gn > maxnorm ? maxnorm / gn : 1.f;
     if (eta != 0.f) {  // gradnoise.t = (gradnoise.t or 0) + 1; sigma = (eta / (1 + t)^gamma)^0.5
@@ -88,7 +99,6 @@ __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb
       scal[3] = __uint_as_float(t);
       scal[2] = (float)sqrt((double)eta / pow(1.0 + (double)t, (double)gamma));
     }
-    if (gradnorm_out) *gradnorm_out = gn;
   }
 }
 
@@ -98,6 +108,7 @@ __global__ __launch_bounds__(256) void opt_adadelta(float* __restrict__ x, float
                                                     float* __restrict__ v, float* __restrict__ u, size_t n,
                                                     const float* scal, float rho, float eps, float wd,
                                                     int noise, unsigned long long seed) {
+  if (scal[4] != 0.f) return;
   const float clip = scal[1];
   const float sigma = noise ? scal[2] : 0.f;
   const unsigned long long key = noise ? mix64(seed * kGolden + __float_as_uint(scal[3])) : 0ull;
@@ -126,7 +137,9 @@ struct MatTable {
 
 // TrainUtils.columnNormConstraint: norm_r = ||W_r||_2 + 1e-8 over each output row (W:norm(2,2));
 // rows with norm >= maxval are divided by norm / maxval, the others kept.  One wave per row.
-__global__ __launch_bounds__(256) void opt_colnorm(float* __restrict__ x, MatTable t, float maxval) {
+__global__ __launch_bounds__(256) void opt_colnorm(float* __restrict__ x, MatTable t, float maxval,
+                                                   const float* scal) {
+  if (scal[4] != 0.f) return;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (row >= t.first[t.n]) return;
   int m = 0;
@@ -150,7 +163,7 @@ size_t optim_state_bytes(size_t n) {
 }
 
 int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
-                        const long* mats, int n_mats, float* gradnorm) {
+                        const long* mats, int n_mats, float* gradnorm, const unsigned* status) {
   const float rho = c.rho, eps = c.eps, wd = c.weightDecay, colnorm_max = c.colnorm_max;
   const int noise = c.gradnoise_eta != 0.f;
   S2S_REQUIRE(x && g && state && n > 0, "optim: null argument");
@@ -159,7 +172,7 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
   const int nb = (int)std::min<size_t>(kNormBlocks, (n + 255) / 256);
   hipLaunchKernelGGL(opt_sumsq, dim3(nb), dim3(256), 0, st, g, n, s.partial);
   hipLaunchKernelGGL(opt_finalize, dim3(1), dim3(256), 0, st, s.partial, nb, c.maxnorm, c.gradnoise_eta,
-                     c.gradnoise_gamma, s.scal, gradnorm);
+                     c.gradnoise_gamma, s.scal, gradnorm, status);
   const int ne = (int)std::min<size_t>(2048, (n + 255) / 256);
   hipLaunchKernelGGL(opt_adadelta, dim3(ne), dim3(256), 0, st, x, g, s.v, s.u, n, s.scal, rho, eps, wd, noise,
                      c.gradnoise_seed);
@@ -176,7 +189,7 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
                   "optim: weight matrix outside the flat buffer");
       t.first[m + 1] = t.first[m] + t.rows[m];
     }
-    hipLaunchKernelGGL(opt_colnorm, dim3((t.first[n_mats] + 3) / 4), dim3(256), 0, st, x, t, colnorm_max);
+    hipLaunchKernelGGL(opt_colnorm, dim3((t.first[n_mats] + 3) / 4), dim3(256), 0, st, x, t, colnorm_max, s.scal);
   }
   S2S_CHECK_HIP(hipGetLastError());
   return 0;

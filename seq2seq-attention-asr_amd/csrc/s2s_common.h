@@ -241,6 +241,7 @@ struct OptimConfig {
   unsigned long long gradnoise_seed;
 };
 int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
-                        const long* mats, int n_mats, float* gradnorm);
+                        const long* mats, int n_mats, float* gradnorm,
+                        const unsigned* status = nullptr);
 
 }  // namespace s2s

@@ -35,11 +35,13 @@ class Adadelta:
     gradient noise table gradnoise = {eta, gamma} (timit.lua:185-189, 310-315; the configs set eta = 0,
     timit.lua's own default is 1e-3).  The noise counter t lives in self.state (checkpointed with it);
     gradnoise_seed must be equal on every data-parallel rank so the replicas stay identical.
-    params / grads: flat float32 CUDA tensors (ChorowskiBaseline.getParameters()), or pass the model."""
+    params / grads: flat float32 CUDA tensors (ChorowskiBaseline.getParameters()), or pass the model.
+    The update runs on the model's context (or ctx): if that context's failure status is set when the update
+    runs on the device (a persistent launch of the step before it timed out), the update is skipped there."""
 
     def __init__(self, model=None, params=None, grads=None, mats=None, rho=0.95, eps=1e-8, maxnorm=1e20,
                  weightDecay=0.0, colnormconstr=False, colnorm_max=1.0, gradnoise_eta=0.0, gradnoise_gamma=0.55,
-                 gradnoise_seed=0x5EED):
+                 gradnoise_seed=0x5EED, ctx=None):
         if model is not None:
             params, grads = model.getParameters()
             if mats is None:
@@ -56,7 +58,9 @@ class Adadelta:
         self._nmats = len(mats)
         self.state = torch.zeros(lib.s2s_optim_state_bytes(self.n), dtype=torch.uint8, device=params.device)
         self.gradnorm = torch.zeros(1, dtype=torch.float32, device=params.device)
-        self.ctx = get_context(params.device.index)
+        if ctx is None:
+            ctx = getattr(model, "ctx", None) or get_context(params.device.index)
+        self.ctx = ctx
 
     def set_noise_step(self, t, stream=None):
         """gradnoise.t of a resumed run (timit/timit.lua:92, 312): the next step draws with t + 1."""

@@ -12,6 +12,9 @@ import torch
 
 from .model import param_shapes
 
+# bias slot of a TemporalConvolutionZeroBias module: a zero column that takes part in the QR and is thrown away
+ZERO_BIAS = "<zero bias>"
+
 
 def orthogonalize(weight, bias=None):
     """TrainUtils.lua:5-26 on one module, in place.  weight (rows, cols), bias (rows,) or None."""
@@ -31,16 +34,20 @@ def modules(cfg):
     """(weight name, bias name or None) of every leaf module of the Chorowski autoencoder that holds a
     weight, in the flat layout's naming (model.param_shapes).  The encoder's GRU gates are
     LinearZeroBias (weight only, GRU.lua:22-25).  V and we are TemporalConvolutionZeroBias: a bias
-    that updateOutput re-zeroes (TemporalConvolutionZeroBias.lua:13-38) and the flat layout drops; a
-    zero bias column changes neither Q's weight columns (QR is column-sequential) nor, in the wide
-    case, Q^T's first columns (its row of w^T is zero, so Q's matching row is zero), so both are
-    orthogonalized as weight-only modules.  Ws / Wy / Wc / Wd / Wm / Wo are nn.Linear (weight + bias);
-    the decoder GRU's gates are LinearZeroBias."""
+    that reset() and updateOutput zero (TemporalConvolutionZeroBias.lua:13-38) and the flat layout drops.
+    TrainUtils.lua:6-15 still sees [W | 0]: a zero column changes neither Q's weight columns in the tall
+    case (QR is column-sequential) nor Q^T's in the wide case (its row of w^T is zero), but a SQUARE W
+    becomes wide and takes the qr(w^T)^T branch, a different Q (V is (Sc, A) = (512, 512) at the
+    defaults).  So both carry ZERO_BIAS: orthogonalized with an explicit zero column, which is dropped.
+    Ws / Wy / Wc / Wd / Wm / Wo are nn.Linear (weight + bias); the decoder GRU's gates are
+    LinearZeroBias."""
     names = [n for n, _ in param_shapes(cfg)]
     out = []
     for n in names:
-        if n.startswith("enc") or n.startswith("dec.") or n in ("V", "we"):
+        if n.startswith("enc") or n.startswith("dec."):
             out.append((n, None))
+        elif n in ("V", "we"):
+            out.append((n, ZERO_BIAS))
     for w, b in (("Ws", "bs"), ("Wy", "by"), ("Wc", "bc"), ("Wd", "bd"), ("Wm", "bm"), ("Wo", "bo")):
         out.append((w, b))
     return out
@@ -51,5 +58,8 @@ def orthogonalize_model(model):
     """TrainUtils.orthogonalizeGraph(model.autoencoder) on a ChorowskiBaseline's flat parameters."""
     v = model.views()
     for w, b in modules(model.cfg):
-        orthogonalize(v[w], v[b] if b is not None else None)
+        if b == ZERO_BIAS:
+            orthogonalize(v[w], torch.zeros(v[w].shape[0], dtype=v[w].dtype, device=v[w].device))
+        else:
+            orthogonalize(v[w], v[b] if b is not None else None)
     return model

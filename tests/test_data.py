@@ -152,7 +152,10 @@ def test_checkpoint_seed_base_is_per_rank():
     b1 = checkpoint.seed_base_for(meta, 1, default=-1)
     assert b0 != b1
     assert b0 == _mix64(1234, 0) and b1 == _mix64(1234, 1)
-    assert checkpoint.seed_base_for({"steps": 5}, 1, default=42) == 42  # older file: keep the model's own
+    with pytest.warns(UserWarning, match="no dropout seed"):
+        assert checkpoint.seed_base_for({"steps": 5}, 1, default=42) == 42  # nothing saved: keep the model's own
+    with pytest.warns(UserWarning, match="older format"):  # an older writer saved its base, not the user seed
+        assert checkpoint.seed_base_for({"steps": 5, "dropout_seed_base": "987"}, 1, default=42) == 987
 
 
 @pytest.mark.gpu

@@ -292,28 +292,59 @@ def _assert_grads(pairs, rtol=RTOL):
     assert not bad, f"max rel err > {rtol:.0e}: {bad}"
 
 
+def _adopt_conv_decisions(convs, pools, ccache, margin=1e-5):
+    """The conv stack's ReLU (1[u > 0]) and TemporalMaxPooling (first maximum) decisions are discrete: where u
+    or the gap between a window's two values sits within fp32 noise of 0, any fp32 implementation -- the
+    reference's CudaTensor path too -- may decide differently from the float64 oracle, and a flipped decision
+    reroutes a whole gradient entry.  Require the GPU's decisions to equal the oracle's wherever the margin is
+    clear (|u| or the window gap > margin * max|u|), then run the oracle's backward under the GPU's decisions
+    (as _adopt_mono_decisions does for MonotonicAlignment, tests/test_gpu_parity.py).  Returns the number of
+    adopted flips per layer."""
+    flips = []
+    for l, (tc, tp) in enumerate(zip(convs, pools)):
+        h, u, idx, Lr = ccache[l]
+        scale = np.abs(u).max()
+        gmask = _np(tc.output) > 0  # the fused ReLU's output: positive exactly where the GPU passed u
+        omask = u > 0
+        clear = np.abs(u) > margin * scale
+        assert np.array_equal(gmask[clear], omask[clear]), f"layer {l}: ReLU decisions differ off the near-tie band"
+        gidx = tp.indices.cpu().numpy().astype(idx.dtype)
+        r = np.maximum(u, 0.0)[:, :2 * idx.shape[1]].reshape(idx.shape[0], idx.shape[1], 2, -1)
+        gap = np.abs(r[:, :, 0] - r[:, :, 1])
+        clear_p = gap > margin * scale
+        assert np.array_equal(gidx[clear_p], idx[clear_p]), f"layer {l}: max-pooling decisions differ off the band"
+        flips.append(int((gmask != omask).sum() + (gidx != idx).sum()))
+        # run the backward under the GPU's decisions: relu_bwd reads only the sign of u
+        ccache[l] = (h, np.where(gmask, 1.0, -1.0), gidx, Lr)
+    return flips
+
+
 @pytest.mark.gpu
 def test_conv_bilstm_encoder_matches_oracle(fe):
-    """timit/timit.lua:108-125 at its sizes (D=123, 256 conv maps, LSTM 128 per direction)."""
+    """timit/timit.lua:108-125 at its sizes (D=123, 256 conv maps, LSTM 128 per direction).  Weights from a seeded
+    generator; the oracle gets the fp32-rounded x / dy the GPU sees; ReLU / max-pooling near ties are adopted from
+    the GPU (_adopt_conv_decisions) -- the bar stays 1e-4 on every tensor."""
     import s2s_amd
     rng = np.random.default_rng(11)
     B, L, D = 4, 64, 123
-    enc = s2s_amd.ConvBiLSTMEncoder(D).cuda()
+    enc = s2s_amd.ConvBiLSTMEncoder(D, generator=torch.Generator().manual_seed(11)).cuda()
     P = {}
     convs = [m for m in enc.convlayer.modules if isinstance(m, fe.TemporalConvolution)]
+    pools = [m for m in enc.convlayer.modules if isinstance(m, fe.TemporalMaxPooling)]
     for l, m in enumerate(convs):
         P[f"conv{l}.W"], P[f"conv{l}.b"] = _np(m.weight), _np(m.bias)
     cells = enc.rnn.cells
     for pre, c in zip(("f.", "b."), cells):
         for k, v in c.named().items():
             P[pre + k] = _np(v)
-    x = rng.standard_normal((B, L, D))
+    x = rng.standard_normal((B, L, D)).astype(np.float32).astype(np.float64)
     y = enc.forward(cu(x))
     yr, cache = fo.conv_bilstm_fwd(x, P)
     assert_rel(_np(y), yr, "y")
-    dy = rng.standard_normal(yr.shape)
+    dy = rng.standard_normal(yr.shape).astype(np.float32).astype(np.float64)
     enc.zeroGradParameters()
     enc.backward(cu(x), cu(dy), 1.0)
+    _adopt_conv_decisions(convs, pools, cache[1])
     G = {k: np.zeros_like(v) for k, v in P.items()}
     fo.conv_bilstm_bwd(P, cache, dy, G)
     torch.cuda.synchronize()
@@ -811,7 +842,8 @@ def test_conv_bilstm_attention_model_step_matches_oracle(fe):
     lins = [m for m in dec.decoder_mlp.modules if isinstance(m, fe.Linear)]
     layers = [("linear", _np(lins[0].weight), _np(lins[0].bias)), ("relu",),
               ("linear", _np(lins[1].weight), _np(lins[1].bias)), ("logsoftmax",)]
-    x = rng.standard_normal((B, L, D))
+    pools = [m for m in enc.convlayer.modules if isinstance(m, fe.TemporalMaxPooling)]
+    x = rng.standard_normal((B, L, D)).astype(np.float32).astype(np.float64)
     labels = rng.integers(0, O, (B, T)).astype(np.int32)
     model.zeroGradParameters()
     nll, logp = model.step(cu(x), cu(labels, torch.int32))
@@ -831,6 +863,7 @@ def test_conv_bilstm_attention_model_step_matches_oracle(fe):
     Gd = {k: np.zeros_like(v) for k, v in Pd.items()}
     dh = orc.attention_bwd(Pd, cfg, acache, None, Gd, sc, dmlp_in=dv.reshape(B, T, -1))
     Ge = {k: np.zeros_like(v) for k, v in P.items()}
+    _adopt_conv_decisions(convs, pools, ecache[1])
     fo.conv_bilstm_bwd(P, ecache, dh, Ge, sc)
     pairs = []
     for l, m in enumerate(convs):

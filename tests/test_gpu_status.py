@@ -121,3 +121,46 @@ def test_injected_abort_model_step_reports_then_recovers(s2s):
     assert m.ctx.status() == 0 and ref.ctx.status() == 0
     assert torch.equal(logp, l2) and torch.equal(nll, n2)
     assert torch.equal(m.grads, ref.grads)
+
+
+def test_optimizer_queued_behind_failed_step_skips_update(s2s):
+    """the host gate only sees a failure after the harvest has run, so an optimizer update already
+    queued in program order behind the failed step would apply its invalid gradients.  The update reads the
+    context's status words on the device and skips itself: parameters, optimizer state and the noise counter
+    stay untouched.  A sleep kernel in front of the step keeps the host from seeing the status before the
+    update is queued (the device-side path is the one exercised)."""
+    from s2s_amd import _lib
+    from s2s_amd.optim import Adadelta
+    cfg = s2s.ModelConfig()
+    m = s2s.ChorowskiBaseline(cfg, overlap=True)
+    opt = Adadelta(m, gradnoise_eta=1e-3)
+    assert opt.ctx is m.ctx
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(4, 24, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (4, 6), generator=g).to(torch.int32).cuda()
+    m.step(x, lab)  # a good step + update first: the state is non-trivial
+    opt.step()
+    torch.cuda.synchronize()
+    p0, s0 = m.params.clone(), opt.state.clone()
+    try:
+        _lib.lib.s2s_debug_inject_abort(1)
+        torch.cuda._sleep(50_000_000)  # ~25 ms of device time ahead of the failing step
+        m.step(x, lab)
+        opt.step()  # queued before the harvest has run
+        _lib.lib.s2s_debug_inject_abort(0)
+        torch.cuda.synchronize()
+        assert m.ctx.status(clear=False) != 0
+    finally:
+        _lib.lib.s2s_debug_inject_abort(0)
+        m.ctx.status(clear=True)
+    assert torch.equal(m.params, p0)
+    # state = v | u (nn floats each) | 512 norm partials | scal: v, u and scal[0..3] (norm, clip, sigma, noise t)
+    nn = (opt.n + 63) // 64 * 64
+    f, f0 = opt.state.view(torch.float32), s0.view(torch.float32)
+    assert torch.equal(f[:2 * nn], f0[:2 * nn])
+    assert torch.equal(f[2 * nn + 512:2 * nn + 516], f0[2 * nn + 512:2 * nn + 516])
+    # after clearing, a good step updates again
+    m.step(x, lab)
+    opt.step()
+    torch.cuda.synchronize()
+    assert not torch.equal(m.params, p0)
