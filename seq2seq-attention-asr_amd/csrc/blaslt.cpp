@@ -29,17 +29,6 @@
 
 namespace s2s {
 
-thread_local LtStage* t_stage = nullptr;  // the calling context's staging buffer (set_lt_stage, per C-ABI call)
-void set_lt_stage(LtStage* s) { t_stage = s; }
-void lt_stage_free(LtStage* s) {
-  if (!s) return;
-  if (s->p) (void)hipFree(s->p);
-  for (void* q : s->old) (void)hipFree(q);
-  s->p = nullptr;
-  s->n = 0;
-  s->old.clear();
-}
-
 std::atomic<int> g_gemm_lt{1};  // s2s_debug_gemm_lt(0): the in-house bf16 GEMM instead (A/B, tests)
 std::atomic<long> g_lt_calls{0};  // hipBLASLt matmuls launched (s2s_debug_gemm_lt_calls)
 std::atomic<int> g_lt_last{0};
@@ -83,22 +72,6 @@ void to_bf16(hipStream_t st, const float* src, long ld, long rows, long cols, __
   const long work = (rows * cols + 3) / 4;
   const unsigned blocks = (unsigned)std::min<long>(4096, std::max<long>(1, (work + 255) / 256));
   hipLaunchKernelGGL(to_bf16_kernel, dim3(blocks), dim3(256), 0, st, src, ld, rows, cols, dst);
-}
-
-// the calling context's staging buffer with at least `bytes`, or nullptr (none, or too small while capturing)
-void* stage_acquire(hipStream_t st, size_t bytes) {
-  LtStage* s = t_stage;
-  if (!s) return nullptr;
-  if (s->n >= bytes) return s->p;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-  void* p = nullptr;
-  const size_t want = std::max(bytes, s->n * 2);
-  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
-  if (s->p) s->old.push_back(s->p);  // may still be read by queued work: freed with the context
-  s->p = p;
-  s->n = want;
-  return p;
 }
 
 // one handle per device, created once under its own lock (callers may or may not hold g_lt_mu)
@@ -167,7 +140,7 @@ bool gemm_lt_enabled() { return g_gemm_lt != 0; }
 
 int gemm_lt(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done) {
   *done = false;
-  if (!g_gemm_lt || !t_stage || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
+  if (!g_gemm_lt || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
   int dev = 0;
   S2S_CHECK_HIP(hipGetDevice(&dev));
   // C^T (N x M) = op(B)^T op(A)^T: A' = B's buffer, B' = A's buffer (see the header comment)

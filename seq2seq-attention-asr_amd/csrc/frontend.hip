@@ -323,7 +323,8 @@ size_t tconv_scratch_bytes(int B, int L, int Din, int Dout, int kW) {
   return kWsBytes + align256(sizeof(float) * (size_t)B * L * Dout) + align256(sizeof(float) * (size_t)B * L * kW * Din);
 }
 
-// A large plain GEMM of the front-end: on hipBLASLt under the bf16 modes (gemm_lt, blaslt.cpp), else gemm_f32.
+// A large plain GEMM of the front-end: on the big-tile bf16 kernel under the bf16 modes (gemm_bf16.hip), else
+// gemm_f32.
 // Problems below ~1 GFLOP stay in-house (launch overhead, and they are not the front-end's time).
 static int big_gemm(hipStream_t st, bool tA, bool tB, int M, int N, int K, float alpha, const float* A, long lda,
                     const float* Bm, long ldb, float beta, float* C, long ldc, const float* bias, int relu,
@@ -332,7 +333,7 @@ static int big_gemm(hipStream_t st, bool tA, bool tB, int M, int N, int K, float
   q.relu = relu;
   if (gemm_precision() == kGemmBf16 && 2.0 * M * (double)N * K >= 1e9) {
     bool done = false;
-    S2S_TRY(gemm_lt(st, q, tA, tB, ws, &done));
+    S2S_TRY(gemm_large_bf16(st, q, tA, tB, ws, &done));
     if (done) return 0;
   }
   return gemm_f32(st, &q, 1, tA, tB, ws);

@@ -1,0 +1,386 @@
+// Large bf16 GEMMs on gfx950 MFMA, in house (the module-level products of the bf16 modes: the VGG front-end's
+// 1x1 TemporalConvolution layers, librispeech/model_vgg.lua:45-52, M = B L' ~ 8128 rows x 2048 x 896..2048, their
+// input and weight gradients, and the attention decoder's Vh / dh / weight-gradient products under that model,
+// Attention.lua:43-47).  Replaces the vendor library for these shapes.
+//
+// Row-major C (M x N) = alpha op(A) op(B) (+ bias[n]) (+ beta C) (ReLU) -- the GemmProblem contract.
+//  1. Staging: each fp32 operand is rounded to bf16 (RNE) into a K-contiguous, zero-padded copy [Rp][Kp] in the
+//     calling context's staging buffer (one pass; a transposed operand goes through a 64 x 64 LDS tile), so the
+//     main loop reads one layout with no guards: A' [Mp][Kp], B' [Np][Kp], C = A' B'^T.
+//  2. gemm_bf16_nt: a BM x BN x 64 tile per workgroup, waves WM x WN, each a (BM/WM) x (BN/WN) block of
+//     v_mfma_f32_16x16x32_bf16 accumulators.  K-tiles are staged global -> LDS by global_load_lds_dwordx4
+//     (LDS-DMA, no register pass), two LDS stages: the next tile's DMA is issued before the current tile's
+//     fragment reads and MFMAs, one vmcnt(0) + barrier per K-tile (cdna_hip_programming.md §5, "Minimum
+//     2-phase").  The LDS image is lane-linear per 1-KB wave instruction (8 rows x 128 B), so the bank swizzle is
+//     applied on the SOURCE address: row r's 16-B chunk p holds k-chunk p ^ ((r >> 1) & 7), and the fragment
+//     reads (16 rows x one k-chunk per 16-lane group) hit 16 distinct 16-B slots of the 256-B bank row.
+//     All LDS lives in one dynamic array (a second __shared__ object made hipcc drain vmcnt early, guide §5 4a).
+//  3. Output tiles are dealt XCD-contiguously (bijective remap), the N tiles of one M panel next to each other
+//     (the A' panel is shared through that XCD's L2).  Too few tiles for the chip: split-K into S slices, each
+//     writing an fp32 slab, summed in slice order by bf16_splitk_reduce (deterministic), which applies the
+//     epilogue.
+// The result equals a float64 product of the bf16-rounded operands to fp32-accumulation accuracy
+// (tests/test_gpu_bf16.py), like the other bf16 kernels of the library.
+#include <algorithm>
+#include <atomic>
+#include <cstdlib>
+#include <cstring>
+
+#include "s2s_common.h"
+
+namespace s2s {
+
+// ------------------------------------------------------------------ the context-owned staging buffer
+thread_local LtStage* t_stage = nullptr;  // the calling context's staging buffer (set_lt_stage, per C-ABI call)
+void set_lt_stage(LtStage* s) { t_stage = s; }
+void lt_stage_free(LtStage* s) {
+  if (!s) return;
+  if (s->p) (void)hipFree(s->p);
+  for (void* q : s->old) (void)hipFree(q);
+  s->p = nullptr;
+  s->n = 0;
+  s->old.clear();
+}
+
+std::atomic<int> g_gemm_big{1};     // s2s_debug_gemm_big(0): these problems stay on gemm_f32's 64 x 64 bf16 tiles
+std::atomic<long> g_big_calls{0};   // big-GEMM calls launched (s2s_debug_gemm_big_calls)
+
+// the calling context's staging buffer with at least `bytes`, or nullptr (none, or too small while capturing)
+void* stage_acquire(hipStream_t st, size_t bytes) {
+  LtStage* s = t_stage;
+  if (!s) return nullptr;
+  if (s->n >= bytes) return s->p;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  void* p = nullptr;
+  const size_t want = std::max(bytes, s->n * 2);
+  if (hipMalloc(&p, want) != hipSuccess) return nullptr;
+  if (s->p) s->old.push_back(s->p);  // may still be read by queued work: freed with the context
+  s->p = p;
+  s->n = want;
+  return p;
+}
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void* lds_void_t;
+typedef __attribute__((address_space(1))) const void* glb_void_t;
+
+constexpr int kBK = 64;  // K-tile (bf16): 128-byte LDS rows
+
+// ---- staging: logical operand (R x K), element (r, k) at src[r * ld + k] -> dst [Rp][Kp] bf16, zero padded.
+// One thread per 8 consecutive k of a row: two float4 loads, one 16-byte store.
+__global__ __launch_bounds__(256) void stage_kc_bf16(const float* __restrict__ src, long ld, int R, int K, int Kp,
+                                                     long n8, int vec, __bf16* __restrict__ dst) {
+  const int kq = Kp / 8;
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const long r = i / kq;
+    const int k = (int)(i - r * kq) * 8;
+    floatx4 a = {0.f, 0.f, 0.f, 0.f}, b = {0.f, 0.f, 0.f, 0.f};
+    if (r < R) {
+      const float* row = src + r * ld;
+      if (vec && k + 8 <= K) {
+        a = *reinterpret_cast<const floatx4*>(row + k);
+        b = *reinterpret_cast<const floatx4*>(row + k + 4);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = k + j < K ? row[k + j] : 0.f;
+          b[j] = k + 4 + j < K ? row[k + 4 + j] : 0.f;
+        }
+      }
+    }
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      v[j] = (__bf16)a[j];
+      v[4 + j] = (__bf16)b[j];
+    }
+    *reinterpret_cast<bf16x8*>(dst + r * Kp + k) = v;
+  }
+}
+
+// transposed operand: element (r, k) at src[k * ld + r] (row-contiguous along r) -> dst [Rp][Kp]; one 64 (r) x 64 (k)
+// tile per workgroup through LDS (coalesced reads along r, 16-byte writes along k)
+__global__ __launch_bounds__(256) void stage_rc_bf16(const float* __restrict__ src, long ld, int R, int K, int Kp,
+                                                     __bf16* __restrict__ dst) {
+  __shared__ float t[64][65];
+  const int r0 = blockIdx.x * 64, k0 = blockIdx.y * 64, tid = threadIdx.x;
+  const int rr = r0 + (tid & 63);
+  for (int kk = tid >> 6; kk < 64; kk += 4) {
+    const int k = k0 + kk;
+    t[kk][tid & 63] = (k < K && rr < R) ? src[(long)k * ld + rr] : 0.f;
+  }
+  __syncthreads();
+  for (int c = tid; c < 512; c += 256) {
+    const int r = c >> 3, kc = (c & 7) * 8;
+    bf16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (__bf16)t[kc + j][r];
+    *reinterpret_cast<bf16x8*>(dst + (long)(r0 + r) * Kp + k0 + kc) = v;
+  }
+}
+
+// ---- the GEMM
+struct BigGemm {
+  const __bf16* A;  // [Mp][Kp]
+  const __bf16* B;  // [Np][Kp]
+  float* C;
+  const float* bias;
+  float* part;      // split-K slabs [S][M][N] or nullptr
+  long ldc;
+  int M, N, Kp, kslice;  // kslice: K-tiles per split (all of them when S = 1)
+  int tiles_m, tiles_n, S, nblocks;
+  float alpha, beta;
+  int relu;
+};
+
+// bijective XCD-contiguous remap of a 1-D grid (hardware deals blockIdx round-robin over the 8 XCDs)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int q = nwg / 8, r = nwg % 8, x = bid % 8;
+  return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+}
+
+// LDS byte offset of (row, k-chunk c) in a [rows][128 B] image whose chunks are swizzled by (row >> 1) & 7
+__device__ __forceinline__ int swz(int row, int c) { return row * 128 + ((c ^ ((row >> 1) & 7)) << 4); }
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(BigGemm g) {
+  constexpr int NW = WM * WN;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int GA = BM / 8 / NW, GB = BN / 8 / NW;  // 1-KB DMA instructions per wave per K-tile
+  constexpr int STAGE = (BM + BN) * 128;             // bytes of one LDS stage
+  static_assert(GA >= 1 && GB >= 1 && BM % (8 * NW) == 0 && BN % (8 * NW) == 0, "tile / wave split");
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int lin = xcd_remap(blockIdx.x, gridDim.x);
+  if (lin >= g.nblocks) return;
+  const int tn = lin % g.tiles_n, rest = lin / g.tiles_n, tm = rest % g.tiles_m, s = rest / g.tiles_m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kt0 = s * g.kslice, nk = min(g.kslice, g.Kp / kBK - kt0);
+
+  // DMA sources: wave instruction j covers rows 8 (wave + NW j) .. + 7 of the tile; lane l -> row + (l >> 3),
+  // LDS chunk l & 7 <- k-chunk (l & 7) ^ swizzle(row)
+  const __bf16* asrc[GA];
+  const __bf16* bsrc[GB];
+#pragma unroll
+  for (int j = 0; j < GA; ++j) {
+    const int row = 8 * (wave + NW * j) + (lane >> 3);
+    asrc[j] = g.A + (long)(m0 + row) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+#pragma unroll
+  for (int j = 0; j < GB; ++j) {
+    const int row = 8 * (wave + NW * j) + (lane >> 3);
+    bsrc[j] = g.B + (long)(n0 + row) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+  }
+  auto stage = [&](int kt, int buf) {
+    char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int j = 0; j < GA; ++j)
+      __builtin_amdgcn_global_load_lds((glb_void_t)(asrc[j] + (long)kt * kBK),
+                                       (lds_void_t)(base + 1024 * (wave + NW * j)), 16, 0, 0);
+#pragma unroll
+    for (int j = 0; j < GB; ++j)
+      __builtin_amdgcn_global_load_lds((glb_void_t)(bsrc[j] + (long)kt * kBK),
+                                       (lds_void_t)(base + BM * 128 + 1024 * (wave + NW * j)), 16, 0, 0);
+  };
+
+  floatx4 acc[FM][FN];
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int q = 0; q < FN; ++q) acc[f][q] = floatx4{0.f, 0.f, 0.f, 0.f};
+
+  const int lr = lane & 15, lq = lane >> 4;
+  if (nk > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int buf = kt & 1;
+      if (kt + 1 < nk) stage(kt + 1, buf ^ 1);  // the next tile's DMA runs under this tile's MFMAs
+      const char* As = smem + buf * STAGE;
+      const char* Bs = As + BM * 128;
+#pragma unroll
+      for (int ks = 0; ks < kBK / 32; ++ks) {
+        bf16x8 a[FM], b[FN];
+#pragma unroll
+        for (int f = 0; f < FM; ++f) {
+          const int row = wm * TM + 16 * f + lr;
+          a[f] = *reinterpret_cast<const bf16x8*>(As + swz(row, 4 * ks + lq));
+        }
+#pragma unroll
+        for (int q = 0; q < FN; ++q) {
+          const int row = wn * TN + 16 * q + lr;
+          b[q] = *reinterpret_cast<const bf16x8*>(Bs + swz(row, 4 * ks + lq));
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int f = 0; f < FM; ++f)
+#pragma unroll
+          for (int q = 0; q < FN; ++q) acc[f][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[f], b[q], acc[f][q], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next stage has landed ...
+      __syncthreads();                                  // ... and every wave is done with this one
+    }
+  }
+
+  // epilogue (16 x 16 accumulator map: column lane & 15, rows 4 (lane >> 4) + r)
+#pragma unroll
+  for (int f = 0; f < FM; ++f)
+#pragma unroll
+    for (int q = 0; q < FN; ++q) {
+      const int col = n0 + wn * TN + 16 * q + lr;
+      if (col >= g.N) continue;
+      const float bv = (!g.part && g.bias) ? g.bias[col] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = m0 + wm * TM + 16 * f + 4 * lq + r;
+        if (row >= g.M) continue;
+        if (g.part) {
+          g.part[((long)s * g.M + row) * g.N + col] = acc[f][q][r];
+        } else {
+          float v = g.alpha * acc[f][q][r] + bv;
+          float* c = g.C + (long)row * g.ldc + col;
+          if (g.beta != 0.f) v += g.beta * *c;
+          if (g.relu) v = fmaxf(v, 0.f);
+          *c = v;
+        }
+      }
+    }
+}
+
+// C = alpha * (sum of the S slabs in slice order) (+ bias) (+ beta C) (ReLU)
+__global__ __launch_bounds__(256) void bf16_splitk_reduce(BigGemm g) {
+  const long mn = (long)g.M * g.N;
+  for (long e = blockIdx.x * 256L + threadIdx.x; e < mn; e += (long)gridDim.x * 256) {
+    float v[8];
+    float sum = 0.f;
+    int s = 0;
+    for (; s + 8 <= g.S; s += 8) {  // eight slabs' loads in flight, summed in order
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = g.part[(s + j) * mn + e];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sum += v[j];
+    }
+    for (; s < g.S; ++s) sum += g.part[s * mn + e];
+    const long row = e / g.N;
+    const int col = (int)(e - row * g.N);
+    float o = g.alpha * sum;
+    if (g.bias) o += g.bias[col];
+    float* c = g.C + row * g.ldc + col;
+    if (g.beta != 0.f) o += g.beta * *c;
+    if (g.relu) o = fmaxf(o, 0.f);
+    *c = o;
+  }
+}
+
+constexpr int kSmall = 128;  // 128 x 128 tiles, 4 waves (2 x 2)
+constexpr int kLarge = 256;  // 256 x 256 tiles, 8 waves (2 x 4)
+
+template <int BM, int BN, int WM, int WN>
+int launch_nt(hipStream_t st, const BigGemm& g) {
+  const size_t lds = 2 * (size_t)(BM + BN) * 128;
+  static std::atomic<int> attr_set{0};
+  if (!attr_set.load(std::memory_order_relaxed)) {
+    S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gemm_bf16_nt<BM, BN, WM, WN>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    attr_set.store(1, std::memory_order_relaxed);
+  }
+  hipLaunchKernelGGL((gemm_bf16_nt<BM, BN, WM, WN>), dim3((unsigned)g.nblocks), dim3(WM * WN * 64), lds, st, g);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+}  // namespace
+
+bool gemm_big_enabled() { return g_gemm_big != 0; }
+
+int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, bool* done) {
+  *done = false;
+  if (!g_gemm_big || !t_stage || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
+  const int M = q.M, N = q.N, K = q.K, Kp = (K + kBK - 1) / kBK * kBK, nkt = Kp / kBK;
+  // tile: 256 x 256 when that still gives >= 128 output tiles, else 128 x 128
+  const long t256 = (long)((M + kLarge - 1) / kLarge) * ((N + kLarge - 1) / kLarge);
+  const bool large = t256 >= 128;
+  const int BM = large ? kLarge : kSmall, BN = BM;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, tiles = tiles_m * tiles_n;
+  // split-K until the grid covers the chip (>= 256 workgroups), keeping >= 8 K-tiles per slice
+  int S = 1;
+  while (tiles * S < 256 && nkt / (2 * S) >= 8 && S < 16) S *= 2;
+  const int kslice = (nkt + S - 1) / S;
+  S = (nkt + kslice - 1) / kslice;
+  const int Mp = tiles_m * BM, Np = tiles_n * BN;
+  const size_t abytes = (size_t)Mp * Kp * 2, bbytes = (size_t)Np * Kp * 2;
+  const size_t slab = S > 1 ? sizeof(float) * (size_t)S * M * N : 0;
+  const size_t off_b = (abytes + 255) / 256 * 256, off_p = off_b + (bbytes + 255) / 256 * 256;
+  char* stg = static_cast<char*>(stage_acquire(st, off_p + slab));
+  if (!stg) return 0;
+  __bf16* Ah = reinterpret_cast<__bf16*>(stg);
+  __bf16* Bh = reinterpret_cast<__bf16*>(stg + off_b);
+  // operands -> [Mp][Kp] / [Np][Kp] (A: element (m, k) at A[m lda + k], or A[k lda + m] when transA; B: (n, k) at
+  // B[n ldb + k] when transB (the NT form), else B[k ldb + n])
+  auto stage_op = [&](const float* src, long ld, int R, int Rp, bool rowc, __bf16* dst) -> int {
+    if (rowc) {
+      hipLaunchKernelGGL(stage_rc_bf16, dim3(Rp / 64, Kp / 64), dim3(256), 0, st, src, ld, R, K, Kp, dst);
+    } else {
+      const long n8 = (long)Rp * Kp / 8;
+      const int vec = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) ? 1 : 0;
+      const unsigned blocks = (unsigned)std::min<long>(4096, (n8 + 255) / 256);
+      hipLaunchKernelGGL(stage_kc_bf16, dim3(blocks), dim3(256), 0, st, src, ld, R, K, Kp, n8, vec, dst);
+    }
+    S2S_CHECK_HIP(hipGetLastError());
+    return 0;
+  };
+  S2S_TRY(stage_op(q.A, q.lda, M, Mp, transA, Ah));
+  S2S_TRY(stage_op(q.B, q.ldb, N, Np, !transB, Bh));
+  BigGemm g{};
+  g.A = Ah;
+  g.B = Bh;
+  g.C = q.C;
+  g.bias = q.bias;
+  g.part = S > 1 ? reinterpret_cast<float*>(stg + off_p) : nullptr;
+  g.ldc = q.ldc;
+  g.M = M;
+  g.N = N;
+  g.Kp = Kp;
+  g.kslice = kslice;
+  g.tiles_m = tiles_m;
+  g.tiles_n = tiles_n;
+  g.S = S;
+  g.nblocks = tiles * S;
+  g.alpha = q.alpha;
+  g.beta = q.beta;
+  g.relu = q.relu;
+  {
+    ProfScope ps(st, "gemm_big_bf16", 2.0 * M * (double)N * K,
+                 4.0 * ((double)M * K + (double)K * N + (double)M * N * (q.beta != 0.f ? 2 : 1)));
+    if (large) S2S_TRY((launch_nt<kLarge, kLarge, 2, 4>(st, g)));
+    else S2S_TRY((launch_nt<kSmall, kSmall, 2, 2>(st, g)));
+  }
+  if (S > 1) {
+    const long mn = (long)M * N;
+    hipLaunchKernelGGL(bf16_splitk_reduce, dim3((unsigned)std::min<long>(2048, (mn + 255) / 256)), dim3(256), 0, st, g);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
+  *done = true;
+  ++g_big_calls;
+  return 0;
+}
+
+int gemm_large_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done) {
+  static const bool lt = [] {
+    const char* e = std::getenv("S2S_GEMM_LT");
+    return e && std::strcmp(e, "1") == 0;
+  }();
+  if (lt) return gemm_lt(st, q, transA, transB, ws, done);
+  return gemm_big_bf16(st, q, transA, transB, done);
+}
+
+}  // namespace s2s
+
+extern "C" void s2s_debug_gemm_big(int on) { s2s::g_gemm_big = on; }
+extern "C" long s2s_debug_gemm_big_calls() { return s2s::g_big_calls; }

@@ -718,15 +718,15 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
   }
   if (used == 0) return 0;
   const bool bf16 = gemm_precision() == kGemmBf16;
-  // large bf16 problems of the module-level entry points (front-end, attention decoder) on hipBLASLt (gemm_lt:
-  // it needs the calling context's staging buffer, which the model step does not provide) -- one call each,
-  // stream-ordered; the rest stay in one in-house launch
-  if (bf16 && gemm_lt_enabled()) {
+  // large bf16 problems of the module-level entry points (front-end, attention decoder) on the big-tile kernel
+  // (gemm_big_bf16: it needs the calling context's staging buffer, which the model step does not provide) -- one
+  // call each, stream-ordered; the rest stay in one launch of this file's kernels
+  if (bf16) {
     int keep = 0;
     for (int i = 0; i < used; ++i) {
       const GemmProblem& q = use[i];
       bool done = false;
-      if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_lt(st, q, transA, transB, ws, &done));
+      if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_large_bf16(st, q, transA, transB, ws, &done));
       if (!done) use[keep++] = q;
     }
     used = keep;

@@ -3,6 +3,13 @@
 
 namespace s2s {
 
+// GRU gate nonlinearities of the encoder kernels (per-step gru.hip and persistent gru_persist.hip, bitwise the
+// same in both): v_exp_f32 + v_rcp_f32 forms instead of expf / an IEEE divide / libm tanhf (~40 dependent
+// instructions per gate on the recurrences' critical path).  sigmoid: relative error ~1e-7 (x*log2e rounding,
+// 1-ulp exp and rcp), saturating to 0 / 1; tanh = 1 - 2 / (exp(2x) + 1): ~1e-7 absolute, saturating to +-1.
+__device__ __forceinline__ float gru_sigmoid(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
+__device__ __forceinline__ float gru_tanh(float x) { return 1.0f - 2.0f * __builtin_amdgcn_rcpf(__expf(2.0f * x) + 1.0f); }
+
 struct GruPackJobs;  // gru_persist.h
 
 // One GRU layer, 1 or 2 directions sharing the same input x (the bidirectional

@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void gru_fwd_p1(GruFwdArgs a) {
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= B) return;
   const long row = (long)b * L + t;
-  const float gate = sigmoidf_(s + g.xp[row * g.ldxp + n]);
+  const float gate = gru_sigmoid(s + g.xp[row * g.ldxp + n]);
   float* sv = g.sv + row * 5 * H;
   if (n < H) {
     sv[n] = gate;  // z
@@ -90,7 +90,7 @@ __global__ __launch_bounds__(256) void gru_fwd_p2(GruFwdArgs a) {
   const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
   if (b >= B) return;
   const long row = (long)b * L + t;
-  const float hh = tanhf(s + g.xp[row * g.ldxp + 2 * H + n]);
+  const float hh = gru_tanh(s + g.xp[row * g.ldxp + 2 * H + n]);
   float* sv = g.sv + row * 5 * H;
   const float z = sv[n], hp = sv[3 * H + n];
   sv[2 * H + n] = hh;

@@ -663,19 +663,21 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     }
     GRU_STAMP(6);
     float sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
-    if (aborted) return;
     GRU_STAMP(7);
     // this step's x-projections from the loader's ring (written before [A] of the previous step)
     const float xpv = xring[s % kRowRing][0][tid], xph = xring[s % kRowRing][1][tid];
+    // r tiles' h_{t-1} (parked before the reduce barrier), read by every thread so the load is issued with the
+    // reduce's reads instead of one more LDS round trip inside the r-tile epilogue
+    const float hpark = hprev[tid >> 4][tid & 15];
     {
-      const float gate = sigmoidf_(sum + xpv);
+      const float gate = gru_sigmoid(sum + xpv);
       float* sv = g.sv + row * 5 * H;
       if (isz) {
         if (live) sv[on] = gate;
         zreg = gate;
       } else {
         const int j = on - H;
-        const float hp = s > 0 ? hprev[tid >> 4][tid & 15] : 0.f;
+        const float hp = s > 0 ? hpark : 0.f;
         const float q = gate * hp;
         if (loc) {  // critical first
           if (live) put_sent(g.s1 + sent_slot(a, s) * slotS + tile_off(ob, j, H), q);
@@ -690,6 +692,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       }
     }
     GRU_STAMP(2);
+    if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
     if (!isz) continue;
     // ---- p2: hh = tanh(Uh q + xp_h); h = (1-z) h_{t-1} + z hh
     acc = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -709,9 +712,8 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       acc = mfma_chunks<NC>(av, w2);
     }
     sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
-    if (aborted) return;
     {
-      const float hh = tanhf(sum + xph);
+      const float hh = gru_tanh(sum + xph);
       const float hp = hreg;
       hreg = (-zreg + 1.0f) * hp + zreg * hh;
       if (t >= lenb) hreg = 0.f;
@@ -726,6 +728,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       }
     }
     GRU_STAMP(5);
+    if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
   }
 }
 
@@ -908,7 +911,6 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 #endif
     floatx4 acc = mfma_chunks<NC>(av, wh);
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
-    if (aborted) return;
     if (loc) {
       if (live) put_sent(g.s1 + sent_slot(a, p) * slotS + tile_off(ob, ok_, H), (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
     } else {
@@ -921,6 +923,7 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       dhp = dh * (-cur.z + 1.0f) + dq * cur.r;
     }
     GRU_STAMP(2);
+    if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
     // ---- p2: dh_{t-1} = dhp + Uzr^T [da_z; da_r]; gate gradients of step t-1
     const int tn = g.reverse ? t + 1 : t - 1;
     float4 azr[2 * NC];
@@ -950,12 +953,12 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     }
     acc = mfma_chunks<2 * NC>(azr, wzr);
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
-    if (aborted) return;
     const Row nxt = s > 0 ? load_row(p + 1) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     if (live && s > 0) dhc = tn < lenb ? dhp + sm : 0.f;
     if (s > 0) gate(tn, nxt, nxt.dy + dhc, p + 1, live);
     cur = nxt;
     GRU_STAMP(5);
+    if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
   }
 }
 

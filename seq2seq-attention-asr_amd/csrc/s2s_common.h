@@ -142,6 +142,14 @@ struct LtStage {
 };
 void set_lt_stage(LtStage* s);  // the calling thread's current context's buffer (set at every C-ABI entry)
 void lt_stage_free(LtStage* s);
+void* stage_acquire(hipStream_t st, size_t bytes);  // that buffer with >= bytes (nullptr: none, or capturing)
+// One large problem on the in-house bf16 GEMM (gemm_bf16.hip: operands staged to bf16 in the context's staging
+// buffer, 256 x 256 / 128 x 128 MFMA tiles, LDS-DMA staging, split-K slabs).  *done = false (nothing launched)
+// when it does not apply (rbias / Mread / Nread, no staging buffer, disabled by s2s_debug_gemm_big(0)).
+bool gemm_big_enabled();
+int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, bool* done);
+// the module-level large bf16 product: gemm_big_bf16, or hipBLASLt (gemm_lt) when S2S_GEMM_LT=1 (A/B only)
+int gemm_large_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done);
 bool gemm_lt_enabled();
 int gemm_lt(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done);
 // Implicit-GEMM SpatialConvolutionMM on bf16 MFMA (conv_bf16.inc): no im2col panel.  Forward y (B, Cout, Ho,

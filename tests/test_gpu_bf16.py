@@ -57,6 +57,55 @@ def test_bf16_gemm_exact_on_rounded_operands(lib, tA, tB, M, N, K):
     assert np.abs(ref - exact).max() / np.abs(exact).max() > 1e-4
 
 
+def _big_run(lib):
+    fn = lib.lib.s2s_debug_gemm_big_run
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p] + [ctypes.c_int] * 5 + [ctypes.c_float, ctypes.c_void_p, ctypes.c_long,
+                   ctypes.c_void_p, ctypes.c_long, ctypes.c_float, ctypes.c_void_p, ctypes.c_long, ctypes.c_void_p,
+                   ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    return fn
+
+
+@pytest.mark.parametrize("tA,tB", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K,bias,relu,beta", [(2000, 4096, 96, True, True, 0.0),     # 256 x 256 tiles, ragged M and K
+                                                  (300, 200, 1030, False, False, 0.25),  # 128 x 128, split-K, ragged K
+                                                  (2048, 512, 8128, False, False, 1.0),  # weight-gradient shape, split-K
+                                                  (77, 45, 133, True, False, 0.5)])      # tiny, every edge ragged
+def test_big_bf16_gemm_exact_on_rounded_operands(lib, tA, tB, M, N, K, bias, relu, beta):
+    """The big-tile bf16 GEMM (gemm_bf16.hip: operands staged to K-contiguous bf16, 256 x 256 / 128 x 128 MFMA
+    tiles fed by LDS-DMA, split-K slabs summed in order): every transpose form, ragged M / N / K, split-K, bias /
+    beta / ReLU epilogue, against the float64 product of the RNE-bf16-rounded operands (<= 2e-5 max|ref|), and
+    two runs are bitwise equal."""
+    import s2s_amd
+    rng = np.random.default_rng(M + N + K + 7 * tA + 3 * tB)
+    A = rng.standard_normal((K, M) if tA else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tB else (K, N)).astype(np.float32)
+    C0 = rng.standard_normal((M, N)).astype(np.float32)
+    bv = rng.standard_normal(N).astype(np.float32) if bias else None
+    Ag, Bg = torch.tensor(A, device="cuda"), torch.tensor(B, device="cuda")
+    bg = torch.tensor(bv, device="cuda") if bias else None
+    ctx = s2s_amd.nn.get_context(0)
+    fn = _big_run(lib)
+    outs = []
+    for _ in range(2):
+        Cg = torch.tensor(C0, device="cuda")
+        done = ctypes.c_int(0)
+        rc = fn(ctx.handle, s2s_amd.nn.stream_ptr(), tA, tB, M, N, K, 0.5, Ag.data_ptr(), A.shape[1], Bg.data_ptr(),
+                B.shape[1], beta, Cg.data_ptr(), N, bg.data_ptr() if bias else None, int(relu), ctypes.byref(done))
+        assert rc == 0 and done.value == 1
+        outs.append(Cg)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    Ar, Br = bf16_round(A), bf16_round(B)
+    ref = 0.5 * ((Ar.T if tA else Ar) @ (Br.T if tB else Br)) + beta * C0.astype(np.float64)
+    if bias:
+        ref = ref + bv.astype(np.float64)
+    if relu:
+        ref = np.maximum(ref, 0.0)
+    err = np.abs(outs[0].cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err <= 2e-5, err
+
+
 def _rel(a, r):
     """relative L2 error ||a - r|| / ||r||"""
     a = np.asarray(a, np.float64).ravel()
@@ -281,16 +330,16 @@ def test_bf16_conv_weight_gradient_exact_on_rounded_operands(lib, implicit, B, C
     assert err <= 2e-5, ("db", err)
 
 
-@pytest.mark.parametrize("lt", [1, 0])
+@pytest.mark.parametrize("big", [1, 0])
 @pytest.mark.parametrize("B,L,Din,Dout,relu", [(4, 508, 896, 2048, True), (3, 300, 2048, 512, False), (2, 50, 64, 40, True)])
-def test_bf16_linear_layer_exact_on_rounded_operands(lib, lt, B, L, Din, Dout, relu):
+def test_bf16_linear_layer_exact_on_rounded_operands(lib, big, B, L, Din, Dout, relu):
     """TemporalConvolution(Din, Dout, 1) (+ReLU) -- the VGG model's 1x1 layers and nn.Linear -- under bf16-all: one
-    GEMM over the B L rows, on hipBLASLt when large (HIPBLAS_COMPUTE_32F_FAST_16BF; lt=0 forces the in-house bf16
-    kernel).  Forward, input gradient and weight / bias gradients equal float64 products of the RNE-bf16-rounded
+    GEMM over the B L rows, on the big-tile bf16 kernel when large (gemm_bf16.hip; big=0 forces gemm_f32's 64 x 64
+    bf16 tiles).  Forward, input gradient and weight / bias gradients equal float64 products of the RNE-bf16-rounded
     operands up to fp32 accumulation order (<= 2e-5 of max|ref|), and two runs are bitwise equal."""
     import s2s_amd
     from s2s_amd import frontend as fe
-    knob = lib.lib.s2s_debug_gemm_lt
+    knob = lib.lib.s2s_debug_gemm_big
     knob.argtypes = [ctypes.c_int]
     rng = np.random.default_rng(B + L + Din)
     m = fe.TemporalConvolution(Din, Dout, 1, relu=relu)
@@ -300,12 +349,11 @@ def test_bf16_linear_layer_exact_on_rounded_operands(lib, lt, B, L, Din, Dout, r
     dy = rng.standard_normal((B, L, Dout)).astype(np.float32)
     m.weight, m.bias = torch.tensor(W, device="cuda"), torch.tensor(b, device="cuda")
     xg, dyg = torch.tensor(x, device="cuda"), torch.tensor(dy, device="cuda")
-    calls = lib.lib.s2s_debug_gemm_lt_calls
+    calls = lib.lib.s2s_debug_gemm_big_calls
     calls.restype = ctypes.c_long
-    last = lib.lib.s2s_debug_gemm_lt_last
     n0 = calls()
     outs = []
-    knob(lt)
+    knob(big)
     try:
         for _ in range(2):
             m.gradWeight, m.gradBias = torch.zeros_like(m.weight), torch.zeros_like(m.bias)
@@ -318,8 +366,8 @@ def test_bf16_linear_layer_exact_on_rounded_operands(lib, lt, B, L, Din, Dout, r
         knob(1)
     for a, c in zip(outs[0], outs[1]):
         assert torch.equal(a, c)
-    big = 2.0 * B * L * Din * Dout >= 1e9
-    assert (calls() - n0 == 6) == (bool(lt) and big), (calls() - n0, last())  # fwd, dx, dW per run
+    large = 2.0 * B * L * Din * Dout >= 1e9
+    assert (calls() - n0 == 6) == (bool(big) and large), calls() - n0  # fwd, dx, dW per run
     y, dx, gw, gb = (t.double().cpu().numpy() for t in outs[0])
     xr, Wr = bf16_round(x).reshape(B * L, Din), bf16_round(W)
     pre = xr @ Wr.T + b.astype(np.float64)
