@@ -808,6 +808,7 @@ int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
   S2S_TRY(fill_lstm_io(io, ndir, B, L, D, H, peepholes, reverse, x, ldx, W, y, ldy, saved));
   S2S_REQUIRE(y != nullptr, "lstm: null y");
   for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "lstm: null y");
+  io.status = ctx->status_dev;
   return lstm_layer_fwd(static_cast<hipStream_t>(stream), io, scratch, scratch_bytes);
 }
 
@@ -827,6 +828,7 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
       S2S_REQUIRE(dW[d * lstm_nparams(io.peep) + p], "lstm: null dW");
   }
   gr.lddy = lddy; gr.dx = dx; gr.lddx = lddx; gr.dx_accumulate = dx_accumulate; gr.dW = dW; gr.scale = scale;
+  io.status = ctx->status_dev;
   return lstm_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
 }
 

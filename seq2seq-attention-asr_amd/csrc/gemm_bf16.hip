@@ -35,29 +35,40 @@ thread_local LtStage* t_stage = nullptr;  // the calling context's staging buffe
 void set_lt_stage(LtStage* s) { t_stage = s; }
 void lt_stage_free(LtStage* s) {
   if (!s) return;
-  if (s->p) (void)hipFree(s->p);
+  for (int i = 0; i < LtStage::kStreams; ++i) {
+    if (s->p[i]) (void)hipFree(s->p[i]);
+    s->p[i] = s->s[i] = nullptr;
+    s->n[i] = 0;
+  }
   for (void* q : s->old) (void)hipFree(q);
-  s->p = nullptr;
-  s->n = 0;
   s->old.clear();
 }
 
 std::atomic<int> g_gemm_big{1};     // s2s_debug_gemm_big(0): these problems stay on gemm_f32's 64 x 64 bf16 tiles
 std::atomic<long> g_big_calls{0};   // big-GEMM calls launched (s2s_debug_gemm_big_calls)
 
-// the calling context's staging buffer with at least `bytes`, or nullptr (none, or too small while capturing)
+// the calling context's staging buffer for stream `st` with at least `bytes`, or nullptr (no context, more streams
+// than slots, or too small while capturing)
 void* stage_acquire(hipStream_t st, size_t bytes) {
   LtStage* s = t_stage;
   if (!s) return nullptr;
-  if (s->n >= bytes) return s->p;
+  int k = -1;
+  for (int i = 0; i < LtStage::kStreams && k < 0; ++i)
+    if (s->p[i] && s->s[i] == static_cast<void*>(st)) k = i;
+  if (k >= 0 && s->n[k] >= bytes) return s->p[k];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
+  if (k < 0)
+    for (int i = 0; i < LtStage::kStreams && k < 0; ++i)
+      if (!s->p[i]) k = i;
+  if (k < 0) return nullptr;
   void* p = nullptr;
-  const size_t want = std::max(bytes, s->n * 2);
+  const size_t want = std::max(bytes, s->n[k] * 2);
   if (hipMalloc(&p, want) != hipSuccess) return nullptr;
-  if (s->p) s->old.push_back(s->p);  // may still be read by queued work: freed with the context
-  s->p = p;
-  s->n = want;
+  if (s->p[k]) s->old.push_back(s->p[k]);
+  s->p[k] = p;
+  s->s[k] = static_cast<void*>(st);
+  s->n[k] = want;
   return p;
 }
 

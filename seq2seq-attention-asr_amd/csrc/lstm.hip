@@ -22,8 +22,6 @@ namespace s2s {
 
 namespace {
 
-enum { SV_I = 0, SV_F, SV_G, SV_O, SV_C, SV_CP, SV_HP, SV_TC, SV_N };
-
 struct LstmFwdDir {
   const float* xp;   // (B, L, ldxp): [i | f | g | o] x-projections + all biases
   long ldxp;
@@ -339,6 +337,7 @@ __global__ void bias_rows_kernel(float* C, long ldc, int rows, int cols, const f
 struct Carve {
   float *Wx4, *bias4, *xp, *dA, *Wb[2], *WocT[2], *dhc[2], *dcc[2], *dcp[2], *dcn[2];
   GemmWs ws;
+  void* sync;  // the persistent launches' hand-off region (lstm_persist_sync_bytes)
   size_t bytes;
 };
 Carve carve(void* scratch, int nd, int B, int L, int D, int H) {
@@ -357,6 +356,7 @@ Carve carve(void* scratch, int nd, int B, int L, int D, int H) {
     c.dcn[d] = bp.take<float>((long)B * H);
   }
   c.ws = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
+  c.sync = bp.take<char>(lstm_persist_sync_bytes(nd, B, L, H));
   c.bytes = bp.off + 256;
   return c;
 }
@@ -389,6 +389,19 @@ int lstm_layer_fwd(hipStream_t st, const LstmLayerIO& io, void* scratch, size_t 
   // xp (B*L, 4*nd*H) = bias4 + x Wx4^T  (GEMM bias epilogue)
   S2S_TRY(gemm1(st, false, true, B * L, 4 * nd * H, D, 1.f, io.x, io.ldx, c.Wx4, D, 0.f, c.xp, 4L * nd * H, c.bias4,
                 c.ws));
+  if (lstm_persist_supported(nd, B, H, io.peep)) {  // the whole sweep in one launch (lstm_persist.hip)
+    LstmPersistArgs f{};
+    f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 4L * nd * H; f.ldy = io.ldy;
+    for (int d = 0; d < nd; ++d) {
+      const float* const* W = io.W + d * np;
+      f.reverse[d] = io.reverse[d];
+      f.xp[d] = c.xp + 4L * d * H;
+      for (int q = 0; q < 4; ++q) f.Wh[d][q] = W[4 * q + 2];
+      f.y[d] = io.y[d];
+      f.sv[d] = io.saved[d];
+    }
+    return lstm_persist_fwd(st, f, c.sync, io.status);
+  }
   LstmFwdArgs a{};
   for (int d = 0; d < nd; ++d) {
     const float* const* W = io.W + d * np;
@@ -435,7 +448,18 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
   }
   a.B = B; a.L = L; a.H = H; a.peep = io.peep;
   const dim3 ge((B * H + 255) / 256, nd), gp(H / 16, (B + 15) / 16, nd), gb(2 * H / 16, (B + 15) / 16, nd);
-  {
+  if (lstm_persist_supported(nd, B, H, io.peep)) {  // the whole BPTT sweep in one launch (lstm_persist.hip)
+    LstmPersistArgs b{};
+    b.ndir = nd; b.B = B; b.L = L; b.H = H; b.lddy = gr.lddy; b.ldA = ldA;
+    for (int d = 0; d < nd; ++d) {
+      b.reverse[d] = io.reverse[d];
+      b.Wb[d] = c.Wb[d];
+      b.sv[d] = io.saved[d];
+      b.dy[d] = gr.dy[d];
+      b.dA[d] = c.dA + 4L * d * H;
+    }
+    S2S_TRY(lstm_persist_bwd(st, b, c.sync, io.status));
+  } else {
     ProfScope ps(st, "lstm_bwd_steps", 2.0 * nd * B * L * 4.0 * H * H * (io.peep ? 1.75 : 1.0), 0.0);
     const dim3 gs(H / 16, (B + 15) / 16, nd);
     for (int s = L - 1; s >= 0; --s) {

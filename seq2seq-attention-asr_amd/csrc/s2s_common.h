@@ -134,11 +134,15 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
 // the MFMA, fp32 accumulate and result; blaslt.cpp) -- the front-end's large plain GEMMs under the bf16 modes.
 // *done = false (nothing launched) when it does not apply (rbias / Mread / Nread, no algorithm, disabled by
 // s2s_debug_gemm_lt(0)); the caller then runs gemm_f32.
-// staging buffer for gemm_lt's bf16 operand copies, owned by a context (grown outside stream capture only)
+// staging buffers for the big bf16 GEMMs' operand copies, owned by a context (grown outside stream capture
+// only): one per stream, so calls the caller issues on different streams never share bytes (a buffer is
+// reused only in its own stream's order)
 struct LtStage {
-  void* p = nullptr;
-  size_t n = 0;
-  std::vector<void*> old;
+  static constexpr int kStreams = 8;
+  void* s[kStreams] = {};   // stream of each buffer
+  void* p[kStreams] = {};
+  size_t n[kStreams] = {};
+  std::vector<void*> old;   // outgrown buffers (queued work may still read them): freed with the context
 };
 void set_lt_stage(LtStage* s);  // the calling thread's current context's buffer (set at every C-ABI entry)
 void lt_stage_free(LtStage* s);

@@ -127,6 +127,59 @@ def test_lstm_layer_matches_oracle(s2s, B, L, D, H, bidir, peep):
     assert_rel(dx, dx_ref, "dx")
 
 
+@pytest.mark.parametrize("local", [1, 0])
+@pytest.mark.parametrize("B,L,D,H", [(32, 14, 256, 128), (5, 9, 40, 64), (20, 31, 64, 128)])
+def test_persistent_lstm_matches_oracle_and_per_step(s2s, monkeypatch, local, B, L, D, H):
+    """The persistent BiLSTM layer (lstm_persist.hip: the whole sweep of both directions in one launch, one
+    hand-off seam per step; XCD-local sentinel slots when local=1, tagged granules when 0) -- at the conv + BiLSTM
+    encoder's shape (timit/timit.lua:108-125: 256 conv maps in, 128 units per direction, 14 frames after the conv
+    stack) and two ragged ones -- against the oracle (1e-4) and bit for bit against the per-step launches
+    (S2S_LSTM_MODE=step: the same chunk order and partial sums), over repeated launches."""
+    import ctypes
+    from s2s_amd import _lib
+    knob = _lib.lib.s2s_debug_lstm_local
+    knob.argtypes = [ctypes.c_int]
+    rng = np.random.default_rng(B * 100 + L)
+    x = rng.standard_normal((B, L, D))
+    cells = [s2s.LSTM(D, H, peepholes=False) for _ in range(2)]
+    Ps = [{k: v.double().numpy() for k, v in c.named().items()} for c in cells]
+    dyn = rng.standard_normal((B, L, 2 * H))
+    outs = {}
+    knob(local)
+    try:
+        for mode in ("step", "persistent"):
+            monkeypatch.setenv("S2S_LSTM_MODE", mode)
+            mod = s2s.BiRNN(cells[0], cells[1]).cuda()
+            res = []
+            for rep in range(2):
+                y = mod.forward(cu(x)).clone()
+                mod.zeroGradParameters()
+                dx = mod.backward(cu(x), cu(dyn), 0.5).clone()
+                res.append((y, dx, [g.clone() for c in cells for g in c.named(grads=True).values()]))
+            torch.cuda.synchronize()
+            outs[mode] = res
+    finally:
+        knob(1)
+    for rep in range(2):
+        a, b = outs["step"][rep], outs["persistent"][rep]
+        assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), rep
+        for i, (ga, gb) in enumerate(zip(a[2], b[2])):
+            assert torch.equal(ga, gb), (rep, i)
+    y, dx, grads = outs["persistent"][0]
+    y, dx = y.cpu().numpy(), dx.cpu().numpy()
+    dx_ref = np.zeros_like(x)
+    gi = 0
+    for i, (P, rev) in enumerate(zip(Ps, (False, True))):
+        yr, sv = orc.lstm_seq_fwd(x, P, rev, False)
+        assert_rel(y[:, :, i * H:(i + 1) * H], yr, f"y[{i}]")
+        G = {k: np.zeros_like(v) for k, v in P.items()}
+        dx_ref += orc.lstm_seq_bwd(x, P, sv, dyn[:, :, i * H:(i + 1) * H], G, rev, False, 0.5)
+        for k in cells[i].named(grads=True):
+            assert_rel(grads[gi].cpu().numpy(), G[k], f"d{k}[{i}]")
+            gi += 1
+    assert_rel(dx, dx_ref, "dx")
+
+
 # --------------------------------------------------------------------------- attention decoder
 
 ATT_CASES = [

@@ -8,12 +8,12 @@ cmd=$1; shift
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 for f in "$@"; do rm -f "gpurun_out/$f"; done
-for attempt in 1 2 3; do
+for attempt in $(seq ${GPU_TRIES:-3}); do
   out=$(/usr/local/graft/bin/gpurun --timeout "$limit" -- "$cmd" 2>&1)
   rc=$?
   echo "$out" | grep -E "^\[gpurun\] (status|GPU-minutes)"
   if echo "$out" | grep -q "status=transient"; then
-    sleep 60
+    sleep ${GPU_WAIT:-60}
     continue
   fi
   exit $rc
