@@ -1345,8 +1345,8 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
   s2s::set_gemm_precision(s2s::kGemmF32);
   return rc;
 }
-// test / bench entry: one problem straight on the big-tile bf16 GEMM (gemm_bf16.hip) with the context's staging
-// buffer; *done = 0 when the kernel declined it (nothing launched)
+// test / bench entry: one problem straight on the big-tile bf16 GEMM (gemm_bf16.hip; hipBLASLt under S2S_GEMM_LT=1, for
+// A/B runs) with the context's staging buffer; *done = 0 when the kernel declined it (nothing launched)
 extern "C" int s2s_debug_gemm_big_run(s2s_ctx* ctx, s2s_stream_t stream, int transA, int transB, int M, int N, int K,
                                       float alpha, const float* A, long lda, const float* B, long ldb, float beta,
                                       float* C, long ldc, const float* bias, int relu, int* done) {
@@ -1355,7 +1355,7 @@ extern "C" int s2s_debug_gemm_big_run(s2s_ctx* ctx, s2s_stream_t stream, int tra
   s2s::GemmProblem q{A, B, C, bias, lda, ldb, ldc, M, N, K, alpha, beta};
   q.relu = relu;
   bool d = false;
-  const int rc = s2s::gemm_big_bf16(static_cast<hipStream_t>(stream), q, transA != 0, transB != 0, &d);
+  const int rc = s2s::gemm_large_bf16(static_cast<hipStream_t>(stream), q, transA != 0, transB != 0, s2s::GemmWs{}, &d);
   *done = d ? 1 : 0;
   return rc;
 }

@@ -4,9 +4,10 @@
 // Attention.lua:43-47).  Replaces the vendor library for these shapes.
 //
 // Row-major C (M x N) = alpha op(A) op(B) (+ bias[n]) (+ beta C) (ReLU) -- the GemmProblem contract.
-//  1. Staging: each fp32 operand is rounded to bf16 (RNE) into a K-contiguous, zero-padded copy [Rp][Kp] in the
-//     calling context's staging buffer (one pass; a transposed operand goes through a 64 x 64 LDS tile), so the
-//     main loop reads one layout with no guards: A' [Mp][Kp], B' [Np][Kp], C = A' B'^T.
+//  1. Staging: each fp32 operand is rounded to bf16 (RNE) into a K-contiguous copy [R][Kp] (K zero-padded to the
+//     K-tile) in the calling context's staging buffer (one pass; a transposed operand goes through a 64 x 64 LDS
+//     tile), so the main loop reads one layout with no guards: A' [M][Kp], B' [N][Kp], C = A' B'^T; tile rows past
+//     M / N read the last row and are never stored.
 //  2. gemm_bf16_nt: a BM x BN x 64 tile per workgroup, waves WM x WN, each a (BM/WM) x (BN/WN) block of
 //     v_mfma_f32_16x16x32_bf16 accumulators.  K-tiles are staged global -> LDS by global_load_lds_dwordx4
 //     (LDS-DMA, no register pass), two LDS stages: the next tile's DMA is issued before the current tile's
@@ -23,6 +24,8 @@
 // (tests/test_gpu_bf16.py), like the other bf16 kernels of the library.
 #include <algorithm>
 #include <atomic>
+#include <cmath>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 
@@ -80,7 +83,8 @@ typedef __attribute__((address_space(1))) const void* glb_void_t;
 
 constexpr int kBK = 64;  // K-tile (bf16): 128-byte LDS rows
 
-// ---- staging: logical operand (R x K), element (r, k) at src[r * ld + k] -> dst [Rp][Kp] bf16, zero padded.
+// ---- staging: logical operand (R x K), element (r, k) at src[r * ld + k] -> dst [R][Kp] bf16, K zero padded (rows
+// are not padded: the GEMM's DMA reads row R - 1 for tile rows past R, and never stores them).
 // One thread per 8 consecutive k of a row: two float4 loads, one 16-byte store.
 __global__ __launch_bounds__(256) void stage_kc_bf16(const float* __restrict__ src, long ld, int R, int K, int Kp,
                                                      long n8, int vec, __bf16* __restrict__ dst) {
@@ -112,7 +116,7 @@ __global__ __launch_bounds__(256) void stage_kc_bf16(const float* __restrict__ s
   }
 }
 
-// transposed operand: element (r, k) at src[k * ld + r] (row-contiguous along r) -> dst [Rp][Kp]; one 64 (r) x 64 (k)
+// transposed operand: element (r, k) at src[k * ld + r] (row-contiguous along r) -> dst [R][Kp]; one 64 (r) x 64 (k)
 // tile per workgroup through LDS (coalesced reads along r, 16-byte writes along k)
 __global__ __launch_bounds__(256) void stage_rc_bf16(const float* __restrict__ src, long ld, int R, int K, int Kp,
                                                      __bf16* __restrict__ dst) {
@@ -129,14 +133,14 @@ __global__ __launch_bounds__(256) void stage_rc_bf16(const float* __restrict__ s
     bf16x8 v;
 #pragma unroll
     for (int j = 0; j < 8; ++j) v[j] = (__bf16)t[kc + j][r];
-    *reinterpret_cast<bf16x8*>(dst + (long)(r0 + r) * Kp + k0 + kc) = v;
+    if (r0 + r < R) *reinterpret_cast<bf16x8*>(dst + (long)(r0 + r) * Kp + k0 + kc) = v;
   }
 }
 
 // ---- the GEMM
 struct BigGemm {
-  const __bf16* A;  // [Mp][Kp]
-  const __bf16* B;  // [Np][Kp]
+  const __bf16* A;  // [M][Kp]
+  const __bf16* B;  // [N][Kp]
   float* C;
   const float* bias;
   float* part;      // split-K slabs [S][M][N] or nullptr
@@ -178,13 +182,13 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(BigGemm g) {
   const __bf16* bsrc[GB];
 #pragma unroll
   for (int j = 0; j < GA; ++j) {
-    const int row = 8 * (wave + NW * j) + (lane >> 3);
-    asrc[j] = g.A + (long)(m0 + row) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    const int row = 8 * (wave + NW * j) + (lane >> 3);  // rows past M read row M - 1 (never stored)
+    asrc[j] = g.A + (long)min(m0 + row, g.M - 1) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
   }
 #pragma unroll
   for (int j = 0; j < GB; ++j) {
     const int row = 8 * (wave + NW * j) + (lane >> 3);
-    bsrc[j] = g.B + (long)(n0 + row) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
+    bsrc[j] = g.B + (long)min(n0 + row, g.N - 1) * g.Kp + (long)kt0 * kBK + 8 * ((lane & 7) ^ ((row >> 1) & 7));
   }
   auto stage = [&](int kt, int buf) {
     char* base = smem + buf * STAGE;
@@ -268,14 +272,14 @@ __global__ __launch_bounds__(WM * WN * 64) void gemm_bf16_nt(BigGemm g) {
 __global__ __launch_bounds__(256) void bf16_splitk_reduce(BigGemm g) {
   const long mn = (long)g.M * g.N;
   for (long e = blockIdx.x * 256L + threadIdx.x; e < mn; e += (long)gridDim.x * 256) {
-    float v[8];
+    float v[16];
     float sum = 0.f;
     int s = 0;
-    for (; s + 8 <= g.S; s += 8) {  // eight slabs' loads in flight, summed in order
+    for (; s + 16 <= g.S; s += 16) {  // sixteen slabs' loads in flight, summed in order
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = g.part[(s + j) * mn + e];
+      for (int j = 0; j < 16; ++j) v[j] = g.part[(s + j) * mn + e];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) sum += v[j];
+      for (int j = 0; j < 16; ++j) sum += v[j];
     }
     for (; s < g.S; ++s) sum += g.part[s * mn + e];
     const long row = e / g.N;
@@ -289,8 +293,6 @@ __global__ __launch_bounds__(256) void bf16_splitk_reduce(BigGemm g) {
   }
 }
 
-constexpr int kSmall = 128;  // 128 x 128 tiles, 4 waves (2 x 2)
-constexpr int kLarge = 256;  // 256 x 256 tiles, 8 waves (2 x 4)
 
 template <int BM, int BN, int WM, int WN>
 int launch_nt(hipStream_t st, const BigGemm& g) {
@@ -313,32 +315,48 @@ bool gemm_big_enabled() { return g_gemm_big != 0; }
 int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, bool* done) {
   *done = false;
   if (!g_gemm_big || !t_stage || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
+  static const bool trace = std::getenv("S2S_GEMM_TRACE") != nullptr;  // diagnostic: the shapes of a workload
+  if (trace)
+    std::fprintf(stderr, "[s2s gemm_big] M %d N %d K %d tA %d tB %d beta %g bias %d relu %d\n", q.M, q.N, q.K,
+                 (int)transA, (int)transB, (double)q.beta, q.bias ? 1 : 0, q.relu);
   const int M = q.M, N = q.N, K = q.K, Kp = (K + kBK - 1) / kBK * kBK, nkt = Kp / kBK;
-  // tile: 256 x 256 when that still gives >= 128 output tiles, else 128 x 128
-  const long t256 = (long)((M + kLarge - 1) / kLarge) * ((N + kLarge - 1) / kLarge);
-  const bool large = t256 >= 128;
-  const int BM = large ? kLarge : kSmall, BN = BM;
+  // Tile and split-K from a time model: per-CU rates of the three tiles (measured on MI355X, tools/gemm_big_bench.py:
+  // 256 x 256 ~3.9, 256 x 128 ~2.9, 128 x 128 ~1.6 TFLOP/s per CU at one workgroup per CU -- the 128 x 128 tile is
+  // bound by its 64 B/clk of staged operands), whole waves of 256 workgroups, and a split's slab round trip (write +
+  // read of S M N floats at ~5 TB/s) plus the reduce launch.
+  struct Cand { int bm, bn; double rate; };
+  const Cand cands[3] = {{256, 256, 3.9e12}, {256, 128, 2.9e12}, {128, 128, 1.6e12}};
+  double best = 1e30;
+  int BM = 128, BN = 128, S = 1;
+  for (const Cand& c : cands) {
+    const long tl = (long)((M + c.bm - 1) / c.bm) * ((N + c.bn - 1) / c.bn);
+    for (int s = 1; s <= 256; s *= 2) {  // (the first VGG layer's 64 x 27 weight gradient: K = 621k pixels)
+      if (s > 1 && nkt / s < 4) break;  // >= 4 K-tiles per slice
+      const int ks = (nkt + s - 1) / s;
+      const long blocks = tl * ((nkt + ks - 1) / ks);
+      const double waves = std::ceil(blocks / 256.0);
+      double t = waves * 2.0 * c.bm * c.bn * (double)ks * kBK / c.rate;
+      if (s > 1) t += 2.0 * s * (double)M * N * 4.0 / 5e12 + 3e-6;
+      if (t < best * 0.98) { best = t; BM = c.bm; BN = c.bn; S = s; }
+    }
+  }
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN, tiles = tiles_m * tiles_n;
-  // split-K until the grid covers the chip (>= 256 workgroups), keeping >= 8 K-tiles per slice
-  int S = 1;
-  while (tiles * S < 256 && nkt / (2 * S) >= 8 && S < 16) S *= 2;
   const int kslice = (nkt + S - 1) / S;
   S = (nkt + kslice - 1) / kslice;
-  const int Mp = tiles_m * BM, Np = tiles_n * BN;
-  const size_t abytes = (size_t)Mp * Kp * 2, bbytes = (size_t)Np * Kp * 2;
+  const size_t abytes = (size_t)M * Kp * 2, bbytes = (size_t)N * Kp * 2;
   const size_t slab = S > 1 ? sizeof(float) * (size_t)S * M * N : 0;
   const size_t off_b = (abytes + 255) / 256 * 256, off_p = off_b + (bbytes + 255) / 256 * 256;
   char* stg = static_cast<char*>(stage_acquire(st, off_p + slab));
   if (!stg) return 0;
   __bf16* Ah = reinterpret_cast<__bf16*>(stg);
   __bf16* Bh = reinterpret_cast<__bf16*>(stg + off_b);
-  // operands -> [Mp][Kp] / [Np][Kp] (A: element (m, k) at A[m lda + k], or A[k lda + m] when transA; B: (n, k) at
+  // operands -> [M][Kp] / [N][Kp] (A: element (m, k) at A[m lda + k], or A[k lda + m] when transA; B: (n, k) at
   // B[n ldb + k] when transB (the NT form), else B[k ldb + n])
-  auto stage_op = [&](const float* src, long ld, int R, int Rp, bool rowc, __bf16* dst) -> int {
+  auto stage_op = [&](const float* src, long ld, int R, bool rowc, __bf16* dst) -> int {
     if (rowc) {
-      hipLaunchKernelGGL(stage_rc_bf16, dim3(Rp / 64, Kp / 64), dim3(256), 0, st, src, ld, R, K, Kp, dst);
+      hipLaunchKernelGGL(stage_rc_bf16, dim3((R + 63) / 64, Kp / 64), dim3(256), 0, st, src, ld, R, K, Kp, dst);
     } else {
-      const long n8 = (long)Rp * Kp / 8;
+      const long n8 = (long)R * Kp / 8;
       const int vec = (ld % 4 == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0) ? 1 : 0;
       const unsigned blocks = (unsigned)std::min<long>(4096, (n8 + 255) / 256);
       hipLaunchKernelGGL(stage_kc_bf16, dim3(blocks), dim3(256), 0, st, src, ld, R, K, Kp, n8, vec, dst);
@@ -346,8 +364,8 @@ int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB
     S2S_CHECK_HIP(hipGetLastError());
     return 0;
   };
-  S2S_TRY(stage_op(q.A, q.lda, M, Mp, transA, Ah));
-  S2S_TRY(stage_op(q.B, q.ldb, N, Np, !transB, Bh));
+  S2S_TRY(stage_op(q.A, q.lda, M, transA, Ah));
+  S2S_TRY(stage_op(q.B, q.ldb, N, !transB, Bh));
   BigGemm g{};
   g.A = Ah;
   g.B = Bh;
@@ -369,8 +387,9 @@ int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB
   {
     ProfScope ps(st, "gemm_big_bf16", 2.0 * M * (double)N * K,
                  4.0 * ((double)M * K + (double)K * N + (double)M * N * (q.beta != 0.f ? 2 : 1)));
-    if (large) S2S_TRY((launch_nt<kLarge, kLarge, 2, 4>(st, g)));
-    else S2S_TRY((launch_nt<kSmall, kSmall, 2, 2>(st, g)));
+    if (BM == 256 && BN == 256) S2S_TRY((launch_nt<256, 256, 2, 4>(st, g)));
+    else if (BM == 256) S2S_TRY((launch_nt<256, 128, 4, 2>(st, g)));
+    else S2S_TRY((launch_nt<128, 128, 2, 2>(st, g)));
   }
   if (S > 1) {
     const long mn = (long)M * N;

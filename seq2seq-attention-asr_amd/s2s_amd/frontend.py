@@ -432,13 +432,16 @@ class GraphStep:
         graphs = self.__dict__.setdefault("_graphs", {})
         g = graphs.get(key)
         if g is None:
-            self.zeroGradParameters()
-            self.step(x, labels, scale, normalizeNLL)
+            # the eager step runs on the capture stream: the library's lazily grown per-stream buffers (the big
+            # bf16 GEMMs' staging copies) are sized for THAT stream before the capture, which cannot allocate them
             cur = torch.cuda.current_stream(x.device)
-            cur.synchronize()
-            graph = torch.cuda.CUDAGraph()
             side = torch.cuda.Stream(x.device)
             side.wait_stream(cur)
+            with torch.cuda.stream(side):
+                self.zeroGradParameters()
+                self.step(x, labels, scale, normalizeNLL)
+            side.synchronize()
+            graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(graph, stream=side, capture_error_mode="thread_local"):
                 self.zeroGradParameters()
                 out = self.step(x, labels, scale, normalizeNLL)

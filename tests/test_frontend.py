@@ -599,6 +599,42 @@ def test_vgg_graph_step_equals_eager(fe, prec):
 
 
 @pytest.mark.gpu
+def test_vgg_graph_step_keeps_big_gemm_path(fe):
+    """At full width (1x1 layers 2048) the VGG model's big products run on the big-tile bf16 GEMM (gemm_bf16.hip),
+    whose staging buffer is per stream and cannot be allocated inside a capture: graph_step's eager warm-up runs on
+    the capture stream, so the captured step takes the same kernels as the eager one (same number of big-GEMM
+    calls) and the replay is bitwise the eager step."""
+    import ctypes
+    import s2s_amd
+    from s2s_amd import _lib
+    calls = _lib.lib.s2s_debug_gemm_big_calls
+    calls.restype = ctypes.c_long
+    rng = np.random.default_rng(14)
+    B, L, Fq, T, O = 2, 256, 40, 20, 29
+
+    def make():
+        return s2s_amd.VGGAttentionModel(Fq, outputFrameSize=512, hidden=2048, outputDepth=O,
+                                         generator=torch.Generator().manual_seed(4), precision="bf16-all").cuda()
+
+    eager, graphed = make(), make()
+    x = cu(rng.standard_normal((B, 3, L, Fq)))
+    labels = cu(np.append(rng.integers(0, O - 1, (B, T - 1)), np.full((B, 1), O - 1), axis=1), torch.int32)
+    n0 = calls()
+    eager.zeroGradParameters()
+    nll_e, logp_e = eager.step(x, labels)
+    torch.cuda.synchronize()
+    per_step = calls() - n0
+    assert per_step > 0
+    n1 = calls()
+    nll_g, logp_g = graphed.graph_step(x.clone(), labels.clone())  # eager warm-up + capture (+ replay)
+    torch.cuda.synchronize()
+    assert calls() - n1 == 2 * per_step, (calls() - n1, per_step)
+    assert torch.equal(logp_e, logp_g) and torch.equal(nll_e, nll_g)
+    for i, (ge, gg) in enumerate(zip(eager.parameters()[1], graphed.parameters()[1])):
+        assert torch.equal(ge, gg), i
+
+
+@pytest.mark.gpu
 def test_conv_bilstm_graph_step_equals_eager(fe):
     """ConvBiLSTMAttentionModel.graph_step (timit/timit.lua:106-145: LSTM decoder, hybrid attention, per-step
     decoder kernels) is bitwise the eager zeroGradParameters() + step(), also with new data in the captured

@@ -70,7 +70,7 @@ def _big_run(lib):
 @pytest.mark.parametrize("M,N,K,bias,relu,beta", [(2000, 4096, 96, True, True, 0.0),     # 256 x 256 tiles, ragged M and K
                                                   (300, 200, 1030, False, False, 0.25),  # 128 x 128, split-K, ragged K
                                                   (2048, 512, 8128, False, False, 1.0),  # weight-gradient shape, split-K
-                                                  (77, 45, 133, True, False, 0.5)])      # tiny, every edge ragged
+                                                  (77, 70, 133, True, False, 0.5)])      # small, every edge ragged
 def test_big_bf16_gemm_exact_on_rounded_operands(lib, tA, tB, M, N, K, bias, relu, beta):
     """The big-tile bf16 GEMM (gemm_bf16.hip: operands staged to K-contiguous bf16, 256 x 256 / 128 x 128 MFMA
     tiles fed by LDS-DMA, split-K slabs summed in order): every transpose form, ragged M / N / K, split-K, bias /
@@ -103,6 +103,28 @@ def test_big_bf16_gemm_exact_on_rounded_operands(lib, tA, tB, M, N, K, bias, rel
     if relu:
         ref = np.maximum(ref, 0.0)
     err = np.abs(outs[0].cpu().numpy() - ref).max() / np.abs(ref).max()
+    assert err <= 2e-5, err
+
+
+@pytest.mark.parametrize("tA,tB", [(0, 1), (1, 0)])
+def test_big_bf16_gemm_narrow_output_deep_split(lib, tA, tB):
+    """The first VGG layer's weight gradient shape (64 x 27 outputs over ~600k pixels): one 128 x 128 tile split over
+    up to 256 K-slices, the slabs summed in slice order -- exact on the bf16-rounded operands (<= 2e-5 max|ref|)."""
+    import s2s_amd
+    rng = np.random.default_rng(27 + tA)
+    M, N, K = 64, 27, 200000
+    A = rng.standard_normal((K, M) if tA else (M, K)).astype(np.float32)
+    B = rng.standard_normal((N, K) if tB else (K, N)).astype(np.float32)
+    Ag, Bg = torch.tensor(A, device="cuda"), torch.tensor(B, device="cuda")
+    C = torch.zeros(M, N, device="cuda")
+    done = ctypes.c_int(0)
+    rc = _big_run(lib)(s2s_amd.nn.get_context(0).handle, s2s_amd.nn.stream_ptr(), tA, tB, M, N, K, 1.0, Ag.data_ptr(),
+                       A.shape[1], Bg.data_ptr(), B.shape[1], 0.0, C.data_ptr(), N, None, 0, ctypes.byref(done))
+    torch.cuda.synchronize()
+    assert rc == 0 and done.value == 1
+    Ar, Br = bf16_round(A), bf16_round(B)
+    ref = (Ar.T if tA else Ar) @ (Br.T if tB else Br)
+    err = np.abs(C.cpu().numpy() - ref).max() / np.abs(ref).max()
     assert err <= 2e-5, err
 
 

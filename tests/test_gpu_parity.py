@@ -144,22 +144,30 @@ def test_persistent_lstm_matches_oracle_and_per_step(s2s, monkeypatch, local, B,
     cells = [s2s.LSTM(D, H, peepholes=False) for _ in range(2)]
     Ps = [{k: v.double().numpy() for k, v in c.named().items()} for c in cells]
     dyn = rng.standard_normal((B, L, 2 * H))
-    outs = {}
+    from s2s_amd import profile as prof
+    outs, ran = {}, {}
     knob(local)
     try:
         for mode in ("step", "persistent"):
             monkeypatch.setenv("S2S_LSTM_MODE", mode)
             mod = s2s.BiRNN(cells[0], cells[1]).cuda()
             res = []
+            _lib.check(_lib.lib.s2s_prof_enable(1))
+            prof.collect()
             for rep in range(2):
                 y = mod.forward(cu(x)).clone()
                 mod.zeroGradParameters()
                 dx = mod.backward(cu(x), cu(dyn), 0.5).clone()
                 res.append((y, dx, [g.clone() for c in cells for g in c.named(grads=True).values()]))
             torch.cuda.synchronize()
+            ran[mode] = prof.collect()
+            _lib.lib.s2s_prof_enable(0)
             outs[mode] = res
     finally:
+        _lib.lib.s2s_prof_enable(0)
         knob(1)
+    assert "lstm_fwd_persist" in ran["persistent"] and "lstm_bwd_persist" in ran["persistent"], sorted(ran["persistent"])
+    assert "lstm_fwd_steps" in ran["step"] and "lstm_fwd_persist" not in ran["step"], sorted(ran["step"])
     for rep in range(2):
         a, b = outs["step"][rep], outs["persistent"][rep]
         assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]), rep

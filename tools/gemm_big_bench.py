@@ -58,14 +58,24 @@ def layer(B, L, Din, Dout):
     return 3 * 2.0 * B * L * Din * Dout / t / 1e12, t * 1e6
 
 
+# the big bf16 products of one config-5 step (S2S_GEMM_TRACE=1 python bench.py --config librispeech_vgg_b16)
+STEP_SHAPES = [(8128, 2048, 2048, 0, 1, 2), (8128, 2048, 2048, 0, 0, 2), (2048, 2048, 8128, 1, 0, 2),
+               (8128, 896, 2048, 0, 0, 1), (8128, 512, 512, 0, 1, 1), (8128, 512, 512, 0, 0, 1),
+               (8128, 512, 2048, 0, 1, 1), (8128, 2048, 896, 0, 1, 1), (8128, 2048, 512, 0, 0, 1),
+               (512, 512, 8128, 1, 0, 1), (512, 2048, 8128, 1, 0, 1), (448, 768, 3200, 1, 0, 1),
+               (3200, 768, 448, 0, 0, 1), (3200, 768, 256, 0, 0, 1), (3200, 448, 768, 0, 1, 1),
+               (3200, 256, 768, 0, 0, 1), (2048, 896, 8128, 1, 0, 1)]
+
 if __name__ == "__main__":
     lt = os.environ.get("S2S_GEMM_LT") == "1"
+    tag = "hipBLASLt" if lt else "in-house"
+    total = 0.0
+    for M, N, K, tA, tB, n in STEP_SHAPES:
+        tf = direct(M, N, K, tA, tB)
+        us = 2.0 * M * N * K / (tf * 1e12) * 1e6
+        total += n * us
+        print(f"{tag:9s} M={M:5d} N={N:5d} K={K:5d} tA={tA} tB={tB} x{n}: {tf:7.1f} TFLOP/s {us:7.1f} us", flush=True)
+    print(f"{tag} step total {total:.1f} us", flush=True)
     if not lt:
-        for M, N, K, tA, tB in ((4096, 4096, 4096, 0, 1), (8192, 8192, 8192, 0, 1), (8128, 2048, 2048, 0, 1),
-                                (8128, 2048, 896, 0, 1), (8128, 2048, 2048, 0, 0), (2048, 2048, 8128, 1, 0),
-                                (8128, 512, 1024, 0, 1)):
-            print(f"direct  M={M:5d} N={N:5d} K={K:5d} tA={tA} tB={tB}: {direct(M, N, K, tA, tB):7.1f} TFLOP/s", flush=True)
-    for B, L, Din, Dout in ((16, 508, 896, 2048), (16, 508, 2048, 2048), (16, 508, 2048, 512)):
-        tf, us = layer(B, L, Din, Dout)
-        print(f"layer{' (hipBLASLt)' if lt else ''} B={B} L={L} {Din}->{Dout} fwd+bwd: {tf:7.1f} TFLOP/s {us:8.1f} us",
-              flush=True)
+        for M, N, K, tA, tB in ((4096, 4096, 4096, 0, 1), (8192, 8192, 8192, 0, 1)):
+            print(f"in-house  M={M:5d} N={N:5d} K={K:5d}: {direct(M, N, K, tA, tB):7.1f} TFLOP/s", flush=True)

@@ -44,9 +44,26 @@ def mfma_table(d):
         out.writerow([k, n, round(f), round(b), round(g), round(u, 4)])
 
 
+def all_counters(d):
+    """Every counter of one pass directory, averaged per dispatch, one row per kernel."""
+    names = set()
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            names.add(r.get("Counter_Name"))
+    tabs = {c: per_kernel(d, c) for c in sorted(n for n in names if n)}
+    kernels = sorted({k for t in tabs.values() for k in t})
+    out = csv.writer(sys.stdout)
+    out.writerow(["kernel", "dispatches"] + list(tabs))
+    for k in kernels:
+        n = max(t.get(k, [0, 0])[1] for t in tabs.values())
+        out.writerow([k, n] + [round(tabs[c][k][0] / tabs[c][k][1]) if k in tabs[c] else "" for c in tabs])
+
+
 def main():
     if sys.argv[1] == "--mfma":
         return mfma_table(sys.argv[2])
+    if sys.argv[1] == "--all":
+        return all_counters(sys.argv[2])
     d = sys.argv[1]
     f = per_kernel(os.path.join(d, "pmc_FETCH_SIZE"), "FETCH_SIZE")
     w = per_kernel(os.path.join(d, "pmc_WRITE_SIZE"), "WRITE_SIZE")
