@@ -252,7 +252,7 @@ def latency_floor(name, steps, avg_us):
 
 # live-timing family -> the kernel symbol rocprofv3 reports
 SYMBOL = {"dec_fwd_xcd": "dec_xcd_fwd", "dec_bwd_xcd": "dec_xcd_bwd"}
-SYMBOL_VGG = {"gemm_bf16": "gemm_bf16_kernel", "gemm_lt_bf16": "Cijk_", "conv_fwd_bf16": "conv_bf16_kernel<false",
+SYMBOL_VGG = {"gemm_bf16": "gemm_bf16_kernel", "gemm_big_bf16": "gemm_bf16_nt", "conv_fwd_bf16": "conv_bf16_kernel<false",
               "conv_dx_bf16": "conv_bf16_kernel<true", "conv_wgrad_bf16": "conv_wgrad_bf16_kernel"}
 
 
@@ -368,8 +368,8 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
         out["kernels"] = {k: {"launches_per_step": v["launches"] / 2, "us_per_step": round(v["total_us"] / 2, 1)}
                           for k, v in agg.items()}
         # the MFMA-bound families of the step (the decoder recurrences beside them are latency-bound): the
-        # in-house GEMM, the hipBLASLt GEMMs of the 1x1 layers and the implicit convolutions
-        fams = (("gemm_bf16", "gemm_lt_bf16", "conv_fwd_bf16", "conv_dx_bf16", "conv_wgrad_bf16") if bf16
+        # 64 x 64 tile GEMM, the big-tile GEMM of the 1x1 layers / decoder products and the implicit convolutions
+        fams = (("gemm_bf16", "gemm_big_bf16", "conv_fwd_bf16", "conv_dx_bf16", "conv_wgrad_bf16") if bf16
                 else ("gemm_f32",))
         peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
         rows = []

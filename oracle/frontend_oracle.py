@@ -82,6 +82,14 @@ def relu_bwd(x: Array, dy: Array) -> Array:
     return np.where(x > 0, dy, 0.0)
 
 
+def relu_gate(u: Array, mask: Optional[Array]):
+    """ReLU with an optionally adopted decision mask: -> (output, gate), relu_bwd(gate, dy) being the backward.
+    Without a mask the gate is u itself."""
+    if mask is None:
+        return np.maximum(u, 0.0), u
+    return np.where(mask, u, 0.0), np.where(mask, 1.0, -1.0)
+
+
 # ---------------------------------------------------------------- SpatialConvolutionMM (3p)
 
 def _im2col(x: Array, kH: int, kW: int) -> Array:
@@ -119,13 +127,15 @@ def sconv_bwd(x: Array, Wt: Array, dy: Array, kH: int, kW: int):
 
 # ---------------------------------------------------------------- SpatialMaxPooling (3p)
 
-def smaxpool_fwd(x: Array, kW: int, kH: int, dW: int, dH: int):
-    """x (B, C, H, W) -> y (B, C, Ho, Wo); idx = i*kW + j of the window's first maximum (scan i then j)."""
+def smaxpool_fwd(x: Array, kW: int, kH: int, dW: int, dH: int, idx: Optional[Array] = None):
+    """x (B, C, H, W) -> y (B, C, Ho, Wo); idx = i*kW + j of the window's first maximum (scan i then j).
+    A given idx (a decision adopted from the implementation under test) is used instead of the argmax."""
     B, C, H, W = x.shape
     Ho, Wo = (H - kH) // dH + 1, (W - kW) // dW + 1
     win = np.stack([x[:, :, i:i + (Ho - 1) * dH + 1:dH, j:j + (Wo - 1) * dW + 1:dW]
                     for i in range(kH) for j in range(kW)], axis=0)
-    idx = np.argmax(win, axis=0)
+    if idx is None:
+        idx = np.argmax(win, axis=0)
     y = np.take_along_axis(win, idx[None], axis=0)[0]
     return y, idx
 
@@ -201,18 +211,30 @@ def vgg_dims(F: int, hidden: int = 2048, out: int = 512):
     return [(128 * Hf, hidden), (hidden, hidden), (hidden, hidden), (hidden, out)]
 
 
-def vgg_fwd(x: Array, P: Dict[str, Array]):
-    """librispeech/model_vgg.lua:23-51 on x (B, 3, L, F) -> (B, (L-8)//2, out)."""
+def vgg_fwd(x: Array, P: Dict[str, Array], decide: Optional[dict] = None, raw: Optional[dict] = None):
+    """librispeech/model_vgg.lua:23-51 on x (B, 3, L, F) -> (B, (L-8)//2, out).
+    decide (tests only): the discrete decisions of an implementation under test, run instead of the oracle's own
+    -- {"conv": [ReLU mask per conv layer], "pool": {layer: SpatialMaxPooling idx}, "lin": [ReLU mask per 1x1
+    layer]}; raw (a dict, filled) then receives the oracle's own pre-activations and pool argmaxes under those
+    upstream decisions, for the caller to check that the two agree off the near-tie band."""
     cache = {"conv": [], "pool": {}, "lin": []}
+    if raw is not None:
+        raw.update({"conv": [], "pool": {}, "pool_in": {}, "lin": []})
+    dc = decide or {}
     h = x
     for l in range(4):
         u = sconv_fwd(h, P[f"vgg{l}.W"], P[f"vgg{l}.b"], 3, 3)
-        r = relu_fwd(u)
-        cache["conv"].append((h, u))
+        r, gate = relu_gate(u, dc["conv"][l] if "conv" in dc else None)
+        cache["conv"].append((h, gate))
+        if raw is not None:
+            raw["conv"].append(u)
         h = r
         if l in VGG_POOLS:
             kW, kH, dW, dH = VGG_POOLS[l]
-            p, idx = smaxpool_fwd(h, kW, kH, dW, dH)
+            if raw is not None:
+                raw["pool"][l] = smaxpool_fwd(h, kW, kH, dW, dH)[1]
+                raw["pool_in"][l] = h
+            p, idx = smaxpool_fwd(h, kW, kH, dW, dH, dc["pool"][l] if "pool" in dc else None)
             cache["pool"][l] = (idx, h.shape)
             h = p
     B, C, Lq, Hf = h.shape
@@ -220,8 +242,11 @@ def vgg_fwd(x: Array, P: Dict[str, Array]):
     h = h.transpose(0, 2, 1, 3).reshape(B, Lq, C * Hf)  # Transpose2({1,2},3) + View(-1, 128*H)
     for l in range(4):
         u = tconv_fwd(h, P[f"lin{l}.W"], P[f"lin{l}.b"], 1)
-        cache["lin"].append((h, u))
-        h = relu_fwd(u)
+        r, gate = relu_gate(u, dc["lin"][l] if "lin" in dc else None)
+        cache["lin"].append((h, gate))
+        if raw is not None:
+            raw["lin"].append(u)
+        h = r
     return h, cache
 
 
@@ -252,18 +277,23 @@ def vgg_bwd(P: Dict[str, Array], cache, dout: Array, G: Dict[str, Array], scale:
 
 # ---------------------------------------------------------------- decoder_mlp stacks (3p nn + Maxout.lua)
 
-def mlp_fwd(v: Array, layers):
+def mlp_fwd(v: Array, layers, maxout_idx=None, raw: Optional[list] = None):
     """A decoder_mlp Sequential on rows v (N, D): layers are ("maxout", W, b, window) (Maxout.lua:14-18:
     Linear + TemporalMaxPooling(window, window) over consecutive groups), ("linear", W, b), ("relu",),
-    ("logsoftmax",)."""
+    ("logsoftmax",).  maxout_idx (tests only): one adopted winner array (N, out) per Maxout layer, in order,
+    run instead of the argmax; raw (a list, filled) then receives each Maxout's pre-activations (N, out, window)."""
     cache = []
     h = v
+    mi = 0
     for L in layers:
         if L[0] == "maxout":
             _, W, b, k = L
             u = h @ W.T + b
             g = u.reshape(u.shape[0], -1, k)
-            am = np.argmax(g, axis=2)
+            if raw is not None:
+                raw.append(g)
+            am = np.argmax(g, axis=2) if maxout_idx is None else maxout_idx[mi]
+            mi += 1
             cache.append((h, am, u.shape))
             h = np.take_along_axis(g, am[..., None], axis=2)[..., 0]
         elif L[0] == "linear":
@@ -304,14 +334,17 @@ def mlp_bwd(layers, cache, dout: Array, grads, scale: float = 1.0) -> Array:
     return d
 
 
-def vgg_model_step(x: Array, labels: Array, P: Dict[str, Array], mlp_layers, cfg):
+def vgg_model_step(x: Array, labels: Array, P: Dict[str, Array], mlp_layers, cfg, decide: Optional[dict] = None,
+                   maxout_idx=None, raw: Optional[dict] = None):
     """librispeech/model_vgg.lua end to end + the trainer's loss seed (train.lua:139-165): VGG encoder,
     attention decoder (GRU recurrence) with the external decoder_mlp stack, nll = -sum onehot * logp,
     dlogp = -onehot, gradients summed over the batch then / B.  P holds the encoder (vgg*/lin*) and the
     decoder's own parameters; cfg an s2s_oracle.ModelConfig for the decoder dims.
+    decide / maxout_idx / raw (tests only): adopted decisions and the oracle's own pre-decision values, as in
+    vgg_fwd and mlp_fwd (raw["mlp"] holds the Maxout pre-activations).
     Returns (nll per utterance, logp, G encoder+decoder, mlp grads)."""
     B = x.shape[0]
-    h, ecache = vgg_fwd(x, P)
+    h, ecache = vgg_fwd(x, P, decide, raw)
     Pd = dict(P)
     S, A, M, k, O = cfg.stateDepth, cfg.annotationDepth, cfg.mlpDepth, cfg.maxoutWindow, cfg.outputDepth
     for name, shp in (("Wm", (M * k, S + A)), ("bm", (M * k,)), ("Wo", (O, M)), ("bo", (O,))):
@@ -319,7 +352,8 @@ def vgg_model_step(x: Array, labels: Array, P: Dict[str, Array], mlp_layers, cfg
     _, acache = orc.attention_fwd(h, labels, Pd, cfg)
     T = labels.shape[1]
     v = acache["v"].reshape(B * T, -1)
-    logp, mcache = mlp_fwd(v, mlp_layers)
+    mraw = raw.setdefault("mlp", []) if raw is not None else None
+    logp, mcache = mlp_fwd(v, mlp_layers, maxout_idx, mraw)
     logp = logp.reshape(B, T, O)
     onehot = np.zeros_like(logp)
     np.put_along_axis(onehot, labels[..., None].astype(np.int64), 1.0, axis=2)

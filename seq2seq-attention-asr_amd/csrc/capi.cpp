@@ -118,7 +118,7 @@ struct s2s_ctx {
   // it without a device sync; s2s_ctx_status reads it after a stream sync and clears it
   unsigned* status_host = nullptr;
   unsigned* status_dev = nullptr;
-  s2s::LtStage lt;  // bf16 operand copies of the hipBLASLt GEMMs (blaslt.cpp)
+  s2s::GemmStage lt;  // bf16 operand copies of the big bf16 GEMMs (gemm_bf16.hip), one buffer per stream
 };
 
 namespace {
@@ -139,7 +139,7 @@ int set_device(s2s_ctx* ctx) {
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
   set_gemm_precision(ctx->precision == S2S_PREC_FP32 ? kGemmF32 : kGemmBf16);
   set_wgrad_bf16(ctx->precision == S2S_PREC_BF16_ALL);
-  set_lt_stage(&ctx->lt);
+  set_gemm_stage(&ctx->lt);
   return 0;
 }
 
@@ -673,7 +673,7 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   for (auto& g : ctx->graphs) (void)drop_graph(ctx, g);
   ctx->graphs.clear();
   if (ctx->seed_dev) (void)hipFree(ctx->seed_dev);
-  s2s::lt_stage_free(&ctx->lt);
+  s2s::gemm_stage_free(&ctx->lt);
   if (ctx->comm) (void)ncclCommDestroy(ctx->comm);
   for (auto& e : ctx->ev)
     if (e) (void)hipEventDestroy(e);
@@ -1122,9 +1122,9 @@ int s2s_model_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_model_dims* d, c
                    const float* x, const int* labels, float scale, int flags, float* logp, float* nll,
                    void* workspace, size_t workspace_bytes) {
   S2S_TRY(set_device(ctx));
-  // the model step keeps its GEMMs in-house: it is captured into a HIP graph at its first call (graph mode), where
-  // hipBLASLt's plan creation and first kernel loads would happen inside the capture
-  set_lt_stage(nullptr);
+  // the model step keeps its GEMMs on gemm_f32's tiles: it is captured into a HIP graph at its first call (graph
+  // mode), where the big GEMM's staging buffer could not be grown
+  set_gemm_stage(nullptr);
   S2S_TRY(check_model_dims(d));
   S2S_REQUIRE(params && grads && x && labels && workspace, "model: null argument");
   S2S_REQUIRE(workspace_bytes >= model_ws(d, nullptr).total, "model: workspace too small");
@@ -1345,8 +1345,8 @@ extern "C" int s2s_debug_gemm(int transA, int transB, int M, int N, int K, float
   s2s::set_gemm_precision(s2s::kGemmF32);
   return rc;
 }
-// test / bench entry: one problem straight on the big-tile bf16 GEMM (gemm_bf16.hip; hipBLASLt under S2S_GEMM_LT=1, for
-// A/B runs) with the context's staging buffer; *done = 0 when the kernel declined it (nothing launched)
+// test / bench entry: one problem straight on the big-tile bf16 GEMM (gemm_bf16.hip) with the context's staging
+// buffer; *done = 0 when the kernel declined it (nothing launched)
 extern "C" int s2s_debug_gemm_big_run(s2s_ctx* ctx, s2s_stream_t stream, int transA, int transB, int M, int N, int K,
                                       float alpha, const float* A, long lda, const float* B, long ldb, float beta,
                                       float* C, long ldc, const float* bias, int relu, int* done) {
@@ -1355,7 +1355,7 @@ extern "C" int s2s_debug_gemm_big_run(s2s_ctx* ctx, s2s_stream_t stream, int tra
   s2s::GemmProblem q{A, B, C, bias, lda, ldb, ldc, M, N, K, alpha, beta};
   q.relu = relu;
   bool d = false;
-  const int rc = s2s::gemm_large_bf16(static_cast<hipStream_t>(stream), q, transA != 0, transB != 0, s2s::GemmWs{}, &d);
+  const int rc = s2s::gemm_big_bf16(static_cast<hipStream_t>(stream), q, transA != 0, transB != 0, &d);
   *done = d ? 1 : 0;
   return rc;
 }

@@ -333,7 +333,7 @@ static int big_gemm(hipStream_t st, bool tA, bool tB, int M, int N, int K, float
   q.relu = relu;
   if (gemm_precision() == kGemmBf16 && 2.0 * M * (double)N * K >= 1e9) {
     bool done = false;
-    S2S_TRY(gemm_large_bf16(st, q, tA, tB, ws, &done));
+    S2S_TRY(gemm_big_bf16(st, q, tA, tB, &done));
     if (done) return 0;
   }
   return gemm_f32(st, &q, 1, tA, tB, ws);

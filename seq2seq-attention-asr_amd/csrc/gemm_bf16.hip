@@ -27,18 +27,17 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
-#include <cstring>
 
 #include "s2s_common.h"
 
 namespace s2s {
 
 // ------------------------------------------------------------------ the context-owned staging buffer
-thread_local LtStage* t_stage = nullptr;  // the calling context's staging buffer (set_lt_stage, per C-ABI call)
-void set_lt_stage(LtStage* s) { t_stage = s; }
-void lt_stage_free(LtStage* s) {
+thread_local GemmStage* t_stage = nullptr;  // the calling context's staging buffer (set_gemm_stage, per C-ABI call)
+void set_gemm_stage(GemmStage* s) { t_stage = s; }
+void gemm_stage_free(GemmStage* s) {
   if (!s) return;
-  for (int i = 0; i < LtStage::kStreams; ++i) {
+  for (int i = 0; i < GemmStage::kStreams; ++i) {
     if (s->p[i]) (void)hipFree(s->p[i]);
     s->p[i] = s->s[i] = nullptr;
     s->n[i] = 0;
@@ -53,16 +52,16 @@ std::atomic<long> g_big_calls{0};   // big-GEMM calls launched (s2s_debug_gemm_b
 // the calling context's staging buffer for stream `st` with at least `bytes`, or nullptr (no context, more streams
 // than slots, or too small while capturing)
 void* stage_acquire(hipStream_t st, size_t bytes) {
-  LtStage* s = t_stage;
+  GemmStage* s = t_stage;
   if (!s) return nullptr;
   int k = -1;
-  for (int i = 0; i < LtStage::kStreams && k < 0; ++i)
+  for (int i = 0; i < GemmStage::kStreams && k < 0; ++i)
     if (s->p[i] && s->s[i] == static_cast<void*>(st)) k = i;
   if (k >= 0 && s->n[k] >= bytes) return s->p[k];
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
   if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
   if (k < 0)
-    for (int i = 0; i < LtStage::kStreams && k < 0; ++i)
+    for (int i = 0; i < GemmStage::kStreams && k < 0; ++i)
       if (!s->p[i]) k = i;
   if (k < 0) return nullptr;
   void* p = nullptr;
@@ -399,15 +398,6 @@ int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB
   *done = true;
   ++g_big_calls;
   return 0;
-}
-
-int gemm_large_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done) {
-  static const bool lt = [] {
-    const char* e = std::getenv("S2S_GEMM_LT");
-    return e && std::strcmp(e, "1") == 0;
-  }();
-  if (lt) return gemm_lt(st, q, transA, transB, ws, done);
-  return gemm_big_bf16(st, q, transA, transB, done);
 }
 
 }  // namespace s2s

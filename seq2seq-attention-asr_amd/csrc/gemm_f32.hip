@@ -726,7 +726,7 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
     for (int i = 0; i < used; ++i) {
       const GemmProblem& q = use[i];
       bool done = false;
-      if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_large_bf16(st, q, transA, transB, ws, &done));
+      if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_big_bf16(st, q, transA, transB, &done));
       if (!done) use[keep++] = q;
     }
     used = keep;

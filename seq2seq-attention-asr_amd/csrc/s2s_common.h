@@ -130,32 +130,24 @@ struct GemmWs {
 constexpr size_t kGemmWsFloats = size_t(8) << 20;  // 32 MiB
 // All problems of one call share transA/transB.
 int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, bool transB, GemmWs ws = GemmWs{});
-// One problem on hipBLASLt with bf16 operand rounding (HIPBLAS_COMPUTE_32F_FAST_16BF: fp32 in HBM, RNE bf16 in
-// the MFMA, fp32 accumulate and result; blaslt.cpp) -- the front-end's large plain GEMMs under the bf16 modes.
-// *done = false (nothing launched) when it does not apply (rbias / Mread / Nread, no algorithm, disabled by
-// s2s_debug_gemm_lt(0)); the caller then runs gemm_f32.
 // staging buffers for the big bf16 GEMMs' operand copies, owned by a context (grown outside stream capture
 // only): one per stream, so calls the caller issues on different streams never share bytes (a buffer is
 // reused only in its own stream's order)
-struct LtStage {
+struct GemmStage {
   static constexpr int kStreams = 8;
   void* s[kStreams] = {};   // stream of each buffer
   void* p[kStreams] = {};
   size_t n[kStreams] = {};
   std::vector<void*> old;   // outgrown buffers (queued work may still read them): freed with the context
 };
-void set_lt_stage(LtStage* s);  // the calling thread's current context's buffer (set at every C-ABI entry)
-void lt_stage_free(LtStage* s);
+void set_gemm_stage(GemmStage* s);  // the calling thread's current context's buffer (set at every C-ABI entry)
+void gemm_stage_free(GemmStage* s);
 void* stage_acquire(hipStream_t st, size_t bytes);  // that buffer with >= bytes (nullptr: none, or capturing)
 // One large problem on the in-house bf16 GEMM (gemm_bf16.hip: operands staged to bf16 in the context's staging
 // buffer, 256 x 256 / 128 x 128 MFMA tiles, LDS-DMA staging, split-K slabs).  *done = false (nothing launched)
 // when it does not apply (rbias / Mread / Nread, no staging buffer, disabled by s2s_debug_gemm_big(0)).
 bool gemm_big_enabled();
 int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, bool* done);
-// the module-level large bf16 product: gemm_big_bf16, or hipBLASLt (gemm_lt) when S2S_GEMM_LT=1 (A/B only)
-int gemm_large_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done);
-bool gemm_lt_enabled();
-int gemm_lt(hipStream_t st, const GemmProblem& q, bool transA, bool transB, GemmWs ws, bool* done);
 // Implicit-GEMM SpatialConvolutionMM on bf16 MFMA (conv_bf16.inc): no im2col panel.  Forward y (B, Cout, Ho,
 // Wo) = conv(x) + bias (per channel), ReLU when relu; input gradient dx (B, Cin, H, W) (+)= transposed
 // convolution of dyt (Cout, B Ho Wo) -- the ReLU-masked output gradient -- with W.  scratch:

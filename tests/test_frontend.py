@@ -415,6 +415,38 @@ def _mlp_layers(rng, dims, O):
     return L
 
 
+def test_oracle_vgg_step_under_its_own_decisions_is_unchanged():
+    """The decision-adoption hooks of the VGG oracle (vgg_fwd / mlp_fwd decide / maxout_idx, used by the bf16
+    config-5 test): adopting the oracle's own ReLU / max-pooling / Maxout decisions reproduces the plain step
+    bit for bit, and raw reports the pre-decision values those decisions came from."""
+    import vgg_case as vc
+    P, layers, cfg = fo.vgg_random_case(F=24, hidden=64, out=32, S=16, Sc=24, O=9, M=8, seed=3, dtype=np.float64)
+    rng = np.random.default_rng(3)
+    x = rng.standard_normal((2, 3, 20, 24))
+    labels = rng.integers(0, 9, (2, 5)).astype(np.int32)
+    raw = {}
+    nll, logp, G, mg = fo.vgg_model_step(x, labels, P, layers, cfg, raw=raw)
+    decide = {"conv": [u > 0 for u in raw["conv"]], "lin": [u > 0 for u in raw["lin"]], "pool": dict(raw["pool"])}
+    mx = [np.argmax(g, axis=2) for g in raw["mlp"]]
+    assert len(raw["conv"]) == 4 and len(raw["lin"]) == 4 and sorted(raw["pool"]) == [1, 3] and len(mx) == 2
+    raw2 = {}
+    nll2, logp2, G2, mg2 = fo.vgg_model_step(x, labels, P, layers, cfg, decide, mx, raw2)
+    assert np.array_equal(logp, logp2) and all(np.array_equal(G[k], G2[k]) for k in G)
+    assert vc.decision_margins(decide, mx, raw2) == {k: (0, 0.0) for k in
+                                                     ("conv0", "conv1", "conv2", "conv3", "lin0", "lin1", "lin2",
+                                                      "lin3", "pool1", "pool3", "maxout0", "maxout1")}
+    # one adopted flip (the smallest |u| of the last 1x1 layer) changes the step and is reported with its margin
+    u = raw["lin"][3]
+    k = np.unravel_index(np.argmin(np.abs(u)), u.shape)
+    decide["lin"][3] = decide["lin"][3].copy()
+    decide["lin"][3][k] = not decide["lin"][3][k]
+    raw3 = {}
+    _, logp3, _, _ = fo.vgg_model_step(x, labels, P, layers, cfg, decide, mx, raw3)
+    m = vc.decision_margins(decide, mx, raw3)
+    assert m["lin3"][0] == 1 and abs(m["lin3"][1] - abs(u[k]) / np.abs(u).max()) < 1e-12
+    assert not np.array_equal(logp, logp3)
+
+
 def test_oracle_mlp_stack_matches_torch():
     rng = np.random.default_rng(21)
     layers = _mlp_layers(rng, (12, 5), 9)

@@ -234,11 +234,25 @@ def test_model_step_bf16_config3_decisions_pinned(lib, B, fused, prec):
     assert errs["logp"] > 1e-6  # bf16 really ran (fp32 reaches ~2e-7 here)
 
 
+# bf16 operands move pre-activations by ~2^-9 of their scale per product, so a decision is "near a tie" within a
+# few 1e-3 of its site's scale: flips there are adopted (measured: at most 5.2e-3 of the scale, pool3); a flip
+# beyond this band would be a kernel error.
+BF16_DECISION_BAND = 1e-2
+# config 5 chains 12 bf16 products (8 encoder layers, the decoder, the decoder_mlp) against config 3's 4, so its
+# pinned bar is twice config 3's (measured with decisions pinned: 1.8e-4 .. 1.05e-2, the deepest layer dvgg2 worst;
+# 7-9e-2 before pinning)
+BF16_PINNED_DEEP_GRAD_RTOL = 2e-2
+
+
 @pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
 def test_vgg_model_step_bf16_config5(lib, prec):
-    """BASELINE config 5 (librispeech/model_vgg.lua, bf16): full width (1x1 layers 2048), B = 1, L = 256,
-    T = 50, against the float64 oracle; tensors the fp32 restatement cannot pin to 1e-5 (cancelling sums,
-    tests/test_gpu_fullsize.py) are reported, not judged.  bf16-all also takes the weight gradients in bf16."""
+    """BASELINE config 5 (librispeech/model_vgg.lua:23-82, bf16): full width (1x1 layers 2048), B = 1, L = 256,
+    T = 50, against the float64 oracle run under the GPU's own discrete decisions (the VGG and 1x1 ReLUs, both
+    SpatialMaxPoolings and the two decoder_mlp Maxouts) -- each adopted flip must sit within BF16_DECISION_BAND of
+    its tie -- so every tensor is held to the operand-rounding bar, as config 3 is (BF16_PINNED_DEEP_GRAD_RTOL).
+    Tensors the fp32 restatement cannot pin to 1e-5 (the attention score layer's cancelling sums dV / dWs / dbs /
+    dwe, tests/test_gpu_fullsize.py) are reported, not judged.  bf16-all also
+    takes the weight gradients in bf16."""
     import s2s_amd
     import vgg_case as vc
     from s2s_amd import frontend as fe
@@ -247,23 +261,31 @@ def test_vgg_model_step_bf16_config5(lib, prec):
     model = s2s_amd.VGGAttentionModel(40, outputFrameSize=512, hidden=2048, outputDepth=29, generator=g,
                                       precision=prec).cuda()
     rng = np.random.default_rng(5)
-    x = rng.standard_normal((B, 3, L, 40))
+    x = rng.standard_normal((B, 3, L, 40)).astype(np.float32).astype(np.float64)
     labels = np.append(rng.integers(0, 28, (B, T - 1)), np.full((B, 1), 28), axis=1).astype(np.int32)
     model.zeroGradParameters()
     nll, logp = model.step(torch.tensor(x, dtype=torch.float32, device="cuda"),
                            torch.tensor(labels, dtype=torch.int32, device="cuda"))
     torch.cuda.synchronize()
-    nll64, logp64, G64, mg64 = vc.oracle_step(model, fe, x, labels, np.float64)
-    nll32, logp32, G32, mg32 = vc.oracle_step(model, fe, x, labels, np.float32)
+    decide, mx = vc.gpu_decisions(model, fe)
+    raw = {}
+    nll64, logp64, G64, mg64 = vc.oracle_step(model, fe, x, labels, np.float64, decide, mx, raw)
+    nll32, logp32, G32, mg32 = vc.oracle_step(model, fe, x, labels, np.float32, decide, mx)
+    margins = vc.decision_margins(decide, mx, raw)
+    print(f"config 5 {prec} adopted flips (count, largest margin / scale):", margins)
+    wide = {k: v for k, v in margins.items() if v[1] > BF16_DECISION_BAND}
+    assert not wide, wide
     errs = {"logp": _rel(logp.cpu().numpy(), logp64)}
     floor = {"logp": _rel(logp32, logp64)}
     for (name, gpu, r64), (_, _, r32) in zip(vc.grad_pairs(model, fe, G64, mg64), vc.grad_pairs(model, fe, G32, mg32)):
         errs[name] = _rel(gpu.detach().cpu().numpy(), r64)
         floor[name] = _rel(r32, r64)
-    print(f"config 5 {prec} max rel errs (fp32 floor):", {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
+    print(f"config 5 {prec} rel L2 errs, decisions pinned (fp32 floor):",
+          {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
     bad = {k: f"{errs[k]:.2e}" for k in errs
-           if floor[k] <= 1e-5 and not errs[k] <= (BF16_LOGP_RTOL if k == "logp" else BF16_GRAD_RTOL)}
+           if floor[k] <= 1e-5 and not errs[k] <= (BF16_PINNED_LOGP_RTOL if k == "logp" else BF16_PINNED_DEEP_GRAD_RTOL)}
     assert not bad, bad
+    assert errs["logp"] > 1e-6  # bf16 really ran
 
 
 @pytest.mark.parametrize("B,Cin,H,W,Cout,relu", [(2, 3, 20, 12, 64, True), (2, 64, 17, 11, 64, False),

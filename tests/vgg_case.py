@@ -58,9 +58,56 @@ def grad_pairs(model, fe, G, mg):
     return pairs
 
 
-def oracle_step(model, fe, x, labels, dtype=np.float64):
+def oracle_step(model, fe, x, labels, dtype=np.float64, decide=None, maxout_idx=None, raw=None):
     P, layers, cfg = oracle_params(model, fe, dtype)
-    return fo.vgg_model_step(x.astype(dtype), labels, P, layers, cfg)
+    return fo.vgg_model_step(x.astype(dtype), labels, P, layers, cfg, decide, maxout_idx, raw)
+
+
+def gpu_decisions(model, fe):
+    """The discrete decisions the GPU step took (after model.step): ReLU masks of the VGG convolutions and 1x1
+    layers (their fused ReLU outputs are positive exactly where u passed), the SpatialMaxPooling indices and the
+    decoder_mlp Maxout winners -> (decide, maxout_idx) for oracle_step."""
+    mods = model.encoder.seq.modules
+    decide = {"conv": [m.output.detach().cpu().numpy() > 0 for m in mods if isinstance(m, fe.SpatialConvolutionMM)],
+              "lin": [m.output.detach().cpu().numpy() > 0 for m in mods if isinstance(m, fe.TemporalConvolution)],
+              "pool": {}}
+    l = -1
+    for m in mods:
+        if isinstance(m, fe.SpatialConvolutionMM):
+            l += 1
+        elif isinstance(m, fe.SpatialMaxPooling):
+            decide["pool"][l] = m.indices.cpu().numpy().astype(np.int64)
+    maxout_idx = [m.pool.indices.cpu().numpy().astype(np.int64)[..., 0]
+                  for m in model.decoder.decoder_mlp.modules if isinstance(m, fe.Maxout)]
+    return decide, maxout_idx
+
+
+def decision_margins(decide, maxout_idx, raw):
+    """For each decision site: (flips, the largest |margin| / scale among them), where a flip is a GPU decision
+    that differs from the oracle's own one under the same upstream decisions and its margin is how far the
+    oracle's value is from the tie (|u| for a ReLU; the winner's lead over the GPU's pick for max-pooling and
+    Maxout)."""
+    out = {}
+    for kind in ("conv", "lin"):
+        for l, (mask, u) in enumerate(zip(decide[kind], raw[kind])):
+            d = mask != (u > 0)
+            out[f"{kind}{l}"] = (int(d.sum()), float(np.abs(u[d]).max() / np.abs(u).max()) if d.any() else 0.0)
+    for l, gidx in decide["pool"].items():
+        own, h = raw["pool"][l], raw["pool_in"][l]
+        d = gidx != own
+        if d.any():
+            from oracle.frontend_oracle import VGG_POOLS, smaxpool_fwd
+            kW, kH, dW, dH = VGG_POOLS[l]
+            lead = smaxpool_fwd(h, kW, kH, dW, dH)[0] - smaxpool_fwd(h, kW, kH, dW, dH, gidx)[0]
+            out[f"pool{l}"] = (int(d.sum()), float(lead[d].max() / np.abs(h).max()))
+        else:
+            out[f"pool{l}"] = (0, 0.0)
+    for i, (am, g) in enumerate(zip(maxout_idx, raw["mlp"])):
+        own = np.argmax(g, axis=2)
+        d = am != own
+        lead = np.take_along_axis(g, own[..., None], 2)[..., 0] - np.take_along_axis(g, am[..., None], 2)[..., 0]
+        out[f"maxout{i}"] = (int(d.sum()), float(lead[d].max() / np.abs(g).max()) if d.any() else 0.0)
+    return out
 
 
 def rel(a, r):

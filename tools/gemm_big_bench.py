@@ -1,6 +1,6 @@
 """Throughput of the big-tile bf16 GEMM (gemm_bf16.hip) on the config-5 shapes and on square problems.
-Run on a GPU box:  python tools/gemm_big_bench.py            (the in-house kernel)
-                   S2S_GEMM_LT=1 python tools/gemm_big_bench.py   (module path on hipBLASLt, for the A/B)
+Run on a GPU box:  python tools/gemm_big_bench.py
+(The round-4 A/B against hipBLASLt, before it left the library: profiles/r04/gemm_big.txt.)
 Prints, per shape: the direct kernel (staging passes included) and the VGG 1x1 layer (TemporalConvolution(Din, Dout,
 1) + ReLU, model_vgg.lua:45-52) forward + backward (3 GEMMs) through the module path, in TFLOP/s."""
 import ctypes
@@ -67,8 +67,7 @@ STEP_SHAPES = [(8128, 2048, 2048, 0, 1, 2), (8128, 2048, 2048, 0, 0, 2), (2048, 
                (3200, 256, 768, 0, 0, 1), (2048, 896, 8128, 1, 0, 1)]
 
 if __name__ == "__main__":
-    lt = os.environ.get("S2S_GEMM_LT") == "1"
-    tag = "hipBLASLt" if lt else "in-house"
+    tag = "in-house"
     total = 0.0
     for M, N, K, tA, tB, n in STEP_SHAPES:
         tf = direct(M, N, K, tA, tB)
@@ -76,6 +75,5 @@ if __name__ == "__main__":
         total += n * us
         print(f"{tag:9s} M={M:5d} N={N:5d} K={K:5d} tA={tA} tB={tB} x{n}: {tf:7.1f} TFLOP/s {us:7.1f} us", flush=True)
     print(f"{tag} step total {total:.1f} us", flush=True)
-    if not lt:
-        for M, N, K, tA, tB in ((4096, 4096, 4096, 0, 1), (8192, 8192, 8192, 0, 1)):
-            print(f"in-house  M={M:5d} N={N:5d} K={K:5d}: {direct(M, N, K, tA, tB):7.1f} TFLOP/s", flush=True)
+    for M, N, K, tA, tB in ((4096, 4096, 4096, 0, 1), (8192, 8192, 8192, 0, 1)):
+        print(f"in-house  M={M:5d} N={N:5d} K={K:5d}: {direct(M, N, K, tA, tB):7.1f} TFLOP/s", flush=True)
