@@ -88,6 +88,13 @@ struct XProj {
   int sA, sB, PA, PB;
   float* slab;
   unsigned* icnt;
+  // XCD-grouped dealing of the whole (unsplit) units (G > 0): the producers come in G groups of gsz, one
+  // group per XCD (consecutive spare-slot indices share a chain slot); group g takes direction g % nd and every
+  // (G / nd)-th slice from sB + g / nd, its members round-robin over that class's (slice, column tile) units.
+  // An XCD then streams one direction's x-weights (K x 4 column tiles: 1.6 MB at config 2) instead of all of
+  // them (3.1 MB) next to its slices' x tiles, which with plain round-robin dealing (two slices x all units
+  // per XCD) overflowed its 4 MB L2 and re-read the weights from memory for every pair of slices.
+  int G, gsz, nsplit;
 };
 constexpr int kXpMaxSplitItems = 64;
 
@@ -112,6 +119,27 @@ __device__ __forceinline__ XUnit xunit(const XProj& q, int nd, int u) {
   x.d = rem / q.ntn;
   x.ct = rem - x.d * q.ntn;
   return x;
+}
+// the it-th unit of producer p (false: none left).  Split units (w < nsplit) and, without grouping, all units:
+// the round-robin w = p + it nprod; with grouping (XProj::G), the whole units of p's group in class order
+__device__ __forceinline__ bool xunit_of(const XProj& q, int nd, int p, int nprod, int it, XUnit& x) {
+  const int w = p + it * nprod;
+  if (q.G == 0 || w < q.nsplit) {
+    if (w >= q.nwork) return false;
+    x = xunit(q, nd, w);
+    return true;
+  }
+  const int nsp = q.nsplit > p ? (q.nsplit - p + nprod - 1) / nprod : 0;  // p's split units
+  const int g = p / q.gsz, v = p - g * q.gsz + (it - nsp) * q.gsz;
+  const int ncls = q.G / nd, i = v / q.ntn;
+  x.sl = q.sB + i * ncls + g / nd;
+  if (x.sl >= q.nslices) return false;
+  x.d = g % nd;
+  x.ct = v - i * q.ntn;
+  x.part = 0;
+  x.P = 1;
+  x.item = -1;
+  return true;
 }
 constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
 
@@ -210,8 +238,8 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
   __shared__ int last_part;  // split item: this block's part was the last to finish
   const int nd = q.nd;
   if (tid >= 256) {  // a 320-thread block's 5th (row loader) wave: only the producer's barriers
-    for (int w = p; w < q.nwork; w += nprod) {
-      const XUnit x = xunit(q, nd, w);
+    XUnit x;
+    for (int it = 0; xunit_of(q, nd, p, nprod, it, x); ++it) {
       const int nb = 1 + nk / x.P + (q.alpha ? 1 : 0);
       for (int i = 0; i < nb; ++i) __syncthreads();
       if (x.P == 1) {
@@ -230,10 +258,10 @@ __device__ __forceinline__ void xproj_produce(const PArgs& a, float* lds, int p,
   float* As[2] = {lds, lds + 64 * LDK};
   float* Bs[2] = {lds + 128 * LDK, lds + 192 * LDK};
   int item = 0;
-  for (int w = p; w < q.nwork; w += nprod, ++item) {
+  XUnit xu;
+  for (; xunit_of(q, nd, p, nprod, item, xu); ++item) {
     if (a.pstamps && tid == 0 && item < kProdStampItems)
       a.pstamps[((long)p * kProdStampItems + item) * 2] = __builtin_amdgcn_s_memrealtime();
-    const XUnit xu = xunit(q, nd, w);
     const int sl = xu.sl, d = xu.d, ct = xu.ct;
     const int nkp = nk / xu.P, kb = xu.part * nkp;  // this unit's K-tiles [kb, kb + nkp)
     const int rev = a.d[d].reverse ^ q.flip;
@@ -1057,6 +1085,7 @@ bool gru_persist_can_prep_next(int ndir, int B, int H, bool fwd) {
 static void xproj_split(XProj& q, int nd, int nprod) {
   q.sA = q.sB = 0;
   q.PA = q.PB = 1;
+  q.nsplit = 0;
   const int nk = q.K / 32, per = nd * q.ntn;
   if (!g_xp_split || nk % 16 != 0 || per <= 0) return;
   const int sA = std::max(1, nprod / (per * 4));
@@ -1064,6 +1093,23 @@ static void xproj_split(XProj& q, int nd, int nprod) {
   if (sB > q.nslices || sB * per > kXpMaxSplitItems || sA >= sB) return;
   q.sA = sA; q.sB = sB; q.PA = 4; q.PB = 2;
   q.nwork = (sA * 4 + (sB - sA) * 2 + (q.nslices - sB)) * per;
+  q.nsplit = (sA * 4 + (sB - sA) * 2) * per;
+}
+
+// s2s_debug_gru_xp_group(1): XCD-grouped dealing of the dy units.  Off by default: at config 2 it cuts the BPTT
+// launch's fetched bytes 170 -> 102 MB (the producers' x-weights stay in L2) but the step is ~20 us slower in a
+// same-box A/B (3.419 -> 3.439 ms; profiles/r04/pmc_xp_group.txt)
+std::atomic<int> g_xp_group{0};
+
+// XCD-grouped dealing (XProj::G) when the spare slots form whole per-XCD groups of gsz producers and every
+// direction gets at least one group
+static void xproj_group(XProj& q, int nd, int nprod, int gsz) {
+  q.G = 0;
+  q.gsz = gsz;
+  if (!g_xp_group || gsz <= 0 || nprod % gsz != 0) return;
+  const int G = nprod / gsz;
+  if (G < nd || G % nd != 0) return;
+  q.G = G;
 }
 
 static void carve_granules(char* sync, int B, int L, int H, unsigned** abort_word, granule_t* (&g)[2][3],
@@ -1121,9 +1167,13 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   if (f.pack) a.pack = *f.pack;
   if (!f.prepared) S2S_TRY(launch_sync_prep(st, sync, prep_bytes(f.B, f.L, f.H), a.next_sync));
   // algorithmic work of the launch: the recurrence, plus the x-projection GEMM when its spare slots compute it
+  // bytes: the recurrence's weights, x-projection reads, saved activations and outputs, plus the in-launch GEMM's
+  // operands and its x-projection writes (x once for both directions, Wx, xp)
   const double xflops = f.x ? 2.0 * f.B * f.L * 3.0 * f.ndir * f.H * f.Kx : 0.0;
+  const double xbytes = f.x ? 4.0 * ((double)f.B * f.L * f.Kx + 3.0 * f.ndir * f.H * f.Kx + 3.0 * f.ndir * f.B * f.L * f.H)
+                            : 0.0;
   ProfScope ps(st, "gru_fwd_persist", 2.0 * f.ndir * f.B * f.L * 3.0 * f.H * f.H + xflops,
-               4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)));
+               4.0 * f.ndir * (3.0 * f.H * f.H + (double)f.B * f.L * (3 * f.H + 5 * f.H + f.H)) + xbytes);
   S2S_TRY(launch(st, a, f.excl != 0, true));
   void* r[1] = {sync};
   return launch_sync_harvest(st, r, 1, f.status);
@@ -1160,6 +1210,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
     q.slab = reinterpret_cast<float*>(static_cast<char*>(sync) + slab_offset(b.B, b.L, b.H));
     const int gch = 8 * ((a.nchains + 7) / 8);
     xproj_split(q, b.ndir, (gch - a.nchains) * a.nmem);
+    xproj_group(q, b.ndir, (gch - a.nchains) * a.nmem, a.nmem);
     a.fused = 1;
   }
   if (b.next_sync) {
@@ -1170,9 +1221,15 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   if (b.prep_event) S2S_CHECK_HIP(hipEventRecord(b.prep_event, st));
   // algorithmic work of the launch: the recurrence, plus the dy its spare slots compute (the layer above's
   // dX GEMM, or the decoder's dh: dVh V and the context term sum_t alpha dc)
+  // bytes: the recurrence's weights, saved activations, dy reads and gate-gradient writes, plus the in-launch GEMM's
+  // operands (dA of the layer above or the decoder's dVh, the weights, the context term's alpha and dc) and its dy
+  // writes
   const double yflops = b.ydA ? 2.0 * b.B * b.L * (double)b.ndir * b.H * (b.yK + b.yT) : 0.0;
+  const double ybytes = b.ydA ? 4.0 * ((double)b.B * b.L * b.yK + (double)b.yK * b.ndir * b.H +
+                                       (double)b.B * b.yT * (b.L + b.ndir * b.H) + (double)b.B * b.L * b.ndir * b.H)
+                              : 0.0;
   ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops,
-               4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)));
+               4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)) + ybytes);
   S2S_TRY(launch(st, a, b.excl != 0, false));
   void* r[1] = {sync};
   return launch_sync_harvest(st, r, 1, b.status);
@@ -1208,6 +1265,7 @@ extern "C" void s2s_debug_gru_local(int allow) { s2s::g_allow_local = allow; }
 extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_xp_split(int on) { s2s::g_xp_split = on; }
+extern "C" void s2s_debug_gru_xp_group(int on) { s2s::g_xp_group = on; }
 // diagnostic: 0 = one sentinel slot per step re-armed at launch start (the round-2 form), else the 4-slot ring
 extern "C" void s2s_debug_gru_ring(int on) { s2s::g_sent_ring = on ? s2s::kSentRing : 0; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {

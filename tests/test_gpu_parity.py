@@ -584,6 +584,38 @@ def test_bucket_events_mark_final_gradients(s2s, graph):
         assert model.grads.abs().sum() > 0
 
 
+@pytest.mark.parametrize("B", [32, 45])
+def test_fused_dy_dealing_does_not_change_the_step(s2s, B):
+    """The BPTT launch's spare-slot producers compute its dy (the layer above's dX) unit by unit
+    in a fixed k order, so how the units are dealt to the producers -- round-robin (default) or XCD-grouped by
+    direction (s2s_debug_gru_xp_group(1)) -- must not change a bit of the step; and the whole step matches the
+    dX computed by a GEMM in front of the BPTT (s2s_debug_gru_fused_dy(0)) to fp32 summation noise."""
+    import ctypes
+    from s2s_amd import _lib
+    fg, fd = _lib.lib.s2s_debug_gru_xp_group, _lib.lib.s2s_debug_gru_fused_dy
+    fg.argtypes = fd.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(B)
+    x = torch.randn(B, 96, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, 20), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, (grp, fused) in {"grouped": (1, 1), "round-robin": (0, 1), "gemm": (0, 0)}.items():
+            fg(grp)
+            fd(fused)
+            nll, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (logp.clone(), model.grads.clone())
+    finally:
+        fg(0)
+        fd(1)
+    assert torch.equal(outs["grouped"][0], outs["round-robin"][0])
+    assert torch.equal(outs["grouped"][1], outs["round-robin"][1])
+    ga, gb = outs["grouped"][1], outs["gemm"][1]
+    assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
+
+
 @pytest.mark.parametrize("local,ring", [(1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("B,H", [(32, 256), (45, 128)])
 def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, ring, B, H):
