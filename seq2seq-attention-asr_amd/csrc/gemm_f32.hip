@@ -728,6 +728,10 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
       bool done = false;
       if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_big_bf16(st, q, transA, transB, &done));
       if (!done) use[keep++] = q;
+      static const bool trace = std::getenv("S2S_GEMM_TRACE") != nullptr;  // diagnostic: the shapes staying here
+      if (trace && !done)
+        std::fprintf(stderr, "[s2s gemm_f32 bf16] M %d N %d K %d tA %d tB %d (%d problems in the call)\n", q.M, q.N,
+                     q.K, (int)transA, (int)transB, used);
     }
     used = keep;
     if (used == 0) return 0;

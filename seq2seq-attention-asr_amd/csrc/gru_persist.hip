@@ -956,7 +956,27 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     const int tn = g.reverse ? t + 1 : t - 1;
     float4 azr[2 * NC];
     GRU_STAMP(3);
-    {
+    bool split = false;
+    if constexpr (NC % 2 == 0 && !S2S_GRU_DIAG) split = loc;
+    if constexpr (NC % 2 == 0 && !S2S_GRU_DIAG) if (split) {
+      // da_z (ready since the previous step) first; da_r (this step's p1) is loaded once before the da_z half of
+      // the K = 2H product runs, checked behind it (polled further only if some tile was not yet published): the
+      // da_z MFMAs overlap the da_r hand-off.  Same instruction sequence as mfma_chunks<2 NC> (bitwise equal).
+      float4 az[NC], ar[NC];
+      uint4 rraw[NC];
+      ok = sweep_sent_tile<NC>(az, zs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
+      sent_tile_issue<NC>(rraw, rs_, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane);
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      __builtin_amdgcn_sched_barrier(0);  // the da_r loads stay ahead of the da_z MFMAs
+      mfma_pairs<NC>(az, wzr, acc0, acc1);
+      __builtin_amdgcn_sched_barrier(0);
+      if (!sent_tile_check<NC>(rraw, ar))
+        ok = ok && sweep_sent_tile<NC>(ar, rs_, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
+      GRU_STAMP(4);
+      mfma_pairs<NC>(ar, wzr + NC, acc0, acc1);
+      acc = acc0 + acc1;
+    }
+    if (!split) {
       // da_z (ready since the previous step) first, then poll da_r (this step's p1) alone: a
       // merged poll of both rows re-reads da_z while waiting for da_r (measured slower)
       float4 az[NC], ar[NC];
@@ -978,8 +998,8 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       // chunk i of the K = 2H product: i < NC reads da_z, i >= NC reads da_r (H % 64 == 0)
 #pragma unroll
       for (int i = 0; i < NC; ++i) { azr[i] = az[i]; azr[NC + i] = ar[i]; }
+      acc = mfma_chunks<2 * NC>(azr, wzr);
     }
-    acc = mfma_chunks<2 * NC>(azr, wzr);
     const float sm = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     const Row nxt = s > 0 ? load_row(p + 1) : Row{0.f, 0.f, 0.f, 0.f, 0.f};
     if (live && s > 0) dhc = tn < lenb ? dhp + sm : 0.f;

@@ -319,6 +319,30 @@ __device__ __forceinline__ bool sweep_sent_tile(float4 (&a)[NC], __amdgpu_buffer
   }
 }
 
+// sweep_sent_tile's first pass split in two: sent_tile_issue loads the tile (no check, so nothing waits for the
+// loads), sent_tile_check later tests and converts what arrived (false: some value is still a sentinel -- the
+// caller then polls with sweep_sent_tile).  Work placed between the two (behind a sched_barrier) runs while the
+// loads are in flight.
+template <int NC>
+__device__ __forceinline__ void sent_tile_issue(uint4 (&raw)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
+                                                int wave, int lane) {
+  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + 4L * 256 * (wave + 4 * i)), 0, 16));
+}
+template <int NC>
+__device__ __forceinline__ bool sent_tile_check(const uint4 (&raw)[NC], float4 (&a)[NC]) {
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    const uint4 p = raw[i];
+    ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
+    a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
+  }
+  return __all(ok);
+}
+
 // sweep_skinny_rows over sentinel rows: all R * NC loads of a pass issued before any check
 template <int NC, int R>
 __device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],
@@ -494,6 +518,26 @@ __device__ __forceinline__ floatx4 mfma_chunks(const float4 (&a)[NC], const floa
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
   }
   return acc0 + acc1;
+}
+
+// mfma_chunks' pairs of chunks accumulated into (acc0, acc1): a K split into two operand halves of NC chunks
+// (NC even) runs as mfma_pairs(first half, w) then mfma_pairs(second half, w + NC) -- mfma_chunks<2 NC> on the
+// concatenation, instruction for instruction (bitwise-equal sums), with the first half's MFMAs free to run before
+// the second half's operands have arrived
+template <int NC>
+__device__ __forceinline__ void mfma_pairs(const float4 (&a)[NC], const float4* w, floatx4& acc0, floatx4& acc1) {
+  static_assert(NC % 2 == 0, "mfma_pairs: NC even");
+#pragma unroll
+  for (int i = 0; i < NC; i += 2) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].x, w[i + 1].x, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].y, w[i + 1].y, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].z, w[i + 1].z, acc1, 0, 0, 0);
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc0, 0, 0, 0);
+    acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i + 1].w, w[i + 1].w, acc1, 0, 0, 0);
+  }
 }
 
 // mfma_chunks with the W fragments held in AGPRs, the accumulator half of gfx950's unified register file: an
