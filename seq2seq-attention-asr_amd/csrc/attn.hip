@@ -646,18 +646,32 @@ __global__ __launch_bounds__(256) void dec_f7_gru2(AttnK k) {
 }
 
 // ---- decoder LSTM (LSTM.lua:16-58 as decoder_recurrent, timit/timit.lua:137): s = h, mem = c
-// LW rows (q*S + n) = [Wqh[n] | Wqx[n]] against HX rows [s_{t-1} | d]; LB = bqx + bqh
+// LW rows interleave the four gates of each unit: row 4 u + q = [Wqh[u] | Wqx[u]] (q = i, f, g, o) against HX rows
+// [s_{t-1} | d]; LB[4 u + q] = bqx + bqh.  (GT, the backward's LW^T, keeps the gate-major column order q S + u of
+// the gate gradients: dec_lstm_gt.)
 __global__ void dec_lstm_pack(AttnK k) {
   const int S = k.S;
   const long n = 4L * S * 2 * S;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    const int r = (int)(i / (2 * S)), c = (int)(i - (long)r * 2 * S), q = r / S, u = r - q * S;
+    const int r = (int)(i / (2 * S)), c = (int)(i - (long)r * 2 * S), u = r >> 2, q = r & 3;
     k.LW[i] = c < S ? k.P.lstm[4 * q + 2][(long)u * S + c] : k.P.lstm[4 * q][(long)u * S + c - S];
     if (c == 0) k.LB[r] = k.P.lstm[4 * q + 1][u] + k.P.lstm[4 * q + 3][u];
   }
 }
+// GT (2S, 4S) = LW^T with the gate-major column order of the gate gradients: GT[n][q S + u] = LW[4 u + q][n]
+__global__ void dec_lstm_gt(AttnK k) {
+  const int S = k.S;
+  const long n = 2L * S * 4 * S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int c = (int)(i / (4 * S)), j = (int)(i - (long)c * 4 * S), q = j / S, u = j - q * S;
+    k.GT[i] = k.LW[(long)(4 * u + q) * 2 * S + c];
+  }
+}
 
-// F6 (LSTM): gate q of unit u = act(LW[q*S+u] . [s_{t-1}; d] + LB)  (N = 4S, K = 2S); act = sigmoid, g: tanh
+// F6 + F7 (LSTM), one launch per step: the block's 16 output rows are the four gates of four units (LW's
+// interleaved rows), gate = act(LW[4u+q] . [s_{t-1}; d] + LB) (N = 4S, K = 2S; act = sigmoid, g: tanh), then
+// the unit's four gates meet in four adjacent lanes and the lane of gate i updates the cell: c = f c_{t-1} + i g,
+// s = o tanh(c).  (The cell update used to be its own launch per decoder step.)
 __global__ __launch_bounds__(512) void dec_f6_lstm(AttnK k) {
   __shared__ SkinnyRed8 red;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -666,26 +680,22 @@ __global__ __launch_bounds__(512) void dec_f6_lstm(AttnK k) {
                             k.LW + (long)(n0 + (lane & 15)) * 2 * S, 2 * S, wave, lane);
   const float s = skinny_reduce8(red, acc, wave, lane, tid);
   if (tid >= 256) return;
-  const int b = b0 + (tid >> 4), n = n0 + (tid & 15);
-  if (b >= k.B) return;
+  const int b = b0 + (tid >> 4), r = n0 + (tid & 15), u = r >> 2, q = r & 3;
+  if (b >= k.B) return;  // (uniform over each group of four lanes: one row)
   const long row = (long)b * k.T + t;
-  const float x = s + k.LB[n];
-  k.GSV[row * 4 * S + n] = (n >= 2 * S && n < 3 * S) ? tanhf(x) : sigmoidf_(x);
-}
-
-// F7 (LSTM): c = f c_{t-1} + i g, s = o tanh(c)
-__global__ void dec_f7_lstm(AttnK k) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x, S = k.S, t = k.t;
-  if (i >= k.B * S) return;
-  const int b = i / S, n = i - b * S;
-  const long row = (long)b * k.T + t;
-  const float* g = k.GSV + row * 4 * S;
-  const float cp = t > 0 ? k.LC[(row - 1) * S + n] : 0.f;
-  const float c = g[S + n] * cp + g[n] * g[2 * S + n];
-  const float snew = g[3 * S + n] * tanhf(c);
-  k.LC[row * S + n] = c;
-  k.VV[row * (S + k.A) + n] = snew;
-  if (t + 1 < k.T) k.HX[(row + 1) * 2 * S + n] = snew;
+  const float x = s + k.LB[r];
+  const float gv = q == 2 ? tanhf(x) : sigmoidf_(x);
+  k.GSV[row * 4 * S + q * S + u] = gv;
+  const int l0 = lane & ~3;
+  const float gi = __shfl(gv, l0, 64), gf = __shfl(gv, l0 + 1, 64), gg = __shfl(gv, l0 + 2, 64),
+              go = __shfl(gv, l0 + 3, 64);
+  if (q != 0) return;
+  const float cp = t > 0 ? k.LC[(row - 1) * S + u] : 0.f;
+  const float c = gf * cp + gi * gg;
+  const float snew = go * tanhf(c);
+  k.LC[row * S + u] = c;
+  k.VV[row * (S + k.A) + u] = snew;
+  if (t + 1 < k.T) k.HX[(row + 1) * 2 * S + u] = snew;
 }
 
 __global__ void dec_init_fwd(AttnK k) {
@@ -1500,7 +1510,6 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     }
     if (d.lstm) {
       hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(512), 0, st, k);
-      hipLaunchKernelGGL(dec_f7_lstm, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
     } else {
       hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
       hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
@@ -1577,7 +1586,10 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_TRY(zero_async(st, k.DWEACC, sizeof(float) * (size_t)B * k.NCH * Sc));
   }
   // packed transposes for the backward products
-  if (d.lstm) S2S_TRY(transpose_f32(st, k.LW, 2L * S, 4 * S, 2 * S, k.GT, 4L * S));  // GT = LW^T
+  if (d.lstm) {  // GT = LW^T in the gate gradients' gate-major order
+    hipLaunchKernelGGL(dec_lstm_gt, dim3(512), dim3(256), 0, st, k);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
   if (!xp.var) {  // (the XCD-local path's operand layouts come from its prologue)
   if (!d.lstm) {
   S2S_TRY(transpose_f32(st, P.Wh, 2L * S, S, S, k.WhT, S));          // WhT[k][n] = Wh[n][k], k < S
@@ -2127,7 +2139,6 @@ int attn_beam_step(hipStream_t st, const AttnDims& d, const AttnParams& P, int K
   hipLaunchKernelGGL(dec_f5_d, dim3(S / 16, bt), dim3(256), 0, st, k);
   if (d.lstm) {
     hipLaunchKernelGGL(dec_f6_lstm, dim3(4 * S / 16, bt), dim3(512), 0, st, k);
-    hipLaunchKernelGGL(dec_f7_lstm, dim3((R * S + 255) / 256), dim3(256), 0, st, k);
   } else {
     hipLaunchKernelGGL(dec_f6_gru1, dim3(2 * S / 16, bt), dim3(256), 0, st, k);
     hipLaunchKernelGGL(dec_f7_gru2, dim3(S / 16, bt), dim3(256), 0, st, k);
