@@ -161,6 +161,9 @@ struct PArgs {
   // sentinel slots in use per role: kSentRing (a ring, re-armed by the loader wave two steps after every
   // consumer has read a slot) or 0 (one slot per step, all re-armed at launch start; s2s_debug_gru_ring(0))
   int ring;
+  // the BPTT's first sweep (da_h) multiplied chunk by chunk as the chunks arrive (sweep_sent_mfma); 0: sweep, then
+  // multiply.  (The forward's sweeps stay whole: streamed, the forward measured 1030 -> 1349 us per config-2 step.)
+  int stream_sweep;
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
 };
@@ -674,6 +677,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
       unsigned npoll[1] = {0};
 #endif
+      {
       if (loc) ok = SWEEP_SENT(0, av, hs, 4 * (sent_slot(a, s - 1) * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, hg, 8 * (((s - 1) & 1) * slot + (long)br * H), tb + s, wave, lane, a.abort_word);
       GRU_STAMP(1);
@@ -681,6 +685,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       GRU_STAMP_V(8, npoll[0]);
 #endif
       acc = mfma_chunks<NC>(av, w1);
+      }
       // r tiles: the swept operand already holds h_{t-1} of this tile's 16 units (chunk it of
       // wave wt); park it in LDS for the q = r * h epilogue (read after the reduce barrier)
       if (!isz && wave == wt) {
@@ -731,6 +736,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
       unsigned npoll[1] = {0};
 #endif
+      {
       if (loc) ok = SWEEP_SENT(0, av, qs, 4 * (sent_slot(a, s) * slotS + tileS), rowt, wave, lane, a.abort_word);
       else ok = sweep_skinny<NC>(av, qg, 8 * ((s & 1) * slot + (long)br * H), tb + s + 1, wave, lane, a.abort_word);
       GRU_STAMP(4);
@@ -738,6 +744,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       GRU_STAMP_V(9, npoll[0]);
 #endif
       acc = mfma_chunks<NC>(av, w2);
+      }
     }
     sum = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     {
@@ -931,13 +938,26 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 #if S2S_GRU_DIAG
     unsigned npoll[3] = {0, 0, 0};
 #endif
-    bool ok = loc ? SWEEP_SENT(0, av, hs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word)
-                  : sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
+    bool ok;
+    floatx4 acc;
+#if !S2S_GRU_DIAG
+    if (loc && a.stream_sweep) {
+      floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+      ok = sweep_sent_mfma<NC>(av, hs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, wh, acc0, acc1,
+                               a.abort_word);
+      GRU_STAMP(1);  // (the last chunk arrived and its MFMAs are issued)
+      acc = acc0 + acc1;
+    } else
+#endif
+    {
+    ok = loc ? SWEEP_SENT(0, av, hs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word)
+             : sweep_skinny<NC>(av, hg, 8 * (sl * slot + (long)br * H), tag, wave, lane, a.abort_word);
     GRU_STAMP(1);
 #if S2S_GRU_DIAG
     GRU_STAMP_V(8, npoll[0]);
 #endif
-    floatx4 acc = mfma_chunks<NC>(av, wh);
+    acc = mfma_chunks<NC>(av, wh);
+    }
     const float dq = reduce_or_abort(red, &abort_lds, ok, acc, wave, lane, tid, &aborted);
     if (loc) {
       if (live) put_sent(g.s1 + sent_slot(a, p) * slotS + tile_off(ob, ok_, H), (dq * cur.hp) * (cur.r * (1.0f - cur.r)));
@@ -970,6 +990,8 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       __builtin_amdgcn_sched_barrier(0);  // the da_r loads stay ahead of the da_z MFMAs
       mfma_pairs<NC>(az, wzr, acc0, acc1);
       __builtin_amdgcn_sched_barrier(0);
+      // (checked whole: multiplying the da_r chunks as they arrive, sent_tile_mfma, measured 1305 -> 1355 us per
+      // config-2 step)
       if (!sent_tile_check<NC>(rraw, ar))
         ok = ok && sweep_sent_tile<NC>(ar, rs_, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
       GRU_STAMP(4);
@@ -1017,6 +1039,7 @@ constexpr int kExclLds = 124 * 1024;
 
 std::atomic<int> g_allow_local{1};
 std::atomic<int> g_sent_ring{kSentRing};  // s2s_debug_gru_ring(0): one sentinel slot per step (A/B)
+std::atomic<int> g_stream_sweep{1};  // s2s_debug_gru_stream_sweep(0): sweep the whole tile, then multiply (A/B)
 
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
@@ -1165,6 +1188,7 @@ int gru_persist_fwd(hipStream_t st, const GruPersistFwd& f, void* sync) {
   a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nwg = (2 * f.H / 16) * MT;
   a.nmem = 2 * f.H / 16; a.nchains = f.ndir * MT; a.allow_local = g_allow_local;
   a.ring = f.L > kSentRing ? (int)g_sent_ring : 0;
+  a.stream_sweep = g_stream_sweep;
   a.stamps = g_gru_stamps[0];
   a.pstamps = g_gru_pstamps[0];
   if (f.x) {  // fused x-projection by the grid's spare slots
@@ -1213,6 +1237,7 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nwg = (b.H / 16) * MT;
   a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.allow_local = g_allow_local;
   a.ring = b.L > kSentRing ? (int)g_sent_ring : 0;
+  a.stream_sweep = g_stream_sweep;
   a.stamps = g_gru_stamps[1];
   a.pstamps = g_gru_pstamps[1];
   if (b.ydA) {  // fused dy (the layer above's dX) by the grid's spare slots
@@ -1286,6 +1311,7 @@ extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_xp_split(int on) { s2s::g_xp_split = on; }
 extern "C" void s2s_debug_gru_xp_group(int on) { s2s::g_xp_group = on; }
+extern "C" void s2s_debug_gru_stream_sweep(int on) { s2s::g_stream_sweep = on; }
 // diagnostic: 0 = one sentinel slot per step re-armed at launch start (the round-2 form), else the 4-slot ring
 extern "C" void s2s_debug_gru_ring(int on) { s2s::g_sent_ring = on ? s2s::kSentRing : 0; }
 extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {

@@ -343,6 +343,49 @@ __device__ __forceinline__ bool sent_tile_check(const uint4 (&raw)[NC], float4 (
   return __all(ok);
 }
 
+// sweep_sent_tile fused with its product, over loads already issued by sent_tile_issue: chunk i is checked (and
+// polled on its own until published) and multiplied in order, so the MFMAs of the chunks that arrived first run
+// while the later ones are still in flight.  Chunk i accumulates into acc0 (i even) / acc1 (i odd) in x, y, z, w
+// order -- the per-accumulator sequences of mfma_chunks / mfma_pairs, so the sums are bitwise the same; acc0 / acc1
+// come in initialised (zero, or a previous half's partials).  a receives the operands (false: gave up, abort).
+template <int NC>
+__device__ __forceinline__ bool sent_tile_mfma(uint4 (&raw)[NC], float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs,
+                                               long tbase, int rowt, int wave, int lane, const float4* w,
+                                               floatx4& acc0, floatx4& acc1, unsigned* abort_word) {
+  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  unsigned spins = 0;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < NC; ++i) {
+    while (true) {
+      const uint4 p = raw[i];
+      if (__all(p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent)) break;
+      if (spin_give_up(spins, abort_word)) {
+        ok = false;
+        break;
+      }
+      raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + 4L * 256 * (wave + 4 * i)), 0, 16));
+    }
+    a[i] = make_float4(__uint_as_float(raw[i].x), __uint_as_float(raw[i].y), __uint_as_float(raw[i].z),
+                       __uint_as_float(raw[i].w));
+    floatx4& acc = (i & 1) ? acc1 : acc0;
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].x, w[i].x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].y, w[i].y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].z, w[i].z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[i].w, w[i].w, acc, 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // chunk i's MFMAs stay ahead of chunk i + 1's check
+  }
+  return ok;
+}
+template <int NC>
+__device__ __forceinline__ bool sweep_sent_mfma(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
+                                                int wave, int lane, const float4* w, floatx4& acc0, floatx4& acc1,
+                                                unsigned* abort_word) {
+  uint4 raw[NC];
+  sent_tile_issue<NC>(raw, rs, tbase, rowt, wave, lane);
+  return sent_tile_mfma<NC>(raw, a, rs, tbase, rowt, wave, lane, w, acc0, acc1, abort_word);
+}
+
 // sweep_skinny_rows over sentinel rows: all R * NC loads of a pass issued before any check
 template <int NC, int R>
 __device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],
