@@ -683,7 +683,10 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf
     if (big.nblocks >= 256) pl = big;
   }
   const int tiles = pl.nblocks;
-  while (tiles < 512 && pl.nblocks < 1024 && pl.kslice / 2 >= 512) {
+  // (an output of fewer tiles than CUs may split down to 256-long slices: the decoder MLP's 1280 x 448 x 768 product
+  // and the last layer's weight gradient, both on the critical path)
+  const int kmin = tiles < 256 ? 256 : 512;
+  while (tiles < 512 && pl.nblocks < 1024 && pl.kslice / 2 >= kmin) {
     GemmPlan nx = pl;
     nx.kslice = (pl.kslice / 2 + kq - 1) / kq * kq;
     if (!count(nx)) break;
