@@ -940,12 +940,21 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 #endif
     bool ok;
     floatx4 acc;
+    // da_z of this step (published with da_h, at the end of the previous step's p2) is loaded here, behind the da_h
+    // sweep, so p2 starts with it in registers instead of with a sweep of its own (checked there; polled further
+    // only if some value was not yet published)
+    uint4 zraw[NC];
+    bool zpre = false;
 #if !S2S_GRU_DIAG
     if (loc && a.stream_sweep) {
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       ok = sweep_sent_mfma<NC>(av, hs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, wh, acc0, acc1,
                                a.abort_word);
       GRU_STAMP(1);  // (the last chunk arrived and its MFMAs are issued)
+      if constexpr (NC % 2 == 0) {
+        sent_tile_issue<NC>(zraw, zs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane);
+        zpre = true;
+      }
       acc = acc0 + acc1;
     } else
 #endif
@@ -984,7 +993,9 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       // da_z MFMAs overlap the da_r hand-off.  Same instruction sequence as mfma_chunks<2 NC> (bitwise equal).
       float4 az[NC], ar[NC];
       uint4 rraw[NC];
-      ok = sweep_sent_tile<NC>(az, zs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
+      ok = true;
+      if (!zpre || !sent_tile_check<NC>(zraw, az))
+        ok = sweep_sent_tile<NC>(az, zs, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane, a.abort_word);
       sent_tile_issue<NC>(rraw, rs_, 4 * (sent_slot(a, p) * slotS + tileS), rowt, wave, lane);
       floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
       __builtin_amdgcn_sched_barrier(0);  // the da_r loads stay ahead of the da_z MFMAs
