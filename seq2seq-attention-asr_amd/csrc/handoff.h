@@ -626,6 +626,62 @@ __device__ __forceinline__ floatx4 mfma_chunks_aw(const float4 (&a)[NC], const f
   return acc0 + acc1;
 }
 
+// mfma_chunks_aw split across operand groups (concatenated K): each call accumulates one group's chunks (pairs
+// into acc0 / acc1, an odd tail into acc0) with its W fragments from AGPRs; the first call of a product passes init
+// (its first product of each accumulator takes C = 0).  mfma_aw_done closes the chain (the XDL result wait) and
+// returns acc0 + acc1.
+template <int NC>
+__device__ __forceinline__ void mfma_aw_acc(const float4 (&a)[NC], const float4 (&w)[NC], floatx4& acc0,
+                                            floatx4& acc1, bool init) {
+#define S2S_MFMA_AW0(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, 0" : "=&v"(acc) : "v"(x), "a"(y))
+#define S2S_MFMA_AW(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "a"(y))
+#pragma unroll
+  for (int i = 0; i + 1 < NC; i += 2) {
+    if (init && i == 0) {
+      S2S_MFMA_AW0(acc0, a[0].x, w[0].x);
+      S2S_MFMA_AW0(acc1, a[1].x, w[1].x);
+    } else {
+      S2S_MFMA_AW(acc0, a[i].x, w[i].x);
+      S2S_MFMA_AW(acc1, a[i + 1].x, w[i + 1].x);
+    }
+    S2S_MFMA_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA_AW(acc1, a[i + 1].y, w[i + 1].y);
+    S2S_MFMA_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA_AW(acc1, a[i + 1].z, w[i + 1].z);
+    S2S_MFMA_AW(acc0, a[i].w, w[i].w);
+    S2S_MFMA_AW(acc1, a[i + 1].w, w[i + 1].w);
+  }
+  if (NC & 1) {
+    constexpr int i = NC - 1;
+    if (init && NC == 1) {
+      S2S_MFMA_AW0(acc0, a[i].x, w[i].x);
+      acc1 = floatx4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      S2S_MFMA_AW(acc0, a[i].x, w[i].x);
+    }
+    S2S_MFMA_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA_AW(acc0, a[i].w, w[i].w);
+  }
+#undef S2S_MFMA_AW0
+#undef S2S_MFMA_AW
+}
+__device__ __forceinline__ floatx4 mfma_aw_done(floatx4 acc0, floatx4 acc1) {
+  asm volatile("s_nop 11" : "+v"(acc0), "+v"(acc1));
+  return acc0 + acc1;
+}
+
+// sweep_sent's first pass, loads only (its layout; checked with sent_tile_check, polled further with sweep_sent)
+template <int NC>
+__device__ __forceinline__ void sent_row_issue(uint4 (&raw)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, int wave,
+                                               int lane) {
+  const long kq = 4 * (lane >> 4);
+#pragma unroll
+  for (int i = 0; i < NC; ++i)
+    raw[i] = __builtin_bit_cast(uint4,
+                                __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(row_off + 4 * (wave * 16 + 64 * i + kq)), 0, 16));
+}
+
 // W operand fragments of one output-unit row (chunk i at wave*16 + 64 i), kept in VGPRs
 template <int NC>
 __device__ __forceinline__ void load_wfrag(float4 (&w)[NC], const float* row, int wave, int lane) {
