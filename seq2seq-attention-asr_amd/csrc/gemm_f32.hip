@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 namespace s2s {
 
@@ -686,6 +687,37 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf
   // (an output of fewer tiles than CUs may split down to 256-long slices: the decoder MLP's 1280 x 448 x 768 product
   // and the last layer's weight gradient, both on the critical path)
   const int kmin = tiles < 256 ? 256 : 512;
+  static const bool fill = [] {
+    const char* e = std::getenv("S2S_GEMM_FILL");  // 0: the older halving rule below (diagnostics)
+    return !(e && std::strcmp(e, "0") == 0);
+  }();
+  if (tiles < 512 && fill && !bf16) {  // (bf16: no step gain measured, config 3 4.063 vs 4.079 ms)
+    // The split whose blocks all fit the chip in one round, with the shortest slice: time ~ rounds x slice,
+    // rounds = ceil(blocks / resident slots), slots = 256 CUs x the blocks one CU holds by LDS.  A split that
+    // leaves a short second round costs a whole slice more (layer 1's weight gradient, 144 tiles x K = 4096:
+    // 8 slices of 512 = 1152 blocks, 2 rounds; 7 slices of 608 = 1008 blocks, one round: 96.3 -> 88.7 us in
+    // tools/gemm_bench; the decoder MLP 22.8 -> 20.1 us; config-2 step 3.309 -> 3.304 ms, same-box A/B).
+    const size_t lds = 2 * (size_t)(pl.bm + pl.bn) * LDK * sizeof(float);
+    const long slots = 256L * std::max<long>(1, std::min<long>(8, (long)(160 * 1024 / lds)));
+    auto cost = [&](const GemmPlan& q) { return (double)((q.nblocks + slots - 1) / slots) * q.kslice; };
+    GemmPlan best = pl;
+    double bc = cost(pl);
+    int prev = pl.kslice;
+    for (int s = 2;; ++s) {
+      GemmPlan nx = pl;
+      nx.kslice = ((kfull + s - 1) / s + kq - 1) / kq * kq;
+      if (nx.kslice < kmin) break;
+      if (nx.kslice == prev) continue;
+      prev = nx.kslice;
+      if (!count(nx)) break;
+      const double c = cost(nx);
+      if (c < bc) {
+        bc = c;
+        best = nx;
+      }
+    }
+    return best;
+  }
   while (tiles < 512 && pl.nblocks < 1024 && pl.kslice / 2 >= kmin) {
     GemmPlan nx = pl;
     nx.kslice = (pl.kslice / 2 + kq - 1) / kq * kq;

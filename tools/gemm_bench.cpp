@@ -162,13 +162,24 @@ int main() {
     tot_rb += mult * ur;
     std::printf("%-18s %8.2f %9.1f %9.1f %9.1f %9.1f %10.2e  x%d\n", c.name.c_str(), fl / 1e9, uo, fl / uo / 1e6, ur,
                 fl / ur / 1e6, mx, mult);
-    if (std::getenv("SWEEP")) {  // forced plans: tile shape x K slice
+    const char* only = std::getenv("SWEEP_CASE");  // sweep one case by name prefix (default: all)
+    if (std::getenv("SWEEP") && (!only || c.name.rfind(only, 0) == 0)) {  // forced plans: tile shape x K slice
       const char* tiles[3] = {"128:128", "128:64", "64:64"};
       int kmax = 0;
       for (const Shape& sh : c.p) kmax = sh.K > kmax ? sh.K : kmax;
+      std::vector<int> kss;
+      if (const char* l = std::getenv("SWEEP_KS")) {  // "352,416,512": explicit K slices
+        for (const char* q = l; *q;) {
+          kss.push_back(std::atoi(q));
+          while (*q && *q != ',') ++q;
+          if (*q == ',') ++q;
+        }
+      } else {
+        for (int ks = 0; ks <= kmax; ks = ks == 0 ? 128 : ks * 2) kss.push_back(ks);
+      }
       for (const char* t : tiles) {
         std::printf("    %-8s", t);
-        for (int ks = 0; ks <= kmax; ks = ks == 0 ? 128 : ks * 2) {
+        for (int ks : kss) {
           char buf[64];
           std::snprintf(buf, sizeof buf, "%s:%d", t, ks);
           setenv("S2S_GEMM_PLAN", buf, 1);
@@ -179,7 +190,19 @@ int main() {
           CK(hipEventSynchronize(e1));
           float ms = 0;
           CK(hipEventElapsedTime(&ms, e0, e1));
-          std::printf(" ks%d=%.1f", ks, 1e3 * ms / reps);
+          // one isolated call (the step's tail: nothing queued behind it), averaged over reps
+          float iso = 0;
+          for (int r = 0; r < reps; ++r) {
+            float m1 = 0;
+            CK(hipStreamSynchronize(st));
+            CK(hipEventRecord(e0, st));
+            run_ours();
+            CK(hipEventRecord(e1, st));
+            CK(hipEventSynchronize(e1));
+            CK(hipEventElapsedTime(&m1, e0, e1));
+            iso += m1;
+          }
+          std::printf(" ks%d=%.1f/%.1f", ks, 1e3 * ms / reps, 1e3 * iso / reps);
         }
         std::printf("\n");
       }
