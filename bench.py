@@ -26,7 +26,7 @@ CONFIGS = {
     # name: (model kwargs, B per GPU, L, T)
     "timit_chorowski_b32": (dict(), 32, 128, 40),
     "librispeech_chorowski_b32": (dict(inputFrameSize=80, outputDepth=29), 32, 400, 200),
-    # BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64 (fp32 here)
+    # BASELINE config 3 class: model_chorowski_baseline_dropout.lua (p = 0.5), B = 64 (bf16 hoisted GEMMs: PRECISION)
     "timit_chorowski_dropout_b64": (dict(dropout=0.5), 64, 128, 40),
     # config 2's model on TIMIT-like variable-length utterances (oracle.timit_like_lengths): length-sorted
     # minibatches of 32, each padded to its longest utterance, masked (s2s_model_dims.frame_lengths /
@@ -39,7 +39,7 @@ CONFIGS = {
 CONFIG_DESC = {
     "timit_chorowski_b32": ("BASELINE config 2", "timit/model_chorowski_baseline.lua"),
     "librispeech_chorowski_b32": ("BASELINE config 4 shape (1 GPU)", "librispeech/model_chorowski_baseline.lua"),
-    "timit_chorowski_dropout_b64": ("BASELINE config 3 (fp32)", "timit/model_chorowski_baseline_dropout.lua"),
+    "timit_chorowski_dropout_b64": ("BASELINE config 3 (bf16)", "timit/model_chorowski_baseline_dropout.lua"),
     "timit_ragged_b32": ("BASELINE config 2 model, TIMIT-like variable lengths", "timit/model_chorowski_baseline.lua"),
     "librispeech_vgg_b16": ("BASELINE config 5 (1 GPU)", "librispeech/model_vgg.lua"),
 }
@@ -592,6 +592,15 @@ def main():
                              "GEMM its spare-slot producers compute inside the launch (forward: the x-projection; "
                              "backward: dy = the layer above's dX, or for the top layer the decoder's dh = "
                              "dVh V + sum_t alpha dc), averaged over the step's launches")
+                # the recurrence alone (what the persistent kernel exists for), priced the same way: rec_frac
+                Hs = [cfg.hiddenFrameSize] * (cfg.numLayers - 1) + [cfg.outputFrameSize]
+                rec = sum(2.0 * 2 * B * L * 3.0 * h * h for h in Hs) / len(Hs)
+                rec_ach = rec / (r["avg_launch_us"] * 1e-6) / 1e12
+                r["rec_flops_per_launch"] = rec
+                r["rec_achieved"] = round(rec_ach, 3)
+                r["rec_frac"] = round(rec_ach / r["peak"], 4)
+                r["rec_what"] = ("the recurrence alone: 2 directions x 2 B L 3H^2 per launch (no in-launch GEMM) / the "
+                                 "same live launch time, against the same fp32 MFMA peak")
         # the decoder recurrences (the attention path): priced against their own hand-off latency floor; the
         # HBM rate is the counters' bytes (the attention operands themselves stay in LDS, profile.py)
         out["roofline_decoder"] = []

@@ -111,16 +111,19 @@ int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
  * W[d*NP + p], NP = 16 (22 with peepholes), W = (out, in):
  *   for q in (i, f, g, o): Wqx (H, D), bqx (H), Wqh (H, H), bqh (H)
  *   peepholes:             Wic (H, H), bic (H), Wfc (H, H), bfc (H), Woc (H, H), boc (H)
- * y / saved / dy / dx / dW conventions as the GRU calls; dW and the bias grads accumulate. */
+ * y / saved / dy / dx / dW conventions as the GRU calls; dW and the bias grads accumulate.
+ * lengths: (B) frames per utterance or NULL, as for the GRU calls: h_t = c_t = 0 on padding frames t >= L_b
+ * (y = 0 there, the reverse direction starts from zero state at the utterance's own last frame), and the
+ * backward treats dL/dh_t = dL/dc_t = 0 there (pass the same lengths to fwd and bwd). */
 size_t s2s_lstm_saved_bytes(int B, int L, int H);
 size_t s2s_lstm_scratch_bytes(int ndir, int B, int L, int D, int H, int peepholes);
 int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
                  const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy,
-                 void* const* saved, void* scratch, size_t scratch_bytes);
+                 void* const* saved, const int* lengths, void* scratch, size_t scratch_bytes);
 int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
                  const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved,
                  const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW,
-                 float scale, void* scratch, size_t scratch_bytes);
+                 float scale, const int* lengths, void* scratch, size_t scratch_bytes);
 
 /* ---------------------------------------------------------------- attention decoder
  * nn.Attention(decoder_recurrent = GRU(S,S), decoder_mlp = Maxout(S+A, M, K) -> Linear(M, O)
@@ -370,6 +373,15 @@ int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, siz
  * queued in program order behind the failed step; calls made after the host has seen it fail outright. */
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
                             float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+/* Data parallel: a rank whose persistent launch failed still sends its (invalid) gradients into the all-reduce,
+ * so every replica must skip that update, not only the failing one.  s2s_ctx_status_flag writes flag[0] = 1.0f
+ * if the context's failure status is set when it runs on `stream` (stream-ordered, no host sync), else 0.0f;
+ * all-reduce it (sum or max) across the ranks and pass it as skip_flag: the update is then skipped on every rank
+ * when *skip_flag != 0 (or the local status is set).  skip_flag NULL = s2s_optim_adadelta_step. */
+int s2s_ctx_status_flag(s2s_ctx* ctx, s2s_stream_t stream, float* flag);
+int s2s_optim_adadelta_step_flag(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                                 float* grads, size_t n, void* state, const long* mats, int n_mats,
+                                 float* gradnorm, const float* skip_flag);
 /* the model's weight matrices (every module weight: encoder W_z/W_r/W_h, V, Ws, we, Wy, Wc, Wd, decoder
  * W_z/W_r/W_h, Wm, Wo) as (offset, rows, cols) triples; returns their count (mats may be NULL) */
 int s2s_model_weight_matrices(const s2s_model_dims* d, long* mats);

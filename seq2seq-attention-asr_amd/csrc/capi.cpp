@@ -802,10 +802,11 @@ static int fill_lstm_io(LstmLayerIO& io, int ndir, int B, int L, int D, int H, i
 
 int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
                  const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy,
-                 void* const* saved, void* scratch, size_t scratch_bytes) {
+                 void* const* saved, const int* lengths, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
   LstmLayerIO io{};
   S2S_TRY(fill_lstm_io(io, ndir, B, L, D, H, peepholes, reverse, x, ldx, W, y, ldy, saved));
+  io.len = lengths;
   S2S_REQUIRE(y != nullptr, "lstm: null y");
   for (int d = 0; d < ndir; ++d) S2S_REQUIRE(y[d] != nullptr, "lstm: null y");
   io.status = ctx->status_dev;
@@ -815,10 +816,11 @@ int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
 int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes,
                  const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved,
                  const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW,
-                 float scale, void* scratch, size_t scratch_bytes) {
+                 float scale, const int* lengths, void* scratch, size_t scratch_bytes) {
   S2S_TRY(set_device(ctx));
   LstmLayerIO io{};
   S2S_TRY(fill_lstm_io(io, ndir, B, L, D, H, peepholes, reverse, x, ldx, W, nullptr, H, saved));
+  io.len = lengths;
   S2S_REQUIRE(dy && dW, "lstm: null dy/dW");
   LstmLayerGrad gr{};
   for (int d = 0; d < ndir; ++d) {
@@ -1258,16 +1260,35 @@ int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, siz
   return optim_set_noise_step(static_cast<hipStream_t>(stream), state, n, t);
 }
 
-int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
-                            float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
+static int adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                         float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm,
+                         const float* skip_flag) {
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(cfg != nullptr, "optim: null config");
   S2S_REQUIRE(cfg->rho >= 0.f && cfg->rho < 1.f && cfg->eps > 0.f && cfg->maxnorm > 0.f, "optim: bad config");
   const OptimConfig c{cfg->rho,           cfg->eps,           cfg->maxnorm,       cfg->weightDecay,
                       cfg->colnorm_max,   cfg->gradnoise_eta, cfg->gradnoise_gamma, cfg->gradnoise_seed};
-  // device-side guard: the update is skipped if the context's failure status is set when it runs
+  // device-side guard: the update is skipped if the context's failure status (or *skip_flag) is set when it runs
   return optim_adadelta_step(static_cast<hipStream_t>(stream), c, params, grads, n, state, mats, n_mats, gradnorm,
-                             ctx->status_dev);
+                             ctx->status_dev, skip_flag);
+}
+
+int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                            float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm) {
+  return adadelta_step(ctx, stream, cfg, params, grads, n, state, mats, n_mats, gradnorm, nullptr);
+}
+
+int s2s_optim_adadelta_step_flag(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params,
+                                 float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm,
+                                 const float* skip_flag) {
+  return adadelta_step(ctx, stream, cfg, params, grads, n, state, mats, n_mats, gradnorm, skip_flag);
+}
+
+int s2s_ctx_status_flag(s2s_ctx* ctx, s2s_stream_t stream, float* flag) {
+  S2S_REQUIRE(ctx != nullptr && flag != nullptr, "null argument");
+  S2S_CHECK_HIP(hipSetDevice(ctx->device));
+  S2S_REQUIRE(ctx->status_dev != nullptr, "context has no status words");
+  return status_flag(static_cast<hipStream_t>(stream), ctx->status_dev, flag);
 }
 
 int s2s_model_bucket_count(const s2s_model_dims* d) {

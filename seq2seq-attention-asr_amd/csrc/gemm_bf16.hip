@@ -63,7 +63,13 @@ void* stage_acquire(hipStream_t st, size_t bytes) {
   if (k < 0)
     for (int i = 0; i < GemmStage::kStreams && k < 0; ++i)
       if (!s->p[i]) k = i;
-  if (k < 0) return nullptr;
+  if (k < 0) {  // every slot holds another stream's buffer: the caller falls back to the 64 x 64 tile GEMM
+    static std::atomic<int> warned{0};
+    if (!warned.exchange(1))
+      std::fprintf(stderr, "s2s: bf16 GEMM staging slots exhausted (%d streams); big GEMMs on further streams use "
+                           "the 64x64 tiles\n", GemmStage::kStreams);
+    return nullptr;
+  }
   void* p = nullptr;
   const size_t want = std::max(bytes, s->n[k] * 2);
   if (hipMalloc(&p, want) != hipSuccess) return nullptr;

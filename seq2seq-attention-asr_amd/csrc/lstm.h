@@ -22,6 +22,8 @@ struct LstmLayerIO {
   float* y[2];  // y[d][(b*L + t)*ldy + j]
   long ldy;
   float* saved[2];  // per direction (B, L, 8H): i | f | g | o | c | c_{t-1} | h_{t-1} | tanh(c)
+  // (B) frames per utterance (device), null = all L: h_t = c_t = 0 for t >= len_b; the backward zeroes dh, dc there
+  const int* len = nullptr;
   // the calling context's status words: the persistent launches are followed by a harvest of their sync region
   // into them (s2s_ctx_status); null = no harvest
   unsigned* status = nullptr;
@@ -51,6 +53,7 @@ struct LstmPersistArgs {
   long lddy;
   float* dA[2];
   long ldA;
+  const int* len;  // (B) frames per utterance or null (LstmLayerIO::len)
 };
 bool lstm_persist_supported(int ndir, int B, int H, int peep);
 size_t lstm_persist_sync_bytes(int ndir, int B, int L, int H);

@@ -35,6 +35,7 @@ struct LstmFwdDir {
 struct LstmFwdArgs {
   LstmFwdDir d[2];
   int B, L, H, peep, step;
+  const int* len;  // (B) frames per utterance or null: h_t = c_t = 0 for t >= len_b
 };
 
 // k1: gate pre-activations.  Workgroup tile = 16 columns of one gate q = n0 / H.
@@ -85,7 +86,8 @@ __global__ void lstm_fwd_cell(LstmFwdArgs a) {
   const long row = (long)b * L + t;
   float* sv = g.sv + row * SV_N * H;
   const float cp = step > 0 ? g.sv[((long)b * L + (g.reverse ? t + 1 : t - 1)) * SV_N * H + SV_C * H + j] : 0.f;
-  const float c = sv[SV_F * H + j] * cp + sv[SV_I * H + j] * sv[SV_G * H + j];
+  float c = sv[SV_F * H + j] * cp + sv[SV_I * H + j] * sv[SV_G * H + j];
+  if (a.len && t >= a.len[b]) c = 0.f;  // padding frame: zero state (the o gate's k3 then gives h = 0)
   sv[SV_C * H + j] = c;
   if (!a.peep) {
     const float tc = tanhf(c);
@@ -123,11 +125,11 @@ __global__ __launch_bounds__(1024) void lstm_fwd_step(LstmFwdArgs a) {
   const float cp = step > 0 ? g.sv[((long)b * L + tp) * SV_N * H + SV_C * H + j] : 0.f;
   sv[SV_HP * H + j] = step > 0 ? g.y[((long)b * L + tp) * g.ldy + j] : 0.f;
   sv[SV_CP * H + j] = cp;
-  const float c = gf * cp + gi * gg;
+  float c = gf * cp + gi * gg, tc = tanhf(c), h = go * tc;
+  if (a.len && t >= a.len[b]) c = tc = h = 0.f;  // padding frame: zero state and output
   sv[SV_C * H + j] = c;
-  const float tc = tanhf(c);
   sv[SV_TC * H + j] = tc;
-  g.y[row * g.ldy + j] = go * tc;
+  g.y[row * g.ldy + j] = h;
 }
 
 // k3 (peepholes): o = sig(pre_o + Woc c'), h' = o * tanh(c')
@@ -170,6 +172,7 @@ struct LstmBwdDir {
 struct LstmBwdArgs {
   LstmBwdDir d[2];
   int B, L, H, peep, step;
+  const int* len;  // (B) frames per utterance or null: dL/dh_t = dL/dc_t = 0 for t >= len_b
 };
 
 // cell-side gate gradients from the complete dL/dc_t (LSTM.lua:118-136 via the graph)
@@ -194,8 +197,9 @@ __global__ void lstm_bwd_elem(LstmBwdArgs a) {
   const long row = (long)b * L + t;
   const float* sv = g.sv + row * SV_N * H;
   const float o = sv[SV_O * H + j], tc = sv[SV_TC * H + j];
-  const float dh = g.dy[row * g.lddy + j] + g.dhc[idx];
-  const float dc = g.dcc[idx] + dh * o * (1.0f - tc * tc);
+  const bool pad = a.len && t >= a.len[b];
+  const float dh = pad ? 0.f : g.dy[row * g.lddy + j] + g.dhc[idx];
+  const float dc = pad ? 0.f : g.dcc[idx] + dh * o * (1.0f - tc * tc);
   g.dA[row * g.ldA + 3 * H + j] = (dh * tc) * (o * (1.0f - o));
   if (a.peep) g.dcn[idx] = dc;
   else lstm_cell_grads(g, H, row, b, j, dc);
@@ -269,8 +273,9 @@ __global__ __launch_bounds__(512) void lstm_bwd_step(LstmBwdArgs a, int first) {
   const long row = (long)b * L + t;
   const float* sv = g.sv + row * SV_N * H;
   const float o = sv[SV_O * H + j], tc = sv[SV_TC * H + j];
-  const float dh = g.dy[row * g.lddy + j] + dhc;
-  const float dc = dcc + dh * o * (1.0f - tc * tc);
+  const bool pad = a.len && t >= a.len[b];
+  const float dh = pad ? 0.f : g.dy[row * g.lddy + j] + dhc;
+  const float dc = pad ? 0.f : dcc + dh * o * (1.0f - tc * tc);
   g.dA[row * g.ldA + 3 * H + j] = (dh * tc) * (o * (1.0f - o));
   lstm_cell_grads(g, H, row, b, j, dc);
 }
@@ -340,7 +345,7 @@ struct Carve {
   void* sync;  // the persistent launches' hand-off region (lstm_persist_sync_bytes)
   size_t bytes;
 };
-Carve carve(void* scratch, int nd, int B, int L, int D, int H) {
+Carve carve(void* scratch, int nd, int B, int L, int D, int H, int peep) {
   Carve c{};
   Bump bp{static_cast<char*>(scratch), 0, 0};
   c.Wx4 = bp.take<float>(4L * nd * H * D);
@@ -356,7 +361,8 @@ Carve carve(void* scratch, int nd, int B, int L, int D, int H) {
     c.dcn[d] = bp.take<float>((long)B * H);
   }
   c.ws = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
-  c.sync = bp.take<char>(lstm_persist_sync_bytes(nd, B, L, H));
+  // the persistent launches' hand-off region, only where they run (lstm_persist_supported)
+  c.sync = lstm_persist_supported(nd, B, H, peep) ? bp.take<char>(lstm_persist_sync_bytes(nd, B, L, H)) : nullptr;
   c.bytes = bp.off + 256;
   return c;
 }
@@ -374,15 +380,14 @@ int check(const LstmLayerIO& io) {
 
 size_t lstm_saved_bytes(int B, int L, int H) { return sizeof(float) * (size_t)B * L * SV_N * H; }
 size_t lstm_scratch_bytes(int ndir, int B, int L, int D, int H, int peep) {
-  (void)peep;
-  return carve(nullptr, ndir, B, L, D, H).bytes;
+  return carve(nullptr, ndir, B, L, D, H, peep).bytes;
 }
 
 int lstm_layer_fwd(hipStream_t st, const LstmLayerIO& io, void* scratch, size_t scratch_bytes) {
   S2S_TRY(check(io));
   const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H, np = lstm_nparams(io.peep);
   S2S_REQUIRE(scratch_bytes >= lstm_scratch_bytes(nd, B, L, D, H, io.peep), "lstm: scratch too small");
-  Carve c = carve(scratch, nd, B, L, D, H);
+  Carve c = carve(scratch, nd, B, L, D, H, io.peep);
   for (int d = 0; d < nd; ++d)
     S2S_TRY(launch_lstm_pack(st, io.W + d * np, H, D, io.peep, c.Wx4 + 4L * d * H * D, c.bias4 + 4L * d * H, nullptr,
                              nullptr));
@@ -391,7 +396,7 @@ int lstm_layer_fwd(hipStream_t st, const LstmLayerIO& io, void* scratch, size_t 
                 c.ws));
   if (lstm_persist_supported(nd, B, H, io.peep)) {  // the whole sweep in one launch (lstm_persist.hip)
     LstmPersistArgs f{};
-    f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 4L * nd * H; f.ldy = io.ldy;
+    f.ndir = nd; f.B = B; f.L = L; f.H = H; f.ldxp = 4L * nd * H; f.ldy = io.ldy; f.len = io.len;
     for (int d = 0; d < nd; ++d) {
       const float* const* W = io.W + d * np;
       f.reverse[d] = io.reverse[d];
@@ -409,7 +414,7 @@ int lstm_layer_fwd(hipStream_t st, const LstmLayerIO& io, void* scratch, size_t 
                         {io.peep ? W[16] : nullptr, io.peep ? W[18] : nullptr, io.peep ? W[20] : nullptr},
                         io.y[d], io.ldy, io.saved[d], io.reverse[d]};
   }
-  a.B = B; a.L = L; a.H = H; a.peep = io.peep;
+  a.B = B; a.L = L; a.H = H; a.peep = io.peep; a.len = io.len;
   const dim3 gg(4 * H / 16, (B + 15) / 16, nd), gc((B * H + 255) / 256, nd), go(H / 16, (B + 15) / 16, nd);
   ProfScope ps(st, "lstm_fwd_steps", 2.0 * nd * B * L * 4.0 * H * H * (io.peep ? 1.75 : 1.0), 0.0);
   const dim3 gs(H / 16, (B + 15) / 16, nd);
@@ -433,7 +438,7 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
   const int nd = io.ndir, B = io.B, L = io.L, D = io.D, H = io.H, np = lstm_nparams(io.peep);
   S2S_REQUIRE(scratch_bytes >= lstm_scratch_bytes(nd, B, L, D, H, io.peep), "lstm: scratch too small");
   S2S_REQUIRE(gr.dW != nullptr, "lstm: null dW");
-  Carve c = carve(scratch, nd, B, L, D, H);
+  Carve c = carve(scratch, nd, B, L, D, H, io.peep);
   const long ldA = 4L * nd * H;
   LstmBwdArgs a{};
   for (int d = 0; d < nd; ++d) {
@@ -446,11 +451,11 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
     a.d[d] = LstmBwdDir{gr.dy[d], gr.lddy, io.saved[d], c.WocT[d], c.Wb[d], c.dA + 4L * d * H, ldA,
                         c.dhc[d], c.dcc[d], c.dcp[d], c.dcn[d], io.reverse[d]};
   }
-  a.B = B; a.L = L; a.H = H; a.peep = io.peep;
+  a.B = B; a.L = L; a.H = H; a.peep = io.peep; a.len = io.len;
   const dim3 ge((B * H + 255) / 256, nd), gp(H / 16, (B + 15) / 16, nd), gb(2 * H / 16, (B + 15) / 16, nd);
   if (lstm_persist_supported(nd, B, H, io.peep)) {  // the whole BPTT sweep in one launch (lstm_persist.hip)
     LstmPersistArgs b{};
-    b.ndir = nd; b.B = B; b.L = L; b.H = H; b.lddy = gr.lddy; b.ldA = ldA;
+    b.ndir = nd; b.B = B; b.L = L; b.H = H; b.lddy = gr.lddy; b.ldA = ldA; b.len = io.len;
     for (int d = 0; d < nd; ++d) {
       b.reverse[d] = io.reverse[d];
       b.Wb[d] = c.Wb[d];

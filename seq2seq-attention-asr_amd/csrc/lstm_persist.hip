@@ -47,6 +47,7 @@ struct LDir {
 };
 struct LArgs {
   LDir d[2];
+  const int* len;  // (B) frames per utterance or null (lstm.h LstmLayerIO::len)
   int B, L, H, MT, nmem, nchains, allow_local;
   unsigned* abort_word;
   unsigned* census;
@@ -113,6 +114,7 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist(LArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = mt * 16, ob = b0 + (tid >> 4), j = m * 16 + (tid & 15);
   const bool live = ob < B;
+  const int lenb = (a.len && live) ? a.len[ob] : L;  // padding frames t >= lenb: zero state and output
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const long slotS = (long)a.MT * 16 * H, tileS = (long)mt * 16 * H, mytile = tileS + (long)m * 256;
@@ -170,9 +172,8 @@ __global__ __launch_bounds__(256) void lstm_fwd_persist(LArgs a) {
     // LSTM.lua:38-50: i, f, o sigmoid, g tanh; c = f c' + i g; h = o tanh(c)  (lstm_fwd_step's expressions)
     const float gi = sigmoidf_(sg[0] + xc[0]), gf = sigmoidf_(sg[1] + xc[1]);
     const float gg = tanhf(sg[2] + xc[2]), go = sigmoidf_(sg[3] + xc[3]);
-    const float c = gf * creg + gi * gg;
-    const float tc = tanhf(c);
-    const float h = go * tc;
+    float c = gf * creg + gi * gg, tc = tanhf(c), h = go * tc;
+    if (t >= lenb) c = tc = h = 0.f;  // lstm_fwd_step's masking
     if (loc) {  // critical first
       if (live) put_sent(g.sent + s * slotS + tile_off(ob, j, H), h);
     } else {
@@ -212,6 +213,7 @@ __global__ __launch_bounds__(512) void lstm_bwd_persist(LArgs a) {
   const bool out = tid < 256;  // threads 0..255 own (utterance, unit) outputs
   const int b0 = mt * 16, ob = b0 + ((tid & 255) >> 4), j = m * 16 + (tid & 15);
   const bool live = out && ob < B;
+  const int lenb = (a.len && live) ? a.len[ob] : L;  // padding frames t >= lenb: dL/dh = dL/dc = 0
   if (tid == 0) abort_lds = 0;
   const unsigned tb = launch_tagbase(a.abort_word, &tb_lds);
   const long slotS = (long)a.MT * 16 * W, tileS = (long)mt * 16 * W;
@@ -269,8 +271,9 @@ __global__ __launch_bounds__(512) void lstm_bwd_persist(LArgs a) {
     const bool aborted = abort_lds != 0;
     if (out) {
       // lstm_bwd_step's expressions: dh = dy + carry; dc = dcc + dh o (1 - tanh^2 c); gate gradients
-      const float dh = cur.dy + (p > 0 ? sh : 0.f);
-      const float dc = (p > 0 ? dcp + 0.f : 0.f) + dh * cur.o * (1.0f - cur.tc * cur.tc);
+      const bool pad = t >= lenb;
+      const float dh = pad ? 0.f : cur.dy + (p > 0 ? sh : 0.f);
+      const float dc = pad ? 0.f : (p > 0 ? dcp + 0.f : 0.f) + dh * cur.o * (1.0f - cur.tc * cur.tc);
       const float dao = (dh * cur.tc) * (cur.o * (1.0f - cur.o));
       const float dai = (dc * cur.gg) * (cur.i * (1.0f - cur.i));
       const float daf = (dc * cur.cp) * (cur.f * (1.0f - cur.f));
@@ -319,18 +322,21 @@ int launch_bwd_nc(hipStream_t st, const LArgs& a) {
 }
 
 size_t census_bytes_l(int nchains, int nmem) { return ((size_t)4 * nchains * nmem + 255) / 256 * 256; }
-size_t gran_bytes_l(int B, int H) { return 2 * sizeof(granule_t) * 2 * (size_t)B * 4 * H; }  // [dir][2][B][4H]
-size_t prep_bytes_l(int B, int H, int nchains, int nmem) { return 256 + census_bytes_l(nchains, nmem) + gran_bytes_l(B, H); }
+// [ndir][2][B][4H] tagged granules: ndir = nchains / row tiles
+size_t gran_bytes_l(int nd, int B, int H) { return (size_t)nd * sizeof(granule_t) * 2 * (size_t)B * 4 * H; }
+size_t prep_bytes_l(int B, int H, int nchains, int nmem) {
+  return 256 + census_bytes_l(nchains, nmem) + gran_bytes_l(nchains / ((B + 15) / 16), B, H);
+}
 
 void carve_sync(char* sync, int B, int L, int H, int nchains, int nmem, LArgs& a) {
   a.abort_word = reinterpret_cast<unsigned*>(sync);
   a.census = reinterpret_cast<unsigned*>(sync + 256);
   granule_t* gp = reinterpret_cast<granule_t*>(sync + 256 + census_bytes_l(nchains, nmem));
   float* sp = reinterpret_cast<float*>(sync + prep_bytes_l(B, H, nchains, nmem));
-  const int MT = (B + 15) / 16;
+  const int MT = (B + 15) / 16, nd = nchains / MT;
   for (int d = 0; d < 2; ++d) {
-    a.d[d].gran = gp + (long)d * 2 * B * 4 * H;
-    a.d[d].sent = sp + (long)d * L * MT * 16 * 4 * H;
+    a.d[d].gran = d < nd ? gp + (long)d * 2 * B * 4 * H : nullptr;
+    a.d[d].sent = d < nd ? sp + (long)d * L * MT * 16 * 4 * H : nullptr;
   }
 }
 
@@ -345,15 +351,16 @@ bool lstm_persist_supported(int ndir, int B, int H, int peep) {
   return nmem * ((nchains + 7) / 8) <= 32;
 }
 
+// the hand-off region of ndir directions (sentinel slots: one per step, [ndir][L][row tiles][16][4H])
 size_t lstm_persist_sync_bytes(int ndir, int B, int L, int H) {
   const int MT = (B + 15) / 16, nchains = ndir * MT, nmem = H / 16;
-  return prep_bytes_l(B, H, nchains, nmem) + sizeof(float) * 2 * (size_t)L * MT * 16 * 4 * H;
+  return prep_bytes_l(B, H, nchains, nmem) + sizeof(float) * (size_t)ndir * L * MT * 16 * 4 * H;
 }
 
 int lstm_persist_fwd(hipStream_t st, const LstmPersistArgs& f, void* sync, unsigned* status) {
   LArgs a{};
   const int MT = (f.B + 15) / 16;
-  a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nmem = f.H / 16; a.nchains = f.ndir * MT;
+  a.B = f.B; a.L = f.L; a.H = f.H; a.MT = MT; a.nmem = f.H / 16; a.nchains = f.ndir * MT; a.len = f.len;
   a.allow_local = g_lstm_local;
   carve_sync(static_cast<char*>(sync), f.B, f.L, f.H, a.nchains, a.nmem, a);
   for (int d = 0; d < f.ndir; ++d) {
@@ -381,7 +388,7 @@ int lstm_persist_fwd(hipStream_t st, const LstmPersistArgs& f, void* sync, unsig
 int lstm_persist_bwd(hipStream_t st, const LstmPersistArgs& b, void* sync, unsigned* status) {
   LArgs a{};
   const int MT = (b.B + 15) / 16;
-  a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nmem = b.H / 16; a.nchains = b.ndir * MT;
+  a.B = b.B; a.L = b.L; a.H = b.H; a.MT = MT; a.nmem = b.H / 16; a.nchains = b.ndir * MT; a.len = b.len;
   a.allow_local = g_lstm_local;
   carve_sync(static_cast<char*>(sync), b.B, b.L, b.H, a.nchains, a.nmem, a);
   for (int d = 0; d < b.ndir; ++d) {

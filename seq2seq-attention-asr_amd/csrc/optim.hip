@@ -76,9 +76,12 @@ __device__ __forceinline__ float noise_normal(unsigned long long key, size_t i) 
 // on this stream).  A set word means a persistent launch of an earlier step timed out and its gradients are
 // invalid: the whole update is skipped on the device (parameters, state and noise counter untouched), so calls
 // already queued in program order behind the failed step cannot apply them before the host gate sees it.
+// skip_flag (optional): a device float, nonzero = skip as well -- data parallel: every rank's failure flag
+// (s2s_ctx_status_flag) summed over the ranks, so a failure on ANY rank (whose invalid gradients went into the
+// all-reduce) makes every replica skip the same update and the replicas stay identical.
 __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb, float maxnorm, float eta,
                                                     float gamma, float* scal, float* gradnorm_out,
-                                                    const unsigned* status) {
+                                                    const unsigned* status, const float* skip_flag) {
   __shared__ float red[4];
   float s = 0.f;
   for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
@@ -86,8 +89,9 @@ __global__ __launch_bounds__(256) void opt_finalize(const float* partial, int nb
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
   __syncthreads();
   if (threadIdx.x == 0) {
-    const bool skip = status && ((__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) |
-                                  __hip_atomic_load(status + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u);
+    const bool skip = (status && ((__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) |
+                                   __hip_atomic_load(status + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u)) ||
+                      (skip_flag && *skip_flag != 0.f);
     scal[4] = skip ? 1.f : 0.f;
     const float gn = sqrtf(((red[0] + red[1]) + red[2]) + red[3]);
     if (gradnorm_out) *gradnorm_out = gn;
@@ -163,7 +167,8 @@ size_t optim_state_bytes(size_t n) {
 }
 
 int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
-                        const long* mats, int n_mats, float* gradnorm, const unsigned* status) {
+                        const long* mats, int n_mats, float* gradnorm, const unsigned* status,
+                        const float* skip_flag) {
   const float rho = c.rho, eps = c.eps, wd = c.weightDecay, colnorm_max = c.colnorm_max;
   const int noise = c.gradnoise_eta != 0.f;
   S2S_REQUIRE(x && g && state && n > 0, "optim: null argument");
@@ -172,7 +177,7 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
   const int nb = (int)std::min<size_t>(kNormBlocks, (n + 255) / 256);
   hipLaunchKernelGGL(opt_sumsq, dim3(nb), dim3(256), 0, st, g, n, s.partial);
   hipLaunchKernelGGL(opt_finalize, dim3(1), dim3(256), 0, st, s.partial, nb, c.maxnorm, c.gradnoise_eta,
-                     c.gradnoise_gamma, s.scal, gradnorm, status);
+                     c.gradnoise_gamma, s.scal, gradnorm, status, skip_flag);
   const int ne = (int)std::min<size_t>(2048, (n + 255) / 256);
   hipLaunchKernelGGL(opt_adadelta, dim3(ne), dim3(256), 0, st, x, g, s.v, s.u, n, s.scal, rho, eps, wd, noise,
                      c.gradnoise_seed);
@@ -191,6 +196,18 @@ int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g
     }
     hipLaunchKernelGGL(opt_colnorm, dim3((t.first[n_mats] + 3) / 4), dim3(256), 0, st, x, t, colnorm_max, s.scal);
   }
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// flag[0] = 1 if the context's failure words are set when this runs on the stream, else 0 (stream-ordered)
+__global__ __launch_bounds__(64) void status_flag_kernel(const unsigned* status, float* flag) {
+  if (threadIdx.x == 0)
+    flag[0] = ((__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) |
+                __hip_atomic_load(status + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) != 0u) ? 1.f : 0.f;
+}
+int status_flag(hipStream_t st, const unsigned* status, float* flag) {
+  hipLaunchKernelGGL(status_flag_kernel, dim3(1), dim3(64), 0, st, status, flag);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }

@@ -246,6 +246,7 @@ struct OptimConfig {
 };
 int optim_adadelta_step(hipStream_t st, const OptimConfig& c, float* x, float* g, size_t n, void* state,
                         const long* mats, int n_mats, float* gradnorm,
-                        const unsigned* status = nullptr);
+                        const unsigned* status = nullptr, const float* skip_flag = nullptr);
+int status_flag(hipStream_t st, const unsigned* status, float* flag);
 
 }  // namespace s2s

@@ -29,8 +29,8 @@ int s2s_gru_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D
 int s2s_gru_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, const int* lengths, void* scratch, size_t scratch_bytes);
 size_t s2s_lstm_saved_bytes(int B, int L, int H);
 size_t s2s_lstm_scratch_bytes(int ndir, int B, int L, int D, int H, int peepholes);
-int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes, const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved, void* scratch, size_t scratch_bytes);
-int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes, const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, void* scratch, size_t scratch_bytes);
+int s2s_lstm_fwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes, const int* reverse, const float* x, long ldx, const float* const* W, float* const* y, long ldy, void* const* saved, const int* lengths, void* scratch, size_t scratch_bytes);
+int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int D, int H, int peepholes, const int* reverse, const float* x, long ldx, const float* const* W, void* const* saved, const float* const* dy, long lddy, float* dx, long lddx, int dx_accumulate, float* const* dW, float scale, const int* lengths, void* scratch, size_t scratch_bytes);
 typedef struct { int B, L, T; int annotationDepth, scoreDepth, stateDepth, outputDepth, mlpDepth, maxoutWindow; float penalty; float dropout; unsigned long long dropout_seed; const float* dropout_mask; int hybridAttendFilterSize, hybridAttendFeatureMaps; int external_mlp; int decoder_lstm; const int* frame_lengths; const int* label_lengths; } s2s_attn_dims;
 size_t s2s_attn_saved_bytes(const s2s_attn_dims* d);
 size_t s2s_attn_scratch_bytes(const s2s_attn_dims* d);
@@ -84,6 +84,8 @@ size_t s2s_optim_state_bytes(size_t n);
 int s2s_optim_reset(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n);
 int s2s_optim_set_noise_step(s2s_ctx* ctx, s2s_stream_t stream, void* state, size_t n, unsigned t);
 int s2s_optim_adadelta_step(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params, float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm);
+int s2s_ctx_status_flag(s2s_ctx* ctx, s2s_stream_t stream, float* flag);
+int s2s_optim_adadelta_step_flag(s2s_ctx* ctx, s2s_stream_t stream, const s2s_optim_config* cfg, float* params, float* grads, size_t n, void* state, const long* mats, int n_mats, float* gradnorm, const float* skip_flag);
 int s2s_model_weight_matrices(const s2s_model_dims* d, long* mats);
 int s2s_prof_enable(int on);
 int s2s_prof_collect(char* buf, size_t cap);

@@ -65,10 +65,10 @@ SIGNATURES = [
     ("s2s_lstm_saved_bytes", c_size_t, [c_int, c_int, c_int]),
     ("s2s_lstm_scratch_bytes", c_size_t, [c_int, c_int, c_int, c_int, c_int, c_int]),
     ("s2s_lstm_fwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p,
-                             c_long, P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_size_t]),
+                             c_long, P(c_void_p), P(c_void_p), c_long, P(c_void_p), c_void_p, c_void_p, c_size_t]),
     ("s2s_lstm_bwd", c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, P(c_int), c_void_p,
                              c_long, P(c_void_p), P(c_void_p), P(c_void_p), c_long, c_void_p, c_long, c_int,
-                             P(c_void_p), c_float, c_void_p, c_size_t]),
+                             P(c_void_p), c_float, c_void_p, c_void_p, c_size_t]),
     ("s2s_attn_saved_bytes", c_size_t, [P(s2s_attn_dims)]),
     ("s2s_attn_scratch_bytes", c_size_t, [P(s2s_attn_dims)]),
     ("s2s_attn_fwd", c_int, [c_void_p, c_void_p, P(s2s_attn_dims), c_void_p, c_void_p, P(c_void_p), c_void_p,
@@ -114,6 +114,9 @@ SIGNATURES = [
     ("s2s_optim_set_noise_step", c_int, [c_void_p, c_void_p, c_void_p, c_size_t, ctypes.c_uint]),
     ("s2s_optim_adadelta_step", c_int, [c_void_p, c_void_p, P(s2s_optim_config), c_void_p, c_void_p, c_size_t,
                                         c_void_p, c_void_p, c_int, c_void_p]),
+    ("s2s_ctx_status_flag", c_int, [c_void_p, c_void_p, c_void_p]),
+    ("s2s_optim_adadelta_step_flag", c_int, [c_void_p, c_void_p, P(s2s_optim_config), c_void_p, c_void_p, c_size_t,
+                                             c_void_p, c_void_p, c_int, c_void_p, c_void_p]),
     ("s2s_model_weight_matrices", c_int, [P(s2s_model_dims), c_void_p]),
     ("s2s_model_bucket_count", c_int, [P(s2s_model_dims)]),
     ("s2s_model_bucket", c_int, [P(s2s_model_dims), c_int, P(c_size_t), P(c_size_t)]),

@@ -61,18 +61,20 @@ def save(path, model, optimizer=None, meta=None):
 def seed_base_for(meta, rank, default):
     """The loading rank's dropout seed base: _mix64(user seed, rank), so replicas resumed from one file keep
     drawing independent nn.Dropout masks (the base mixes in the rank, model.py).  A checkpoint without the
-    user seed but with the saved base of an older writer (meta['dropout_seed_base'], one rank's base) resumes
-    from that base, with a warning: the mask sequence continues for the rank that wrote it.  A checkpoint with
-    neither leaves `default` (the model's own base) in place, also with a warning."""
+    user seed but with the saved base of an older writer (meta['dropout_seed_base'], rank 0's base) resumes
+    rank 0 from that base, with a warning -- its mask sequence continues -- and every other rank from
+    _mix64(base, rank), so the replicas still draw independent masks.  A checkpoint with neither
+    leaves `default` (the model's own base) in place, also with a warning."""
     import warnings
 
     from .model import _mix64
     if "seed" in meta:
         return _mix64(int(meta["seed"]), int(rank))
     if "dropout_seed_base" in meta:
-        warnings.warn("checkpoint has no user seed (older format): resuming from its saved dropout seed base; "
-                      "data-parallel replicas share that base")
-        return int(meta["dropout_seed_base"])
+        warnings.warn("checkpoint has no user seed (older format): rank 0 resumes from its saved dropout seed "
+                      "base, the other ranks from that base mixed with their rank")
+        base = int(meta["dropout_seed_base"])
+        return base if int(rank) == 0 else _mix64(base, int(rank))
     warnings.warn("checkpoint has no dropout seed: the resumed run draws a new nn.Dropout mask sequence")
     return default
 

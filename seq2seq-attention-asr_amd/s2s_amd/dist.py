@@ -71,3 +71,13 @@ def allreduce_mean_scalar(x: float, device=None) -> float:
     t = torch.tensor([x], dtype=torch.float64, device=device)
     dist.all_reduce(t)
     return float(t.item()) / world()
+
+
+def reduce_failure_flag(flag: torch.Tensor) -> torch.Tensor:
+    """MAX of every rank's failure flag (Adadelta.failure_flag: 1.0 where a persistent launch of the step failed),
+    in place.  A failing rank's invalid gradients are already in every replica's all-reduced sum, so the update
+    must be skipped on EVERY rank (Adadelta.step(skip_flag=flag)), or the replicas diverge.  Issued on the
+    current stream (RCCL) or as a gloo collective on CPU tensors."""
+    if world() > 1:
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    return flag

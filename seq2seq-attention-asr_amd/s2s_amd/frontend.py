@@ -434,8 +434,12 @@ class GraphStep:
         if g is None:
             # the eager step runs on the capture stream: the library's lazily grown per-stream buffers (the big
             # bf16 GEMMs' staging copies) are sized for THAT stream before the capture, which cannot allocate them
+            # one capture stream per model: the library keeps a few per-stream staging buffers, so a
+            # fresh stream per key would use them up with shapes (ragged batches) and leave dead streams' buffers
             cur = torch.cuda.current_stream(x.device)
-            side = torch.cuda.Stream(x.device)
+            side = self.__dict__.get("_capture_stream")
+            if side is None or side.device != x.device:
+                side = self.__dict__["_capture_stream"] = torch.cuda.Stream(x.device)
             side.wait_stream(cur)
             with torch.cuda.stream(side):
                 self.zeroGradParameters()

@@ -278,8 +278,6 @@ class _GruSeq(Module):
     def _lengths_ptr(self, B, L, dev):
         if self.lengths is None:
             return ctypes.c_void_p(0)
-        if self.lstm:
-            raise S2SArgumentError("lengths: variable-length batches run on the GRU encoder only")
         self._len_dev = lengths_tensor(self.lengths, B, L, dev)
         return dptr(self._len_dev)
 
@@ -301,7 +299,7 @@ class _GruSeq(Module):
             scr = _bytes(lib.s2s_lstm_scratch_bytes(nd, B, L, D, H, self.peep), dev)
             sv = ptr_array([s.data_ptr() for s in self._saved])
             check(lib.s2s_lstm_fwd(ctx, stream_ptr(), nd, B, L, D, H, self.peep, rev, dptr(input), D, W, y, nd * H, sv,
-                                   dptr(scr), scr.numel()))
+                                   self._lengths_ptr(B, L, dev), dptr(scr), scr.numel()))
         else:
             self._saved = [_bytes(lib.s2s_gru_saved_bytes(B, L, H), dev) for _ in range(nd)]
             scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
@@ -327,7 +325,8 @@ class _GruSeq(Module):
         if self.lstm:
             scr = _bytes(lib.s2s_lstm_scratch_bytes(nd, B, L, D, H, self.peep), dev)
             check(lib.s2s_lstm_bwd(ctx, stream_ptr(), nd, B, L, D, H, self.peep, rev, dptr(input), D, W, sv, dy, nd * H,
-                                   dptr(dx), D, 0, dW, float(scale), dptr(scr), scr.numel()))
+                                   dptr(dx), D, 0, dW, float(scale), self._lengths_ptr(B, L, dev), dptr(scr),
+                                   scr.numel()))
         else:
             scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
             check(lib.s2s_gru_bwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv, dy, nd * H, dptr(dx),

@@ -5,6 +5,13 @@ sequence of kernels (libs2s_hip.so: s2s_optim_adadelta_step), no host round trip
     opt = Adadelta(model, rho=0.95, eps=1e-8, colnormconstr=True)   # exp_logmel7_..._colnorm.lua
     model.step(x, labels)                                           # grads = mean over the batch
     opt.step()                                                      # x updated in place
+
+Data parallel (one process per GPU): every rank's gradients went into the all-reduce, so a rank whose persistent
+launch failed poisons every replica's sum -- all ranks must skip that update together:
+
+    flag = opt.failure_flag()                   # 1.0 on a rank whose step failed (device, stream-ordered)
+    dist.reduce_failure_flag(flag)              # MAX over the ranks
+    opt.step(skip_flag=flag)                    # skipped on every rank if any rank failed
 """
 import ctypes
 
@@ -67,9 +74,27 @@ class Adadelta:
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
         check(lib.s2s_optim_set_noise_step(self.ctx.handle, st, dptr(self.state), self.n, int(t)))
 
-    def step(self, stream=None):
-        """One update; self.gradnorm holds ||g|| before clipping (timit.lua:297 gradnorms)."""
+    def failure_flag(self, stream=None, out=None):
+        """A one-float device tensor: 1.0 if this context's failure status is set when it runs on the stream, else
+        0.0 (stream-ordered, no host sync).  Data parallel: all-reduce it across the ranks (dist.reduce_failure_flag)
+        and pass it to step(skip_flag=...), so a failure on any rank skips the update on every rank."""
         st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
-        check(lib.s2s_optim_adadelta_step(self.ctx.handle, st, ctypes.byref(self.cfg), dptr(self.params),
-                                          dptr(self.grads), self.n, dptr(self.state), self._mats, self._nmats,
-                                          dptr(self.gradnorm)))
+        if out is None:
+            out = torch.zeros(1, dtype=torch.float32, device=self.params.device)
+        check(lib.s2s_ctx_status_flag(self.ctx.handle, st, dptr(out)))
+        return out
+
+    def step(self, stream=None, skip_flag=None):
+        """One update; self.gradnorm holds ||g|| before clipping (timit.lua:297 gradnorms).  skip_flag: a one-float
+        device tensor (the all-reduced failure_flag of every rank); nonzero when the update runs = skip it."""
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else stream_ptr()
+        if skip_flag is None:
+            check(lib.s2s_optim_adadelta_step(self.ctx.handle, st, ctypes.byref(self.cfg), dptr(self.params),
+                                              dptr(self.grads), self.n, dptr(self.state), self._mats, self._nmats,
+                                              dptr(self.gradnorm)))
+            return
+        if not (skip_flag.is_cuda and skip_flag.dtype == torch.float32 and skip_flag.numel() >= 1):
+            raise ValueError("skip_flag must be a float32 CUDA tensor")
+        check(lib.s2s_optim_adadelta_step_flag(self.ctx.handle, st, ctypes.byref(self.cfg), dptr(self.params),
+                                               dptr(self.grads), self.n, dptr(self.state), self._mats, self._nmats,
+                                               dptr(self.gradnorm), dptr(skip_flag)))

@@ -154,8 +154,15 @@ def test_checkpoint_seed_base_is_per_rank():
     assert b0 == _mix64(1234, 0) and b1 == _mix64(1234, 1)
     with pytest.warns(UserWarning, match="no dropout seed"):
         assert checkpoint.seed_base_for({"steps": 5}, 1, default=42) == 42  # nothing saved: keep the model's own
-    with pytest.warns(UserWarning, match="older format"):  # an older writer saved its base, not the user seed
-        assert checkpoint.seed_base_for({"steps": 5, "dropout_seed_base": "987"}, 1, default=42) == 987
+    # an older writer saved its (rank 0) base, not the user seed: rank 0 continues that sequence, every other rank
+    # mixes its rank in, so the replicas' masks stay independent
+    old = {"steps": 5, "dropout_seed_base": "987"}
+    with pytest.warns(UserWarning, match="older format"):
+        assert checkpoint.seed_base_for(old, 0, default=42) == 987
+    with pytest.warns(UserWarning, match="older format"):
+        bases = [checkpoint.seed_base_for(old, r, default=42) for r in range(4)]
+    assert bases[0] == 987 and bases[1:] == [_mix64(987, r) for r in range(1, 4)]
+    assert len(set(bases)) == 4
 
 
 @pytest.mark.gpu

@@ -108,3 +108,33 @@ def test_dp_allreduce_equals_global_batch(tmp_path, buckets):
     x, labels = orc.synthetic_batch(cfg, B * world, 6, 4, seed=9, pad=1, eos=2)
     _, G, _, _ = orc.training_step(x, labels, P, cfg)
     np.testing.assert_allclose(got, orc.flatten(G, cfg), rtol=1e-10, atol=1e-13)
+
+
+def _flag_worker(rank, world, port, out_path, failing):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "s2s_dist", os.path.join(ROOT, "seq2seq-attention-asr_amd", "s2s_amd", "dist.py"))
+    sd = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sd)
+    # Adadelta.failure_flag's value on this rank: 1.0 where the step's persistent launch failed
+    flag = torch.tensor([1.0 if rank == failing else 0.0], dtype=torch.float32)
+    sd.reduce_failure_flag(flag)
+    np.save(f"{out_path}.{rank}.npy", flag.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("failing", [-1, 0, 1])
+def test_failure_flag_reduced_across_ranks(tmp_path, failing):
+    """a rank whose persistent launch failed has already sent invalid gradients into the all-reduce,
+    so every rank must skip that update.  dist.reduce_failure_flag (the MAX all-reduce of Adadelta.failure_flag)
+    gives every rank the same flag: 1 if any rank failed, else 0 (world size 2, gloo)."""
+    world = 2
+    out = str(tmp_path / "f")
+    mp.start_processes(_flag_worker, args=(world, _free_port(), out, failing), nprocs=world, start_method="spawn")
+    got = [float(np.load(f"{out}.{r}.npy")[0]) for r in range(world)]
+    assert got == [0.0 if failing < 0 else 1.0] * world

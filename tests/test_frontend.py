@@ -432,7 +432,7 @@ def test_oracle_vgg_step_under_its_own_decisions_is_unchanged():
     raw2 = {}
     nll2, logp2, G2, mg2 = fo.vgg_model_step(x, labels, P, layers, cfg, decide, mx, raw2)
     assert np.array_equal(logp, logp2) and all(np.array_equal(G[k], G2[k]) for k in G)
-    assert vc.decision_margins(decide, mx, raw2) == {k: (0, 0.0) for k in
+    assert vc.decision_margins(decide, mx, raw2) == {k: (0, 0.0, 0.0, 0.0) for k in
                                                      ("conv0", "conv1", "conv2", "conv3", "lin0", "lin1", "lin2",
                                                       "lin3", "pool1", "pool3", "maxout0", "maxout1")}
     # one adopted flip (the smallest |u| of the last 1x1 layer) changes the step and is reported with its margin
@@ -443,7 +443,10 @@ def test_oracle_vgg_step_under_its_own_decisions_is_unchanged():
     raw3 = {}
     _, logp3, _, _ = fo.vgg_model_step(x, labels, P, layers, cfg, decide, mx, raw3)
     m = vc.decision_margins(decide, mx, raw3)
-    assert m["lin3"][0] == 1 and abs(m["lin3"][1] - abs(u[k]) / np.abs(u).max()) < 1e-12
+    assert m["lin3"][0] == 1 and abs(m["lin3"][1] - 1.0 / u.size) < 1e-15
+    assert abs(m["lin3"][2] - abs(u[k]) / np.abs(u).max()) < 1e-12
+    # its local scale is the unit row (b, l) of the 1x1 layer's output
+    assert abs(m["lin3"][3] - abs(u[k]) / np.abs(u[k[:-1]]).max()) < 1e-12 and m["lin3"][3] >= m["lin3"][2]
     assert not np.array_equal(logp, logp3)
 
 

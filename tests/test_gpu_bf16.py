@@ -238,6 +238,11 @@ def test_model_step_bf16_config3_decisions_pinned(lib, B, fused, prec):
 # few 1e-3 of its site's scale: flips there are adopted (measured: at most 5.2e-3 of the scale, pool3); a flip
 # beyond this band would be a kernel error.
 BF16_DECISION_BAND = 1e-2
+# and at most this fraction of a site's decisions may be adopted flips (measured: at most 3.3e-3, pool3; 1.4e-3 the
+# deepest conv ReLU).  (The local-scale margins are reported only: a pooling window's reaches 1.0 where an adopted
+# ReLU flip -- a slightly negative oracle value under the GPU's "active" mask -- competes with a zero; that lead
+# is the flip's own |u|, already bounded at its ReLU site.)
+BF16_FLIP_FRACTION = 1e-2
 # config 5 chains 12 bf16 products (8 encoder layers, the decoder, the decoder_mlp) against config 3's 4, so its
 # pinned bar is twice config 3's (measured with decisions pinned: 1.8e-4 .. 1.05e-2, the deepest layer dvgg2 worst;
 # 7-9e-2 before pinning)
@@ -272,9 +277,13 @@ def test_vgg_model_step_bf16_config5(lib, prec):
     nll64, logp64, G64, mg64 = vc.oracle_step(model, fe, x, labels, np.float64, decide, mx, raw)
     nll32, logp32, G32, mg32 = vc.oracle_step(model, fe, x, labels, np.float32, decide, mx)
     margins = vc.decision_margins(decide, mx, raw)
-    print(f"config 5 {prec} adopted flips (count, largest margin / scale):", margins)
-    wide = {k: v for k, v in margins.items() if v[1] > BF16_DECISION_BAND}
+    print(f"config 5 {prec} adopted flips (count, fraction, largest margin / layer scale, / local scale):", margins)
+    wide = {k: v for k, v in margins.items() if v[2] > BF16_DECISION_BAND}
     assert not wide, wide
+    # near-tie flips are rare: a kernel error that flips many small units stays inside the layer-wide band but not
+    # inside this count bound
+    many = {k: v for k, v in margins.items() if v[1] > BF16_FLIP_FRACTION}
+    assert not many, many
     errs = {"logp": _rel(logp.cpu().numpy(), logp64)}
     floor = {"logp": _rel(logp32, logp64)}
     for (name, gpu, r64), (_, _, r32) in zip(vc.grad_pairs(model, fe, G64, mg64), vc.grad_pairs(model, fe, G32, mg32)):

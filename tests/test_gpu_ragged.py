@@ -85,6 +85,72 @@ def test_bigru_lengths_match_per_utterance(s2s, monkeypatch, mode, B, L, D, H):
     assert (y[pad] == 0).all() and (dx[pad] == 0).all()
 
 
+@pytest.mark.parametrize("mode,peep", [("persistent", False), ("step", False), ("step", True)])
+@pytest.mark.parametrize("B,L,D,H", [(32, 14, 256, 128), (7, 19, 40, 64)])
+def test_bilstm_lengths_match_per_utterance(s2s, monkeypatch, mode, peep, B, L, D, H):
+    """nn.RNN(LSTM) forward + reverse directions on a padded batch (the conv + BiLSTM encoder's
+    recurrence, timit/timit.lua:108-125, at its shape B = 32, 256 maps, 128 units, 14 frames, and a ragged one):
+    each utterance's outputs, dx and the summed weight gradients equal the oracle run on the utterance alone
+    (h = c = 0 on padding frames, the reverse direction starting from zero state at the utterance's own last
+    frame); zeros on padding frames.  The persistent kernels (lstm_persist.hip) and the per-step launches (with
+    and without peepholes) both take the lengths."""
+    monkeypatch.setenv("S2S_LSTM_MODE", mode)
+    rng = np.random.default_rng(B * 37 + L)
+    lens = rng.integers(1, L + 1, B)
+    lens[0] = L
+    lens[-1] = 1
+    x = rng.standard_normal((B, L, D))
+    cells = [s2s.LSTM(D, H, peepholes=peep) for _ in range(2)]
+    Ps = [{k: v.double().numpy() for k, v in c.named().items()} for c in cells]
+    mod = s2s.BiRNN(cells[0], cells[1]).cuda()
+    mod.lengths = lens
+    xs = cu(x)
+    y = mod.forward(xs).cpu().numpy()
+    dy = rng.standard_normal(y.shape)
+    mod.zeroGradParameters()
+    dx = mod.backward(xs, cu(dy), 0.5).cpu().numpy()
+    torch.cuda.synchronize()
+    errs = {}
+    dx_ref = np.zeros_like(x)
+    for i, (P, rev) in enumerate(zip(Ps, [False, True])):
+        G = {k: np.zeros_like(v) for k, v in P.items()}
+        yr = np.zeros((B, L, H))
+        for b in range(B):
+            xb = x[b:b + 1, :lens[b]]
+            yb, sv = orc.lstm_seq_fwd(xb, P, rev, peep)
+            yr[b, :lens[b]] = yb[0]
+            dxb = orc.lstm_seq_bwd(xb, P, sv, dy[b:b + 1, :lens[b], i * H:(i + 1) * H], G, rev, peep, 0.5)
+            dx_ref[b, :lens[b]] += dxb[0]
+        errs[f"y[{i}]"] = rel(y[:, :, i * H:(i + 1) * H], yr)
+        for k, g in cells[i].named(grads=True).items():
+            errs[f"d{k}[{i}]"] = rel(g.cpu().numpy(), G[k])
+    errs["dx"] = rel(dx, dx_ref)
+    check(errs)
+    pad = np.arange(L)[None, :] >= lens[:, None]
+    assert (y[pad] == 0).all() and (dx[pad] == 0).all()
+
+
+def test_bilstm_full_lengths_bitwise_equal_unmasked(s2s):
+    """lengths all = L is the unmasked path bit for bit (the persistent BiLSTM at the encoder's shape)."""
+    rng = np.random.default_rng(4)
+    B, L, D, H = 32, 14, 256, 128
+    x = cu(rng.standard_normal((B, L, D)))
+    dyv = cu(rng.standard_normal((B, L, 2 * H)))
+    cells = [s2s.LSTM(D, H) for _ in range(2)]
+    res = []
+    for lengths in (None, [L] * B):
+        mod = s2s.BiRNN(cells[0], cells[1]).cuda()
+        mod.lengths = lengths
+        y = mod.forward(x).clone()
+        mod.zeroGradParameters()
+        dx = mod.backward(x, dyv, 1.0).clone()
+        res.append((y, dx, [g.clone() for c in cells for g in c.named(grads=True).values()]))
+    torch.cuda.synchronize()
+    (y0, dx0, g0), (y1, dx1, g1) = res
+    assert torch.equal(y0, y1) and torch.equal(dx0, dx1)
+    assert all(torch.equal(a, b) for a, b in zip(g0, g1))
+
+
 # (B, L, T, A, Sc, S, O, M, K, penalty): XCD-local decoder shapes (Chorowski sizes; S=64 ones with the
 # penalty on, ragged last chain), and a per-step-kernel shape
 RAGGED_ATT = [

@@ -164,3 +164,51 @@ def test_optimizer_queued_behind_failed_step_skips_update(s2s):
     opt.step()
     torch.cuda.synchronize()
     assert not torch.equal(m.params, p0)
+
+
+def test_failure_on_one_replica_skips_every_replica(s2s):
+    """ADVICE r4 (data parallel): two replicas (two contexts on this GPU) with identical parameters; replica A's
+    step fails (injected abort), replica B's succeeds.  Their gradients would both go into the all-reduce, so both
+    must skip the update.  Each replica's failure flag (s2s_ctx_status_flag, on the device) is summed as the
+    all-reduce would (dist.reduce_failure_flag takes the MAX; any nonzero skips), and both optimizers run with it:
+    neither replica's parameters change, so the replicas stay identical.  Without the reduced flag B would apply
+    the update alone (checked: B's own flag is 0)."""
+    from s2s_amd import _lib
+    from s2s_amd.optim import Adadelta
+    cfg = s2s.ModelConfig()
+    a = s2s.ChorowskiBaseline(cfg, overlap=True)
+    b = s2s.ChorowskiBaseline(cfg, overlap=True)
+    b.params.copy_(a.params)
+    assert a.ctx is not b.ctx
+    oa, ob = Adadelta(a), Adadelta(b)
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(4, 24, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (4, 6), generator=g).to(torch.int32).cuda()
+    p0 = a.params.clone()
+    try:
+        _lib.lib.s2s_debug_inject_abort(1)
+        torch.cuda._sleep(50_000_000)  # the host queues everything below before the failure is visible to it
+        a.step(x, lab)
+        _lib.lib.s2s_debug_inject_abort(0)
+        b.step(x, lab)
+        fa, fb = oa.failure_flag(), ob.failure_flag()
+        flag = fa + fb  # the cross-rank reduction (a sum or a max: nonzero iff any replica failed)
+        oa.step(skip_flag=flag)
+        ob.step(skip_flag=flag)
+        torch.cuda.synchronize()
+        assert float(fa.item()) == 1.0 and float(fb.item()) == 0.0
+        assert a.ctx.status(clear=False) != 0
+    finally:
+        _lib.lib.s2s_debug_inject_abort(0)
+        a.ctx.status(clear=True)
+    assert b.ctx.status() == 0
+    assert torch.equal(a.params, p0) and torch.equal(b.params, p0)
+    # a clear flag lets both replicas update again, identically
+    z = torch.zeros(1, dtype=torch.float32, device="cuda")
+    a.step(x, lab)
+    b.step(x, lab)
+    oa.step(skip_flag=z)
+    ob.step(skip_flag=z)
+    torch.cuda.synchronize()
+    assert not torch.equal(a.params, p0)
+    assert torch.equal(a.params, b.params)

@@ -83,15 +83,23 @@ def gpu_decisions(model, fe):
 
 
 def decision_margins(decide, maxout_idx, raw):
-    """For each decision site: (flips, the largest |margin| / scale among them), where a flip is a GPU decision
-    that differs from the oracle's own one under the same upstream decisions and its margin is how far the
-    oracle's value is from the tie (|u| for a ReLU; the winner's lead over the GPU's pick for max-pooling and
-    Maxout)."""
+    """For each decision site: (flips, flipped fraction of the site's decisions, the largest |margin| / the layer's
+    scale, the largest |margin| / the decision's LOCAL scale), where a flip is a GPU decision that differs from the
+    oracle's own one under the same upstream decisions and its margin is how far the oracle's value is from the tie
+    (|u| for a ReLU; the winner's lead over the GPU's pick for max-pooling and Maxout).  Local scale: a
+    ReLU's row (the channel plane of a convolution output, the unit row of a 1x1 layer), a max-pooling window's
+    largest |input|, a Maxout group's largest |input| -- a kernel error that flips many decisions of small units
+    would show in the fraction and in the local margin even where the layer-wide one stays small."""
     out = {}
     for kind in ("conv", "lin"):
         for l, (mask, u) in enumerate(zip(decide[kind], raw[kind])):
             d = mask != (u > 0)
-            out[f"{kind}{l}"] = (int(d.sum()), float(np.abs(u[d]).max() / np.abs(u).max()) if d.any() else 0.0)
+            # conv u: (B, C, H, W) -> per (b, c) plane; lin u: (B, L, C) -> per (b, l) row
+            loc = (np.abs(u).max(axis=(2, 3), keepdims=True) if u.ndim == 4 else np.abs(u).max(axis=-1, keepdims=True))
+            loc = np.broadcast_to(loc, u.shape)
+            out[f"{kind}{l}"] = (int(d.sum()), float(d.mean()),
+                                 float(np.abs(u[d]).max() / np.abs(u).max()) if d.any() else 0.0,
+                                 float((np.abs(u[d]) / np.maximum(loc[d], 1e-30)).max()) if d.any() else 0.0)
     for l, gidx in decide["pool"].items():
         own, h = raw["pool"][l], raw["pool_in"][l]
         d = gidx != own
@@ -99,14 +107,18 @@ def decision_margins(decide, maxout_idx, raw):
             from oracle.frontend_oracle import VGG_POOLS, smaxpool_fwd
             kW, kH, dW, dH = VGG_POOLS[l]
             lead = smaxpool_fwd(h, kW, kH, dW, dH)[0] - smaxpool_fwd(h, kW, kH, dW, dH, gidx)[0]
-            out[f"pool{l}"] = (int(d.sum()), float(lead[d].max() / np.abs(h).max()))
+            win = smaxpool_fwd(np.abs(h), kW, kH, dW, dH)[0]  # the window's largest |input|
+            out[f"pool{l}"] = (int(d.sum()), float(d.mean()), float(lead[d].max() / np.abs(h).max()),
+                               float((lead[d] / np.maximum(win[d], 1e-30)).max()))
         else:
-            out[f"pool{l}"] = (0, 0.0)
+            out[f"pool{l}"] = (0, 0.0, 0.0, 0.0)
     for i, (am, g) in enumerate(zip(maxout_idx, raw["mlp"])):
         own = np.argmax(g, axis=2)
         d = am != own
         lead = np.take_along_axis(g, own[..., None], 2)[..., 0] - np.take_along_axis(g, am[..., None], 2)[..., 0]
-        out[f"maxout{i}"] = (int(d.sum()), float(lead[d].max() / np.abs(g).max()) if d.any() else 0.0)
+        grp = np.abs(g).max(axis=2)
+        out[f"maxout{i}"] = (int(d.sum()), float(d.mean()), float(lead[d].max() / np.abs(g).max()) if d.any() else 0.0,
+                             float((lead[d] / np.maximum(grp[d], 1e-30)).max()) if d.any() else 0.0)
     return out
 
 
