@@ -184,10 +184,17 @@ def test_failure_on_one_replica_skips_every_replica(s2s):
     g = torch.Generator().manual_seed(9)
     x = torch.randn(4, 24, cfg.inputFrameSize, generator=g).cuda()
     lab = torch.randint(0, cfg.outputDepth, (4, 6), generator=g).to(torch.int32).cuda()
+    z = torch.zeros(1, dtype=torch.float32, device="cuda")
+    for m, o in ((a, oa), (b, ob)):  # warm-up: every lazily sized buffer exists, so nothing below syncs the host
+        m.step(x, lab)
+        o.failure_flag()
+        o.step(skip_flag=z)
+    torch.cuda.synchronize()
+    assert torch.equal(a.params, b.params)
     p0 = a.params.clone()
     try:
         _lib.lib.s2s_debug_inject_abort(1)
-        torch.cuda._sleep(50_000_000)  # the host queues everything below before the failure is visible to it
+        torch.cuda._sleep(200_000_000)  # the host queues everything below before the failure is visible to it
         a.step(x, lab)
         _lib.lib.s2s_debug_inject_abort(0)
         b.step(x, lab)
@@ -204,7 +211,6 @@ def test_failure_on_one_replica_skips_every_replica(s2s):
     assert b.ctx.status() == 0
     assert torch.equal(a.params, p0) and torch.equal(b.params, p0)
     # a clear flag lets both replicas update again, identically
-    z = torch.zeros(1, dtype=torch.float32, device="cuda")
     a.step(x, lab)
     b.step(x, lab)
     oa.step(skip_flag=z)
