@@ -295,6 +295,21 @@ int mark_bucket(hipEvent_t* bev, int i, hipStream_t s) {
 }
 
 // S2S_PROLOGUE=0|1|2 (diagnostics; see model_step_impl), read once
+// S2S_HEAD_FUSED=0 (A/B): pad, pack and the first sync prep as three launches instead of gru_step_head's one
+std::atomic<int> g_head_fused{[] {
+  const char* e = std::getenv("S2S_HEAD_FUSED");
+  return e ? std::atoi(e) : 1;
+}()};
+// Where the model step forks its side stream (S2S_FORK_MODE): 0 = at the top (default); 1 = after the step's head
+// (the side work depends on the head); 2 = the side branch depends on the head, but its nodes are created after
+// layer 1's forward launch (a replayed graph dispatches nodes in creation order).  Modes 1 and 2 start layer 1
+// earlier (14 vs 21-24 us into the step) but measured slower (same box: 3.283 / 3.291 / 3.295 ms for 0 / 1 / 2):
+// the decoder prologue's kernels on the side stream then start after layer 1 holds every CU, each of them is
+// stretched over a whole GRU layer, and the last one finished after layer 3 -- 48 us in front of the decoder
+std::atomic<int> g_fork_mode{[] {
+  const char* e = std::getenv("S2S_FORK_MODE");
+  return e ? std::atoi(e) : 0;
+}()};
 int prologue_mode() {
   static const int m = [] {
     const char* e = std::getenv("S2S_PROLOGUE");
@@ -341,9 +356,19 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // gradients are first written by the side stream's weight-gradient work when split: zero them
   // there (the fork precedes every gradient writer), off the critical path
   const int pmode = prologue_mode();
-  if (split) S2S_TRY(fork_to(st, side, ev[13]));
-  if (flags & S2S_ZERO_GRADS)
-    S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
+  const int fmode = pmode == 1 ? 0 : (int)g_fork_mode;
+  // fork point (fmode): the side stream waits for ev[13]; mode 2 records it after the head and issues the side
+  // work after layer 1's forward launch (side_work below)
+  auto fork_side = [&](bool wait_only) -> int {
+    if (split) {
+      if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
+      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[13], 0));
+    }
+    if (flags & S2S_ZERO_GRADS)
+      S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
+    return 0;
+  };
+  if (fmode == 0) S2S_TRY(fork_side(false));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
@@ -387,7 +412,9 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     io.excl = split ? 1 : 0;
     return io;  // io.status stays null: the step harvests every sync region once, at its end
   };
-  if (w.xpad) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
+  // the step's head (pad, pack, the first persistent launch's sync prep) as one launch when layer 1 is persistent
+  const bool head_fused = g_head_fused && g_sync_handover && gru_layer_persistent(layer_io(0));
+  if (w.xpad && !head_fused) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
   // weight packing for every layer (both passes) and the decoder's parameter folds need only params
   // and labels: layer 1 on the critical path, the rest beside layer 1's recurrence when split
   // weight packing for every layer and both passes: one launch on the critical path (~10 us); the
@@ -400,25 +427,40 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     std::vector<GruLayerIO> ios;
     for (int l = 0; l < nl; ++l) ios.push_back(layer_io(l));
     defer_pack = g_defer_pack && 2 * nl <= kMaxPackJobs && gru_layer_preps_next(ios[0], true);
-    S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
+    if (head_fused)
+      S2S_TRY(gru_step_head(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr, x,
+                            d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp, w.gsync[0],
+                            gru_layer_sync_prep_bytes(ios[0]), w.gsync[1]));
+    else
+      S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
   }
-  // decoder parameter folds + dlogp = -labelmask (params and labels only). Mode 0: on the side
-  // stream, joined before the decoder (the persistent GRU launches hold every CU, so it runs in the
-  // gaps between layers); 1: beside pad + pack, joined before layer 1; 2: inline on the main stream
-  if (split && pmode != 2) {
-    S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));  // dlogp = -labelmask
-    if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
-    S2S_CHECK_HIP(hipEventRecord(ev[14], side));
-    if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
-  } else {
-    S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
-    if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
+  if (fmode == 1) S2S_TRY(fork_side(false));
+  if (fmode == 2) {
+    if (split) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
+    else S2S_TRY(fork_side(false));  // (no side stream: the gradient zeroing on the main stream, here)
   }
+  // decoder parameter folds + dlogp = -labelmask (params and labels only): side_work, issued here or (fmode 2)
+  // right after layer 1's forward launch.  Prologue mode 0: on the side stream, joined before the decoder (the
+  // persistent GRU launches hold every CU, so it runs in their gaps); 1: beside pad + pack, joined before layer 1;
+  // 2: inline on the main stream
+  auto side_work = [&]() -> int {
+    if (split && pmode != 2) {
+      S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));  // dlogp = -labelmask
+      if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+      S2S_CHECK_HIP(hipEventRecord(ev[14], side));
+      if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
+    } else {
+      S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
+      if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
+    }
+    return 0;
+  };
+  if (fmode != 2 || !split) S2S_TRY(side_work());
   // the persistent GRU launches of the step (forward layers 1..nl, then backward nl..1) alternate between
   // two sync regions; a launch with spare slots prepares the next launch's region itself, so only the
   // first launch has a sync_prep in front of it
   int glaunch = 0;
-  bool gprepared = false;
+  bool gprepared = head_fused;  // the step head prepared the first launch's region
   bool gused[2] = {false, false};  // a persistent launch of this step used the region (harvested at the end)
   auto hand_over = [&](GruLayerIO& io, bool fwd, const GruLayerIO* next) {
     if (!g_sync_handover) return;
@@ -445,6 +487,10 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     hand_over(io, true, &next);
     if (l == 0 && defer_pack) io.pack_jobs = &deferred;
     S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
+    if (l == 0 && fmode == 2 && split) {  // the side branch (forked after the head), created behind layer 1
+      S2S_TRY(fork_side(true));
+      S2S_TRY(side_work());
+    }
   }
   // ---- attention decoder forward
   if (split && pmode == 0) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));

@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <vector>
 
 #include "gru_persist.h"
 #include "skinny.h"
@@ -252,20 +253,9 @@ static PackView pack_view(const float* pk, int nd, int H) {
   v.Wx = pk;
   return v;
 }
-int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer) {
-  PackBatch b{};
-  int n = 0;
-  long most = 0;
-  auto flush = [&]() -> int {
-    if (n == 0) return 0;
-    int blocks = (int)((most + 255) / 256);
-    if (blocks > 512) blocks = 512;
-    hipLaunchKernelGGL(gru_pack_multi, dim3(blocks, n), dim3(256), 0, st, b);
-    S2S_CHECK_HIP(hipGetLastError());
-    n = 0;
-    most = 0;
-    return 0;
-  };
+// the pack jobs of `ios` (now) and, with defer, the jobs left to layer 1's spare slots
+static int pack_jobs(const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer,
+                     std::vector<PackArgs>& now) {
   for (int l = 0; l < nlayers; ++l) {
     const GruLayerIO& io = ios[l];
     const int nd = io.ndir, D = io.D, H = io.H;
@@ -285,12 +275,47 @@ int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed,
         defer->j[defer->n++] = later;
         if (l > 0) continue;
       }
-      if (n == kMaxPack) S2S_TRY(flush());
-      b.p[n++] = job;
-      most = std::max(most, 3L * H * (H + Kx));
+      now.push_back(job);
     }
   }
+  return 0;
+}
+
+int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer) {
+  std::vector<PackArgs> now;
+  S2S_TRY(pack_jobs(ios, packed, nlayers, defer, now));
+  PackBatch b{};
+  int n = 0;
+  long most = 0;
+  auto flush = [&]() -> int {
+    if (n == 0) return 0;
+    int blocks = (int)((most + 255) / 256);
+    if (blocks > 512) blocks = 512;
+    hipLaunchKernelGGL(gru_pack_multi, dim3(blocks, n), dim3(256), 0, st, b);
+    S2S_CHECK_HIP(hipGetLastError());
+    n = 0;
+    most = 0;
+    return 0;
+  };
+  for (const PackArgs& job : now) {
+    if (n == kMaxPack) S2S_TRY(flush());
+    b.p[n++] = job;
+    most = std::max(most, 3L * job.H * (job.H + job.Kx));
+  }
   return flush();
+}
+
+int gru_step_head(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer,
+                  const float* x, long ldx, float* xpad, int rows, int cols, int dcols, void* sync, size_t prep_bytes,
+                  void* clear) {
+  std::vector<PackArgs> now;
+  S2S_TRY(pack_jobs(ios, packed, nlayers, defer, now));
+  GruStepHead h{};
+  S2S_REQUIRE((int)now.size() <= kMaxPackJobs, "gru: too many pack jobs for the step head");
+  for (const PackArgs& job : now) h.pack.j[h.pack.n++] = job;
+  h.src = x; h.lds = ldx; h.dst = xpad; h.rows = xpad ? rows : 0; h.cols = cols; h.dcols = dcols;
+  h.sync = static_cast<char*>(sync); h.prep_bytes = prep_bytes; h.clear = static_cast<char*>(clear);
+  return gru_persist_step_head(st, h);
 }
 
 int gru_layer_pack(hipStream_t st, const GruLayerIO& io, float* packed) {

@@ -42,6 +42,20 @@ __device__ __forceinline__ void gru_pack_elems(const GruPackJob& p, long i0, lon
   }
 }
 
+// the model step's head in one launch (gru_step_head, gru.hip): pad the layer-1 input, pack jobs, prepare the
+// first persistent launch's sync region (sync_prep's work: sync null = none)
+struct GruStepHead {
+  const float* src;
+  long lds;
+  float* dst;
+  int rows, cols, dcols;  // rows = 0: no padding
+  GruPackJobs pack;
+  char* sync;
+  size_t prep_bytes;
+  char* clear;
+};
+int gru_persist_step_head(hipStream_t st, const GruStepHead& h);
+
 struct GruPersistFwd {
   int ndir, B, L, H;
   // fused x-projection (gru_persist_fused_xproj): x (B*L, ldx) with Kx readable columns and the

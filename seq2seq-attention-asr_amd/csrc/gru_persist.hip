@@ -833,6 +833,9 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       // also those of padding rows or frames, which load no dy
       if (a.fused) xproj_wait(a.xq, dir, q / a.xq.tpt, yready, lane, a.abort_word);
       if (!lv) return;
+#ifdef S2S_EXP_NOLOAD  // diagnostic (timing only, wrong results): no HBM row loads in the BPTT loader wave
+      return;
+#endif
       const int t = g.reverse ? q : L - 1 - q;
       const long row = (long)bl * L + t;
       const float* sv = g.sv + row * 5 * H + u;
@@ -862,15 +865,27 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       __syncthreads();  // [A]
       if (abort_lds) return;
       put(p + 2, ra);   // loaded during the previous step
+      // The next rows' loads are issued behind [A] and drained before [B] (the vmcnt(0) below): they are then in
+      // this CU's memory queue only during the da_r hand-off -- whose consumers run the da_z half of their product
+      // meanwhile -- and never beside the da_h sweep behind [B], which gates the step (an HBM load in the queue slows
+      // the sweeps behind it: loader loads switched off entirely, backward step 2.78 -> 2.66 us).  Same box, config-2
+      // step: 3.268 ms issued behind [B] (round 4), 3.295 issued behind [A] but left in flight across [B], 3.244
+      // issued behind [A] and drained.
+#ifndef S2S_EXP_LOADB
+      issue(p + 3, ra);
+#endif
       if (ring && p >= 1) {  // step p-1's slots: every member has finished with them (header comment)
         rearm_tile(g.s0, a, p - 1, mytile, lane);
         rearm_tile(g.s1, a, p - 1, mytile, lane);
         rearm_tile(g.s2, a, p - 1, mytile, lane);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // landed before the member publishes step p+1
       }
+      // the re-arms land before the member publishes step p+1 (and the row loads before [B])
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();  // [B]
       if (abort_lds) return;
+#ifdef S2S_EXP_LOADB  // A/B: the round-4 placement behind [B]
       issue(p + 3, ra);
+#endif
     }
     return;
   }
@@ -915,10 +930,12 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       put_granule_pair(g.g2, off, dah, tb + pn + 1, pub);
       put_granule_pair(g.g0, off, daz, tb + pn + 1, pub);
     }
+#ifndef S2S_EXP_NODA  // diagnostic (timing only): no dA stores
     if (pub) {
       g.dA[row * g.ldA + ok_] = daz;
       g.dA[row * g.ldA + 2 * H + ok_] = dah;
     }
+#endif
   };
 
   const int tl = g.reverse ? 0 : L - 1;
@@ -975,7 +992,9 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     }
     if (live) {
       const float dar = (dq * cur.hp) * (cur.r * (1.0f - cur.r));
+#ifndef S2S_EXP_NODA
       g.dA[row * g.ldA + H + ok_] = dar;
+#endif
       const float dh = cur.dy + dhc;
       dhp = dh * (-cur.z + 1.0f) + dq * cur.r;
     }
@@ -1312,7 +1331,83 @@ int handoff_timeout_probe_launch(hipStream_t st, void* sync, unsigned* status) {
   return launch_sync_harvest(st, r, 1, status);
 }
 
+// The model step's head (gru_step_head): one grid-stride pass over the layer-1 input padding, the pack jobs and
+// the first persistent launch's sync-region preparation (sync_prep's work, in this translation unit so the epoch
+// comes from the same counter as every other GRU region's)
+__global__ __launch_bounds__(256) void step_head_kernel(GruStepHead h, unsigned abort0) {
+  const long gid = blockIdx.x * 256L + threadIdx.x, gsz = (long)gridDim.x * 256;
+  if (h.sync && gid == 0) {
+    if (h.clear) {
+      unsigned* c = reinterpret_cast<unsigned*>(h.clear);
+      __hip_atomic_exchange(c + kStickyWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_exchange(c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    unsigned* hdr = reinterpret_cast<unsigned*>(h.sync);
+    const unsigned e = __hip_atomic_fetch_add(&g_s2s_epoch_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+    __hip_atomic_exchange(hdr + kEpochWord, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(hdr + kStickyWord, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_exchange(hdr, abort0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (h.sync) {
+    const size_t body = h.prep_bytes - 256, n16 = body / 16;
+    uint4* p = reinterpret_cast<uint4*>(h.sync + 256);
+    for (long i = gid; i < (long)n16; i += gsz) p[i] = make_uint4(0u, 0u, 0u, 0u);
+    unsigned* t = reinterpret_cast<unsigned*>(h.sync + 256 + n16 * 16);
+    for (long i = gid; i < (long)((body % 16) / 4); i += gsz) t[i] = 0u;
+  }
+  const long n = (long)h.rows * h.dcols;
+  for (long i = gid; i < n; i += gsz) {
+    const long r = i / h.dcols, c = i - r * h.dcols;
+    h.dst[i] = c < h.cols ? h.src[r * h.lds + c] : 0.f;
+  }
+  for (int j = 0; j < h.pack.n; ++j) gru_pack_elems(h.pack.j[j], gid, gsz);
+}
+int gru_persist_step_head(hipStream_t st, const GruStepHead& h) {
+  long most = (long)h.rows * h.dcols;
+  for (int j = 0; j < h.pack.n; ++j) most = std::max(most, 3L * h.pack.j[j].H * (h.pack.j[j].H + h.pack.j[j].Kx));
+  if (h.sync) most = std::max<long>(most, (long)((h.prep_bytes - 256) / 16));
+  const int blocks = (int)std::max<long>(1, std::min<long>(1024, (most + 255) / 256));
+  hipLaunchKernelGGL(step_head_kernel, dim3(blocks), dim3(256), 0, st, h, inject_abort_take() ? 2u : 0u);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
+// Test stand-in for a collective beside the persistent launches (RCCL's all-reduce kernels run on a
+// communication stream while the encoder BPTT runs): nwg workgroups that each hold lds_bytes of dynamic LDS and stay
+// resident for `ticks` of the 100 MHz real-time clock, touching their LDS and sleeping -- a bounded kernel, so
+// whatever the dispatcher does with the persistent launch behind it, every workgroup eventually runs.
+__global__ __launch_bounds__(256) void lds_hog_kernel(float* out, int n, unsigned long long ticks) {
+  extern __shared__ float hog[];
+  for (int i = threadIdx.x; i < n; i += 256) hog[i] = (float)i;
+  __syncthreads();
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  float acc = 0.f;
+  int k = threadIdx.x;
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+    k = (k * 7 + 13) % n;
+    acc += hog[k];
+    __builtin_amdgcn_s_sleep(8);
+  }
+  if (acc == -1.f) out[blockIdx.x] = acc;  // never: keeps the loop
+}
+int lds_hog_launch(hipStream_t st, int nwg, int lds_bytes, double usec, float* out) {
+  S2S_REQUIRE(nwg > 0 && nwg <= 4096 && lds_bytes >= 1024 && lds_bytes <= 160 * 1024 && usec > 0 && usec < 1e6,
+              "lds hog: bad arguments");
+  S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(lds_hog_kernel),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lds_bytes));
+  hipLaunchKernelGGL(lds_hog_kernel, dim3(nwg), dim3(256), lds_bytes, st, out, lds_bytes / 4,
+                     (unsigned long long)(usec * 100.0));
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace s2s
+
+// test stand-in for a collective on another stream (tests/test_gpu_coresident.py): nwg resident workgroups holding
+// lds_bytes of LDS each for usec microseconds
+extern "C" int s2s_debug_lds_hog(void* stream, int nwg, int lds_bytes, double usec, float* out) {
+  return s2s::lds_hog_launch(static_cast<hipStream_t>(stream), nwg, lds_bytes, usec, out);
+}
 
 // diagnostic: the next persistent GRU launches fill these with stamps (tools/gru_stamps.py);
 // nullptr turns it off.  Not part of the C ABI header.

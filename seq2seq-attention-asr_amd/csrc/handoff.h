@@ -100,7 +100,13 @@ __device__ __forceinline__ bool spin_give_up(unsigned& spins, unsigned* abort_wo
       return true;
     }
   }
+  // Polls run back to back (no s_sleep between passes): a poll pass is already one L2 round trip, and the
+  // sleep delayed the pass that sees the value -- measured (same box, config-2 step): 3.308 -> 3.278 ms without
+  // the sleep, the GRU forward step 2.62 -> 2.50 us; sleeping only after the first 16 / 64 passes was slower
+  // (3.33 ms).  S2S_SPIN_SLEEP=1 (a build flag) restores the sleep.
+#if defined(S2S_SPIN_SLEEP) && S2S_SPIN_SLEEP
   __builtin_amdgcn_s_sleep(1);
+#endif
   return false;
 }
 

@@ -8,8 +8,10 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 ks = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Queue_Id"], r["Kernel_Name"]) for r in rows]
 ks.sort()
-# a step starts at the first pad_cols_kernel (layer-1 input padding) of the model step
-starts = [i for i, k in enumerate(ks) if "pad_cols_kernel" in k[3]]
+# a step starts at its head: step_head_kernel (pad + pack + first sync prep in one launch), or pad_cols_kernel
+# (the layer-1 input padding) when the head runs as separate launches (S2S_HEAD_FUSED=0)
+starts = [i for i, k in enumerate(ks) if "step_head_kernel" in k[3]] or \
+    [i for i, k in enumerate(ks) if "pad_cols_kernel" in k[3]]
 a, b = starts[-2], starts[-1]
 step = ks[a:b]
 t0 = step[0][0]
