@@ -20,6 +20,7 @@
 //   * every wait is bounded: on timeout a wave raises the launch's abort word, every waiting
 //     wave sees it within 64 polls, all workgroups leave at their next barrier.
 #include <algorithm>
+#include <cstdlib>
 
 #include "gru.h"
 #include "gru_persist.h"
@@ -1169,10 +1170,15 @@ static void xproj_split(XProj& q, int nd, int nprod) {
   q.nsplit = (sA * 4 + (sB - sA) * 2) * per;
 }
 
-// s2s_debug_gru_xp_group(1): XCD-grouped dealing of the dy units.  Off by default: at config 2 it cuts the BPTT
-// launch's fetched bytes 170 -> 102 MB (the producers' x-weights stay in L2) but the step is ~20 us slower in a
-// same-box A/B (3.419 -> 3.439 ms; profiles/r04/pmc_xp_group.txt)
-std::atomic<int> g_xp_group{0};
+// XCD-grouped dealing of the dy units (s2s_debug_gru_xp_group / S2S_XP_GROUP; on by default since round 5): at
+// config 2 the BPTT launch moves 214 -> 144 MB (the producers' x-weights stay in their XCD's L2), at config 4
+// 1,089 -> 806 MB.  Round 4 measured the step ~20 us slower with it; round 5 (sleepless polls, the loader's
+// rows drained before [B]) measures no difference: 3.2295 vs 3.2305 ms over three alternating runs each, same box
+// (profiles/r05/ab_xp_group.txt)
+std::atomic<int> g_xp_group{[] {
+  const char* e = std::getenv("S2S_XP_GROUP");
+  return e ? std::atoi(e) : 1;
+}()};
 
 // XCD-grouped dealing (XProj::G) when the spare slots form whole per-XCD groups of gsz producers and every
 // direction gets at least one group

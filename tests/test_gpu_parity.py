@@ -587,8 +587,8 @@ def test_bucket_events_mark_final_gradients(s2s, graph):
 @pytest.mark.parametrize("B", [32, 45])
 def test_fused_dy_dealing_does_not_change_the_step(s2s, B):
     """The BPTT launch's spare-slot producers compute its dy (the layer above's dX) unit by unit
-    in a fixed k order, so how the units are dealt to the producers -- round-robin (default) or XCD-grouped by
-    direction (s2s_debug_gru_xp_group(1)) -- must not change a bit of the step; and the whole step matches the
+    in a fixed k order, so how the units are dealt to the producers -- XCD-grouped by direction (the default,
+    s2s_debug_gru_xp_group(1)) or round-robin (0) -- must not change a bit of the step; and the whole step matches the
     dX computed by a GEMM in front of the BPTT (s2s_debug_gru_fused_dy(0)) to fp32 summation noise."""
     import ctypes
     from s2s_amd import _lib
@@ -608,7 +608,7 @@ def test_fused_dy_dealing_does_not_change_the_step(s2s, B):
             torch.cuda.synchronize()
             outs[arm] = (logp.clone(), model.grads.clone())
     finally:
-        fg(0)
+        fg(1)
         fd(1)
     assert torch.equal(outs["grouped"][0], outs["round-robin"][0])
     assert torch.equal(outs["grouped"][1], outs["round-robin"][1])
