@@ -306,6 +306,11 @@ std::atomic<int> g_head_fused{[] {
 // earlier (14 vs 21-24 us into the step) but measured slower (same box: 3.283 / 3.291 / 3.295 ms for 0 / 1 / 2):
 // the decoder prologue's kernels on the side stream then start after layer 1 holds every CU, each of them is
 // stretched over a whole GRU layer, and the last one finished after layer 3 -- 48 us in front of the decoder
+// S2S_ZERO_LATE=1 (A/B): gradient zeroing on the side stream after the decoder backward (see zero_late)
+std::atomic<int> g_zero_late{[] {
+  const char* e = std::getenv("S2S_ZERO_LATE");
+  return e ? std::atoi(e) : 0;
+}()};
 std::atomic<int> g_fork_mode{[] {
   const char* e = std::getenv("S2S_FORK_MODE");
   return e ? std::atoi(e) : 0;
@@ -359,16 +364,20 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   const int fmode = pmode == 1 ? 0 : (int)g_fork_mode;
   // fork point (fmode): the side stream waits for ev[13]; mode 2 records it after the head and issues the side
   // work after layer 1's forward launch (side_work below)
+  // zero_late (S2S_ZERO_LATE, split only): the gradient zeroing runs on the side stream right after the decoder
+  // backward's fork (ahead of every gradient writer, beside the top BPTT) instead of at the step's top
+  const bool zero_late = split && g_zero_late;
   auto fork_side = [&](bool wait_only) -> int {
     if (split) {
       if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[13], 0));
     }
-    if (flags & S2S_ZERO_GRADS)
+    if ((flags & S2S_ZERO_GRADS) && !zero_late)
       S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
     return 0;
   };
   if (fmode == 0) S2S_TRY(fork_side(false));
+  if (fmode == 3 && split) S2S_CHECK_HIP(hipEventRecord(ev[13], st));  // mode 3: recorded at the top
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
@@ -435,6 +444,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
   }
   if (fmode == 1) S2S_TRY(fork_side(false));
+  if (fmode == 3) S2S_TRY(fork_side(split));  // mode 3: independent of the head, created after it
   if (fmode == 2) {
     if (split) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
     else S2S_TRY(fork_side(false));  // (no side stream: the gradient zeroing on the main stream, here)
@@ -512,6 +522,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
                         w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr, g_fuse_dh ? &dht : nullptr));
   if (split) S2S_TRY(fork_to(st, side, ev[0]));
+  if (zero_late && (flags & S2S_ZERO_GRADS)) S2S_TRY(zero_async(side, grads, sizeof(float) * (size_t)off));
   S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
   S2S_TRY(mark_bucket(bev, 0, split ? side : st));
   // the reported nll (timit.lua:268-272) beside the encoder BPTT

@@ -167,6 +167,10 @@ struct PArgs {
   int stream_sweep;
   unsigned long long* stamps;  // diagnostic: [grid][L][8] s_memrealtime, or nullptr
   unsigned long long* pstamps;  // diagnostic: producers [producer][kProdStampItems][2] item start / end
+  // BPTT row prefetchers (bwd only): prefetch = lookahead in steps (0: off), progress = [nchains][nmem] words each
+  // member's loader sets to its step (zeroed with the region)
+  int prefetch, prefetch_wg;  // lookahead, prefetcher workgroups per chain
+  unsigned* progress;
 };
 
 // diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
@@ -778,6 +782,67 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
 // per step; it writes row q + 2 between [A] and [B] of step q, which the recurrence waves read after
 // [B] of step q + 1.
 constexpr int kBwdThreads = 320;
+
+// BPTT row prefetcher (one workgroup on an idle CU of each chain's XCD): the saved activations of a layer's BPTT
+// were written by its forward pass a whole layer-stack earlier and, for the lower layers, have left the Infinity
+// Cache: a member's loader wave then waits on HBM misses, either in front of the p2 barrier (its loads drained
+// there) or beside the next sweep (in flight across it) -- the lower layers' BPTT step measured ~0.3 us longer
+// than the top layer's even with the dy GEMM outside the launch.  The prefetcher reads the rows every member's
+// loader will load `a.prefetch` steps before it does (following member 0's progress), so their loads hit this
+// XCD's L2.  dy rows are touched only once their slice is complete (an earlier copy left in L2 would be served
+// to the loader's sc1 loads: stale).  One workgroup per chain, not one per member: the other idle CUs stay free
+// for the side stream's weight-gradient GEMMs (with a prefetcher per member the step measured 3.22 -> 3.59 ms
+// before the skip-ahead below, 3.46 after it).  A prefetcher that starts late (its CU still held by a side-stream
+// GEMM) skips the rows the loader has already taken, so it never holds the launch open past the chains.
+// prefetcher w of nwg for chain `chain` takes members [w nmem / nwg, (w + 1) nmem / nwg): 64 nmem / nwg loader lanes
+template <int NC>  // NC = H / 64 (nmem = 4 NC members, 256 NC (member, lane) tasks per chain and step)
+__device__ __forceinline__ void bptt_prefetch(const PArgs& a, int chain, int w, int nwg) {
+  if (threadIdx.x >= 256) return;
+  const int tid = threadIdx.x, L = a.L, H = a.H, B = a.B, nmem = a.nmem;
+  const int tasks = 64 * nmem / nwg, task0 = w * tasks;
+  const int dir = chain / a.MT, mt = chain % a.MT;
+  const PDir& g = a.d[dir];
+  const unsigned* prog = a.progress + (long)chain * nmem;  // member 0's step
+  int yready = 0, have = 0;
+  float sink = 0.f;
+  // the (member, lane) tasks of one step, 256 at a time (member = task / 64, the loader's lane = task % 64), every
+  // load of a step in flight together
+  constexpr int kMaxTasks = NC;  // 64 nmem / 256 with nmem = H / 16
+  for (int q = 3; q < L; ++q) {
+    unsigned spins = 0;
+    while (have + 3 + a.prefetch < q) {  // member 0's loader loads row q at its step q - 3
+      have = (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (have + 3 + a.prefetch >= q) break;
+      if (spin_give_up(spins, a.abort_word)) return;
+    }
+    if (q < have + 4) q = have + 4;  // rows the loader has loaded (or is loading) already: skip ahead
+    if (q >= L) break;
+    if (a.fused && tid < 64) xproj_wait(a.xq, dir, q / a.xq.tpt, yready, tid, a.abort_word);  // one wave, all lanes
+    if (a.fused) __syncthreads();
+    const int t = g.reverse ? q : L - 1 - q;
+    float4 v[kMaxTasks][5];
+#pragma unroll
+    for (int k = 0; k < kMaxTasks; ++k) {
+      if (256 * k >= tasks) break;  // (uniform)
+      // (unconditional loads from valid rows -- the values are discarded: padding utterances read the last one)
+      const int kt = tid + 256 * k, task = task0 + (kt < tasks ? kt : 0), m = task >> 6, lane = task & 63;
+      const int bl = min(mt * 16 + (lane >> 2), B - 1), u = m * 16 + 4 * (lane & 3);
+      const long row = (long)bl * L + t;
+      const float* sv = g.sv + row * 5 * H + u;
+#pragma unroll
+      for (int f = 0; f < 4; ++f) v[k][f] = *reinterpret_cast<const float4*>(sv + f * H);
+      v[k][4] = *reinterpret_cast<const float4*>(g.dy + row * g.lddy + u);
+    }
+#pragma unroll
+    for (int k = 0; k < kMaxTasks; ++k) {
+      if (256 * k >= tasks) break;
+#pragma unroll
+      for (int f = 0; f < 5; ++f) sink += v[k][f].x;
+    }
+  }
+  asm volatile("" ::"v"(sink));  // the loads stay
+}
+
 template <int NC>
 __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   __shared__ SkinnyRed red;
@@ -787,8 +852,13 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   extern __shared__ __attribute__((aligned(16))) float ylds[];  // producer tiles (fused dy)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
+  const int gch = 8 * ((a.nchains + 7) / 8);
+  if ((int)blockIdx.x >= chain_grid(a.nchains, a.nmem)) {  // (a.prefetch) chain c's row prefetchers, on its XCD
+    const int e = (int)blockIdx.x - chain_grid(a.nchains, a.nmem), c = e & 7, w = e >> 3;
+    if (c < a.nchains) bptt_prefetch<NC>(a, c, w, a.prefetch_wg);
+    return;
+  }
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: dy producer (or idle)
-    const int gch = 8 * ((a.nchains + 7) / 8);
     const int sp = (cs.chain - a.nchains) * a.nmem + cs.member, nsp = (gch - a.nchains) * a.nmem;
     prep_next_sync(a, sp, nsp);
     if (a.fused) xproj_produce_any<true>(a, ylds, sp, nsp);
@@ -862,10 +932,12 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     issue(2, ra);
     __syncthreads();  // [P]
     const bool ring = a.ring && loc;
+    unsigned* prog = a.progress ? a.progress + (long)cs.chain * a.nmem + c : nullptr;
     for (int p = 0; p < L; ++p) {
       __syncthreads();  // [A]
       if (abort_lds) return;
       put(p + 2, ra);   // loaded during the previous step
+      if (prog && lane == 0) __hip_atomic_store(prog, (unsigned)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // The next rows' loads are issued behind [A] and drained before [B] (the vmcnt(0) below): they are then in
       // this CU's memory queue only during the da_r hand-off -- whose consumers run the da_z half of their product
       // meanwhile -- and never beside the da_h sweep behind [B], which gates the step (an HBM load in the queue slows
@@ -1068,13 +1140,28 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 // workgroup (37 KB of LDS) can share its CU; the GEMMs fill the CUs the recurrence leaves idle.
 constexpr int kExclLds = 124 * 1024;
 
+// S2S_BPTT_PREFETCH_WG: prefetcher workgroups per chain.  Same box, config-2 step (three alternating runs each,
+// profiles/r05/ab_bptt_prefetch.txt): none 3.248 ms, 1 per chain 3.250 (one workgroup cannot keep 8 steps of rows
+// in flight), 2 per chain 3.182, 4 per chain 3.184, 16 (one per member) 3.463 (the side stream's weight-gradient
+// GEMMs lose the chain XCDs' idle CUs); the lower layers' BPTT step 3.05 -> 2.68 us (tools/gru_stamps.py, 2 layers)
+std::atomic<int> g_bptt_prefetch_wg{[] {
+  const char* e = std::getenv("S2S_BPTT_PREFETCH_WG");
+  return e ? std::atoi(e) : 2;
+}()};
+// S2S_BPTT_PREFETCH: lookahead (steps) of the BPTT row prefetchers (bptt_prefetch), 0 = off (4 / 8 / 12 measured
+// alike; 8)
+std::atomic<int> g_bptt_prefetch{[] {
+  const char* e = std::getenv("S2S_BPTT_PREFETCH");
+  return e ? std::atoi(e) : 8;
+}()};
 std::atomic<int> g_allow_local{1};
 std::atomic<int> g_sent_ring{kSentRing};  // s2s_debug_gru_ring(0): one sentinel slot per step (A/B)
 std::atomic<int> g_stream_sweep{1};  // s2s_debug_gru_stream_sweep(0): sweep the whole tile, then multiply (A/B)
 
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
-  const dim3 grid(chain_grid(a.nchains, a.nmem));
+  // (the BPTT's row prefetchers: 8 prefetch_wg more workgroups, chain c's at chain_grid + 8 w + c, on its XCD)
+  const dim3 grid(chain_grid(a.nchains, a.nmem) + (!fwd && a.prefetch ? 8 * a.prefetch_wg : 0));
   // exclusive only while one chain per XCD fits one workgroup per CU (32 CUs per XCD)
   const bool excl = excl_req && a.nchains <= 8 && a.nmem <= 32;
   const unsigned shm = excl ? kExclLds : (a.fused ? kXpLds : 0);
@@ -1135,8 +1222,10 @@ static size_t census_bytes(int B, int H) { return 4 * (size_t)(2 * ((B + 15) / 1
 // sentinel rows (re-armed in-kernel)
 // slice counters [2][L] and split-item counters [kXpMaxSplitItems]
 static size_t xcount_words(int L) { return 2 * (size_t)L + kXpMaxSplitItems; }
+// header | granules | census | slice / item counters | prefetch progress words (as many as census words)
 static size_t prep_bytes(int B, int L, int H) {
-  return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H) + 4 * xcount_words(L);
+  return 256 + 2 * 3 * 2 * sizeof(unsigned long long) * (size_t)B * H + census_bytes(B, H) + 4 * xcount_words(L) +
+         census_bytes(B, H);
 }
 static size_t sent_offset(int B, int L, int H) { return (prep_bytes(B, L, H) + 255) / 256 * 256; }
 // sentinel rows are tile-major: 16 rows per row tile (handoff.h tile_off)
@@ -1266,6 +1355,16 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   float* sr[2][3];
   unsigned* xcount = nullptr;
   carve_granules(static_cast<char*>(sync), b.B, b.L, b.H, &a.abort_word, gr, sr, &a.census, &xcount);
+  // row prefetchers: one workgroup per chain on an idle CU of its XCD (the chain's members leave at least one)
+  {
+    const int MTp = (b.B + 15) / 16, nch = b.ndir * MTp, nm = b.H / 16;
+    const int nwg = std::max(1, std::min((int)g_bptt_prefetch_wg, nm));
+    if (g_bptt_prefetch > 0 && nch <= 8 && nm + nwg <= 32 && nm % nwg == 0) {
+      a.prefetch = g_bptt_prefetch;
+      a.prefetch_wg = nwg;
+      a.progress = xcount + xcount_words(b.L);
+    }
+  }
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
                   b.reverse[d], gr[d][0], gr[d][1], gr[d][2], sr[d][0], sr[d][1], sr[d][2]};
