@@ -306,11 +306,25 @@ std::atomic<int> g_head_fused{[] {
 // earlier (14 vs 21-24 us into the step) but measured slower (same box: 3.283 / 3.291 / 3.295 ms for 0 / 1 / 2):
 // the decoder prologue's kernels on the side stream then start after layer 1 holds every CU, each of them is
 // stretched over a whole GRU layer, and the last one finished after layer 3 -- 48 us in front of the decoder
+// S2S_DEC_WGRAD_LATE=1 (A/B): the decoder weight-gradient nodes created after the top BPTT's launch.  Measured
+// 3.167 -> 3.680 ms: the replayed graph then ran the whole side branch (decoder and every GRU weight gradient)
+// after the last BPTT -- though the three BPTT launches, alone on the chip, took 355 / 373 / 370 us instead of
+// ~385 / 409 / 406 beside the weight-gradient GEMMs (profiles/r05/trace_step_dec_wgrad_late.txt)
+std::atomic<int> g_dec_wgrad_late{[] {
+  const char* e = std::getenv("S2S_DEC_WGRAD_LATE");
+  return e ? std::atoi(e) : 0;
+}()};
+// S2S_HEAD_EXTRA=0 (A/B): the loss seed and the gradient zeroing as side-stream kernels instead of in the step head
+std::atomic<int> g_head_extra{[] {
+  const char* e = std::getenv("S2S_HEAD_EXTRA");
+  return e ? std::atoi(e) : 1;
+}()};
 // S2S_ZERO_LATE=1 (A/B): gradient zeroing on the side stream after the decoder backward (see zero_late)
 std::atomic<int> g_zero_late{[] {
   const char* e = std::getenv("S2S_ZERO_LATE");
   return e ? std::atoi(e) : 0;
 }()};
+static bool zero_late_knob() { return g_zero_late != 0; }
 std::atomic<int> g_fork_mode{[] {
   const char* e = std::getenv("S2S_FORK_MODE");
   return e ? std::atoi(e) : 0;
@@ -362,6 +376,16 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // there (the fork precedes every gradient writer), off the critical path
   const int pmode = prologue_mode();
   const int fmode = pmode == 1 ? 0 : (int)g_fork_mode;
+  // the step head (when fused) also writes the loss seed dlogp = -labelmask and zeroes the gradients: no side-stream
+  // kernel then runs in front of it (a replayed graph ran the side branch's first two kernels -- the zeroing and the
+  // seed, 15 us -- before the head)
+  GruLayerIO io0{};
+  io0.ndir = 2;
+  io0.B = d->B;
+  io0.H = layers[0].H;
+  const bool head_fused = g_head_fused && g_sync_handover && gru_layer_persistent(io0);
+  const bool head_seed = head_fused && split && g_head_extra;                               // dlogp in the head
+  const bool head_zero = head_seed && (flags & S2S_ZERO_GRADS) && !zero_late_knob();      // zeroing in the head
   // fork point (fmode): the side stream waits for ev[13]; mode 2 records it after the head and issues the side
   // work after layer 1's forward launch (side_work below)
   // zero_late (S2S_ZERO_LATE, split only): the gradient zeroing runs on the side stream right after the decoder
@@ -372,7 +396,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[13], 0));
     }
-    if ((flags & S2S_ZERO_GRADS) && !zero_late)
+    if ((flags & S2S_ZERO_GRADS) && !zero_late && !head_zero)
       S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
     return 0;
   };
@@ -422,7 +446,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     return io;  // io.status stays null: the step harvests every sync region once, at its end
   };
   // the step's head (pad, pack, the first persistent launch's sync prep) as one launch when layer 1 is persistent
-  const bool head_fused = g_head_fused && g_sync_handover && gru_layer_persistent(layer_io(0));
   if (w.xpad && !head_fused) S2S_TRY(pad_cols_f32(st, x, d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp));
   // weight packing for every layer (both passes) and the decoder's parameter folds need only params
   // and labels: layer 1 on the critical path, the rest beside layer 1's recurrence when split
@@ -436,10 +459,19 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     std::vector<GruLayerIO> ios;
     for (int l = 0; l < nl; ++l) ios.push_back(layer_io(l));
     defer_pack = g_defer_pack && 2 * nl <= kMaxPackJobs && gru_layer_preps_next(ios[0], true);
-    if (head_fused)
+    if (head_fused) {
+      GruStepHead extra{};
+      if (head_seed) {
+        extra.dlogp = w.dlogp; extra.labels = labels; extra.tlen = d->label_lengths;
+        extra.B = B; extra.T = T; extra.O = O;
+      }
+      if (head_zero) {
+        extra.zero = grads; extra.zero_n4 = (size_t)off / 4; extra.zero_tail = (int)(off % 4);
+      }
       S2S_TRY(gru_step_head(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr, x,
                             d->inputFrameSize, w.xpad, B * L, d->inputFrameSize, w.Dp, w.gsync[0],
-                            gru_layer_sync_prep_bytes(ios[0]), w.gsync[1]));
+                            gru_layer_sync_prep_bytes(ios[0]), w.gsync[1], &extra));
+    }
     else
       S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
   }
@@ -455,7 +487,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // 2: inline on the main stream
   auto side_work = [&]() -> int {
     if (split && pmode != 2) {
-      S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));  // dlogp = -labelmask
+      if (!head_seed)  // dlogp = -labelmask
+        S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
       if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
       S2S_CHECK_HIP(hipEventRecord(ev[14], side));
       if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
@@ -521,14 +554,25 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   AttnDhTerms dht{};
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
                         w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr, g_fuse_dh ? &dht : nullptr));
-  if (split) S2S_TRY(fork_to(st, side, ev[0]));
-  if (zero_late && (flags & S2S_ZERO_GRADS)) S2S_TRY(zero_async(side, grads, sizeof(float) * (size_t)off));
-  S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
-  S2S_TRY(mark_bucket(bev, 0, split ? side : st));
-  // the reported nll (timit.lua:268-272) beside the encoder BPTT
-  if (split)
-    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr,
-                     d->label_lengths));
+  // the decoder's weight gradients beside the top BPTT (side stream).  dec_wgrad_late: their nodes are created
+  // after the top BPTT's launch (the fork event recorded here), so a replayed graph dispatches the BPTT first
+  const bool dec_late = split && g_dec_wgrad_late;
+  auto dec_wgrad = [&](bool wait_only) -> int {
+    if (split) {
+      if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[0], st));
+      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
+    }
+    if (zero_late && (flags & S2S_ZERO_GRADS)) S2S_TRY(zero_async(side, grads, sizeof(float) * (size_t)off));
+    S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
+    S2S_TRY(mark_bucket(bev, 0, split ? side : st));
+    // the reported nll (timit.lua:268-272) beside the encoder BPTT
+    if (split)
+      S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr,
+                       d->label_lengths));
+    return 0;
+  };
+  if (dec_late) S2S_CHECK_HIP(hipEventRecord(ev[0], st));
+  else S2S_TRY(dec_wgrad(false));
   // ---- encoder backward
   const bool defer = split && wgrad_fork_mode() == 1;
   int pending = -1;  // layer whose weight gradients wait for the next BPTT's sync prep
@@ -588,6 +632,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     gr.scale = scale;
     if (defer && pending >= 0) gr.prep_event = ev[1 + pending];
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
+    if (dec_late && l == nl - 1) S2S_TRY(dec_wgrad(true));
     if (defer) {
       if (pending >= 0) {  // the layer above: after this BPTT's dispatch point
         S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1 + pending], 0));

@@ -86,9 +86,10 @@ int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed,
 // there) and, when sync != null, the sync_prep of the step's first persistent launch (its region, prep bytes and
 // the other region's header `clear`) -- three back-to-back launches on the critical path before (pad_cols_kernel,
 // gru_pack_multi, sync_prep: 24 us in the r05 trace)
+struct GruStepHead;
 int gru_step_head(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer,
                   const float* x, long ldx, float* xpad, int rows, int cols, int dcols, void* sync, size_t prep_bytes,
-                  void* clear);
+                  void* clear, const GruStepHead* extra = nullptr);
 int gru_layer_fwd(hipStream_t st, const GruLayerIO& io, void* scratch, size_t scratch_bytes);
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes);
 // split form used by the model step: core = weight packing + BPTT + dx (critical path), writing the

@@ -307,10 +307,11 @@ int gru_layers_pack(hipStream_t st, const GruLayerIO* ios, float* const* packed,
 
 int gru_step_head(hipStream_t st, const GruLayerIO* ios, float* const* packed, int nlayers, GruPackJobs* defer,
                   const float* x, long ldx, float* xpad, int rows, int cols, int dcols, void* sync, size_t prep_bytes,
-                  void* clear) {
+                  void* clear, const GruStepHead* extra) {
   std::vector<PackArgs> now;
   S2S_TRY(pack_jobs(ios, packed, nlayers, defer, now));
-  GruStepHead h{};
+  GruStepHead h = extra ? *extra : GruStepHead{};
+  h.pack.n = 0;
   S2S_REQUIRE((int)now.size() <= kMaxPackJobs, "gru: too many pack jobs for the step head");
   for (const PackArgs& job : now) h.pack.j[h.pack.n++] = job;
   h.src = x; h.lds = ldx; h.dst = xpad; h.rows = xpad ? rows : 0; h.cols = cols; h.dcols = dcols;

@@ -53,6 +53,15 @@ struct GruStepHead {
   char* sync;
   size_t prep_bytes;
   char* clear;
+  // optional: the loss seed dlogp = -labelmask ((B, T, O), steps t >= tlen[b] zero; nll_seed's dlogp) and a zero
+  // fill of n4 16-byte words at zero (the step's gradient zeroing)
+  float* dlogp = nullptr;
+  const int* labels = nullptr;
+  const int* tlen = nullptr;
+  int B = 0, T = 0, O = 0;
+  void* zero = nullptr;
+  size_t zero_n4 = 0;
+  int zero_tail = 0;  // floats after the n4 words (< 4)
 };
 int gru_persist_step_head(hipStream_t st, const GruStepHead& h);
 

@@ -1466,11 +1466,24 @@ __global__ __launch_bounds__(256) void step_head_kernel(GruStepHead h, unsigned 
     h.dst[i] = c < h.cols ? h.src[r * h.lds + c] : 0.f;
   }
   for (int j = 0; j < h.pack.n; ++j) gru_pack_elems(h.pack.j[j], gid, gsz);
+  if (h.dlogp) {
+    const long nd = (long)h.B * h.T * h.O;
+    for (long i = gid; i < nd; i += gsz) {
+      const long bt = i / h.O;
+      const int o = (int)(i - bt * h.O), b = (int)(bt / h.T), t = (int)(bt - (long)b * h.T);
+      const bool hit = t < (h.tlen ? h.tlen[b] : h.T) && h.labels[bt] == o;
+      h.dlogp[i] = hit ? -1.f : 0.f;
+    }
+  }
+  uint4* z = static_cast<uint4*>(h.zero);
+  for (long i = gid; i < (long)h.zero_n4; i += gsz) z[i] = make_uint4(0u, 0u, 0u, 0u);
+  if (gid < h.zero_tail) reinterpret_cast<float*>(z + h.zero_n4)[gid] = 0.f;
 }
 int gru_persist_step_head(hipStream_t st, const GruStepHead& h) {
   long most = (long)h.rows * h.dcols;
   for (int j = 0; j < h.pack.n; ++j) most = std::max(most, 3L * h.pack.j[j].H * (h.pack.j[j].H + h.pack.j[j].Kx));
   if (h.sync) most = std::max<long>(most, (long)((h.prep_bytes - 256) / 16));
+  most = std::max<long>(most, std::max<long>((long)h.B * h.T * h.O, (long)h.zero_n4));
   const int blocks = (int)std::max<long>(1, std::min<long>(1024, (most + 255) / 256));
   hipLaunchKernelGGL(step_head_kernel, dim3(blocks), dim3(256), 0, st, h, inject_abort_take() ? 2u : 0u);
   S2S_CHECK_HIP(hipGetLastError());
