@@ -212,6 +212,7 @@ struct ModelWs {
   size_t scratch_bytes;
   float *dlogp, *nll, *logp, *dY0, *dY1;
   GemmWs gws_side;  // split-K slabs of the encoder weight-gradient GEMMs (may run on the side stream)
+  float* wpart;     // the first layer's in-launch weight gradients: utterance tiles' partials (S2S_BPTT_WGRAD)
   char* gsync[2];   // the persistent GRU launches' sync regions, alternating (gru_layer_preps_next)
   float* xpad;      // (B*L, Dp) zero-padded copy of the input when inputFrameSize % 32 != 0, else null
   int Dp;
@@ -245,6 +246,13 @@ ModelWs model_ws(const s2s_model_dims* d, void* base) {
   w.dY0 = bp.take<float>(B * L * 2 * hmax);
   w.dY1 = bp.take<float>(B * L * 2 * hmax);
   w.gws_side = GemmWs{bp.take<float>(kGemmWsFloats), kGemmWsFloats};
+  {
+    const LayerDims l0 = enc_layers(d)[0];
+    GruLayerIO io{};
+    io.ndir = 2; io.B = d->B; io.L = d->L; io.D = l0.D; io.H = l0.H;
+    const size_t n = gru_layer_wgrad_part_floats(io);
+    w.wpart = n ? bp.take<float>(n) : nullptr;
+  }
   {
     size_t sb = 0;
     for (auto& ld : enc_layers(d)) sb = std::max(sb, gru_persist_sync_bytes(d->B, d->L, ld.H));
@@ -318,6 +326,12 @@ std::atomic<int> g_dec_wgrad_late{[] {
 std::atomic<int> g_head_extra{[] {
   const char* e = std::getenv("S2S_HEAD_EXTRA");
   return e ? std::atoi(e) : 1;
+}()};
+// S2S_BPTT_WGRAD: the first encoder layer's weight gradients inside its BPTT launch (gru_persist.hip bptt_wgrad)
+// instead of a GEMM behind it on the side stream; 0 = the GEMM (A/B)
+std::atomic<int> g_bptt_wgrad{[] {
+  const char* e = std::getenv("S2S_BPTT_WGRAD");
+  return e ? std::atoi(e) : 0;
 }()};
 // S2S_ZERO_LATE=1 (A/B): gradient zeroing on the side stream after the decoder backward (see zero_late)
 std::atomic<int> g_zero_late{[] {
@@ -630,6 +644,12 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       S2S_REQUIRE(gr.yWx != nullptr && up.ldx == 2L * H, "model step: dX of layer above needs packed weights");
     }
     gr.scale = scale;
+    // the first layer's weight gradients inside its BPTT launch: nothing behind the step's last recurrence
+    const bool wg_in = l == 0 && g_bptt_wgrad && gru_layer_wgrad_fused(io);
+    if (wg_in) {
+      gr.wgrad = 1;
+      gr.wpart = w.wpart;
+    }
     if (defer && pending >= 0) gr.prep_event = ev[1 + pending];
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
     if (dec_late && l == nl - 1) S2S_TRY(dec_wgrad(true));
@@ -639,10 +659,14 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
         S2S_TRY(issue_wgrad(pending));
       }
       pending = l;
-      if (l == 0) {  // the last BPTT: nothing left to dispatch ahead of layer 1's GEMMs
+      if (l == 0 && wg_in) {
+        S2S_TRY(mark_bucket(bev, nl, st));
+      } else if (l == 0) {  // the last BPTT: nothing left to dispatch ahead of layer 1's GEMMs
         S2S_TRY(fork_to(st, side, ev[1 + l]));
         S2S_TRY(issue_wgrad(l));
       }
+    } else if (wg_in) {
+      S2S_TRY(mark_bucket(bev, nl - l, st));
     } else {
       if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
       S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
@@ -759,7 +783,18 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
     S2S_REQUIRE(false, "ctx: host-coherent status word allocation failed");
   }
   if (c->status_host) std::memset(c->status_host, 0, 64);
-  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) c->side = nullptr;
+  // S2S_SIDE_PRIORITY=1 (A/B): the side stream (weight-gradient GEMMs) at the lowest queue priority, so the
+  // dispatcher serves the persistent launches' workgroups first
+  static const int side_prio = [] {
+    const char* e = std::getenv("S2S_SIDE_PRIORITY");
+    return e ? std::atoi(e) : 0;
+  }();
+  int least = 0, greatest = 0;
+  if (side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) {
+    if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least) != hipSuccess) c->side = nullptr;
+  } else if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+    c->side = nullptr;
+  }
   for (auto& e : c->ev)
     if (c->side && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) {
       (void)hipStreamDestroy(c->side);
@@ -1510,3 +1545,5 @@ int s2s::inject_abort_take() {
 extern "C" void s2s_debug_sync_handover(int on) { g_sync_handover = on; }
 extern "C" void s2s_debug_dec_sync_prologue(int on) { g_dec_sync_prologue = on; }
 extern "C" void s2s_debug_defer_pack(int on) { g_defer_pack = on; }
+// diagnostic: the first encoder layer's weight gradients inside its BPTT launch (1) or by the GEMM behind it (0)
+extern "C" void s2s_debug_bptt_wgrad(int on) { g_bptt_wgrad = on; }

@@ -68,9 +68,17 @@ struct GruLayerGrad {
   const float* yalpha = nullptr;
   const float* ydc = nullptr;
   int yT = 0;
+  // optional (persistent BPTT, gru_layer_wgrad_fused): the launch computes this layer's weight gradients itself
+  // (dW += scale ..., gru_layer_wgrad's products) -- no gru_layer_wgrad after it; wpart: gru_layer_wgrad_part_floats
+  int wgrad = 0;
+  float* wpart = nullptr;
 };
 
 size_t gru_layer_scratch_bytes(int ndir, int B, int L, int D, int H);
+// the layer's persistent BPTT launch can carry its weight gradients (GruLayerGrad::wgrad), and the partials'
+// workspace that needs (floats)
+bool gru_layer_wgrad_fused(const GruLayerIO& io);
+size_t gru_layer_wgrad_part_floats(const GruLayerIO& io);
 // the layer's recurrences run as persistent launches (sync regions, hand-offs) rather than per-step kernels
 bool gru_layer_persistent(const GruLayerIO& io);
 // Every kernel layout of one layer's weights (recurrent Uzr/Uh and their transposes, the padded

@@ -467,6 +467,7 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
   const bool persist = use_persistent(nd, B, H);
   const bool yfuse = gru_layer_dy_fused(io, gr);
   S2S_REQUIRE(!gr.yalpha || yfuse, "gru: the dh context term is only produced inside the fused BPTT launch");
+  S2S_REQUIRE(!gr.wgrad || persist, "gru: in-launch weight gradients need the persistent BPTT");
   if (gr.ydA && !yfuse) {  // the layer above's dX as one GEMM in front of the BPTT (same order as in-launch)
     GemmProblem p{gr.ydA, gr.yWx, const_cast<float*>(gr.dy[0]), nullptr, gr.yldA, gr.yldw, gr.lddy, B * L, gr.yN,
                   gr.yK, 1.f, 0.f};
@@ -493,6 +494,15 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     }
     f.excl = io.excl;
     f.status = io.status;
+    if (gr.wgrad) {
+      S2S_REQUIRE(gru_layer_wgrad_fused(io), "gru: in-launch weight gradients need a persistent BPTT that fits them");
+      f.wgrad = 1;
+      for (int d = 0; d < 2; ++d)
+        for (int g = 0; g < 3; ++g) f.wdW[d][g] = gr.dW[d][g];
+      f.wscale = gr.scale;
+      f.wx = io.x; f.wldx = io.ldx; f.wD = D;
+      f.wpart = gr.wpart;
+    }
     S2S_TRY(gru_persist_bwd(st, f, sync));
   } else {
     ProfScope ps(st, "gru_bwd_steps", 2.0 * nd * B * L * 3.0 * H * H, 0.0);
@@ -514,6 +524,14 @@ int gru_layer_bwd_core(hipStream_t st, const GruLayerIO& io, const GruLayerGrad&
     S2S_TRY(gemm_f32(st, &p, 1, false, false, layer_gemm_ws(scratch, nd, B, L, D, H)));
   }
   return 0;
+}
+
+bool gru_layer_wgrad_fused(const GruLayerIO& io) {
+  return use_persistent(io.ndir, io.B, io.H) && gru_persist_wgrad_fits(io.ndir, io.B, io.H, io.D);
+}
+size_t gru_layer_wgrad_part_floats(const GruLayerIO& io) {
+  const int MT = (io.B + 15) / 16;
+  return (size_t)io.ndir * MT * 3 * io.H * (io.H + (io.D + 15) / 16 * 16);
 }
 
 bool gru_layer_preps_next(const GruLayerIO& io, bool fwd) {
@@ -572,6 +590,7 @@ int gru_layer_wgrad(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr
 
 int gru_layer_bwd(hipStream_t st, const GruLayerIO& io, const GruLayerGrad& gr, void* scratch, size_t scratch_bytes) {
   S2S_TRY(gru_layer_bwd_core(st, io, gr, nullptr, scratch, scratch_bytes));
+  if (gr.wgrad) return 0;  // computed inside the BPTT launch
   return gru_layer_wgrad(st, io, gr, gru_layer_dA(io, scratch),
                          layer_gemm_ws(scratch, io.ndir, io.B, io.L, io.D, io.H));
 }

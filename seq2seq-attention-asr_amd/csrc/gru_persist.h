@@ -122,9 +122,21 @@ struct GruPersistBwd {
   size_t next_prep = 0;
   int excl = 0;
   unsigned* status = nullptr;
+  // optional in-launch weight gradients (gru_persist_wgrad_fits): wdW[d][g] += wscale dA^T [h_{t-1} or q | x]
+  // (gru_layer_wgrad's products) by workers beside the chains; wx (B*L, wldx) the layer input, wD columns;
+  // wpart: ndir * ceil(B/16) * 3H * (H + round_up(wD, 16)) floats of the utterance tiles' partials
+  int wgrad = 0;
+  float* wdW[2][3] = {};
+  float wscale = 1.f;
+  const float* wx = nullptr;
+  long wldx = 0;
+  int wD = 0;
+  float* wpart = nullptr;
 };
 
 bool gru_persist_supported(int ndir, int B, int H);
+// the BPTT launch can carry its layer's weight gradients (GruPersistBwd::wgrad) at this shape (input width D)
+bool gru_persist_wgrad_fits(int ndir, int B, int H, int D);
 // the backward's spare slots can produce its dy (the dX GEMM of the layer above) in-launch
 bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy);
 bool gru_persist_fused_xproj(int ndir, int B, int H, int Kx);

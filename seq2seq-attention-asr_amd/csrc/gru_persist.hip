@@ -144,6 +144,21 @@ __device__ __forceinline__ bool xunit_of(const XProj& q, int nd, int p, int npro
 }
 constexpr int kXpLds = 4 * 64 * 36 * 4;  // producer LDS: A and B tiles, double-buffered
 
+// In-launch weight gradients of a BPTT (bptt_wgrad; gru_persist_bwd's wgrad): nw = 3H/64 workers per chain, or 0
+struct WArgs {
+  int nw;
+  float* dW[2][3];  // dW[d][gate] (3 gates x H rows, H + D columns): dW += scale dA^T [h_{t-1} or q | x]
+  float scale;
+  const float* x;  // the layer input (B*L, ldx), D columns read (zero past D)
+  long ldx;
+  int D, NP;        // x columns; partial row length H + round_up(D, 16)
+  float* part;      // [ndir][MT][3H][NP] the 16-utterance tiles' partial sums (MT > 1)
+  unsigned* ticket;  // [ndir][nw] arrival counters (zeroed with the sync region)
+  // diagnostic (s2s_debug_gru_wg_stamps): [nchains][nw][L + 4] s_memrealtime at entry, census checked, each
+  // step's products issued, loop end, exit
+  unsigned long long* stamps;
+};
+
 struct PArgs {
   XProj xq;
   int fused;
@@ -171,6 +186,7 @@ struct PArgs {
   // member's loader sets to its step (zeroed with the region)
   int prefetch, prefetch_wg;  // lookahead, prefetcher workgroups per chain
   unsigned* progress;
+  WArgs wg;  // bwd: in-launch weight gradients (wg.nw = 0: off); needs progress
 };
 
 // diagnostic stamps (s2s_debug_gru_stamps): per (workgroup, step) at p1 sweep start / done /
@@ -217,6 +233,7 @@ __device__ __forceinline__ bool sweep_sent_n(float4 (&a)[NC], __amdgpu_buffer_rs
 #endif
 std::atomic<unsigned long long*> g_gru_stamps[2] = {{nullptr}, {nullptr}};
 std::atomic<unsigned long long*> g_gru_pstamps[2] = {{nullptr}, {nullptr}};
+std::atomic<unsigned long long*> g_gru_wstamps{nullptr};
 constexpr int kProdStampItems = 32;
 
 // cross-wave sum + abort agreement at the same barrier
@@ -833,14 +850,225 @@ __device__ __forceinline__ void bptt_prefetch(const PArgs& a, int chain, int w, 
       for (int f = 0; f < 4; ++f) v[k][f] = *reinterpret_cast<const float4*>(sv + f * H);
       v[k][4] = *reinterpret_cast<const float4*>(g.dy + row * g.lddy + u);
     }
+    // the in-launch weight-gradient workers' own operand rows (bptt_wgrad): q = r h (sv + 4H, which the members do
+    // not read) and the layer input x of the chain's 16 utterances at this step, one float4 per thread and 64 B
+    float4 wv[2] = {make_float4(0.f, 0.f, 0.f, 0.f), make_float4(0.f, 0.f, 0.f, 0.f)};
+    if (a.wg.nw) {
+      const int bl = min(mt * 16 + (tid >> 4), B - 1), cq = 4 * (tid & 15);  // 16 threads per utterance
+      const long row = (long)bl * L + t;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (cq + 64 * i < H) wv[0].x += g.sv[row * 5 * H + 4 * H + cq + 64 * i];
+      if (cq < a.wg.D) wv[1].x = a.wg.x[row * a.wg.ldx + cq] + a.wg.x[row * a.wg.ldx + min(cq + 64, a.wg.D - 1)];
+    }
 #pragma unroll
     for (int k = 0; k < kMaxTasks; ++k) {
       if (256 * k >= tasks) break;
 #pragma unroll
       for (int f = 0; f < 5; ++f) sink += v[k][f].x;
     }
+    sink += wv[0].x + wv[1].x;
   }
   asm volatile("" ::"v"(sink));  // the loads stay
+}
+
+// In-launch weight gradients (gru_persist_bwd's wgrad: the model step's first encoder layer, whose BPTT is the
+// step's last recurrence -- its weight-gradient GEMM used to follow the launch, ~90 us on the critical path):
+//   dW_d[gate] += scale sum_{b, t} dA_d[b, t, gate]^T [h_{t-1} (q = r h for the candidate) | x]_{b, t}
+// the GemmProblems of gru_layer_wgrad (LinearZeroBias.lua:67-74 accGradParameters, RNN.lua:194), computed by nw =
+// 3H/64 workgroups on each chain's XCD (blockIdx = 8 w + chain past the prefetchers) step by step behind the chain:
+// worker w of chain (dir, mt) owns the 64 gate rows [64 w, 64 w + 64) of direction dir (one gate) and every column,
+// summed over the chain's 16 utterances; four waves of 16 x 16 x 4 fp32 MFMAs, wave v taking column blocks
+// [kWgCB v, kWgCB (v + 1)).  Step p's gate gradients are final once every member's loader has passed [A] of step
+// p + 3 (the member's p2 sweep of step p + 1 waited for loads issued after all its dA stores of step p: vmcnt retires
+// in order), or at the members' final mark (L + 3, behind a vmcnt(0) + barrier after their last step).  The chain's
+// dA rows stay in its XCD's L2 (plain stores), so a worker must share that XCD: one that does not (never seen; the
+// round-robin placement every chain relies on) fails the launch rather than read stale rows.  The utterance tiles'
+// partials are written through (sc1) and the last arriving tile (ticket) adds them in tile order into dW (guide's
+// valid form: sc1 stores drained, one agent-scope add, sc1 loads) with one flat, coalesced loop.
+constexpr int kWgCB = 6;  // column blocks of 16 per wave (H + D <= 384)
+template <int NC>
+__device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, unsigned* tb_lds, int* flag_lds) {
+  if (threadIdx.x >= 256) return;
+  const WArgs& q = a.wg;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int H = a.H, L = a.L, B = a.B, nmem = a.nmem, NP = q.NP, nblk = NP / 16;
+  const int dir = chain / a.MT, mt = chain % a.MT;
+  const PDir& g = a.d[dir];
+  const int row0 = 64 * w, gate = row0 / H;
+  unsigned long long* ws = q.stamps ? q.stamps + ((long)chain * q.nw + w) * (L + 4) : nullptr;
+  auto stamp = [&](int k) {
+    if (ws && tid == 0) ws[k] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
+  const unsigned tb = launch_tagbase(a.abort_word, tb_lds);
+  if (tid < 64) {  // co-location with every member of the chain (their census words)
+    const unsigned me = tb | 0x100u | (__builtin_amdgcn_s_getreg(kXccIdHwreg) & 15u);
+    bool same = true;
+    if (lane < nmem) {
+      unsigned spins = 0, v;
+      while (((v = __hip_atomic_load(a.census + (long)chain * nmem + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) &
+              0xffff0100u) != (tb | 0x100u))
+        if (spin_give_up(spins, a.abort_word)) break;
+      same = v == me;
+    }
+    const bool all = __ballot(!same) == 0ull;
+    if (lane == 0) *flag_lds = all ? 1 : 0;
+  }
+  __syncthreads();
+  if (!*flag_lds) {
+    if (tid == 0) __hip_atomic_store(a.abort_word, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  stamp(1);
+  const unsigned* prog = a.progress + (long)chain * nmem;
+  const long svo = (gate == 2 ? 4L : 3L) * H;
+  const int jl = lane & 15, kq = lane >> 4, cb0 = wave * kWgCB;
+  // every member's loader at [A] of step p + 3 or later (lanes past nmem read as done)
+  // nrdy = steps known final: p < nrdy once every member's loader is past [A] of step p + 3 (the slowest member's
+  // progress word v gives v - 2 steps; the final mark L + 3 gives all).  Re-read only when the next step is not
+  // among them: a worker behind the chain issues no poll (whose wait would also drain its operand loads)
+#ifdef S2S_EXP_WG_NOWAIT  // diagnostic (timing only, wrong results): the workers do not wait for the chain
+  int nrdy = L;
+#else
+  int nrdy = 0;
+#endif
+  auto refresh = [&]() {
+    unsigned v = lane < nmem ? __hip_atomic_load(prog + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : ~0u;
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) v = min(v, (unsigned)__shfl_xor((int)v, o, 64));
+    v = (unsigned)__builtin_amdgcn_readfirstlane((int)v);
+    const int n = v >= (unsigned)L + 3u ? L : (int)v - 2;
+    nrdy = max(nrdy, min(n, L));
+  };
+  auto ready = [&](int p) -> bool {
+    if (p >= nrdy) refresh();
+    return p < nrdy;
+  };
+  auto wait = [&](int p) -> bool {
+    unsigned spins = 0;
+    while (!ready(p)) {
+      if (spin_give_up(spins, a.abort_word)) return false;
+      __builtin_amdgcn_s_sleep(4);
+    }
+    return true;
+  };
+  // Iteration i = 4 p + kk: processing step p, utterances mt*16 + 4 kk + (0..3) as one K = 4 slice (lane: k = lane >> 4,
+  // row / column lane & 15): 4 A values (dA, 64 gate rows) and kWgCB B values (this wave's columns) per lane, then
+  // 4 kWgCB MFMAs (~0.3 us).  A ring of kWgRing operand sets keeps kWgRing - 1 iterations of loads in flight behind
+  // the products (the loop is unrolled by the ring size, so the code stays a few KB: the instruction cache is shared
+  // with a chain member's CU).  Buffer loads with 32-bit offsets; dA sc1 (the chain's rows, L2-resident).
+  constexpr int kWgRing = 8;
+  const __amdgpu_buffer_rsrc_t ar = rsrc_of(g.dA), sr = rsrc_of(g.sv), xr = rsrc_of(q.x);
+  const int ldA = (int)g.ldA, ldx = (int)q.ldx, s5 = 5 * H, svoi = (int)svo;
+  float ra[kWgRing][4], rb[kWgRing][kWgCB];
+  auto issue = [&](int i, float (&av)[4], float (&bv)[kWgCB]) {
+    const int p = i >> 2, kk = i & 3;
+    const int t = g.reverse ? p : L - 1 - p;
+    const int b = mt * 16 + 4 * kk + kq;
+    const bool live = b < B;
+    const int row = min(b, B - 1) * L + t;
+#ifdef S2S_EXP_WG_NOLOAD  // diagnostic (timing only, wrong results): operands from registers
+#pragma unroll
+    for (int r = 0; r < 4; ++r) av[r] = (float)(row + r);
+#pragma unroll
+    for (int c = 0; c < kWgCB; ++c) bv[c] = (float)(kk + c);
+    return;
+#endif
+    const int oa = 4 * (row * ldA + row0 + jl);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ar, oa + 64 * r, 0, 16));
+      av[r] = live ? v : 0.f;
+    }
+    const int os = 4 * (row * s5 + svoi + cb0 * 16 + jl), ox = 4 * (row * ldx + cb0 * 16 + jl - H);
+#pragma unroll
+    for (int c = 0; c < kWgCB; ++c) {
+      const int cb = cb0 + c;
+      if (cb >= nblk) {
+        bv[c] = 0.f;
+      } else if (cb * 16 < H) {  // (uniform: a block is all h or all x, H % 16 == 0)
+        bv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sr, os + 64 * c, 0, 0));
+      } else {
+        const int xc = cb * 16 + jl - H;
+        const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xc < q.D ? ox + 64 * c : 0, 0, 0));
+        bv[c] = xc < q.D ? v : 0.f;
+      }
+    }
+  };
+  floatx4 acc[4][kWgCB];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < kWgCB; ++c) acc[r][c] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const float (&av)[4], const float (&bv)[kWgCB]) {
+#ifdef S2S_EXP_WG_NOMMA  // diagnostic (timing only, wrong results): one add per operand instead of the products
+#pragma unroll
+    for (int c = 0; c < kWgCB; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r][c][0] += av[r] + bv[c];
+    return;
+#endif
+#pragma unroll
+    for (int c = 0; c < kWgCB; ++c) {
+      if (cb0 + c >= nblk) continue;  // (uniform)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[c], acc[r][c], 0, 0, 0);
+    }
+  };
+  // the steps a group of kWgRing iterations will load are checked final once, in front of the group (the poll's
+  // wait would drain the loads in flight anyway), so the unrolled body has no wait in it
+  const int niter = 4 * L;
+  auto need = [&](int last_iter) -> bool { return wait(min(last_iter, niter - 1) >> 2); };
+  if (!need(kWgRing - 2)) return;
+#pragma unroll
+  for (int u = 0; u < kWgRing - 1; ++u)
+    if (u < niter) issue(u, ra[u], rb[u]);
+  for (int i = 0; i < niter; i += kWgRing) {
+    if (i + kWgRing < niter && !need(i + 2 * kWgRing - 2)) return;
+#pragma unroll
+    for (int u = 0; u < kWgRing; ++u) {
+      const int nx = i + u + kWgRing - 1;
+      if (nx < niter) issue(nx, ra[(u + kWgRing - 1) % kWgRing], rb[(u + kWgRing - 1) % kWgRing]);
+      if (i + u < niter) mma(ra[u], rb[u]);
+      if (((i + u) & 3) == 3) stamp(2 + ((i + u) >> 2));
+    }
+  }
+  stamp(L + 2);
+  // D[i][j] of block (r, c) at lane (j = lane & 15, i = 4 (lane >> 4) + e): gate row row0 + 16 r + 4 kq + e
+  const int D = q.D;
+  const __amdgpu_buffer_rsrc_t pr = rsrc_of(q.part);
+  const int tile = 3 * H * NP;  // one utterance tile's partial (per direction: MT tiles)
+  const int mine = (dir * a.MT + mt) * tile + row0 * NP + (4 * kq) * NP + cb0 * 16 + jl;
+#pragma unroll
+  for (int c = 0; c < kWgCB; ++c) {
+    if (cb0 + c >= nblk) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(acc[r][c][e]), pr, 4 * (mine + (16 * r + e) * NP + 16 * c),
+                                              0, 16);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    *flag_lds = (int)__hip_atomic_fetch_add(q.ticket + dir * q.nw + w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  if (*flag_lds != a.MT - 1) return;
+  // the last tile to arrive: dW rows [u0, u0 + 64) of (dir, gate) += scale * (sum of the MT partials in tile order)
+  const long ldw = (long)H + D;
+  float* dW = q.dW[dir][gate];
+  const int u0 = row0 - gate * H, first = dir * a.MT * tile + row0 * NP;
+  for (int idx = tid; idx < 64 * NP; idx += 256) {
+    const int rr = idx / NP, j = idx - rr * NP;
+    if (j >= H + D) continue;
+    float sum = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, 4 * (first + idx), 0, 16));
+    for (int m = 1; m < a.MT; ++m)
+      sum += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(pr, 4 * (first + m * tile + idx), 0, 16));
+    float* o = dW + (long)(u0 + rr) * ldw + j;
+    *o = q.scale * sum + *o;
+  }
 }
 
 template <int NC>
@@ -853,9 +1081,15 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
   const int gch = 8 * ((a.nchains + 7) / 8);
-  if ((int)blockIdx.x >= chain_grid(a.nchains, a.nmem)) {  // (a.prefetch) chain c's row prefetchers, on its XCD
-    const int e = (int)blockIdx.x - chain_grid(a.nchains, a.nmem), c = e & 7, w = e >> 3;
-    if (c < a.nchains) bptt_prefetch<NC>(a, c, w, a.prefetch_wg);
+  if ((int)blockIdx.x >= chain_grid(a.nchains, a.nmem)) {
+    const int pre = chain_grid(a.nchains, a.nmem) + (a.prefetch ? 8 * a.prefetch_wg : 0);
+    if ((int)blockIdx.x < pre) {  // (a.prefetch) chain c's row prefetchers, on its XCD
+      const int e = (int)blockIdx.x - chain_grid(a.nchains, a.nmem), c = e & 7, w = e >> 3;
+      if (c < a.nchains) bptt_prefetch<NC>(a, c, w, a.prefetch_wg);
+      return;
+    }
+    const int e = (int)blockIdx.x - pre, c = e & 7, w = e >> 3;  // (a.wg.nw) chain c's weight-gradient workers
+    if (c < a.nchains) bptt_wgrad<NC>(a, c, w, &tb_lds, &abort_lds);
     return;
   }
   if (cs.chain >= a.nchains) {  // spare slot of the placement grid: dy producer (or idle)
@@ -959,6 +1193,10 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 #ifdef S2S_EXP_LOADB  // A/B: the round-4 placement behind [B]
       issue(p + 3, ra);
 #endif
+    }
+    if (a.wg.nw) {  // the weight-gradient workers' final mark: every dA store of this member has landed ([C])
+      __syncthreads();  // [C]
+      if (lane == 0) __hip_atomic_store(prog, (unsigned)L + 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     return;
   }
@@ -1133,6 +1371,10 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
     GRU_STAMP(5);
     if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
   }
+  if (a.wg.nw) {  // [C]: the loader's final mark for the weight-gradient workers follows this wave's last dA stores
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
 }
 
 // Exclusive-CU mode (set while weight-gradient GEMMs run on a side stream beside the recurrence):
@@ -1154,6 +1396,12 @@ std::atomic<int> g_bptt_prefetch{[] {
   const char* e = std::getenv("S2S_BPTT_PREFETCH");
   return e ? std::atoi(e) : 8;
 }()};
+// prefetcher workgroups per chain of a BPTT launch of this shape (0: none)
+int bptt_prefetch_wg(int ndir, int B, int H) {
+  const int nch = ndir * ((B + 15) / 16), nm = H / 16;
+  const int nwg = std::max(1, std::min((int)g_bptt_prefetch_wg, nm));
+  return g_bptt_prefetch > 0 && nch <= 8 && nm + nwg <= 32 && nm % nwg == 0 ? nwg : 0;
+}
 std::atomic<int> g_allow_local{1};
 std::atomic<int> g_sent_ring{kSentRing};  // s2s_debug_gru_ring(0): one sentinel slot per step (A/B)
 std::atomic<int> g_stream_sweep{1};  // s2s_debug_gru_stream_sweep(0): sweep the whole tile, then multiply (A/B)
@@ -1161,7 +1409,9 @@ std::atomic<int> g_stream_sweep{1};  // s2s_debug_gru_stream_sweep(0): sweep the
 template <int NC>
 int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
   // (the BPTT's row prefetchers: 8 prefetch_wg more workgroups, chain c's at chain_grid + 8 w + c, on its XCD)
-  const dim3 grid(chain_grid(a.nchains, a.nmem) + (!fwd && a.prefetch ? 8 * a.prefetch_wg : 0));
+  // and the in-launch weight-gradient workers: 8 nw more, chain c's worker w at the prefetchers' end + 8 w + c)
+  const dim3 grid(chain_grid(a.nchains, a.nmem) + (!fwd && a.prefetch ? 8 * a.prefetch_wg : 0) +
+                  (!fwd ? 8 * a.wg.nw : 0));
   // exclusive only while one chain per XCD fits one workgroup per CU (32 CUs per XCD)
   const bool excl = excl_req && a.nchains <= 8 && a.nmem <= 32;
   const unsigned shm = excl ? kExclLds : (a.fused ? kXpLds : 0);
@@ -1206,6 +1456,13 @@ bool gru_persist_fused_dy(int ndir, int B, int H, int K, long ldw, long lddy) {
   if (!g_fuse_xproj || !g_fuse_dy || B > 64 || K % 32 != 0 || H % 64 != 0 || ldw % 4 != 0 || lddy < (long)ndir * H) return false;
   const int MT = (B + 15) / 16, nchains = ndir * MT, nmem = H / 16;
   return chain_grid(nchains, nmem) - nchains * nmem >= 32;  // spare slots to produce on
+}
+
+bool gru_persist_wgrad_fits(int ndir, int B, int H, int D) {
+  const int nch = ndir * ((B + 15) / 16), nm = H / 16, nw = 3 * H / 64;
+  // one chain per XCD, its members, prefetchers and workers one per CU; a worker wave's columns fit kWgCB blocks
+  return H % 64 == 0 && D > 0 && nch <= 8 && nm + bptt_prefetch_wg(ndir, B, H) + nw <= 32 &&
+         H + (D + 15) / 16 * 16 <= 4 * kWgCB * 16;
 }
 
 bool gru_persist_supported(int ndir, int B, int H) {
@@ -1357,13 +1614,26 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   carve_granules(static_cast<char*>(sync), b.B, b.L, b.H, &a.abort_word, gr, sr, &a.census, &xcount);
   // row prefetchers: one workgroup per chain on an idle CU of its XCD (the chain's members leave at least one)
   {
-    const int MTp = (b.B + 15) / 16, nch = b.ndir * MTp, nm = b.H / 16;
-    const int nwg = std::max(1, std::min((int)g_bptt_prefetch_wg, nm));
-    if (g_bptt_prefetch > 0 && nch <= 8 && nm + nwg <= 32 && nm % nwg == 0) {
+    const int nwg = bptt_prefetch_wg(b.ndir, b.B, b.H);
+    if (nwg) {
       a.prefetch = g_bptt_prefetch;
       a.prefetch_wg = nwg;
       a.progress = xcount + xcount_words(b.L);
     }
+  }
+  if (b.wgrad) {  // in-launch weight gradients (bptt_wgrad)
+    S2S_REQUIRE(gru_persist_wgrad_fits(b.ndir, b.B, b.H, b.wD) && b.wx && b.wpart,
+                "gru persistent bwd: in-launch weight gradients do not fit this shape");
+    WArgs& q = a.wg;
+    q.nw = 3 * b.H / 64;
+    for (int d = 0; d < 2; ++d)
+      for (int g = 0; g < 3; ++g) q.dW[d][g] = b.wdW[d][g];
+    q.scale = b.wscale;
+    q.x = b.wx; q.ldx = b.wldx; q.D = b.wD; q.NP = b.H + (b.wD + 15) / 16 * 16;
+    q.part = b.wpart;
+    q.stamps = g_gru_wstamps;
+    a.progress = xcount + xcount_words(b.L);
+    q.ticket = a.progress + (long)b.ndir * MT * (b.H / 16);  // past the progress words (census-sized region)
   }
   for (int d = 0; d < b.ndir; ++d)
     a.d[d] = PDir{nullptr, 0, b.UhT[d], b.UzrT[d], nullptr, 0, b.sv[d], b.dy[d], b.lddy, b.dA[d], b.ldA,
@@ -1408,8 +1678,13 @@ int gru_persist_bwd(hipStream_t st, const GruPersistBwd& b, void* sync) {
   const double ybytes = b.ydA ? 4.0 * ((double)b.B * b.L * b.yK + (double)b.yK * b.ndir * b.H +
                                        (double)b.B * b.yT * (b.L + b.ndir * b.H) + (double)b.B * b.L * b.ndir * b.H)
                               : 0.0;
-  ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops,
-               4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)) + ybytes);
+  // (+ the in-launch weight gradients: dA, the h / q rows and x read once more, dW read and written)
+  const double wflops = b.wgrad ? 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * (b.H + b.wD) : 0.0;
+  const double wbytes = b.wgrad ? 4.0 * ((double)b.B * b.L * (b.ndir * 3.0 * b.H + b.ndir * 2.0 * b.H + b.wD) +
+                                         2.0 * b.ndir * 3.0 * b.H * (b.H + b.wD))
+                                : 0.0;
+  ProfScope ps(st, "gru_bwd_persist", 2.0 * b.ndir * b.B * b.L * 3.0 * b.H * b.H + yflops + wflops,
+               4.0 * b.ndir * (3.0 * b.H * b.H + (double)b.B * b.L * (5 * b.H + b.H + 3 * b.H)) + ybytes + wbytes);
   S2S_TRY(launch(st, a, b.excl != 0, false));
   void* r[1] = {sync};
   return launch_sync_harvest(st, r, 1, b.status);
@@ -1519,7 +1794,33 @@ int lds_hog_launch(hipStream_t st, int nwg, int lds_bytes, double usec, float* o
   return 0;
 }
 
+// Diagnostic clock probe (tools/clock_probe.py): nwg single-lane workgroups (workgroup w on XCD w % 8) that record
+// (real-time 100 MHz, shader-clock) counter pairs every `period` real-time ticks, n pairs each: the shader clock's rate
+// over the window is the XCD's core frequency while the step runs beside it.
+__global__ __launch_bounds__(64) void clock_probe_kernel(unsigned long long* out, int n, unsigned long long period) {
+  if (threadIdx.x != 0) return;
+  unsigned long long* o = out + 2ull * n * blockIdx.x;
+  for (int i = 0; i < n; ++i) {
+    const unsigned long long r = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long c = __builtin_amdgcn_s_memtime();
+    o[2 * i] = r;
+    o[2 * i + 1] = c;
+    while (__builtin_amdgcn_s_memrealtime() - r < period) __builtin_amdgcn_s_sleep(2);
+  }
+}
+int clock_probe_launch(hipStream_t st, int nwg, int n, int period, unsigned long long* out) {
+  S2S_REQUIRE(nwg > 0 && nwg <= 64 && n > 0 && n <= (1 << 20) && period > 0 && (double)n * period < 2e8,
+              "clock probe: bad arguments");
+  hipLaunchKernelGGL(clock_probe_kernel, dim3(nwg), dim3(64), 0, st, out, n, (unsigned long long)period);
+  S2S_CHECK_HIP(hipGetLastError());
+  return 0;
+}
+
 }  // namespace s2s
+
+extern "C" int s2s_debug_clock_probe(void* stream, int nwg, int n, int period, unsigned long long* out) {
+  return s2s::clock_probe_launch(static_cast<hipStream_t>(stream), nwg, n, period, out);
+}
 
 // test stand-in for a collective on another stream (tests/test_gpu_coresident.py): nwg resident workgroups holding
 // lds_bytes of LDS each for usec microseconds
@@ -1542,6 +1843,8 @@ extern "C" void s2s_debug_gru_stamps(void* fwd, void* bwd) {
   s2s::g_gru_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_gru_stamps[1] = static_cast<unsigned long long*>(bwd);
 }
+// diagnostic: in-launch weight-gradient worker stamps [nchains][nw][L + 4] of the next BPTT launches (nullptr: off)
+extern "C" void s2s_debug_gru_wg_stamps(void* p) { s2s::g_gru_wstamps = static_cast<unsigned long long*>(p); }
 // diagnostic: producer item stamps [producer][32][2] of the next fused persistent launches (nullptr: off)
 extern "C" void s2s_debug_gru_prod_stamps(void* fwd, void* bwd) {
   s2s::g_gru_pstamps[0] = static_cast<unsigned long long*>(fwd);

@@ -616,6 +616,48 @@ def test_fused_dy_dealing_does_not_change_the_step(s2s, B):
     assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
 
 
+@pytest.mark.parametrize("B,ragged", [(8, False), (32, False), (32, True), (45, False), (64, False)])
+def test_bptt_inlaunch_wgrad_matches_the_gemm(s2s, B, ragged):
+    """The first encoder layer's weight gradients computed inside its BPTT launch by workers beside the chains
+    (s2s_debug_bptt_wgrad(1), gru_persist.hip bptt_wgrad: one utterance tile written directly at B <= 16, the
+    tiles' partials met by a ticket otherwise) against the weight-gradient GEMM behind the launch (0): the same
+    products in another summation order, so layer 1's six dW tensors agree to fp32 summation noise (1e-5 of each
+    tensor's max) and every other gradient is bitwise unchanged; two in-launch steps are bitwise equal."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_bptt_wgrad
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(B)
+    L, T = 96, 20
+    x = torch.randn(B, L, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, T), generator=g).to(torch.int32).cuda()
+    kw = {}
+    if ragged:
+        fl = torch.randint(L // 3, L + 1, (B,), generator=g).tolist()
+        fl[0] = L
+        kw = dict(frame_lengths=fl, label_lengths=[T] * B)
+    outs = {}
+    try:
+        for arm, on in (("gemm", 0), ("inlaunch", 1), ("again", 1)):
+            fn(on)
+            model.step(x, lab, **kw)
+            torch.cuda.synchronize()
+            outs[arm] = model.grads.clone()
+    finally:
+        fn(0)
+    H, D = cfg.hiddenFrameSize, cfg.inputFrameSize
+    n0 = 6 * H * (H + D)  # layer 1's six (H, H + D) gate weights lead the flat gradient vector
+    assert torch.equal(outs["inlaunch"], outs["again"])
+    assert torch.equal(outs["inlaunch"][n0:], outs["gemm"][n0:])
+    for i in range(6):
+        a = outs["inlaunch"][i * H * (H + D):(i + 1) * H * (H + D)]
+        b = outs["gemm"][i * H * (H + D):(i + 1) * H * (H + D)]
+        assert b.abs().max().item() > 0
+        assert (a - b).abs().max().item() <= 1e-5 * b.abs().max().item(), (i, (a - b).abs().max().item())
+
+
 @pytest.mark.parametrize("local,ring", [(1, 1), (1, 0), (0, 1)])
 @pytest.mark.parametrize("B,H", [(32, 256), (45, 128)])
 def test_persistent_gru_bitwise_equals_per_step_launches(s2s, monkeypatch, local, ring, B, H):
