@@ -891,7 +891,9 @@ template <int NC>
 __device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, unsigned* tb_lds, int* flag_lds) {
   if (threadIdx.x >= 256) return;
   const WArgs& q = a.wg;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (wave through readfirstlane: the column-block branches below are then scalar, not divergent -- as divergent
+  // branches each B load was followed by its own vmcnt(0), ~3.5 us per step instead of ~1.3)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int H = a.H, L = a.L, B = a.B, nmem = a.nmem, NP = q.NP, nblk = NP / 16;
   const int dir = chain / a.MT, mt = chain % a.MT;
   const PDir& g = a.d[dir];
@@ -965,9 +967,7 @@ __device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, uns
   auto issue = [&](int i, float (&av)[4], float (&bv)[kWgCB]) {
     const int p = i >> 2, kk = i & 3;
     const int t = g.reverse ? p : L - 1 - p;
-    const int b = mt * 16 + 4 * kk + kq;
-    const bool live = b < B;
-    const int row = min(b, B - 1) * L + t;
+    const int row = min(mt * 16 + 4 * kk + kq, B - 1) * L + t;
 #ifdef S2S_EXP_WG_NOLOAD  // diagnostic (timing only, wrong results): operands from registers
 #pragma unroll
     for (int r = 0; r < 4; ++r) av[r] = (float)(row + r);
@@ -975,25 +975,19 @@ __device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, uns
     for (int c = 0; c < kWgCB; ++c) bv[c] = (float)(kk + c);
     return;
 #endif
+    // no select behind a load (the compiler would wait for the load right there): padding utterances' dA is zeroed
+    // where the products use it (mma), x columns past D load column D - 1 into output columns that are not stored
     const int oa = 4 * (row * ldA + row0 + jl);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ar, oa + 64 * r, 0, 16));
-      av[r] = live ? v : 0.f;
-    }
-    const int os = 4 * (row * s5 + svoi + cb0 * 16 + jl), ox = 4 * (row * ldx + cb0 * 16 + jl - H);
+    for (int r = 0; r < 4; ++r) av[r] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(ar, oa + 64 * r, 0, 16));
+    const int os = 4 * (row * s5 + svoi + cb0 * 16 + jl), ox = 4 * (row * ldx + cb0 * 16 + jl - H),
+              oxl = 4 * (row * ldx + q.D - 1);
 #pragma unroll
-    for (int c = 0; c < kWgCB; ++c) {
-      const int cb = cb0 + c;
-      if (cb >= nblk) {
-        bv[c] = 0.f;
-      } else if (cb * 16 < H) {  // (uniform: a block is all h or all x, H % 16 == 0)
-        bv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(sr, os + 64 * c, 0, 0));
-      } else {
-        const int xc = cb * 16 + jl - H;
-        const float v = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xc < q.D ? ox + 64 * c : 0, 0, 0));
-        bv[c] = xc < q.D ? v : 0.f;
-      }
+    for (int c = 0; c < kWgCB; ++c) {  // one unconditional load per column block (branch-free: exact vmcnt waits)
+      const int cb = cb0 + c, xc = cb * 16 + jl - H;
+      const bool hp = cb * 16 < H;  // (uniform: a block is all h or all x, H % 16 == 0; blocks past nblk load x)
+      const __amdgpu_buffer_rsrc_t rs = hp ? sr : xr;
+      bv[c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, hp ? os + 64 * c : (xc < q.D ? ox + 64 * c : oxl), 0, 0));
     }
   };
   floatx4 acc[4][kWgCB];
@@ -1001,7 +995,8 @@ __device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, uns
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < kWgCB; ++c) acc[r][c] = floatx4{0.f, 0.f, 0.f, 0.f};
-  auto mma = [&](const float (&av)[4], const float (&bv)[kWgCB]) {
+  auto mma = [&](const float (&av)[4], const float (&bv)[kWgCB], int kk) {
+    const bool live = mt * 16 + 4 * kk + kq < B;
 #ifdef S2S_EXP_WG_NOMMA  // diagnostic (timing only, wrong results): one add per operand instead of the products
 #pragma unroll
     for (int c = 0; c < kWgCB; ++c)
@@ -1010,29 +1005,41 @@ __device__ __forceinline__ void bptt_wgrad(const PArgs& a, int chain, int w, uns
     return;
 #endif
 #pragma unroll
-    for (int c = 0; c < kWgCB; ++c) {
-      if (cb0 + c >= nblk) continue;  // (uniform)
+    for (int c = 0; c < kWgCB; ++c)  // (blocks past nblk too, unbranched: their columns are never stored)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[r], bv[c], acc[r][c], 0, 0, 0);
-    }
+      for (int r = 0; r < 4; ++r)
+        acc[r][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(live ? av[r] : 0.f, bv[c], acc[r][c], 0, 0, 0);
   };
   // the steps a group of kWgRing iterations will load are checked final once, in front of the group (the poll's
-  // wait would drain the loads in flight anyway), so the unrolled body has no wait in it
-  const int niter = 4 * L;
+  // wait would drain the loads in flight anyway), so the unrolled body has no wait and no branch in it (a branch
+  // there made the compiler's vmcnt waits assume fewer loads in flight); the last group is peeled
+  const int niter = 4 * L;  // a multiple of kWgRing / 2
   auto need = [&](int last_iter) -> bool { return wait(min(last_iter, niter - 1) >> 2); };
   if (!need(kWgRing - 2)) return;
 #pragma unroll
   for (int u = 0; u < kWgRing - 1; ++u)
     if (u < niter) issue(u, ra[u], rb[u]);
-  for (int i = 0; i < niter; i += kWgRing) {
-    if (i + kWgRing < niter && !need(i + 2 * kWgRing - 2)) return;
+  int i = 0;
+  for (; i + 2 * kWgRing - 2 < niter; i += kWgRing) {
+    if (!need(i + 2 * kWgRing - 2)) return;
+#pragma unroll
+    for (int u = 0; u < kWgRing; ++u) {
+      issue(i + u + kWgRing - 1, ra[(u + kWgRing - 1) % kWgRing], rb[(u + kWgRing - 1) % kWgRing]);
+      __builtin_amdgcn_sched_barrier(0);  // each iteration's loads stay ahead of the products behind them
+      mma(ra[u], rb[u], u & 3);  // (i is a multiple of 4: iteration i + u has kk = u & 3)
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    stamp(2 + (i >> 2));
+  }
+  for (; i < niter; i += kWgRing) {
+    if (!need(niter - 1)) return;
 #pragma unroll
     for (int u = 0; u < kWgRing; ++u) {
       const int nx = i + u + kWgRing - 1;
       if (nx < niter) issue(nx, ra[(u + kWgRing - 1) % kWgRing], rb[(u + kWgRing - 1) % kWgRing]);
-      if (i + u < niter) mma(ra[u], rb[u]);
-      if (((i + u) & 3) == 3) stamp(2 + ((i + u) >> 2));
+      if (i + u < niter) mma(ra[u], rb[u], u & 3);
     }
+    stamp(2 + (i >> 2));
   }
   stamp(L + 2);
   // D[i][j] of block (r, c) at lane (j = lane & 15, i = 4 (lane >> 4) + e): gate row row0 + 16 r + 4 kq + e
