@@ -577,7 +577,10 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
     }
     if (zero_late && (flags & S2S_ZERO_GRADS)) S2S_TRY(zero_async(side, grads, sizeof(float) * (size_t)off));
-    S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
+    {
+      GemmBigTiles bt((wgrad_tile128_knob() & 4) != 0);  // (not tied to split: overlap on / off stay bitwise equal)
+      S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
+    }
     S2S_TRY(mark_bucket(bev, 0, split ? side : st));
     // the reported nll (timit.lua:268-272) beside the encoder BPTT
     if (split)
@@ -589,6 +592,13 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   else S2S_TRY(dec_wgrad(false));
   // ---- encoder backward
   const bool defer = split && wgrad_fork_mode() == 1;
+  // S2S_WGRAD_TILE128 (bit flags): the weight-gradient GEMMs on 128 x 128 tiles -- 1: every encoder layer's; 2: the
+  // encoder layers' that run beside a later BPTT (not the first layer's, which follows the last BPTT on the critical
+  // path); 4: the decoder's (beside the top BPTT)
+  auto wgrad_tiles128 = [&](int l) {
+    const int k = wgrad_tile128_knob();
+    return (k & 1) || ((k & 2) && l > 0);
+  };
   int pending = -1;  // layer whose weight gradients wait for the next BPTT's sync prep
   auto issue_wgrad = [&](int l) -> int {
     const GruLayerIO io = layer_io(l);
@@ -596,6 +606,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     for (int dd = 0; dd < 2; ++dd)
       for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
     gr.scale = scale;
+    GemmBigTiles bt(wgrad_tiles128(l));
     S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
     S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
     return 0;
@@ -669,6 +680,7 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       S2S_TRY(mark_bucket(bev, nl - l, st));
     } else {
       if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
+      GemmBigTiles bt(wgrad_tiles128(l));
       S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
       S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
     }

@@ -626,6 +626,16 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 }  // namespace
 
 static thread_local int g_gemm_prec = kGemmF32;
+static thread_local int g_gemm_big = 0;
+void set_gemm_big_tiles(int on) { g_gemm_big = on; }
+int gemm_big_tiles() { return g_gemm_big; }
+int wgrad_tile128_knob() {
+  static const int v = [] {
+    const char* e = std::getenv("S2S_WGRAD_TILE128");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 static thread_local bool g_wgrad_bf16 = false;
 void set_gemm_precision(int p) { g_gemm_prec = p; }
 int gemm_precision() { return g_gemm_prec; }
@@ -682,6 +692,12 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf
     big.bn = 128;
     count(big);
     if (big.nblocks >= 256) pl = big;
+  }
+  if (!bf16 && g_gemm_big) {  // (GemmBigTiles) 128 x 128 tiles, K split by the fill rule below
+    GemmPlan big = pl;
+    big.bm = big.bn = 128;
+    count(big);
+    pl = big;
   }
   const int tiles = pl.nblocks;
   // (an output of fewer tiles than CUs may split down to 256-long slices: the decoder MLP's 1280 x 448 x 768 product

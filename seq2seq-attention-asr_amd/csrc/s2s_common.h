@@ -121,6 +121,16 @@ struct WgradPrecision {
   }
   ~WgradPrecision() { set_gemm_precision(prev); }
 };
+// fp32 GEMMs planned on 128 x 128 tiles (instead of the planner's 64 x 64) while a GemmBigTiles scope is live on
+// this thread -- the encoder weight gradients under S2S_WGRAD_TILE128 (A/B): half the staged bytes per flop
+void set_gemm_big_tiles(int on);
+int gemm_big_tiles();
+int wgrad_tile128_knob();
+struct GemmBigTiles {
+  int prev;
+  explicit GemmBigTiles(int on) : prev(gemm_big_tiles()) { set_gemm_big_tiles(on); }
+  ~GemmBigTiles() { set_gemm_big_tiles(prev); }
+};
 // Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs
 // fit; without a workspace every problem runs unsplit.  Concurrent calls need disjoint ones.
 struct GemmWs {
