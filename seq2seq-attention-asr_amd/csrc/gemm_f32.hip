@@ -469,17 +469,22 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
   const long mn = (long)M * N;
   const float alpha = q.p.alpha, beta = q.p.beta;
   const float* __restrict__ bias = q.p.bias;
-  const bool vec = (N % 4 == 0) && (q.p.ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.p.C) & 15) == 0) &&
-                   ((reinterpret_cast<uintptr_t>(q.part) & 15) == 0);
+  // float4 slab reads whenever the slab rows allow them; float4 C writes only when C's rows do too (the GRU weight
+  // gradients' [H | D] rows of 379 floats take the scalar stores, their h-part slabs the float4 reads)
+  const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.part) & 15) == 0);
+  const bool vc = (q.p.ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.p.C) & 15) == 0);
   if (vec) {
     for (long e = 4 * (blockIdx.x * 256L + threadIdx.x); e < mn; e += 4L * gridDim.x * 256) {
       floatx4 sum = {0.f, 0.f, 0.f, 0.f};
       // every slab's load in flight before the first add (a runtime-bounded loop issued them one by
       // one behind each add); the sum order is the slice order either way
-      switch (q.splits) {
+      switch (q.splits) {  // (the planner's fill rule picks any count, e.g. 7 for the encoder weight gradients)
         case 2: sum = slab_sum<2>(q.part, mn, e); break;
         case 3: sum = slab_sum<3>(q.part, mn, e); break;
         case 4: sum = slab_sum<4>(q.part, mn, e); break;
+        case 5: sum = slab_sum<5>(q.part, mn, e); break;
+        case 6: sum = slab_sum<6>(q.part, mn, e); break;
+        case 7: sum = slab_sum<7>(q.part, mn, e); break;
         case 8: sum = slab_sum<8>(q.part, mn, e); break;
         default:
           for (int s = 0; s < q.splits; ++s) sum += *reinterpret_cast<const floatx4*>(q.part + s * mn + e);
@@ -488,12 +493,23 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
       floatx4 v = alpha * sum;
       if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
       if (q.p.rbias) v += q.p.rbias[row];
-      floatx4* c = reinterpret_cast<floatx4*>(q.p.C + (long)row * q.p.ldc + col);
-      if (beta != 0.f) v += beta * *c;
-      if (q.p.relu)
+      float* cp = q.p.C + (long)row * q.p.ldc + col;
+      if (vc) {
+        floatx4* c = reinterpret_cast<floatx4*>(cp);
+        if (beta != 0.f) v += beta * *c;
+        if (q.p.relu)
 #pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) v[e2] = fmaxf(v[e2], 0.f);
-      *c = v;
+          for (int e2 = 0; e2 < 4; ++e2) v[e2] = fmaxf(v[e2], 0.f);
+        *c = v;
+      } else {
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) {
+          float w = v[e2];
+          if (beta != 0.f) w += beta * cp[e2];
+          if (q.p.relu) w = fmaxf(w, 0.f);
+          cp[e2] = w;
+        }
+      }
     }
     return;
   }
@@ -505,6 +521,9 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
       case 2: sum = slab_sum1<2>(q.part, mn, e); break;
       case 3: sum = slab_sum1<3>(q.part, mn, e); break;
       case 4: sum = slab_sum1<4>(q.part, mn, e); break;
+      case 5: sum = slab_sum1<5>(q.part, mn, e); break;
+      case 6: sum = slab_sum1<6>(q.part, mn, e); break;
+      case 7: sum = slab_sum1<7>(q.part, mn, e); break;
       case 8: sum = slab_sum1<8>(q.part, mn, e); break;
       default:
         for (int s = 0; s < q.splits; ++s) sum += q.part[s * mn + e];
