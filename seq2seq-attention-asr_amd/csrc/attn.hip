@@ -47,6 +47,11 @@ struct AttnK {
   int* AM;
   // fwd scratch
   float *PM, *PL, *PC, *U;
+  // the MLP GEMM's unreduced split-K slabs (UPS > 1: U = sum of UP[s * UPMN + e] in slice order + bm, summed by the
+  // MLP head instead of a reduce launch in front of it), or null
+  const float* UP;
+  int UPS;
+  long UPMN;
   // bwd scratch
   float *DO, *DU, *DV, *DGA, *DS, *DSP, *DSPF, *DD, *DCY, *DC, *DVH, *PDWS, *DWS, *DWEACC, *YP;
   // hybrid attention: HGT (kW, Sc) = (U W)^T and HCU (Sc) = U b (saved); QA [2][B][L][kW] the
@@ -716,11 +721,19 @@ __device__ __forceinline__ void mlp_head_body(const AttnK& k, int rows, int blk)
   float* mv = sm + wave * M;
   if (r < rows) {
     const float* u = k.U + (long)r * M * Kw;
+    // U[r][c] from the MLP GEMM's slabs when it left them unreduced: splitk_reduce's expression (alpha = 1)
+    auto uv = [&](int c) -> float {
+      if (!k.UP) return u[c];
+      const long e = (long)r * M * Kw + c;
+      float sum = 0.f;
+      for (int s = 0; s < k.UPS; ++s) sum += k.UP[s * k.UPMN + e];
+      return 1.f * sum + k.P.bm[c];
+    };
     for (int j = lane; j < M; j += 64) {
-      float best = u[j * Kw];
+      float best = uv(j * Kw);
       int bi = 0;
       for (int i = 1; i < Kw; ++i) {
-        const float v = u[j * Kw + i];
+        const float v = uv(j * Kw + i);
         if (v > best) { best = v; bi = i; }
       }
       mv[j] = best;
@@ -1347,6 +1360,11 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
 }
 
 static std::atomic<int> g_dec_allow_local{1};
+// S2S_HEAD_SUMS_SLABS=0 (A/B): the decoder MLP GEMM's split-K reduce as its own launch in front of the MLP head
+static std::atomic<int> g_head_sums_slabs{[] {
+  const char* e = std::getenv("S2S_HEAD_SUMS_SLABS");
+  return e ? std::atoi(e) : 1;
+}()};
 static std::atomic<int> g_merge_alpha_head{1};  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
 
 template <int S, int A, int SC>
@@ -1527,8 +1545,18 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
                        d.dropout_mask);
     S2S_CHECK_HIP(hipGetLastError());
   }
-  S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
-                (long)d.M * d.K, P.bm, gws));
+  {
+    // the merged head sums the MLP GEMM's split-K slabs itself (no reduce launch between them)
+    GemmDeferred dr{};
+    GemmDeferReduce scope(merge_head && g_head_sums_slabs ? &dr : nullptr);
+    S2S_TRY(gemm1(st, false, true, rows, d.M * d.K, S + d.A, 1.f, k.VV, S + d.A, P.Wm, S + d.A, 0.f, k.U,
+                  (long)d.M * d.K, P.bm, gws));
+    if (dr.splits > 1) {
+      k.UP = dr.part;
+      k.UPS = dr.splits;
+      k.UPMN = dr.mn;
+    }
+  }
   if (merge_head)
     hipLaunchKernelGGL(dec_xcd_alpha_vbar_head, dim3(T * B + ((d.Sc + 63) / 64) * B + (rows + 3) / 4), dim3(256),
                        4 * d.M * sizeof(float), st, k, x, rows);
@@ -2241,6 +2269,8 @@ int nll_seed(hipStream_t st, int B, int T, int O, const float* logp, const int* 
 // diagnostic: 0 forces write-through (sc1) hand-offs in every XCD-local decoder chain
 extern "C" void s2s_debug_dec_local(int allow) { s2s::g_dec_allow_local = allow; }
 extern "C" void s2s_debug_merge_alpha_head(int on) { s2s::g_merge_alpha_head = on; }
+// diagnostic: the merged MLP head sums the MLP GEMM's split-K slabs (1) or a reduce launch runs in front of it (0)
+extern "C" void s2s_debug_head_sums_slabs(int on) { s2s::g_head_sums_slabs = on; }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);

@@ -646,6 +646,9 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 
 static thread_local int g_gemm_prec = kGemmF32;
 static thread_local int g_gemm_big = 0;
+static thread_local GemmDeferred* g_gemm_defer = nullptr;
+void set_gemm_defer_reduce(GemmDeferred* d) { g_gemm_defer = d; }
+GemmDeferred* gemm_defer_reduce() { return g_gemm_defer; }
 void set_gemm_big_tiles(int on) { g_gemm_big = on; }
 int gemm_big_tiles() { return g_gemm_big; }
 int wgrad_tile128_knob() {
@@ -841,7 +844,13 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
   else if (!transA && transB) launch_tiles<false, true>(st, pl, grid, L, bf16);
   else if (transA && !transB) launch_tiles<true, false>(st, pl, grid, L, bf16);
   else launch_tiles<true, true>(st, pl, grid, L, bf16);
-  if (split) {
+  GemmDeferred* dr = g_gemm_defer;
+  if (dr) dr->splits = 0;
+  if (split && dr && used == 1 && L.q[0].p.alpha == 1.f && L.q[0].p.beta == 0.f && !L.q[0].p.rbias && !L.q[0].p.relu) {
+    dr->part = L.q[0].part;  // (GemmDeferReduce) the consumer sums the slabs
+    dr->splits = L.q[0].splits;
+    dr->mn = (long)L.q[0].p.M * L.q[0].p.N;
+  } else if (split) {
     long mn_max = 0;
     for (int i = 0; i < used; ++i)
       if (L.q[i].part) mn_max = std::max(mn_max, (long)L.q[i].p.M * L.q[i].p.N);

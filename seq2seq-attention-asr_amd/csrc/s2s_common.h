@@ -131,6 +131,22 @@ struct GemmBigTiles {
   explicit GemmBigTiles(int on) : prev(gemm_big_tiles()) { set_gemm_big_tiles(on); }
   ~GemmBigTiles() { set_gemm_big_tiles(prev); }
 };
+// A single-problem split-K GEMM issued while a GemmDeferReduce scope is live on this thread leaves its slabs
+// unreduced and describes them here (splits = 0: the GEMM wrote C itself); the consumer sums them in slice order
+// as splitk_reduce would (C = alpha * sum + bias; alpha = 1, beta = 0, no row bias, no ReLU only) -- the decoder
+// MLP's output, read once by the MLP head
+struct GemmDeferred {
+  const float* part = nullptr;
+  int splits = 0;
+  long mn = 0;
+};
+void set_gemm_defer_reduce(GemmDeferred* d);
+GemmDeferred* gemm_defer_reduce();
+struct GemmDeferReduce {
+  GemmDeferred* prev;
+  explicit GemmDeferReduce(GemmDeferred* d) : prev(gemm_defer_reduce()) { set_gemm_defer_reduce(d); }
+  ~GemmDeferReduce() { set_gemm_defer_reduce(prev); }
+};
 // Split-K partial-slab workspace (floats).  A call may cut K into slices only when the slabs
 // fit; without a workspace every problem runs unsplit.  Concurrent calls need disjoint ones.
 struct GemmWs {

@@ -616,6 +616,33 @@ def test_fused_dy_dealing_does_not_change_the_step(s2s, B):
     assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
 
 
+@pytest.mark.parametrize("B", [32, 45])
+def test_mlp_head_summing_slabs_is_bitwise_the_reduce(s2s, B):
+    """The merged MLP head of the XCD-local decoder sums the MLP GEMM's split-K slabs itself (GemmDeferReduce,
+    s2s_debug_head_sums_slabs(1)) in the reduce kernel's slice order and expression, so logp, nll and every gradient
+    are bitwise those of the separate splitk_reduce launch (0)."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_head_sums_slabs
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(7 + B)
+    x = torch.randn(B, 96, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, 40), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, on in (("reduce", 0), ("head", 1)):
+            fn(on)
+            nll, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (nll.clone(), logp.clone(), model.grads.clone())
+    finally:
+        fn(1)
+    for a, b in zip(outs["reduce"], outs["head"]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B,ragged", [(8, False), (32, False), (32, True), (45, False), (64, False)])
 def test_bptt_inlaunch_wgrad_matches_the_gemm(s2s, B, ragged):
     """The first encoder layer's weight gradients computed inside its BPTT launch by workers beside the chains
