@@ -586,6 +586,10 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   __shared__ unsigned tb_lds;
   __shared__ __attribute__((aligned(16))) float hprev[16][16];  // r tiles: h_{t-1} of the tile's units
   __shared__ __attribute__((aligned(16))) float xring[kRowRing][2][256];  // [step % ring][gate | candidate][thread]
+  // this step's saved activations and output, staged for the loader wave's global stores: z tiles [z | hh | h],
+  // r tiles [r | h_{t-1} | q] (a recurrence wave's own global stores sat in its vmcnt queue in front of its next
+  // sweep: forward step 2.52 -> 2.40 us with them switched off)
+  __shared__ __attribute__((aligned(16))) float stg[2][3][256];
   extern __shared__ __attribute__((aligned(16))) float xlds[];  // producer tiles (fused x-projection)
   const int H = a.H, B = a.B, L = a.L;
   const ChainSlot cs = chain_slot(a.nmem);
@@ -642,6 +646,26 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       *reinterpret_cast<float4*>(&xring[q % kRowRing][0][4 * lane]) = r[0];
       *reinterpret_cast<float4*>(&xring[q % kRowRing][1][4 * lane]) = r[1];
     };
+    // step q's staged values -> saved activations / output (float4 of this lane's 4 columns)
+    auto store = [&](int q) {
+      if (!lv) return;
+      const int t = g.reverse ? L - 1 - q : q;
+      const long row = (long)bl * L + t;
+      const float4 v0 = *reinterpret_cast<const float4*>(&stg[q & 1][0][4 * lane]);
+      const float4 v1 = *reinterpret_cast<const float4*>(&stg[q & 1][1][4 * lane]);
+      const float4 v2 = *reinterpret_cast<const float4*>(&stg[q & 1][2][4 * lane]);
+      float* sv = g.sv + row * 5 * H;
+      if (isz) {
+        *reinterpret_cast<float4*>(sv + col) = v0;
+        *reinterpret_cast<float4*>(sv + 2 * H + col) = v1;
+        *reinterpret_cast<float4*>(g.y + row * g.ldy + col) = v2;
+      } else {
+        const int j = col - H;
+        *reinterpret_cast<float4*>(sv + H + j) = v0;
+        *reinterpret_cast<float4*>(sv + 3 * H + j) = v1;
+        *reinterpret_cast<float4*>(sv + 4 * H + j) = v2;
+      }
+    };
     float4 ra[2], rb[2];
     issue(0, ra);
     issue(1, rb);
@@ -654,6 +678,7 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       if (ring) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last step's re-arms have landed
       __syncthreads();  // [A]
       if (abort_lds) return;
+      if (s > 0) store(s - 1);  // written by the recurrence waves before this barrier
       put(s + 2, ra);   // loaded during the previous step
       issue(s + 3, ra);
       if (ring) {  // slots every member has finished with (h_{s-2} of z tiles, q_{s-1} of r tiles)
@@ -664,6 +689,8 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       __syncthreads();  // [B]
       if (abort_lds) return;
     }
+    __syncthreads();  // [C]: the last step's values are staged
+    store(L - 1);
     return;
   }
 
@@ -689,7 +716,6 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
   __syncthreads();  // [P]
   for (int s = 0; s < L; ++s) {
     const int t = g.reverse ? L - 1 - s : s;
-    const long row = (long)ob * L + t;
     // ---- p1: [z | r] = sig(Uzr h_{t-1} + xp)
     floatx4 acc = {0.f, 0.f, 0.f, 0.f};
     bool ok = true;
@@ -726,9 +752,9 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
     const float hpark = hprev[tid >> 4][tid & 15];
     {
       const float gate = gru_sigmoid(sum + xpv);
-      float* sv = g.sv + row * 5 * H;
+      float* st3 = &stg[s & 1][0][tid];  // [0] / [256] / [512]: the three staged values of this step
       if (isz) {
-        if (live) sv[on] = gate;
+        st3[0] = gate;
         zreg = gate;
       } else {
         const int j = on - H;
@@ -739,11 +765,9 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
         } else {
           put_granule_pair(g.g1, (s & 1) * slot + (long)ob * H + j, q, tb + s + 1, live);
         }
-        if (live) {
-          sv[H + j] = gate;
-          sv[3 * H + j] = hp;
-          sv[4 * H + j] = q;
-        }
+        st3[0] = gate;
+        st3[256] = hp;
+        st3[512] = q;
       }
     }
     GRU_STAMP(2);
@@ -779,14 +803,13 @@ __global__ __launch_bounds__(kFwdThreads) void gru_fwd_persist(PArgs a) {
       } else {
         put_granule_pair(g.g0, (s & 1) * slot + (long)ob * H + on, hreg, tb + s + 1, live);
       }
-      if (live) {
-        g.sv[row * 5 * H + 2 * H + on] = hh;
-        g.y[row * g.ldy + on] = hreg;
-      }
+      stg[s & 1][1][tid] = hh;
+      stg[s & 1][2][tid] = hreg;
     }
     GRU_STAMP(5);
     if (aborted) return;  // checked after the epilogue: its LDS read is issued with the reduce's reads
   }
+  __syncthreads();  // [C]: the loader stores the last step's staged values
 }
 
 // ------------------------------------------------------------------------------ backward
