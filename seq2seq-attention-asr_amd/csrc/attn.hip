@@ -1367,12 +1367,22 @@ static std::atomic<int> g_head_sums_slabs{[] {
 }()};
 static std::atomic<int> g_merge_alpha_head{1};  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
 
+// S2S_DEC_R4=0 / s2s_debug_dec_r4(0) (A/B): chains of <= 4 utterances keep the 16 x 16 x 4 skinny products
+static std::atomic<int> g_dec_r4{[] {
+  const char* e = std::getenv("S2S_DEC_R4");
+  return e ? std::atoi(e) : 1;
+}()};
+template <int S, int A, int SC, bool R4>
+static const void* xcd_kernel(bool fwd, int res) {
+  return res == 2 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 2, R4> : (const void*)dec_xcd_bwd<S, A, SC, 2, R4>)
+       : res == 1 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 1, R4> : (const void*)dec_xcd_bwd<S, A, SC, 1, R4>)
+                  : (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 0, R4> : (const void*)dec_xcd_bwd<S, A, SC, 0, R4>);
+}
 template <int S, int A, int SC>
 static int launch_xcd_t(bool fwd, int res, hipStream_t st, AttnK& k, XArgs& x) {
   const size_t lds = xdec_lds<S, A, SC>(x.XLC, res);
-  const void* fn = res == 2 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 2> : (const void*)dec_xcd_bwd<S, A, SC, 2>)
-                 : res == 1 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 1> : (const void*)dec_xcd_bwd<S, A, SC, 1>)
-                            : (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 0> : (const void*)dec_xcd_bwd<S, A, SC, 0>);
+  // a chain of at most 4 utterances (B <= 32): its skinny products on the 4 x 4 x 1 MFMA (handoff.h mfma4_aw_acc)
+  const void* fn = x.U <= 4 && g_dec_r4.load() ? xcd_kernel<S, A, SC, true>(fwd, res) : xcd_kernel<S, A, SC, false>(fwd, res);
   if (lds) S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {&k, &x};
   S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
@@ -2271,6 +2281,7 @@ extern "C" void s2s_debug_dec_local(int allow) { s2s::g_dec_allow_local = allow;
 extern "C" void s2s_debug_merge_alpha_head(int on) { s2s::g_merge_alpha_head = on; }
 // diagnostic: the merged MLP head sums the MLP GEMM's split-K slabs (1) or a reduce launch runs in front of it (0)
 extern "C" void s2s_debug_head_sums_slabs(int on) { s2s::g_head_sums_slabs = on; }
+extern "C" void s2s_debug_dec_r4(int on) { s2s::g_dec_r4 = on; }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);

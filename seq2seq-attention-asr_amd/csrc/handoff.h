@@ -255,6 +255,20 @@ __device__ __forceinline__ void put_sent(float* p, float v) {
 // re-arm rows [r0, r0 + nr) x columns [c0, c0 + nc) (nc % 4 == 0, 16-byte aligned) of slots
 // 0..nslots-1 (slot stride `slot`, row stride ld floats); all 256 threads call it; the producer's
 // re-arms end with rearm_done() before its census word
+// rearm_rect over a chain-interleaved slot (the XCD decoder's 4 x 4 form, dec_xcd.inc ilv): a chain's rows b0 ..
+// b0 + nU - 1 of a [B][W] slot are stored quad-major, element (b0 + r, n) at b0 W + (n / 4) 4 nU + 4 r + n % 4, so
+// one k-quad of all its rows is 16 nU contiguous bytes; rows r0 .. r0 + nr - 1, columns [c0, c0 + nc) re-armed
+__device__ __forceinline__ void rearm_ilv(float* base, long slot, int nslots, long W, int b0, int nU, int r0, int nr,
+                                          int c0, int nc) {
+  const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
+                                __uint_as_float(kSent));
+  const int n4 = nc / 4, per = nr * n4;
+  if (per <= 0) return;
+  for (int i = threadIdx.x; i < nslots * per; i += 256) {
+    const int s = i / per, rem = i - s * per, r = rem / n4, c = rem - r * n4;
+    *reinterpret_cast<float4*>(base + s * slot + (long)b0 * W + (long)(c0 / 4 + c) * 4 * nU + 4 * (r0 + r)) = sv;
+  }
+}
 __device__ __forceinline__ void rearm_rect(float* base, long slot, int nslots, long ld, int r0, int nr, int c0,
                                            int nc) {
   const float4 sv = make_float4(__uint_as_float(kSent), __uint_as_float(kSent), __uint_as_float(kSent),
@@ -279,14 +293,14 @@ __device__ __forceinline__ void rearm_done() {
 // sweep_skinny's operand layout over a sentinel row (row_off in bytes): one 16-byte load per chunk
 template <int NC>
 __device__ __forceinline__ bool sweep_sent(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, int wave,
-                                           int lane, unsigned* abort_word) {
+                                           int lane, unsigned* abort_word, int kmul = 1) {
   const long kq = 4 * (lane >> 4);
   unsigned spins = 0;
   while (true) {
     bool ok = true;
 #pragma unroll
     for (int i = 0; i < NC; ++i) {
-      const long off = row_off + 4 * (wave * 16 + 64 * i + kq);
+      const long off = row_off + 4L * kmul * (wave * 16 + 64 * i + kq);
       const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)off, 0, 16));
       ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
       a[i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
@@ -395,7 +409,8 @@ __device__ __forceinline__ bool sweep_sent_mfma(float4 (&a)[NC], __amdgpu_buffer
 // sweep_skinny_rows over sentinel rows: all R * NC loads of a pass issued before any check
 template <int NC, int R>
 __device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdgpu_buffer_rsrc_t (&rs)[R],
-                                                const long (&row_off)[R], int wave, int lane, unsigned* abort_word) {
+                                                const long (&row_off)[R], int wave, int lane, unsigned* abort_word,
+                                                int kmul = 1) {
   const long kq = 4 * (lane >> 4);
   unsigned spins = 0;
   while (true) {
@@ -404,7 +419,7 @@ __device__ __forceinline__ bool sweep_sent_rows(float4 (&a)[R][NC], const __amdg
     for (int r = 0; r < R; ++r)
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
-        const long off = row_off[r] + 4 * (wave * 16 + 64 * i + kq);
+        const long off = row_off[r] + 4L * kmul * (wave * 16 + 64 * i + kq);
         const uint4 p = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs[r], (int)off, 0, 16));
         ok = ok && p.x != kSent && p.y != kSent && p.z != kSent && p.w != kSent;
         a[r][i] = make_float4(__uint_as_float(p.x), __uint_as_float(p.y), __uint_as_float(p.z), __uint_as_float(p.w));
@@ -677,15 +692,97 @@ __device__ __forceinline__ floatx4 mfma_aw_done(floatx4 acc0, floatx4 acc1) {
   return acc0 + acc1;
 }
 
+// The same products for a chain of at most 4 live rows on v_mfma_f32_4x4x1_16b_f32 (16 blocks of 4 x 4 x 1: 9.3
+// cycles against the 16 x 16 x 4 form's 32.5 for a quarter of its multiply-adds, all of them live instead of 4 of 16
+// rows; tools/mfma4_probe.hip).  The operand registers are the 16 x 16 x 4 form's, with the activation rows dealt
+// by lane & 3 instead of lane & 15: lane l = 16 q + 4 g + j holds row j (A) and unit 4 g + j (B) of k-quad q, so
+// block b = g + 4 q multiplies rows 0..3 by units 4g..4g+3 over k-quad q, and lane l's result register i is row i,
+// unit l & 15, summed over k-quad q only.  mfma4_fold adds the four k-quads (lanes l, l ^ 16, l ^ 32, l ^ 48; the
+// same order in every lane) and leaves the 16 x 16 form's layout: lanes 0..15 rows 0..3, every other row 0 -- so
+// skinny_reduce / dec_sync sum the waves exactly as before.
+template <int NC>
+__device__ __forceinline__ void mfma4_aw_acc(const float4 (&a)[NC], const float4 (&w)[NC], floatx4& acc0,
+                                             floatx4& acc1, bool init) {
+#define S2S_MFMA4_AW0(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, 0" : "=&v"(acc) : "v"(x), "a"(y))
+#define S2S_MFMA4_AW(acc, x, y) asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(acc) : "v"(x), "a"(y))
+#pragma unroll
+  for (int i = 0; i + 1 < NC; i += 2) {
+    if (init && i == 0) {
+      S2S_MFMA4_AW0(acc0, a[0].x, w[0].x);
+      S2S_MFMA4_AW0(acc1, a[1].x, w[1].x);
+    } else {
+      S2S_MFMA4_AW(acc0, a[i].x, w[i].x);
+      S2S_MFMA4_AW(acc1, a[i + 1].x, w[i + 1].x);
+    }
+    S2S_MFMA4_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA4_AW(acc1, a[i + 1].y, w[i + 1].y);
+    S2S_MFMA4_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA4_AW(acc1, a[i + 1].z, w[i + 1].z);
+    S2S_MFMA4_AW(acc0, a[i].w, w[i].w);
+    S2S_MFMA4_AW(acc1, a[i + 1].w, w[i + 1].w);
+  }
+  if (NC & 1) {
+    constexpr int i = NC - 1;
+    if (init && NC == 1) {
+      S2S_MFMA4_AW0(acc0, a[i].x, w[i].x);
+      acc1 = floatx4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      S2S_MFMA4_AW(acc0, a[i].x, w[i].x);
+    }
+    S2S_MFMA4_AW(acc0, a[i].y, w[i].y);
+    S2S_MFMA4_AW(acc0, a[i].z, w[i].z);
+    S2S_MFMA4_AW(acc0, a[i].w, w[i].w);
+  }
+#undef S2S_MFMA4_AW0
+#undef S2S_MFMA4_AW
+}
+__device__ __forceinline__ floatx4 mfma4_fold(floatx4 acc0, floatx4 acc1, int lane) {
+  asm volatile("s_nop 11" : "+v"(acc0), "+v"(acc1));
+  const floatx4 s = acc0 + acc1;
+  floatx4 r;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const unsigned x = __float_as_uint(s[e]);
+    const auto p = __builtin_amdgcn_permlane32_swap(x, x, false, false);  // {lanes' low-half value, high-half value}
+    const float y = __uint_as_float(p[0]) + __uint_as_float(p[1]);      // k-quads q + (q ^ 2)
+    const unsigned yu = __float_as_uint(y);
+    const auto q = __builtin_amdgcn_permlane16_swap(yu, yu, false, false);
+    r[e] = lane < 16 ? __uint_as_float(q[0]) + __uint_as_float(q[1]) : 0.f;
+  }
+  return r;
+}
+// mfma_chunks_aw / mfma_aw_acc + mfma_aw_done in the 16 x 16 form, or (R4) the 4 x 4 form + fold
+template <bool R4, int NC>
+__device__ __forceinline__ floatx4 mfma_rows_aw(const float4 (&a)[NC], const float4 (&w)[NC], int lane) {
+  if constexpr (R4) {
+    floatx4 acc0, acc1;
+    mfma4_aw_acc<NC>(a, w, acc0, acc1, true);
+    return mfma4_fold(acc0, acc1, lane);
+  } else {
+    return mfma_chunks_aw<NC>(a, w);
+  }
+}
+template <bool R4, int NC>
+__device__ __forceinline__ void mfma_rows_acc(const float4 (&a)[NC], const float4 (&w)[NC], floatx4& acc0,
+                                              floatx4& acc1, bool init) {
+  if constexpr (R4) mfma4_aw_acc<NC>(a, w, acc0, acc1, init);
+  else mfma_aw_acc<NC>(a, w, acc0, acc1, init);
+}
+template <bool R4>
+__device__ __forceinline__ floatx4 mfma_rows_done(floatx4 acc0, floatx4 acc1, int lane) {
+  if constexpr (R4) return mfma4_fold(acc0, acc1, lane);
+  else return mfma_aw_done(acc0, acc1);
+}
+
 // sweep_sent's first pass, loads only (its layout; checked with sent_tile_check, polled further with sweep_sent)
 template <int NC>
 __device__ __forceinline__ void sent_row_issue(uint4 (&raw)[NC], __amdgpu_buffer_rsrc_t rs, long row_off, int wave,
-                                               int lane) {
+                                               int lane, int kmul = 1) {
   const long kq = 4 * (lane >> 4);
 #pragma unroll
   for (int i = 0; i < NC; ++i)
-    raw[i] = __builtin_bit_cast(uint4,
-                                __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(row_off + 4 * (wave * 16 + 64 * i + kq)), 0, 16));
+    raw[i] = __builtin_bit_cast(
+        uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(row_off + 4L * kmul * (wave * 16 + 64 * i + kq)), 0, 16));
 }
 
 // W operand fragments of one output-unit row (chunk i at wave*16 + 64 i), kept in VGPRs

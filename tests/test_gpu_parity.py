@@ -643,6 +643,37 @@ def test_mlp_head_summing_slabs_is_bitwise_the_reduce(s2s, B):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [32, 20, 9])
+def test_decoder_four_row_products_match_the_sixteen_row_form(s2s, B):
+    """Chains of at most 4 utterances (B <= 32) run the XCD-local decoder's skinny products on
+    v_mfma_f32_4x4x1_16b_f32 (s2s_debug_dec_r4(1): handoff.h mfma4_aw_acc + mfma4_fold) instead of the 16 x 16 x 4
+    form with 12 padding rows (0): the same products with the four k-quads added in another order, so logp, nll and
+    every gradient agree to fp32 summation noise, and two steps of the 4 x 4 form are bitwise equal."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_dec_r4
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(11 + B)
+    x = torch.randn(B, 96, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, 40), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, on in (("r16", 0), ("r4", 1), ("r4b", 1)):
+            fn(on)
+            nll, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (nll.clone(), logp.clone(), model.grads.clone())
+    finally:
+        fn(1)
+    for a, b in zip(outs["r4"], outs["r4b"]):
+        assert torch.equal(a, b)
+    for a, b in zip(outs["r4"], outs["r16"]):
+        assert torch.isfinite(a).all()
+        assert (a - b).abs().max().item() <= 2e-5 * max(b.abs().max().item(), 1e-30)
+
+
 @pytest.mark.parametrize("B,ragged", [(8, False), (32, False), (32, True), (45, False), (64, False)])
 def test_bptt_inlaunch_wgrad_matches_the_gemm(s2s, B, ragged):
     """The first encoder layer's weight gradients computed inside its BPTT launch by workers beside the chains

@@ -37,6 +37,38 @@ __global__ void timing_kernel(const float* X, float* out, long long* cyc) {
   if (l == 0) cyc[0] = t1 - t0;
 }
 
+
+// the production forms: inline asm, W operand from AGPRs, s_nop 1 before each MFMA, two alternating accumulators
+template <int FORM>
+__global__ void asm_kernel(const float* X, float* out, long long* cyc) {
+  const int l = threadIdx.x;
+  float a[8], w[8];
+  for (int i = 0; i < 8; ++i) { a[i] = X[l] + i; w[i] = X[64 + l] - i; }
+  floatx4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = acc0;
+  __syncthreads();
+  const long long t0 = __builtin_amdgcn_s_memtime();
+  for (int rep = 0; rep < 32; ++rep) {
+#pragma unroll
+    for (int i = 0; i < 8; i += 2) {
+      if (FORM == 0) {
+        asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(acc0) : "v"(a[i]), "a"(w[i]));
+        asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(acc1) : "v"(a[i + 1]), "a"(w[i + 1]));
+      } else if (FORM == 1) {
+        asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc0) : "v"(a[i]), "a"(w[i]));
+        asm volatile("s_nop 1\n\tv_mfma_f32_16x16x4_f32 %0, %1, %2, %0" : "+v"(acc1) : "v"(a[i + 1]), "a"(w[i + 1]));
+      } else {
+        asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(acc0) : "v"(a[i]), "v"(w[i]));
+        asm volatile("s_nop 1\n\tv_mfma_f32_4x4x1_16b_f32 %0, %1, %2, %0" : "+v"(acc1) : "v"(a[i + 1]), "v"(w[i + 1]));
+      }
+    }
+  }
+  asm volatile("s_nop 11" : "+v"(acc0), "+v"(acc1));
+  const floatx4 s = acc0 + acc1;
+  const long long t1 = __builtin_amdgcn_s_memtime();
+  out[l] = s[0] + s[1] + s[2] + s[3];
+  if (l == 0) cyc[0] = t1 - t0;
+}
+
 int main() {
   float hA[64], hB[64], hD[256];
   for (int l = 0; l < 64; ++l) {
@@ -80,6 +112,19 @@ int main() {
     }
     printf("%s: %.1f cycles per MFMA (512 in two chains)\n", form == 0 ? "v_mfma_f32_4x4x1_16b_f32" : "v_mfma_f32_16x16x4_f32",
            best / 512.0);
+  }
+  for (int form = 0; form < 3; ++form) {
+    long long best = 1LL << 60;
+    for (int rep = 0; rep < 5; ++rep) {
+      if (form == 0) asm_kernel<0><<<1, 64>>>(dX, dO, dC);
+      else if (form == 1) asm_kernel<1><<<1, 64>>>(dX, dO, dC);
+      else asm_kernel<2><<<1, 64>>>(dX, dO, dC);
+      long long c;
+      hipMemcpy(&c, dC, 8, hipMemcpyDeviceToHost);
+      if (c < best) best = c;
+    }
+    const char* nm[3] = {"asm 4x4x1_16b, W in AGPRs", "asm 16x16x4, W in AGPRs", "asm 4x4x1_16b, W in VGPRs"};
+    printf("%s: %.1f cycles per MFMA (256 in two chains, s_nop 1 each)\n", nm[form], best / 256.0);
   }
   return 0;
 }
