@@ -211,7 +211,7 @@ constexpr int kStampSlots = S2S_GRU_DIAG ? 16 : 8;
 template <int NC>
 __device__ __forceinline__ bool sweep_sent_n(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
                                              int wave, int lane, unsigned* abort_word, unsigned& n) {
-  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  const long lo = tbase + 4 * tile_lane(rowt, lane);
   unsigned spins = 0;
   while (true) {
     ++n;

@@ -315,15 +315,27 @@ __device__ __forceinline__ bool sweep_sent(float4 (&a)[NC], __amdgpu_buffer_rsrc
 // one writer -- and chunk i of a sweeping wave (columns wave * 16 + 64 i .. + 15 = column tile wave + 4 i) is
 // one wave instruction over that 1-KB tile instead of 64 B of each of 16 rows.  Measured (tools/sweepbench.hip:
 // 16 members, H = 256, one seam per step): 1.18-1.20 -> 1.00-1.04 us per seam.
+// Inside a 16 x 16 tile the floats are quad-major (S2S_TILE_QUAD, default): element (r, c) at (c / 4) 64 + 4 r + c % 4,
+// so the float4 a sweeping lane loads (row r, k-quad c / 4) sits next to its neighbour lanes' rows: each quad of
+// lanes reads one 64-byte run (one line) instead of four rows 64 bytes apart (two lines) -- the per-instruction
+// line count that bounds a sweep pass (the XCD decoder's interleaved slots, dec_xcd.inc, measured the effect).
+#ifndef S2S_TILE_QUAD
+#define S2S_TILE_QUAD 1
+#endif
+__device__ __forceinline__ int tile_in(int r, int c) { return S2S_TILE_QUAD ? (c >> 2) * 64 + r * 4 + (c & 3) : r * 16 + c; }
+// float offset of the float4 a lane loads from a tile: row rowt, k-quad lane >> 4
+__device__ __forceinline__ int tile_lane(int rowt, int lane) {
+  return S2S_TILE_QUAD ? (lane >> 4) * 64 + rowt * 4 : rowt * 16 + 4 * (lane >> 4);
+}
 __device__ __forceinline__ long tile_off(int row, int col, int H) {
-  return (long)(row >> 4) * 16 * H + (long)(col >> 4) * 256 + (row & 15) * 16 + (col & 15);
+  return (long)(row >> 4) * 16 * H + (long)(col >> 4) * 256 + tile_in(row & 15, col & 15);
 }
 // sweep_sent's operand layout over a tile-major slot: tbase = byte offset of the slot's row tile, rowt = this
 // lane's row within it
 template <int NC>
 __device__ __forceinline__ bool sweep_sent_tile(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
                                                 int wave, int lane, unsigned* abort_word) {
-  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  const long lo = tbase + 4 * tile_lane(rowt, lane);
   unsigned spins = 0;
   while (true) {
     bool ok = true;
@@ -346,7 +358,7 @@ __device__ __forceinline__ bool sweep_sent_tile(float4 (&a)[NC], __amdgpu_buffer
 template <int NC>
 __device__ __forceinline__ void sent_tile_issue(uint4 (&raw)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
                                                 int wave, int lane) {
-  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  const long lo = tbase + 4 * tile_lane(rowt, lane);
 #pragma unroll
   for (int i = 0; i < NC; ++i)
     raw[i] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(lo + 4L * 256 * (wave + 4 * i)), 0, 16));
@@ -372,7 +384,7 @@ template <int NC>
 __device__ __forceinline__ bool sent_tile_mfma(uint4 (&raw)[NC], float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs,
                                                long tbase, int rowt, int wave, int lane, const float4* w,
                                                floatx4& acc0, floatx4& acc1, unsigned* abort_word) {
-  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  const long lo = tbase + 4 * tile_lane(rowt, lane);
   unsigned spins = 0;
   bool ok = true;
 #pragma unroll

@@ -58,7 +58,7 @@ struct LArgs {
 template <int NC, int NW>
 __device__ __forceinline__ bool sweep_tile_w(float4 (&a)[NC], __amdgpu_buffer_rsrc_t rs, long tbase, int rowt,
                                              int wave, int lane, unsigned* abort_word) {
-  const long lo = tbase + 4 * (rowt * 16 + 4 * (lane >> 4));
+  const long lo = tbase + 4 * tile_lane(rowt, lane);
   unsigned spins = 0;
   while (true) {
     bool ok = true;
