@@ -2282,6 +2282,10 @@ extern "C" void s2s_debug_merge_alpha_head(int on) { s2s::g_merge_alpha_head = o
 // diagnostic: the merged MLP head sums the MLP GEMM's split-K slabs (1) or a reduce launch runs in front of it (0)
 extern "C" void s2s_debug_head_sums_slabs(int on) { s2s::g_head_sums_slabs = on; }
 extern "C" void s2s_debug_dec_r4(int on) { s2s::g_dec_r4 = on; }
+extern "C" void s2s_debug_dvh_wide(int on) {
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(s2s::g_dvh_force_wide), &v, sizeof(int));
+}
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);
   s2s::g_dec_stamps[1] = static_cast<unsigned long long*>(bwd);

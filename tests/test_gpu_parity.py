@@ -674,6 +674,35 @@ def test_decoder_four_row_products_match_the_sixteen_row_form(s2s, B):
         assert (a - b).abs().max().item() <= 2e-5 * max(b.abs().max().item(), 1e-30)
 
 
+@pytest.mark.parametrize("B", [32, 20])
+def test_dvh_product_form_matches_the_per_term_form(s2s, B):
+    """dec_xcd_dvh sums its tanh terms as r = 1 / (2^(K Vh) 2^(K ws) + 1) when every |K ws|, |K Vh| of the workgroup is
+    <= 63 (one v_exp per four terms), else as r = 1 / (2^(K (ws + Vh)) + 1); s2s_debug_dvh_wide(1) forces the latter
+    everywhere.  The two forms round differently, so the step's gradients agree to fp32 noise, not bitwise."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_dvh_wide
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(23 + B)
+    x = torch.randn(B, 96, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, 40), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, on in (("product", 0), ("per_term", 1)):
+            fn(on)
+            nll, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (logp.clone(), model.grads.clone())
+    finally:
+        fn(0)
+    assert torch.equal(outs["product"][0], outs["per_term"][0])  # the forward does not use dvh
+    ga, gb = outs["product"][1], outs["per_term"][1]
+    assert torch.isfinite(ga).all()
+    assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
+
+
 @pytest.mark.parametrize("B,ragged", [(8, False), (32, False), (32, True), (45, False), (64, False)])
 def test_bptt_inlaunch_wgrad_matches_the_gemm(s2s, B, ragged):
     """The first encoder layer's weight gradients computed inside its BPTT launch by workers beside the chains
