@@ -108,7 +108,7 @@ struct XArgs {
   granule_t *gDGZ, *gDGR, *gDGH, *gDC, *gPDWS, *gDWS;  // backward (inside bsync)
   unsigned *fcensus, *bcensus;
   // sentinel rows of XCD-local chains (handoff.h), [T slots][B][...] floats, outside the zeroed regions
-  float *sS, *sQ, *sC;  // forward: s_t, q_t (S), c_t (A)
+  float *sS, *sQ, *sC, *sWS;  // forward: s_t, q_t (S), c_t (A), ws_t (Sc)
   float *sDGZ, *sDGR, *sDGH, *sDC, *sDWS;  // backward: da_z, da_r, da_h (S), dc (A), dws (Sc)
 };
 constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder, LDS-resident
@@ -253,6 +253,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* xsS = f.take<float>(BT * S);
   float* xsQ = f.take<float>(BT * S);
   float* xsC = f.take<float>(BT * A);
+  float* xsWS = f.take<float>(BT * Sc);
   char* bsync = g.take<char>(256);
   granule_t* gZ = g.take<granule_t>(2 * B * S);
   granule_t* gR = g.take<granule_t>(2 * B * S);
@@ -302,7 +303,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     x->gS = xgS; x->gWS = xgWS; x->gPM = xgPM; x->gPL = xgPL; x->gPC = xgPC; x->gC = xgC; x->gQ = xgQ;
     x->gDGZ = xgDGZ; x->gDGR = xgDGR; x->gDGH = xgDGH; x->gDC = xgDC; x->gPDWS = xgPDWS; x->gDWS = xgDWS;
     x->fcensus = fcensus; x->bcensus = bcensus;
-    x->sS = xsS; x->sQ = xsQ; x->sC = xsC;
+    x->sS = xsS; x->sQ = xsQ; x->sC = xsC; x->sWS = xsWS;
     x->sDGZ = xsDGZ; x->sDGR = xsDGR; x->sDGH = xsDGH; x->sDC = xsDC; x->sDWS = xsDWS;
   }
   if (k && scratch) {  // headers behind the GEMM slabs (attn_scratch_bytes)
