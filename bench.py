@@ -576,6 +576,11 @@ def main():
             "lengths": "TIMIT-like: dur ~ N(3.1 s, 0.9 s) in [1, 7.8] s, hop 512 @ 16 kHz + 20 pad frames, "
                        "12.3 phones/s + EOS; length-sorted batches, padded + masked; value counts real frames"}
         x, labels = batches[RAGGED_BATCHES // 2][:2]  # the profiled steps (unmasked, median batch)
+    # the profiled launches' own shape (the ragged line profiles its median batch, padded to that batch's longest
+    # utterance: its L / T, not the workload's caps, price the rec_frac and the latency floors)
+    Lp, Tp = int(x.shape[1]), int(labels.shape[1])
+    if ragged:
+        out["config"]["ragged"]["profiled_batch"] = {"L": Lp, "T": Tp, "what": "the median batch, padded, unmasked"}
     if rank == 0 and not args.no_kernel_timing:
         with torch.cuda.stream(stream):
             out["roofline"], out["kernels"], dec = s2s_profile.dominant_kernel_roofline(
@@ -586,7 +591,7 @@ def main():
             r["traffic"] = round(t) if t is not None else None
             r["traffic_detail"] = detail
             r["mfma_counters"] = mfma_of(pmc, r["kernel"], r["avg_launch_us"])
-            r["latency_floor"] = latency_floor(r["kernel"], L, r["avg_launch_us"])
+            r["latency_floor"] = latency_floor(r["kernel"], Lp, r["avg_launch_us"])
             if r["kernel"].startswith("gru_"):
                 r["work"] = ("the launch's algorithmic flops: the recurrence (2 B L 3H^2 per direction) plus the "
                              "GEMM its spare-slot producers compute inside the launch (forward: the x-projection; "
@@ -594,7 +599,7 @@ def main():
                              "dVh V + sum_t alpha dc), averaged over the step's launches")
                 # the recurrence alone (what the persistent kernel exists for), priced the same way: rec_frac
                 Hs = [cfg.hiddenFrameSize] * (cfg.numLayers - 1) + [cfg.outputFrameSize]
-                rec = sum(2.0 * 2 * B * L * 3.0 * h * h for h in Hs) / len(Hs)
+                rec = sum(2.0 * 2 * B * Lp * 3.0 * h * h for h in Hs) / len(Hs)
                 rec_ach = rec / (r["avg_launch_us"] * 1e-6) / 1e12
                 r["rec_flops_per_launch"] = rec
                 r["rec_achieved"] = round(rec_ach, 3)
@@ -613,7 +618,7 @@ def main():
                 e["hbm"] = {"achieved": round(gbs, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                             "frac": round(gbs / PEAK_HBM_GBS, 4), "source": "PMC traffic / live launch time"}
             e["mfma_counters"] = mfma_of(pmc, e["kernel"], e["avg_launch_us"])
-            e["latency_floor"] = latency_floor(e["kernel"], T, e["avg_launch_us"])
+            e["latency_floor"] = latency_floor(e["kernel"], Tp, e["avg_launch_us"])
             out["roofline_decoder"].append(e)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(kw, L, T, args.cpu_seconds)

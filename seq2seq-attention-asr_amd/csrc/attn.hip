@@ -124,10 +124,17 @@ constexpr int kXWG = 32;     // workgroups per chain
 struct XPlan {
   int var = 0, U = 0, nchains = 0, XLC = 0, NCH = 0, res = 1;
 };
+// S2S_DEC_MODE=step / persist (tests, A/B): force the per-step launches / the 7-seam persistent kernels; read once
+int dec_mode() {
+  static const int m = [] {
+    const char* e = std::getenv("S2S_DEC_MODE");
+    return e && std::strcmp(e, "step") == 0 ? 1 : e && std::strcmp(e, "persist") == 0 ? 2 : 0;
+  }();
+  return m;
+}
 XPlan dec_xcd_plan(const AttnDims& d) {
   XPlan p;
-  const char* m = std::getenv("S2S_DEC_MODE");
-  if (m && (std::strcmp(m, "step") == 0 || std::strcmp(m, "persist") == 0)) return p;
+  if (dec_mode() != 0) return p;
   if (d.hf > 0 || d.lstm) return p;  // hybrid attention / LSTM decoder: per-step kernels only
   int var = 0;
   if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
@@ -1280,8 +1287,7 @@ const float* attn_saved_dropout_mask(const AttnDims& d, const void* saved) {
 static std::atomic<unsigned long long*> g_dec_stamps[2] = {{nullptr}, {nullptr}};
 
 static int dec_persist_variant(const AttnDims& d) {
-  const char* m = std::getenv("S2S_DEC_MODE");
-  if (m && std::strcmp(m, "step") == 0) return 0;
+  if (dec_mode() == 1) return 0;
   if (d.hf > 0 || d.lstm) return 0;
   if (d.flen || d.tlen) return 0;  // variable-length batches: the XCD-local or the per-step kernels
   if ((d.L + LC - 1) / LC > 256) return 0;
@@ -1314,10 +1320,8 @@ static bool co_resident(const void* fn, int grid, size_t dyn_lds) {
   return (long)per_cu * cus >= grid;
 }
 
-// resident-chunk variant (attn_persist.inc) unless S2S_DEC_RES=0
+// resident-chunk variant (attn_persist.inc) when the chunks fit
 static bool dec_res_enabled(const AttnDims& d) {
-  const char* m = std::getenv("S2S_DEC_RES");
-  if (m && std::strcmp(m, "0") == 0) return false;
   return 16 * ((d.L + LC - 1) / LC) <= kDecWG;
 }
 
@@ -1361,18 +1365,12 @@ static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, Attn
 }
 
 static std::atomic<int> g_dec_allow_local{1};
-// S2S_HEAD_SUMS_SLABS=0 (A/B): the decoder MLP GEMM's split-K reduce as its own launch in front of the MLP head
-static std::atomic<int> g_head_sums_slabs{[] {
-  const char* e = std::getenv("S2S_HEAD_SUMS_SLABS");
-  return e ? std::atoi(e) : 1;
-}()};
+// s2s_debug_head_sums_slabs(0) (A/B): the decoder MLP GEMM's split-K reduce as its own launch in front of the MLP head
+static std::atomic<int> g_head_sums_slabs{1};
 static std::atomic<int> g_merge_alpha_head{1};  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
 
-// S2S_DEC_R4=0 / s2s_debug_dec_r4(0) (A/B): chains of <= 4 utterances keep the 16 x 16 x 4 skinny products
-static std::atomic<int> g_dec_r4{[] {
-  const char* e = std::getenv("S2S_DEC_R4");
-  return e ? std::atoi(e) : 1;
-}()};
+// s2s_debug_dec_r4(0) (A/B): chains of <= 4 utterances keep the 16 x 16 x 4 skinny products
+static std::atomic<int> g_dec_r4{1};
 template <int S, int A, int SC, bool R4>
 static const void* xcd_kernel(bool fwd, int res) {
   return res == 2 ? (fwd ? (const void*)dec_xcd_fwd<S, A, SC, 2, R4> : (const void*)dec_xcd_bwd<S, A, SC, 2, R4>)

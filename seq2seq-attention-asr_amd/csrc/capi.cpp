@@ -302,65 +302,9 @@ int mark_bucket(hipEvent_t* bev, int i, hipStream_t s) {
   return 0;
 }
 
-// S2S_PROLOGUE=0|1|2 (diagnostics; see model_step_impl), read once
-// S2S_HEAD_FUSED=0 (A/B): pad, pack and the first sync prep as three launches instead of gru_step_head's one
-std::atomic<int> g_head_fused{[] {
-  const char* e = std::getenv("S2S_HEAD_FUSED");
-  return e ? std::atoi(e) : 1;
-}()};
-// Where the model step forks its side stream (S2S_FORK_MODE): 0 = at the top (default); 1 = after the step's head
-// (the side work depends on the head); 2 = the side branch depends on the head, but its nodes are created after
-// layer 1's forward launch (a replayed graph dispatches nodes in creation order).  Modes 1 and 2 start layer 1
-// earlier (14 vs 21-24 us into the step) but measured slower (same box: 3.283 / 3.291 / 3.295 ms for 0 / 1 / 2):
-// the decoder prologue's kernels on the side stream then start after layer 1 holds every CU, each of them is
-// stretched over a whole GRU layer, and the last one finished after layer 3 -- 48 us in front of the decoder
-// S2S_DEC_WGRAD_LATE=1 (A/B): the decoder weight-gradient nodes created after the top BPTT's launch.  Measured
-// 3.167 -> 3.680 ms: the replayed graph then ran the whole side branch (decoder and every GRU weight gradient)
-// after the last BPTT -- though the three BPTT launches, alone on the chip, took 355 / 373 / 370 us instead of
-// ~385 / 409 / 406 beside the weight-gradient GEMMs (profiles/r05/trace_step_dec_wgrad_late.txt)
-std::atomic<int> g_dec_wgrad_late{[] {
-  const char* e = std::getenv("S2S_DEC_WGRAD_LATE");
-  return e ? std::atoi(e) : 0;
-}()};
-// S2S_HEAD_EXTRA=0 (A/B): the loss seed and the gradient zeroing as side-stream kernels instead of in the step head
-std::atomic<int> g_head_extra{[] {
-  const char* e = std::getenv("S2S_HEAD_EXTRA");
-  return e ? std::atoi(e) : 1;
-}()};
-// S2S_BPTT_WGRAD: the first encoder layer's weight gradients inside its BPTT launch (gru_persist.hip bptt_wgrad)
-// instead of a GEMM behind it on the side stream; 0 = the GEMM (A/B)
-std::atomic<int> g_bptt_wgrad{[] {
-  const char* e = std::getenv("S2S_BPTT_WGRAD");
-  return e ? std::atoi(e) : 0;
-}()};
-// S2S_ZERO_LATE=1 (A/B): gradient zeroing on the side stream after the decoder backward (see zero_late)
-std::atomic<int> g_zero_late{[] {
-  const char* e = std::getenv("S2S_ZERO_LATE");
-  return e ? std::atoi(e) : 0;
-}()};
-static bool zero_late_knob() { return g_zero_late != 0; }
-std::atomic<int> g_fork_mode{[] {
-  const char* e = std::getenv("S2S_FORK_MODE");
-  return e ? std::atoi(e) : 0;
-}()};
-int prologue_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("S2S_PROLOGUE");
-    return e ? std::atoi(e) : 0;
-  }();
-  return m;
-}
-// S2S_WGRAD_FORK=1 (default): layer l's side-stream weight-gradient GEMMs wait for layer l-1's BPTT
-// sync prep, so the persistent BPTT is dispatched before the GEMM's workgroups take the CUs (the
-// replayed graph otherwise started the GEMM first and layers 2 and 1's BPTT ran 590-618 us instead of
-// 533-540 us, profiles/r01 kernel trace); 0: fork right after layer l's own BPTT + dX (previous layout)
-int wgrad_fork_mode() {
-  static const int m = [] {
-    const char* e = std::getenv("S2S_WGRAD_FORK");
-    return e ? std::atoi(e) : 1;
-  }();
-  return m;
-}
+// s2s_debug_bptt_wgrad(1) (A/B, tests): the first encoder layer's weight gradients inside its BPTT launch
+// (gru_persist.hip bptt_wgrad) instead of a GEMM behind it on the side stream (measured slower)
+std::atomic<int> g_bptt_wgrad{0};
 // process-wide diagnostic knobs (s2s_debug_*, not in the C ABI header; A/B tools and tests only), read when a
 // call issues its launches; no per-step state lives in globals (exclusive-CU mode, precision and the failure
 // status are per call / per context)
@@ -368,7 +312,6 @@ std::atomic<int> g_defer_pack{1};  // s2s_debug_defer_pack(0): every layer packe
 std::atomic<int> g_dec_sync_prologue{1};  // s2s_debug_dec_sync_prologue(0): decoder sync preps in place
 std::atomic<int> g_sync_handover{1};  // s2s_debug_sync_handover(0): a sync_prep in front of every GRU launch
 std::atomic<int> g_fuse_dh{1};  // s2s_debug_fuse_dh(0): the decoder's dh by GEMMs in front of the top BPTT
-std::atomic<int> g_dec_side{0};  // decoder's vbar / alpha / dVh on the side stream (measured: no gain)
 // seed_dev: the context's dropout seed word when a captured step reads its seed from the device (the
 // host writes it before each replay), else null (the seed is d->dropout_seed)
 int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t* bev, const s2s_model_dims* d,
@@ -388,8 +331,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   }
   // gradients are first written by the side stream's weight-gradient work when split: zero them
   // there (the fork precedes every gradient writer), off the critical path
-  const int pmode = prologue_mode();
-  const int fmode = pmode == 1 ? 0 : (int)g_fork_mode;
   // the step head (when fused) also writes the loss seed dlogp = -labelmask and zeroes the gradients: no side-stream
   // kernel then runs in front of it (a replayed graph ran the side branch's first two kernels -- the zeroing and the
   // seed, 15 us -- before the head)
@@ -397,25 +338,17 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   io0.ndir = 2;
   io0.B = d->B;
   io0.H = layers[0].H;
-  const bool head_fused = g_head_fused && g_sync_handover && gru_layer_persistent(io0);
-  const bool head_seed = head_fused && split && g_head_extra;                               // dlogp in the head
-  const bool head_zero = head_seed && (flags & S2S_ZERO_GRADS) && !zero_late_knob();      // zeroing in the head
-  // fork point (fmode): the side stream waits for ev[13]; mode 2 records it after the head and issues the side
-  // work after layer 1's forward launch (side_work below)
-  // zero_late (S2S_ZERO_LATE, split only): the gradient zeroing runs on the side stream right after the decoder
-  // backward's fork (ahead of every gradient writer, beside the top BPTT) instead of at the step's top
-  const bool zero_late = split && g_zero_late;
-  auto fork_side = [&](bool wait_only) -> int {
-    if (split) {
-      if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
-      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[13], 0));
-    }
-    if ((flags & S2S_ZERO_GRADS) && !zero_late && !head_zero)
-      S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
-    return 0;
-  };
-  if (fmode == 0) S2S_TRY(fork_side(false));
-  if (fmode == 3 && split) S2S_CHECK_HIP(hipEventRecord(ev[13], st));  // mode 3: recorded at the top
+  const bool head_fused = g_sync_handover && gru_layer_persistent(io0);
+  const bool head_seed = head_fused && split;                               // dlogp in the head
+  const bool head_zero = head_seed && (flags & S2S_ZERO_GRADS);            // zeroing in the head
+  // the side stream forks at the step's top (ev[13]).  Measured and rejected: forking after the head, or
+  // creating the side branch's nodes after layer 1's launch (the decoder prologue then starts after layer 1 holds
+  // every CU and is stretched over whole GRU layers); zeroing the gradients late on the side stream
+  if (split) {
+    S2S_CHECK_HIP(hipEventRecord(ev[13], st));
+    S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[13], 0));
+  }
+  if ((flags & S2S_ZERO_GRADS) && !head_zero) S2S_TRY(zero_async(split ? side : st, grads, sizeof(float) * (size_t)off));
   const int B = d->B, L = d->L, T = d->T, O = d->outputDepth;
   const int nl = (int)layers.size();
   AttnDims ad = model_attn(d);
@@ -429,8 +362,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     pp[i] = P[6 * nl + i];
     gp[i] = G[6 * nl + i];
   }
-  // prologue mode 1: beside pad + pack, joined before the first recurrence
-  if (split && pmode == 1) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
   // layer-1 input padded to a multiple of 32 columns: its GEMMs then run on aligned full tiles
   const float* x0 = x;
   long ldx0 = d->inputFrameSize;
@@ -489,30 +420,16 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     else
       S2S_TRY(gru_layers_pack(st, ios.data(), w.pack.data(), nl, defer_pack ? &deferred : nullptr));
   }
-  if (fmode == 1) S2S_TRY(fork_side(false));
-  if (fmode == 3) S2S_TRY(fork_side(split));  // mode 3: independent of the head, created after it
-  if (fmode == 2) {
-    if (split) S2S_CHECK_HIP(hipEventRecord(ev[13], st));
-    else S2S_TRY(fork_side(false));  // (no side stream: the gradient zeroing on the main stream, here)
+  // decoder parameter folds + dlogp = -labelmask (params and labels only): on the side stream, joined before the
+  // decoder (the persistent GRU launches hold every CU, so it runs in their gaps); inline without a side stream
+  if (split) {
+    if (!head_seed)  // dlogp = -labelmask
+      S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
+    S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
+    S2S_CHECK_HIP(hipEventRecord(ev[14], side));
+  } else {
+    S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
   }
-  // decoder parameter folds + dlogp = -labelmask (params and labels only): side_work, issued here or (fmode 2)
-  // right after layer 1's forward launch.  Prologue mode 0: on the side stream, joined before the decoder (the
-  // persistent GRU launches hold every CU, so it runs in their gaps); 1: beside pad + pack, joined before layer 1;
-  // 2: inline on the main stream
-  auto side_work = [&]() -> int {
-    if (split && pmode != 2) {
-      if (!head_seed)  // dlogp = -labelmask
-        S2S_TRY(nll_seed(side, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
-      if (pmode == 0) S2S_TRY(attn_fwd_prologue(side, ad, labels, ap, w.attn_saved, w.attn_scratch));
-      S2S_CHECK_HIP(hipEventRecord(ev[14], side));
-      if (pmode == 1) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
-    } else {
-      S2S_TRY(attn_fwd_prologue(st, ad, labels, ap, w.attn_saved, w.attn_scratch));
-      if (split) S2S_TRY(nll_seed(st, B, T, O, nullptr, labels, 0, nullptr, w.dlogp, d->label_lengths));
-    }
-    return 0;
-  };
-  if (fmode != 2 || !split) S2S_TRY(side_work());
   // the persistent GRU launches of the step (forward layers 1..nl, then backward nl..1) alternate between
   // two sync regions; a launch with spare slots prepares the next launch's region itself, so only the
   // first launch has a sync_prep in front of it
@@ -544,17 +461,12 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     hand_over(io, true, &next);
     if (l == 0 && defer_pack) io.pack_jobs = &deferred;
     S2S_TRY(gru_layer_fwd(st, io, w.scratch, w.scratch_bytes));
-    if (l == 0 && fmode == 2 && split) {  // the side branch (forked after the head), created behind layer 1
-      S2S_TRY(fork_side(true));
-      S2S_TRY(side_work());
-    }
   }
   // ---- attention decoder forward
-  if (split && pmode == 0) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
+  if (split) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[14], 0));
   float* lp = logp ? logp : w.logp;
-  hipStream_t dside = (split && g_dec_side) ? side : nullptr;
   S2S_TRY(attn_fwd(st, ad, w.Y[nl - 1], labels, ap, lp, w.attn_saved, w.attn_scratch, w.attn_scratch_bytes, true,
-                   dside, dside ? ev + 16 : nullptr));
+                   nullptr, nullptr));
   // ---- loss seed: dlogp = -labelmask needs only the labels (computed beside the encoder when split);
   // the reported nll (timit.lua:268-272) is computed on the side stream at the end of the step
   if (!split)
@@ -567,38 +479,24 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   // (gru_layer_dy_fused), otherwise by GEMMs in front of it
   AttnDhTerms dht{};
   S2S_TRY(attn_bwd_core(st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, w.dlogp, dYcur, 0, w.attn_scratch,
-                        w.attn_scratch_bytes, dside, dside ? ev + 16 : nullptr, g_fuse_dh ? &dht : nullptr));
-  // the decoder's weight gradients beside the top BPTT (side stream).  dec_wgrad_late: their nodes are created
-  // after the top BPTT's launch (the fork event recorded here), so a replayed graph dispatches the BPTT first
-  const bool dec_late = split && g_dec_wgrad_late;
-  auto dec_wgrad = [&](bool wait_only) -> int {
-    if (split) {
-      if (!wait_only) S2S_CHECK_HIP(hipEventRecord(ev[0], st));
-      S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
-    }
-    if (zero_late && (flags & S2S_ZERO_GRADS)) S2S_TRY(zero_async(side, grads, sizeof(float) * (size_t)off));
-    {
-      GemmBigTiles bt((wgrad_tile128_knob() & 4) != 0);  // (not tied to split: overlap on / off stay bitwise equal)
-      S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
-    }
-    S2S_TRY(mark_bucket(bev, 0, split ? side : st));
-    // the reported nll (timit.lua:268-272) beside the encoder BPTT
-    if (split)
-      S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr,
-                       d->label_lengths));
-    return 0;
-  };
-  if (dec_late) S2S_CHECK_HIP(hipEventRecord(ev[0], st));
-  else S2S_TRY(dec_wgrad(false));
-  // ---- encoder backward
-  const bool defer = split && wgrad_fork_mode() == 1;
-  // S2S_WGRAD_TILE128 (bit flags): the weight-gradient GEMMs on 128 x 128 tiles -- 1: every encoder layer's; 2: the
-  // encoder layers' that run beside a later BPTT (not the first layer's, which follows the last BPTT on the critical
-  // path); 4: the decoder's (beside the top BPTT)
-  auto wgrad_tiles128 = [&](int l) {
-    const int k = wgrad_tile128_knob();
-    return (k & 1) || ((k & 2) && l > 0);
-  };
+                        w.attn_scratch_bytes, nullptr, nullptr, g_fuse_dh ? &dht : nullptr));
+  // the decoder's weight gradients beside the top BPTT (side stream).  (Creating their nodes after the top BPTT's
+  // launch measured 3.167 -> 3.680 ms: the replayed graph then ran the whole side branch after the last BPTT.)
+  if (split) {
+    S2S_CHECK_HIP(hipEventRecord(ev[0], st));
+    S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[0], 0));
+  }
+  S2S_TRY(attn_bwd_wgrad(split ? side : st, ad, w.Y[nl - 1], labels, ap, w.attn_saved, ag, scale, w.attn_scratch));
+  S2S_TRY(mark_bucket(bev, 0, split ? side : st));
+  // the reported nll (timit.lua:268-272) beside the encoder BPTT
+  if (split)
+    S2S_TRY(nll_seed(side, B, T, O, lp, labels, (flags & S2S_NORMALIZE_NLL) ? 1 : 0, nll ? nll : w.nll, nullptr,
+                     d->label_lengths));
+  // ---- encoder backward.  Layer l's weight-gradient GEMMs (side stream) wait for an event recorded between layer
+  // l-1's BPTT sync prep and its launch, so the persistent BPTT is dispatched before the GEMM's workgroups take the
+  // CUs (forked right after layer l's own BPTT, the replayed graph started the GEMM first and layers 2 and 1's BPTT
+  // ran 590-618 us instead of 533-540 us, profiles/r01)
+  const bool defer = split;
   int pending = -1;  // layer whose weight gradients wait for the next BPTT's sync prep
   auto issue_wgrad = [&](int l) -> int {
     const GruLayerIO io = layer_io(l);
@@ -606,7 +504,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     for (int dd = 0; dd < 2; ++dd)
       for (int g = 0; g < 3; ++g) gr.dW[dd][g] = G[6 * l + 3 * dd + g];
     gr.scale = scale;
-    GemmBigTiles bt(wgrad_tiles128(l));
     S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
     S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
     return 0;
@@ -663,7 +560,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
     }
     if (defer && pending >= 0) gr.prep_event = ev[1 + pending];
     S2S_TRY(gru_layer_bwd_core(st, io, gr, w.dA[l], w.scratch, w.scratch_bytes));
-    if (dec_late && l == nl - 1) S2S_TRY(dec_wgrad(true));
     if (defer) {
       if (pending >= 0) {  // the layer above: after this BPTT's dispatch point
         S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[1 + pending], 0));
@@ -680,7 +576,6 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
       S2S_TRY(mark_bucket(bev, nl - l, st));
     } else {
       if (split) S2S_TRY(fork_to(st, side, ev[1 + l]));
-      GemmBigTiles bt(wgrad_tiles128(l));
       S2S_TRY(gru_layer_wgrad(split ? side : st, io, gr, w.dA[l], w.gws_side));
       S2S_TRY(mark_bucket(bev, nl - l, split ? side : st));
     }
@@ -795,16 +690,8 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
     S2S_REQUIRE(false, "ctx: host-coherent status word allocation failed");
   }
   if (c->status_host) std::memset(c->status_host, 0, 64);
-  // S2S_SIDE_PRIORITY=1 (A/B): the side stream (weight-gradient GEMMs) at the lowest queue priority, so the
-  // dispatcher serves the persistent launches' workgroups first
-  static const int side_prio = [] {
-    const char* e = std::getenv("S2S_SIDE_PRIORITY");
-    return e ? std::atoi(e) : 0;
-  }();
-  int least = 0, greatest = 0;
-  if (side_prio && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess) {
-    if (hipStreamCreateWithPriority(&c->side, hipStreamNonBlocking, least) != hipSuccess) c->side = nullptr;
-  } else if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
+  // (the side stream at the lowest queue priority measured no change)
+  if (hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess) {
     c->side = nullptr;
   }
   for (auto& e : c->ev)
@@ -1502,7 +1389,6 @@ int s2s_allreduce_sum(s2s_ctx* ctx, s2s_stream_t stream, float* buf, size_t coun
 }  // extern "C"
 
 // diagnostic: 1 runs the decoder's off-path kernels (vbar, alpha/indicators, dVh) on the side stream
-extern "C" void s2s_debug_dec_side(int on) { g_dec_side = on; }
 
 // diagnostic (not part of the C ABI header): one GEMM C = alpha op(A) op(B) + beta C through the library's
 // MFMA GEMM (bf16 = 1: the bf16-operand kernels), on the legacy default stream; for the layout tests

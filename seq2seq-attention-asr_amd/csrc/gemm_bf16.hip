@@ -320,10 +320,6 @@ bool gemm_big_enabled() { return g_gemm_big != 0; }
 int gemm_big_bf16(hipStream_t st, const GemmProblem& q, bool transA, bool transB, bool* done) {
   *done = false;
   if (!g_gemm_big || !t_stage || q.M <= 0 || q.N <= 0 || q.K <= 0 || q.rbias || q.Mread || q.Nread) return 0;
-  static const bool trace = std::getenv("S2S_GEMM_TRACE") != nullptr;  // diagnostic: the shapes of a workload
-  if (trace)
-    std::fprintf(stderr, "[s2s gemm_big] M %d N %d K %d tA %d tB %d beta %g bias %d relu %d\n", q.M, q.N, q.K,
-                 (int)transA, (int)transB, (double)q.beta, q.bias ? 1 : 0, q.relu);
   const int M = q.M, N = q.N, K = q.K, Kp = (K + kBK - 1) / kBK * kBK, nkt = Kp / kBK;
   // Tile and split-K from a time model: per-CU rates of the three tiles (measured on MI355X, tools/gemm_big_bench.py:
   // 256 x 256 ~3.9, 256 x 128 ~2.9, 128 x 128 ~1.6 TFLOP/s per CU at one workgroup per CU -- the 128 x 128 tile is

@@ -645,19 +645,9 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 }  // namespace
 
 static thread_local int g_gemm_prec = kGemmF32;
-static thread_local int g_gemm_big = 0;
 static thread_local GemmDeferred* g_gemm_defer = nullptr;
 void set_gemm_defer_reduce(GemmDeferred* d) { g_gemm_defer = d; }
 GemmDeferred* gemm_defer_reduce() { return g_gemm_defer; }
-void set_gemm_big_tiles(int on) { g_gemm_big = on; }
-int gemm_big_tiles() { return g_gemm_big; }
-int wgrad_tile128_knob() {
-  static const int v = [] {
-    const char* e = std::getenv("S2S_WGRAD_TILE128");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
 static thread_local bool g_wgrad_bf16 = false;
 void set_gemm_precision(int p) { g_gemm_prec = p; }
 int gemm_precision() { return g_gemm_prec; }
@@ -689,14 +679,6 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf
     return slab <= (double)ws_floats;
   };
   GemmPlan pl;
-  if (const char* o = std::getenv("S2S_GEMM_PLAN")) {  // "bm:bn:kslice" (diagnostics)
-    int bm = 0, bn = 0, ks = 0;
-    if (std::sscanf(o, "%d:%d:%d", &bm, &bn, &ks) == 3 && (bm == 128 || bm == 64) && (bn == 128 || bn == 64) &&
-        !(bm == 64 && bn == 128) && ks % kq == 0) {
-      pl.bm = bm; pl.bn = bn; pl.kslice = ks > 0 ? ks : kfull;
-      if (count(pl)) return pl;
-    }
-  }
   // Measured on MI355X (tools/gemm_bench.cpp, every GEMM shape of the training step): 64 x 64
   // tiles are the fastest or within a few % everywhere at these sizes (more blocks per CU hide
   // the global->LDS latency); split-K pays only while the output has fewer than 512 tiles
@@ -715,21 +697,12 @@ static GemmPlan plan_gemm(const GemmProblem* p, int n, size_t ws_floats, bool bf
     count(big);
     if (big.nblocks >= 256) pl = big;
   }
-  if (!bf16 && g_gemm_big) {  // (GemmBigTiles) 128 x 128 tiles, K split by the fill rule below
-    GemmPlan big = pl;
-    big.bm = big.bn = 128;
-    count(big);
-    pl = big;
-  }
+  // (128 x 128 fp32 tiles for the encoder weight gradients: half the staged bytes per flop, no step gain)
   const int tiles = pl.nblocks;
   // (an output of fewer tiles than CUs may split down to 256-long slices: the decoder MLP's 1280 x 448 x 768 product
   // and the last layer's weight gradient, both on the critical path)
   const int kmin = tiles < 256 ? 256 : 512;
-  static const bool fill = [] {
-    const char* e = std::getenv("S2S_GEMM_FILL");  // 0: the older halving rule below (diagnostics)
-    return !(e && std::strcmp(e, "0") == 0);
-  }();
-  if (tiles < 512 && fill && !bf16) {  // (bf16: no step gain measured, config 3 4.063 vs 4.079 ms)
+  if (tiles < 512 && !bf16) {  // (bf16: no step gain measured, config 3 4.063 vs 4.079 ms)
     // The split whose blocks all fit the chip in one round, with the shortest slice: time ~ rounds x slice,
     // rounds = ceil(blocks / resident slots), slots = 256 CUs x the blocks one CU holds by LDS.  A split that
     // leaves a short second round costs a whole slice more (layer 1's weight gradient, 144 tiles x K = 4096:
@@ -801,10 +774,6 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
       bool done = false;
       if (2.0 * q.M * (double)q.N * q.K >= 1e9) S2S_TRY(gemm_big_bf16(st, q, transA, transB, &done));
       if (!done) use[keep++] = q;
-      static const bool trace = std::getenv("S2S_GEMM_TRACE") != nullptr;  // diagnostic: the shapes staying here
-      if (trace && !done)
-        std::fprintf(stderr, "[s2s gemm_f32 bf16] M %d N %d K %d tA %d tB %d (%d problems in the call)\n", q.M, q.N,
-                     q.K, (int)transA, (int)transB, used);
     }
     used = keep;
     if (used == 0) return 0;

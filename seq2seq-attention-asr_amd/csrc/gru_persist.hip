@@ -845,17 +845,36 @@ __device__ __forceinline__ void bptt_prefetch(const PArgs& a, int chain, int w, 
   const unsigned* prog = a.progress + (long)chain * nmem;  // member 0's step
   int yready = 0, have = 0;
   float sink = 0.f;
+  // member 0's progress is read by thread 0 alone and handed to the workgroup through LDS behind a barrier, so every
+  // wave takes the same rows q: waves that polled on their own could skip ahead to different rows, and the fused-dy
+  // barrier below would then line one wave's row q + 1 up with wave 0's readiness check for row q (a dy row of an
+  // unfinished slice loaded into L2 early would later be served stale to the loader's sc1 loads).  Double-buffered by
+  // iteration, so one barrier per row suffices (thread 0 rewrites a slot only after every thread passed the barrier
+  // behind which it was last read).
+  __shared__ int have_lds[2];
+  int it = 0;
   // the (member, lane) tasks of one step, 256 at a time (member = task / 64, the loader's lane = task % 64), every
   // load of a step in flight together
   constexpr int kMaxTasks = NC;  // 64 nmem / 256 with nmem = H / 16
-  for (int q = 3; q < L; ++q) {
-    unsigned spins = 0;
-    while (have + 3 + a.prefetch < q) {  // member 0's loader loads row q at its step q - 3
-      have = (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (have + 3 + a.prefetch >= q) break;
-      if (spin_give_up(spins, a.abort_word)) return;
+  for (int q = 3; q < L; ++q, ++it) {
+    if (tid == 0) {
+      unsigned spins = 0;
+      bool gave_up = false;
+      while (have + 3 + a.prefetch < q) {  // member 0's loader loads row q at its step q - 3
+        have = (int)__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (have + 3 + a.prefetch >= q) break;
+        if (spin_give_up(spins, a.abort_word)) {
+          gave_up = true;
+          break;
+        }
+      }
+      have_lds[it & 1] = gave_up ? -1 : have;
     }
-    if (q < have + 4) q = have + 4;  // rows the loader has loaded (or is loading) already: skip ahead
+    __syncthreads();
+    const int hv = have_lds[it & 1];
+    if (hv < 0) return;  // (uniform) aborted launch
+    have = hv;
+    if (q < have + 4) q = have + 4;  // rows the loader has loaded (or is loading) already: skip ahead (uniform)
     if (q >= L) break;
     if (a.fused && tid < 64) xproj_wait(a.xq, dir, q / a.xq.tpt, yready, tid, a.abort_word);  // one wave, all lanes
     if (a.fused) __syncthreads();
@@ -1412,20 +1431,13 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
 // workgroup (37 KB of LDS) can share its CU; the GEMMs fill the CUs the recurrence leaves idle.
 constexpr int kExclLds = 124 * 1024;
 
-// S2S_BPTT_PREFETCH_WG: prefetcher workgroups per chain.  Same box, config-2 step (three alternating runs each,
+// Prefetcher workgroups per chain (s2s_debug_bptt_prefetch(wg, lookahead) for A/Bs).  Same box, config-2 step (three alternating runs each,
 // profiles/r05/ab_bptt_prefetch.txt): none 3.248 ms, 1 per chain 3.250 (one workgroup cannot keep 8 steps of rows
 // in flight), 2 per chain 3.182, 4 per chain 3.184, 16 (one per member) 3.463 (the side stream's weight-gradient
 // GEMMs lose the chain XCDs' idle CUs); the lower layers' BPTT step 3.05 -> 2.68 us (tools/gru_stamps.py, 2 layers)
-std::atomic<int> g_bptt_prefetch_wg{[] {
-  const char* e = std::getenv("S2S_BPTT_PREFETCH_WG");
-  return e ? std::atoi(e) : 2;
-}()};
-// S2S_BPTT_PREFETCH: lookahead (steps) of the BPTT row prefetchers (bptt_prefetch), 0 = off (4 / 8 / 12 measured
-// alike; 8)
-std::atomic<int> g_bptt_prefetch{[] {
-  const char* e = std::getenv("S2S_BPTT_PREFETCH");
-  return e ? std::atoi(e) : 8;
-}()};
+std::atomic<int> g_bptt_prefetch_wg{2};
+// lookahead (steps) of the BPTT row prefetchers (bptt_prefetch), 0 = off (4 / 8 / 12 measured alike; 8)
+std::atomic<int> g_bptt_prefetch{8};
 // prefetcher workgroups per chain of a BPTT launch of this shape (0: none)
 int bptt_prefetch_wg(int ndir, int B, int H) {
   const int nch = ndir * ((B + 15) / 16), nm = H / 16;
@@ -1546,15 +1558,12 @@ static void xproj_split(XProj& q, int nd, int nprod) {
   q.nsplit = (sA * 4 + (sB - sA) * 2) * per;
 }
 
-// XCD-grouped dealing of the dy units (s2s_debug_gru_xp_group / S2S_XP_GROUP; on by default since round 5): at
+// XCD-grouped dealing of the dy units (s2s_debug_gru_xp_group; on by default since round 5): at
 // config 2 the BPTT launch moves 214 -> 144 MB (the producers' x-weights stay in their XCD's L2), at config 4
 // 1,089 -> 806 MB.  Round 4 measured the step ~20 us slower with it; round 5 (sleepless polls, the loader's
 // rows drained before [B]) measures no difference: 3.2295 vs 3.2305 ms over three alternating runs each, same box
 // (profiles/r05/ab_xp_group.txt)
-std::atomic<int> g_xp_group{[] {
-  const char* e = std::getenv("S2S_XP_GROUP");
-  return e ? std::atoi(e) : 1;
-}()};
+std::atomic<int> g_xp_group{1};
 
 // XCD-grouped dealing (XProj::G) when the spare slots form whole per-XCD groups of gsz producers and every
 // direction gets at least one group
@@ -1866,6 +1875,10 @@ extern "C" void s2s_debug_gru_fused_xproj(int on) { s2s::g_fuse_xproj = on; }
 extern "C" void s2s_debug_gru_fused_dy(int on) { s2s::g_fuse_dy = on; }
 extern "C" void s2s_debug_gru_xp_split(int on) { s2s::g_xp_split = on; }
 extern "C" void s2s_debug_gru_xp_group(int on) { s2s::g_xp_group = on; }
+extern "C" void s2s_debug_bptt_prefetch(int wg, int lookahead) {
+  s2s::g_bptt_prefetch_wg = wg;
+  s2s::g_bptt_prefetch = lookahead;
+}
 extern "C" void s2s_debug_gru_stream_sweep(int on) { s2s::g_stream_sweep = on; }
 // diagnostic: 0 = one sentinel slot per step re-armed at launch start (the round-2 form), else the 4-slot ring
 extern "C" void s2s_debug_gru_ring(int on) { s2s::g_sent_ring = on ? s2s::kSentRing : 0; }

@@ -121,16 +121,6 @@ struct WgradPrecision {
   }
   ~WgradPrecision() { set_gemm_precision(prev); }
 };
-// fp32 GEMMs planned on 128 x 128 tiles (instead of the planner's 64 x 64) while a GemmBigTiles scope is live on
-// this thread -- the encoder weight gradients under S2S_WGRAD_TILE128 (A/B): half the staged bytes per flop
-void set_gemm_big_tiles(int on);
-int gemm_big_tiles();
-int wgrad_tile128_knob();
-struct GemmBigTiles {
-  int prev;
-  explicit GemmBigTiles(int on) : prev(gemm_big_tiles()) { set_gemm_big_tiles(on); }
-  ~GemmBigTiles() { set_gemm_big_tiles(prev); }
-};
 // A single-problem split-K GEMM issued while a GemmDeferReduce scope is live on this thread leaves its slabs
 // unreduced and describes them here (splits = 0: the GEMM wrote C itself); the consumer sums them in slice order
 // as splitk_reduce would (C = alpha * sum + bias; alpha = 1, beta = 0, no row bias, no ReLU only) -- the decoder

@@ -7,15 +7,13 @@ float64 oracle.
   h-from-L2) decoder kernels the B = 32 bench runs, run exactly as the bench runs it (hipGraph replay,
   side-stream weight gradients).  Tolerance: the fp32 bar, max|gpu - ref| <= 1e-4 max|ref| per tensor.
 * Config 5 (librispeech/model_vgg.lua:23-82): the VGG stack on (B, 3, 1024, 40), 1x1 layers 2048 wide,
-  A = 512, S = 256, Sc = 512, T = 200 chars, default init (no rescaling), B = 2.  At the default init
-  some gradients are sums whose terms cancel to ~1e-5 .. 1e-8 of their size (dWs max |.| ~1e-11: the
-  attention is nearly uniform); the reference's own fp32 arithmetic cannot get those to 1e-4.  Per
-  tensor the bar is max(1e-4, 16 e32), with e32 = the relative error of the fp32 run of the same
-  restatement (identical algorithm, numpy's summation order) against float64 on these inputs: a
-  tensor is pinned as tightly as fp32 evaluation of the reference algorithm allows, with a factor 16
-  for a different (equally valid) fp32 summation order -- the weight-gradient GEMMs accumulate
-  K ~ 1e4 products in blocked sequential MFMA chains plus split-K partials, numpy sums pairwise
-  (measured: dvgg3.W 5.8e-4 on the GPU vs e32 = 8.3e-5).
+  A = 512, S = 256, Sc = 512, T = 200 chars, B = 2, at the conditioned test point of tests/vgg_case.py
+  (`condition`: He gain on the encoder weights, we x 4 -- at the default init the annotations are bias-dominated,
+  the attention is uniform and the score layer's gradients cancel to ~1e-11, so they could not be judged).  Every
+  tensor is held to 1e-4 except the VGG convolutions' weight / bias gradients, sums over ~1e5 pixels whose fp32
+  evaluation in any order reaches ~1e-4 (the fp32 run of the same restatement against float64: e32 up to ~4e-4 on
+  the first layer): those are held to 16 e32 (a different, equally valid blocked summation order), and e32 itself
+  must stay below 1e-3 so the escape is bounded.
 """
 import numpy as np
 import pytest
@@ -25,10 +23,10 @@ from oracle import s2s_oracle as orc
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-4
-# ill-conditioned tensors: bar = max(RTOL, FLOOR_FACTOR x the fp32 restatement's own error), see
-# tests/test_gpu_fullsize.py
+# the VGG convolutions' weight / bias gradients (long pixel sums): bar = max(RTOL, FLOOR_FACTOR x the fp32
+# restatement's own error), that error itself bounded by FLOOR_CAP
 FLOOR_FACTOR = 16
-
+FLOOR_CAP = 1e-3
 
 @pytest.fixture(scope="module")
 def s2s():
@@ -79,8 +77,9 @@ def test_vgg_model_step_config5_full_width(s2s):
     g = torch.Generator().manual_seed(5)
     B, L, T = 2, 1024, 200
     model = s2s.VGGAttentionModel(40, outputFrameSize=512, hidden=2048, outputDepth=29, generator=g).cuda()
+    vc.condition(model, fe)
     rng = np.random.default_rng(5)
-    x = rng.standard_normal((B, 3, L, 40))
+    x = rng.standard_normal((B, 3, L, 40)).astype(np.float32).astype(np.float64)
     labels = np.append(rng.integers(0, 28, (B, T - 1)), np.full((B, 1), 28), axis=1).astype(np.int32)
     model.zeroGradParameters()
     nll, logp = model.step(cu(x), cu(labels, torch.int32))
@@ -95,8 +94,12 @@ def test_vgg_model_step_config5_full_width(s2s):
         errs[name] = rel(gpu.detach().cpu().numpy(), r64)
         floor[name] = rel(r32, r64)
     print("config 5 max rel errs (fp32 floor):", {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
-    bad = {k: f"{errs[k]:.2e} (fp32 floor {floor[k]:.2e})" for k in errs if not errs[k] <= max(RTOL, FLOOR_FACTOR * floor[k])}
+    # the attention score layer's gradients are conditioned at this test point: their fp32 floor is far below the bar
+    att = {k: f"{floor[k]:.1e}" for k in ("dV", "dWs", "dbs", "dwe") if not floor[k] <= 1e-5}
+    assert not att, att
+    conv = {k for k in errs if k.startswith("dvgg")}
+    uncapped = {k: f"{floor[k]:.1e}" for k in conv if not floor[k] <= FLOOR_CAP}
+    assert not uncapped, uncapped
+    bad = {k: f"{errs[k]:.2e} (fp32 floor {floor[k]:.2e})" for k in errs
+           if not errs[k] <= (max(RTOL, FLOOR_FACTOR * floor[k]) if k in conv else RTOL)}
     assert not bad, bad
-    # every tensor the fp32 restatement gets to 1e-5 must also be within the plain 1e-4 bar
-    strict = {k: f"{errs[k]:.2e}" for k in errs if floor[k] <= 1e-5 and not errs[k] <= RTOL}
-    assert not strict, strict

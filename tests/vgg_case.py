@@ -39,6 +39,27 @@ def oracle_params(model, fe, dtype=np.float64):
     return P, layers, cfg
 
 
+# Test-input conditioning.  At the reference's default init (U(+-1/sqrt(fan_in)) weights AND
+# biases) the signal shrinks ~3x per layer through the eight encoder layers, so the annotations are bias-dominated:
+# their spread across frames is ~3 % of their size (h std over frames 2.6e-4 at |h| ~ 8e-3), Vh barely varies with
+# l, the attention is uniform and the score layer's gradients dV / dWs / dbs / dwe are sums that cancel to ~1e-11
+# (fp32 floor up to 0.9 of the tensor: nothing can be judged).  A He gain on the encoder weights (sqrt(6): variance
+# 2 / fan_in with ReLU) keeps the input's variation through the stack (h spread 0.33 at std 1.4) and we x 4 spreads
+# the scores over ~2 nats: the attention is peaked and those gradients are ordinary sums (fp32 floor 3-7e-6 on
+# /tmp-probed CPU runs of this restatement at L = 256, T = 50), so they are held to the plain bars.
+HE_GAIN = 6.0 ** 0.5
+WE_SCALE = 4.0
+
+
+def condition(model, fe):
+    """Scale a VGGAttentionModel's parameters in place to the conditioned test point above."""
+    for m in model.encoder.seq.modules:
+        if isinstance(m, (fe.SpatialConvolutionMM, fe.TemporalConvolution)):
+            m.weight.mul_(HE_GAIN)
+    we = model.decoder._tensors(False)[3]
+    we.mul_(WE_SCALE)
+
+
 def grad_pairs(model, fe, G, mg):
     """[(name, gpu gradient tensor, oracle gradient)] over every parameter of the model."""
     enc_mods = model.encoder.seq.modules
