@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 #include <vector>
 
 #include "handoff.h"
@@ -2284,6 +2285,10 @@ extern "C" void s2s_debug_dec_r4(int on) { s2s::g_dec_r4 = on; }
 extern "C" void s2s_debug_dvh_wide(int on) {
   const int v = on ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(s2s::g_dvh_force_wide), &v, sizeof(int));
+}
+extern "C" void s2s_debug_dec_pf(int on) {  // 0: the XCD decoder's per-term attention form everywhere (A/B, tests)
+  const int v = on ? 1 : 0;
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(s2s::g_dec_pf), &v, sizeof(int));
 }
 extern "C" int s2s_debug_dec_stamps(void* fwd, void* bwd) {
   s2s::g_dec_stamps[0] = static_cast<unsigned long long*>(fwd);

@@ -703,11 +703,53 @@ def test_dvh_product_form_matches_the_per_term_form(s2s, B):
     assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
 
 
+@pytest.mark.parametrize("B,L,T,vscale", [(32, 96, 40, 1.0), (25, 400, 60, 1.0), (32, 96, 24, 5000.0)])
+def test_decoder_attention_product_form_matches_the_per_term_form(s2s, B, L, T, vscale):
+    """The XCD-local decoder's attention terms (dec_xcd.inc stage_vh): r = 1 / (2^(K Vh) 2^(K ws) + 1) with 2^(K Vh)
+    staged once per launch (the product form, default) against r = 1 / (2^(K (ws + Vh)) + 1) per term
+    (s2s_debug_dec_pf(0)), in F2's scores and B4's dws sums: the same values rounded differently, so logp and every
+    gradient agree to fp32 noise (1e-5 of the tensor's max).  L = 400 runs the streamed level (Vh resident, h from
+    L2).  vscale = 5000: V scaled so |K Vh| exceeds the product form's range (kPfMax) in every chunk -- the kernels
+    then take the per-term form themselves and the two runs are bitwise equal."""
+    import ctypes
+    from s2s_amd import _lib
+    from oracle import s2s_oracle as orc
+    fn = _lib.lib.s2s_debug_dec_pf
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    ocfg = orc.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    if vscale != 1.0:
+        P = orc.unflatten(model.params.cpu().double().numpy(), ocfg)
+        P["V"] = P["V"] * vscale
+        model.params.copy_(torch.tensor(orc.flatten(P, ocfg), dtype=torch.float32))
+    g = torch.Generator().manual_seed(7 + B + L)
+    x = torch.randn(B, L, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, T), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, on in (("product", 1), ("per_term", 0)):
+            fn(on)
+            model.step(x, lab)
+            _, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (logp.clone(), model.grads.clone())
+    finally:
+        fn(1)
+    (la, ga), (lb, gb) = outs["product"], outs["per_term"]
+    assert torch.isfinite(ga).all() and torch.isfinite(la).all()
+    if vscale != 1.0:
+        assert torch.equal(la, lb) and torch.equal(ga, gb)
+        return
+    assert (la - lb).abs().max().item() <= 1e-5 * lb.abs().max().item()
+    assert (ga - gb).abs().max().item() <= 1e-5 * gb.abs().max().item()
+
+
 @pytest.mark.parametrize("B,ragged", [(8, False), (32, False), (32, True), (45, False), (64, False)])
 def test_bptt_inlaunch_wgrad_matches_the_gemm(s2s, B, ragged):
     """The first encoder layer's weight gradients computed inside its BPTT launch by workers beside the chains
-    (s2s_debug_bptt_wgrad(1), gru_persist.hip bptt_wgrad: one utterance tile written directly at B <= 16, the
-    tiles' partials met by a ticket otherwise) against the weight-gradient GEMM behind the launch (0): the same
+    (s2s_debug_bptt_wgrad(1), gru_persist.hip bptt_wgrad: each utterance tile's partials written through and the
+    last arriving tile, by a ticket, adding them in tile order) against the weight-gradient GEMM behind the launch (0): the same
     products in another summation order, so layer 1's six dW tensors agree to fp32 summation noise (1e-5 of each
     tensor's max) and every other gradient is bitwise unchanged; two in-launch steps are bitwise equal."""
     import ctypes
