@@ -112,6 +112,27 @@ struct XArgs {
   float *sS, *sQ, *sC, *sWS;  // forward: s_t, q_t (S), c_t (A), ws_t (Sc)
   float *sDGZ, *sDGR, *sDGH, *sDC, *sDWS;  // backward: da_z, da_r, da_h (S), dc (A), dws (Sc)
 };
+// extra operands of the LSTM / hybrid kernels (carve, dec_xcd_lstm_prologue)
+struct XLArgs {
+  int S;          // real state width (the kernels carry SP)
+  int hk, pl;     // hybrid taps kW and the left pad
+  float* WG;      // (4SP, SP)  Wq_h, gate-major rows q SP + u, zero-padded             (saved)
+  float* WXG;     // (4SP, A)   Wq_x Wd_c Wc, rows as WG                                 (saved)
+  float* WSP;     // (Sc, SP)   Ws with zero columns past S                              (saved)
+  float* WUT;     // (SP, 4SP)  WUT[n][q SP + u] = Wq_h[u][n]                            (saved)
+  float* WXGT;    // (A, 4SP)   WXG^T                                                    (saved)
+  float* WSTP;    // (SP, SCP)  Ws^T, zero-padded                                        (saved)
+  float* WXD4;    // (4S, S)    [Wi_x; Wf_x; Wg_x; Wo_x] (the weight gradients' dd)      (saved)
+  float* BQ;      // (4S)       bq_x + bq_h                                              (fwd scratch)
+  float* KXG;     // (B T, 4SP) Wq_x KD_t + bq, zero-padded                              (fwd scratch)
+  float* sS;      // [T][B][SP] s_t (chain-interleaved sentinel rows)                    (fwd)
+  float* sDG[4];  // [T][B][SP] da_q (chain-interleaved)                                 (bwd)
+  float* sDC[2];  // [T][B][A] the two K halves of dc                                    (bwd)
+  float* sDWS;    // [T][B][SCP] dws (chain-interleaved; columns past Sc published as 0)  (bwd)
+  granule_t *gS, *gE;                       // [2][B][SP], [2][B][L] scores (hybrid halo)       (inside fsync)
+  granule_t *gDG[4], *gDC[2], *gDWS, *gQA;  // [2][B][SP] x 4, [2][B][A] x 2, [2][B][SCP], [2][B][L][kW] (bsync)
+  float* PDG;     // [B NX][kW][Sc] dG partials per (utterance, chunk)                   (bwd scratch)
+};
 constexpr int kXLC = 32;     // largest attention chunk (frames) of the XCD-local decoder, LDS-resident
 constexpr int kXLCStream = 64;  // largest chunk when h / Vh rows are read from global memory each step
 constexpr int kXMaxCh = 16;  // chunks per utterance
@@ -125,24 +146,32 @@ constexpr int kXWG = 32;     // workgroups per chain
 struct XPlan {
   int var = 0, U = 0, nchains = 0, XLC = 0, NCH = 0, res = 1;
 };
-// S2S_DEC_MODE=step / persist (tests, A/B): force the per-step launches / the 7-seam persistent kernels; read once
+// S2S_DEC_MODE=step / persist (tests, A/B): force the per-step launches / the 7-seam persistent kernels; read once.
+// s2s_debug_dec_mode(m) overrides it in-process (m = 0 auto, 1 step, 2 persist; -1 back to the environment's)
+std::atomic<int> g_dec_mode_force{-1};
 int dec_mode() {
   static const int m = [] {
     const char* e = std::getenv("S2S_DEC_MODE");
     return e && std::strcmp(e, "step") == 0 ? 1 : e && std::strcmp(e, "persist") == 0 ? 2 : 0;
   }();
-  return m;
+  const int f = g_dec_mode_force.load();
+  return f >= 0 ? f : m;
 }
 XPlan dec_xcd_plan(const AttnDims& d) {
   XPlan p;
   if (dec_mode() != 0) return p;
-  if (d.hf > 0 || d.lstm) return p;  // hybrid attention / LSTM decoder: per-step kernels only
   int var = 0;
-  if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
-  else if (d.S == 64 && d.A == 128 && d.Sc == 128) var = 2;
+  if (d.lstm) {
+    // the LSTM decoder with hybrid attention (dec_xcd_lstm.inc): the conv + BiLSTM model's shape (timit/timit.lua:
+    // 127-155: S = 400, A = 256, scoreDepth 150 padded to 160, kW = 5), chains of <= 4 utterances, resident chunks
+    if (d.hf > 0 && d.hk == 5 && d.S == 400 && d.A == 256 && d.Sc == 160) var = 3;
+  } else if (d.hf == 0) {  // (hybrid attention with the GRU decoder: the per-step kernels)
+    if (d.S == 256 && d.A == 512 && d.Sc == 512) var = 1;
+    else if (d.S == 64 && d.A == 128 && d.Sc == 128) var = 2;
+  }
   if (!var) return p;
   const int U = (d.B + kXChains - 1) / kXChains;
-  if (U > 16) return p;
+  if (U > 16 || (var == 3 && U > 4)) return p;
   const int nmax = std::min(kXMaxCh, kXWG / U);
   const int xlc = ((d.L + nmax - 1) / nmax + 3) / 4 * 4;
   if (xlc > kXLCStream || d.T > 256) return p;  // (dec_xcd_dvh stages up to 256 steps)
@@ -153,6 +182,7 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   p.res = xlc <= kXLC ? 2 : 1;
   if (fs && std::strcmp(fs, "1") == 0) p.res = 1;
   if (fs && std::strcmp(fs, "0") == 0) p.res = 0;
+  if (var == 3 && p.res != 2) return p;  // (the LSTM kernels keep their chunks resident)
   p.var = var;
   p.U = U;
   p.nchains = (d.B + U - 1) / U;
@@ -161,7 +191,8 @@ XPlan dec_xcd_plan(const AttnDims& d) {
   return p;
 }
 
-Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x = nullptr) {
+constexpr int kXlSP = 448, kXlSCP = 192;  // the LSTM kernels' padded S and Sc (var 3: S = 400, Sc = 160)
+Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x = nullptr, XLArgs* y = nullptr) {
   const long B = d.B, L = d.L, T = d.T, A = d.A, Sc = d.Sc, S = d.S, O = d.O, M = d.M, Mk = (long)d.M * d.K;
   const long NCH = (d.L + LC - 1) / LC, BT = B * T;
   Bump sv{saved, 0, 0};
@@ -195,7 +226,18 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   const long HK = d.hf > 0 ? d.hk : 0;
   float* HGT = HK ? sv.take<float>(HK * Sc) : nullptr;
   float* HCU = HK ? sv.take<float>(Sc) : nullptr;
-  const long NX = std::max(1, dec_xcd_plan(d).NCH);
+  const XPlan xpl = dec_xcd_plan(d);
+  const long NX = std::max(1, xpl.NCH);
+  // the LSTM / hybrid XCD-local kernels' operands (var 3; empty otherwise)
+  const bool v3 = xpl.var == 3;
+  const long SP = v3 ? kXlSP : 0, SCP = v3 ? kXlSCP : 0, S4 = v3 ? 4 * S : 0;
+  float* lWG = sv.take<float>(4 * SP * SP);
+  float* lWXG = sv.take<float>(4 * SP * A);
+  float* lWSP = sv.take<float>(v3 ? Sc * SP : 0);
+  float* lWUT = sv.take<float>(SP * 4 * SP);
+  float* lWXGT = sv.take<float>(v3 ? A * 4 * SP : 0);
+  float* lWSTP = sv.take<float>(SP * SCP);
+  float* lWXD4 = sv.take<float>(S4 * (v3 ? S : 0));
   Bump f{scratch, 0, 0};
   float* PM = f.take<float>(B * NCH);
   float* PL = f.take<float>(B * NCH);
@@ -210,6 +252,8 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   float* KX = f.take<float>(BT * 3 * S);
   float* KD = f.take<float>(BT * S);
   float* BKD = f.take<float>(S);
+  float* lBQ = f.take<float>(S4);
+  float* lKXG = f.take<float>(v3 ? BT * 4 * SP : 0);
   Bump g{scratch, 0, 0};
   float* DO = g.take<float>(BT * O);
   float* DU = g.take<float>(BT * Mk);
@@ -256,8 +300,11 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   granule_t* xgPC = f.take<granule_t>(2 * B * NX * A);
   granule_t* xgC = f.take<granule_t>(2 * B * A);
   granule_t* xgQ = f.take<granule_t>(2 * B * S);
+  granule_t* lgS = f.take<granule_t>(2 * B * SP);
+  granule_t* lgE = f.take<granule_t>(v3 ? 2 * B * L : 0);
   unsigned* fcensus = f.take<unsigned>(kXChains * kXWG);
   const size_t fsync_bytes = f.off - (size_t)(fsync - scratch);
+  float* lsS = f.take<float>(BT * SP);
   float* xsS = f.take<float>(BT * S);
   float* xsQ = f.take<float>(BT * S);
   float* xsC = f.take<float>(BT * A);
@@ -277,8 +324,20 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   granule_t* xgDC = g.take<granule_t>(2 * B * A);
   granule_t* xgPDWS = g.take<granule_t>(2 * B * NX * Sc);
   granule_t* xgDWS = g.take<granule_t>(2 * B * Sc);
+  granule_t* lgDG[4];
+  for (auto& q : lgDG) q = g.take<granule_t>(2 * B * SP);
+  granule_t* lgDC[2];
+  for (auto& q : lgDC) q = g.take<granule_t>(v3 ? 2 * B * A : 0);
+  granule_t* lgDWS = g.take<granule_t>(2 * B * SCP);
+  granule_t* lgQA = g.take<granule_t>(v3 ? 2 * B * L * HK : 0);
   unsigned* bcensus = g.take<unsigned>(kXChains * kXWG);
   const size_t bsync_bytes = g.off - (size_t)(bsync - scratch);
+  float* lsDG[4];
+  for (auto& q : lsDG) q = g.take<float>(BT * SP);
+  float* lsDC[2];
+  for (auto& q : lsDC) q = g.take<float>(v3 ? BT * A : 0);
+  float* lsDWS = g.take<float>(BT * SCP);
+  float* lPDG = g.take<float>(v3 ? B * NX * HK * Sc : 0);
   float* xsDGZ = g.take<float>(BT * S);
   float* xsDGR = g.take<float>(BT * S);
   float* xsDGH = g.take<float>(BT * S);
@@ -313,6 +372,14 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
     x->fcensus = fcensus; x->bcensus = bcensus;
     x->sS = xsS; x->sQ = xsQ; x->sC = xsC; x->sWS = xsWS;
     x->sDGZ = xsDGZ; x->sDGR = xsDGR; x->sDGH = xsDGH; x->sDC = xsDC; x->sDWS = xsDWS;
+  }
+  if (y) {
+    y->S = d.S; y->hk = (int)HK; y->pl = HK ? (HK % 2 ? (int)(HK - 1) / 2 : (int)HK / 2) : 0;
+    y->WG = lWG; y->WXG = lWXG; y->WSP = lWSP; y->WUT = lWUT; y->WXGT = lWXGT; y->WSTP = lWSTP; y->WXD4 = lWXD4;
+    y->BQ = lBQ; y->KXG = lKXG; y->sS = lsS; y->gS = lgS; y->gE = lgE;
+    for (int q = 0; q < 4; ++q) { y->sDG[q] = lsDG[q]; y->gDG[q] = lgDG[q]; }
+    for (int q = 0; q < 2; ++q) { y->sDC[q] = lsDC[q]; y->gDC[q] = lgDC[q]; }
+    y->sDWS = lsDWS; y->gDWS = lgDWS; y->gQA = lgQA; y->PDG = lPDG;
   }
   if (k && scratch) {  // headers behind the GEMM slabs (attn_scratch_bytes)
     const size_t hoff = ((std::max(f.off + 256, g.off + 256) + 255) & ~size_t(255)) + sizeof(float) * kGemmWsFloats;
@@ -1221,6 +1288,7 @@ __global__ void dec_dropout_bwd(AttnK k) {
 
 #include "attn_persist.inc"
 #include "dec_xcd.inc"
+#include "dec_xcd_lstm.inc"
 
 }  // namespace
 
@@ -1392,6 +1460,43 @@ static int launch_xcd(const XPlan& xp, bool fwd, hipStream_t st, AttnK& k, XArgs
   if (xp.var == 1) return launch_xcd_t<256, 512, 512>(fwd, xp.res, st, k, x);
   return launch_xcd_t<64, 128, 128>(fwd, xp.res, st, k, x);
 }
+// the LSTM / hybrid kernels (var 3: S = 400 carried as 448, A = 256, Sc = 160, resident chunks, 4 x 4 x 1 products)
+static int launch_xcd_lstm(bool fwd, hipStream_t st, AttnK& k, XArgs& x, XLArgs& y) {
+  const size_t lds = xdec_lds<kXlSP, 256, 160>(x.XLC, 2);
+  const void* fn = fwd ? (const void*)dec_xcd_lstm_fwd<kXlSP, 256, 160, 5, true>
+                       : (const void*)dec_xcd_lstm_bwd<kXlSP, 256, 160, kXlSCP, 5, true>;
+  if (lds) S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  void* args[] = {&k, &x, &y};
+  S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
+  return 0;
+}
+
+// Folds and teacher-forced constants of the LSTM / hybrid kernels (params and labels only): the re-layouts, y_in,
+// BKD, the hybrid fold (HGT, HCU), WDC = Wd_c Wc, KD = y_in Wd_y^T + BKD, then per gate q: WXG_q = Wq_x WDC and
+// KXG_q = KD Wq_x^T + bq (the padded rows / columns stay zero), WXGT = WXG^T.
+static int dec_xcd_lstm_prologue(hipStream_t st, const AttnDims& d, AttnK& k, const XArgs& x, const XLArgs& y,
+                                 const GemmWs& gws) {
+  WgradPrecision wp;  // the folds are reused by every step: fp32
+  const int S = d.S, A = d.A, rows = d.B * d.T;
+  const long SP = kXlSP;
+  hipLaunchKernelGGL(dec_xcd_lstm_pack, dim3(1024), dim3(256), 0, st, k, y, kXlSP, kXlSCP);
+  hipLaunchKernelGGL(dec_xcd_bkd, dim3((S + 3) / 4), dim3(256), 0, st, k, x.BKD);
+  hipLaunchKernelGGL(dec_hyb_fold, dim3((d.Sc + 255) / 256), dim3(256), 0, st, k);
+  S2S_CHECK_HIP(hipGetLastError());
+  S2S_TRY(zero_async(st, y.WXG, sizeof(float) * 4 * SP * A));
+  S2S_TRY(zero_async(st, y.KXG, sizeof(float) * (size_t)rows * 4 * SP));
+  S2S_TRY(gemm1(st, false, false, S, A, S, 1.f, k.P.Wd, 2L * S, k.P.Wc, A, 0.f, x.WDC, A, nullptr, gws));
+  S2S_TRY(gemm1(st, false, true, rows, S, S, 1.f, k.CY + S, 2L * S, k.P.Wd + S, 2L * S, 0.f, x.KD, S, x.BKD, gws));
+  GemmProblem pw[4], pk[4];
+  for (int q = 0; q < 4; ++q) {
+    pw[q] = GemmProblem{y.WXD4 + (long)q * S * S, x.WDC, y.WXG + q * SP * A, nullptr, S, A, A, S, A, S, 1.f, 0.f};
+    pk[q] = GemmProblem{x.KD, y.WXD4 + (long)q * S * S, y.KXG + q * SP, y.BQ + (long)q * S, S, S, 4 * SP, rows, S, S,
+                        1.f, 0.f};
+  }
+  S2S_TRY(gemm_f32(st, pw, 4, false, false, gws));
+  S2S_TRY(gemm_f32(st, pk, 4, false, true, gws));
+  return transpose_f32(st, y.WXG, A, (int)(4 * SP), A, y.WXGT, 4 * SP);
+}
 
 // Weight folds and teacher-forced constants of the XCD-local decoder (params and labels only, so
 // the model step runs it on the side stream beside the encoder).
@@ -1439,10 +1544,12 @@ int attn_fwd_prologue(hipStream_t st, const AttnDims& d, const int* labels, cons
   if (!xp.var) return 0;
   AttnK k{};
   XArgs x{};
-  carve(d, &k, (char*)saved, (char*)scratch, &x);
+  XLArgs y{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x, &y);
   k.P = P;
   k.labels = labels;
-  S2S_TRY(dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch)));
+  if (xp.var == 3) S2S_TRY(dec_xcd_lstm_prologue(st, d, k, x, y, attn_gemm_ws(d, scratch)));
+  else S2S_TRY(dec_xcd_prologue(st, d, k, x, attn_gemm_ws(d, scratch)));
   if (d.syncs_in_prologue) {  // both decoder launches' sync regions, off the decoder's critical path
     S2S_TRY(launch_sync_prep(st, k.fsync, k.fsync_bytes, nullptr, k.fhdr));
     S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, nullptr, k.bhdr));
@@ -1456,7 +1563,8 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
   XArgs x{};
-  carve(d, &k, (char*)saved, (char*)scratch, &x);
+  XLArgs y{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x, &y);
   k.P = P;
   k.h = h;
   k.labels = labels;
@@ -1475,7 +1583,8 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   const int pvar = xp.var ? 0 : dec_persist_variant(d);
   const PersistLaunch pf = pvar ? pick_dec_fwd(pvar, d, pgrid) : PersistLaunch{};
   if (xp.var) {
-    if (!prologue_done) S2S_TRY(dec_xcd_prologue(st, d, k, x, gws));
+    if (!prologue_done)
+      S2S_TRY(xp.var == 3 ? dec_xcd_lstm_prologue(st, d, k, x, y, gws) : dec_xcd_prologue(st, d, k, x, gws));
     x.U = xp.U;
     x.nchains = xp.nchains;
     x.XLC = xp.XLC;
@@ -1485,8 +1594,9 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
     {
       // algorithmic units: the attention re-streams Vh and h every step, T B L (Sc + A) 4 bytes
       // per forward; flops = the step products + the attention contractions
-      ProfScope ps(st, "dec_fwd_xcd", dec_flops(d, false), 4.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
-      S2S_TRY(launch_xcd(xp, true, st, k, x));
+      ProfScope ps(st, xp.var == 3 ? "dec_fwd_xcd_lstm" : "dec_fwd_xcd", dec_flops(d, false),
+                   4.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
+      S2S_TRY(xp.var == 3 ? launch_xcd_lstm(true, st, k, x, y) : launch_xcd(xp, true, st, k, x));
     }
     // alpha / MonotonicAlignment indicators from the saved scores and VBAR (the backward's dws reference
     // point) from Vh, in one launch: only the backward (and alpha()) read them, so beside the MLP head
@@ -1603,7 +1713,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   S2S_REQUIRE(scratch_bytes >= attn_scratch_bytes(d), "attn: scratch too small");
   AttnK k{};
   XArgs x{};
-  carve(d, &k, (char*)saved, (char*)scratch, &x);
+  XLArgs y{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x, &y);
   k.P = P;
   k.h = h;
   k.labels = labels;
@@ -1624,7 +1735,7 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     S2S_TRY(zero_async(st, k.DWEACC, sizeof(float) * (size_t)B * k.NCH * Sc));
   }
   // packed transposes for the backward products
-  if (d.lstm) {  // GT = LW^T in the gate gradients' gate-major order
+  if (d.lstm && !xp.var) {  // GT = LW^T in the gate gradients' gate-major order
     hipLaunchKernelGGL(dec_lstm_gt, dim3(512), dim3(256), 0, st, k);
     S2S_CHECK_HIP(hipGetLastError());
   }
@@ -1674,15 +1785,23 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
     if (!d.syncs_in_prologue) S2S_TRY(launch_sync_prep(st, k.bsync, k.bsync_bytes, nullptr, k.bhdr));
     if (side) S2S_CHECK_HIP(hipStreamWaitEvent(st, ev[2], 0));  // VBAR, ALPHA, IND from the forward's side stream
     {
-      ProfScope ps(st, "dec_bwd_xcd", dec_flops(d, true), 8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
-      S2S_TRY(launch_xcd(xp, false, st, k, x));
+      ProfScope ps(st, xp.var == 3 ? "dec_bwd_xcd_lstm" : "dec_bwd_xcd", dec_flops(d, true),
+                   8.0 * d.T * d.B * d.L * (double)(d.Sc + d.A));
+      S2S_TRY(xp.var == 3 ? launch_xcd_lstm(false, st, k, x, y) : launch_xcd(xp, false, st, k, x));
     }
     // dVh / dwe (dec_xcd_dvh) beside the alpha^T dc GEMMs when split; both feed dh
     if (side) {
       S2S_CHECK_HIP(hipEventRecord(ev[3], st));
       S2S_CHECK_HIP(hipStreamWaitEvent(side, ev[3], 0));
     }
-    {
+    if (d.hf > 0) {  // the location features inside the tanh terms (dec_xcd_lstm.inc)
+      const size_t lds = dec_xcd_dvh_hyb_lds(T);
+      if (lds > 64 * 1024)
+        S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_xcd_dvh_hyb),
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL(dec_xcd_dvh_hyb, dim3((Sc + 63) / 64, k.NCH, B), dim3(256), lds, side ? side : st, k, x);
+      S2S_CHECK_HIP(hipGetLastError());
+    } else {
       const size_t lds = dec_xcd_dvh_lds(T);
       if (lds > 64 * 1024)
         S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_xcd_dvh),
@@ -1752,13 +1871,23 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
   WgradPrecision wp;
   AttnK k{};
   XArgs x{};
-  carve(d, &k, (char*)saved, (char*)scratch, &x);
+  XLArgs y{};
+  carve(d, &k, (char*)saved, (char*)scratch, &x, &y);
   k.labels = labels;
   const int B = d.B, L = d.L, T = d.T, S = d.S, A = d.A, Sc = d.Sc, O = d.O, Mk = d.M * d.K;
   const int rows = B * T;
   hipLaunchKernelGGL(dec_onehot_prev, dim3(256), dim3(256), 0, st, k);
   S2S_CHECK_HIP(hipGetLastError());
-  if (dec_xcd_plan(d).var) {
+  const XPlan xpw = dec_xcd_plan(d);
+  if (xpw.var == 3) {
+    // the LSTM kernels folded c -> c_in -> d away as well: c_in, d = HX[:, S:] (the LSTM input), dd = dGA WXD4 (the
+    // four gates' x-weights) and [dc_in | dy_in] = dd Wd for the weight gradients, all B*T rows at once
+    const GemmWs gws = attn_gemm_ws(d, scratch);
+    S2S_TRY(gemm1(st, false, true, rows, S, A, 1.f, k.C, A, P.Wc, A, 0.f, k.CY, 2L * S, P.bc, gws));
+    S2S_TRY(gemm1(st, false, true, rows, S, 2 * S, 1.f, k.CY, 2L * S, P.Wd, 2L * S, 0.f, k.HX + S, 2L * S, P.bd, gws));
+    S2S_TRY(gemm1(st, false, false, rows, S, 4 * S, 1.f, k.DGA, 4L * S, y.WXD4, S, 0.f, k.DD, S, nullptr, gws));
+    S2S_TRY(gemm1(st, false, false, rows, 2 * S, S, 1.f, k.DD, S, P.Wd, 2L * S, 0.f, k.DCY, 2L * S, nullptr, gws));
+  } else if (xpw.var) {
     // the XCD-local loop folded c -> c_in -> d away: recompute them (and dd, [dc_in | dy_in]) for
     // the weight gradients, all B*T rows at once
     const GemmWs gws = attn_gemm_ws(d, scratch);
@@ -1813,7 +1942,10 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
   S2S_TRY(colsum_f32(st, k.DWEACC, Sc, B * k.NCH, Sc, scale, 1.f, G.we, cws));
   if (d.hf > 0) {  // hybrid features: dG (sum over utterances, chunks; steps summed in the loop), dcu = sum dws
     k.P = P;
-    S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT, cws));
+    if (xpw.var == 3)  // the XCD-local chunks' partials (dec_xcd_lstm_bwd)
+      S2S_TRY(colsum_f32(st, y.PDG, (long)d.hk * Sc, B * xpw.NCH, d.hk * Sc, 1.f, 0.f, k.DGT, cws));
+    else
+      S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT, cws));
     S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, 1.f, 0.f, k.DCU, cws));
     const int n = Sc * d.hf + d.hf * d.hk + d.hf;
     hipLaunchKernelGGL(dec_hyb_wgrad, dim3((n + 255) / 256), dim3(256), 0, st, k, G, scale);
@@ -2286,6 +2418,7 @@ extern "C" void s2s_debug_dvh_wide(int on) {
   const int v = on ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(s2s::g_dvh_force_wide), &v, sizeof(int));
 }
+extern "C" void s2s_debug_dec_mode(int m) { s2s::g_dec_mode_force = m; }
 extern "C" void s2s_debug_dec_pf(int on) {  // 0: the XCD decoder's per-term attention form everywhere (A/B, tests)
   const int v = on ? 1 : 0;
   (void)hipMemcpyToSymbol(HIP_SYMBOL(s2s::g_dec_pf), &v, sizeof(int));

@@ -1081,3 +1081,103 @@ def test_host_parameters_are_refused_not_launched(fe):
     rnn = s2s_amd.RNN(s2s_amd.GRU(8, 16))
     with pytest.raises(s2s_amd.nn.S2SArgumentError, match="cuda"):
         rnn.forward(torch.ones(2, 5, 8, device="cuda"))
+
+
+def _timit_lstm_dec_case(rng, S, A, Sc, O, kW, nF):
+    """timit/timit.lua:127-155's decoder parameters at the reference's default init scale (U(+-1/sqrt(fan_in)) ->
+    standard deviation 1/sqrt(3 fan_in)), in the oracle's dict layout."""
+    from oracle import s2s_oracle as orc
+    cfg = orc.ModelConfig(inputFrameSize=8, hiddenFrameSize=16, outputFrameSize=A // 2, scoreDepth=Sc, stateDepth=S,
+                          outputDepth=O, mlpDepth=4, maxoutWindow=3, numLayers=1, hybridAttendFilterSize=kW,
+                          hybridAttendFeatureMaps=nF, decoderLSTM=True)
+
+    def u(shape, fan):
+        return rng.uniform(-1.0, 1.0, shape) / np.sqrt(fan)
+    P = {"V": u((Sc, A), A), "Ws": u((Sc, S), S), "bs": u(Sc, S), "we": u((1, Sc), Sc), "Wy": u((S, O), O),
+         "by": u(S, O), "Wc": u((S, A), A), "bc": u(S, A), "Wd": u((S, 2 * S), 2 * S), "bd": u(S, 2 * S),
+         "Wm": u((12, S + A), S + A), "bm": u(12, S + A), "Wo": u((O, 4), 4), "bo": u(O, 4),
+         "hybW": u((nF, kW), kW), "hybb": u(nF, kW), "hybU": u((Sc, nF), nF)}
+    for q in "ifgo":
+        P[f"dec.W{q}x"], P[f"dec.b{q}x"] = u((S, S), S), u(S, S)
+        P[f"dec.W{q}h"], P[f"dec.b{q}h"] = u((S, S), S), u(S, S)
+    return cfg, P
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,L,T,pen", [(32, 62, 12, 0.0), (25, 62, 10, 0.3)])
+def test_timit_lstm_hybrid_decoder_xcd_matches_oracle(fe, B, L, T, pen):
+    """The timit/timit.lua:127-155 decoder at the reference's own shape -- LSTM(400, 400) decoder_recurrent, scoreDepth
+    150 (run on 160 zero-padded channels), hybrid attention kW = 5 / 16 maps, annotations 2 x 128, external ReLU
+    decoder_mlp, 62 phonemes, the 62 annotation frames of a 512-frame utterance -- runs on the XCD-local LSTM kernels
+    (dec_xcd_lstm.inc; the live kernel profile names them: B = 32 is 8 chains of 4 utterances, B = 25 leaves a last
+    chain of one), and every output and gradient matches the float64 oracle at the 1e-4 bar (MonotonicAlignment
+    decisions adopted as in tests/test_gpu_parity.py) and the per-step launches (s2s_debug_dec_mode(1)) to 1e-4, the
+    oracle bar itself: the folded c -> d -> gates products and the chunked sums reassociate, and the score layer's
+    cancelling sums (dbs, dWs, the hybrid fold's dhybb / dhybU) differ by up to 8.8e-5 with the penalty on; every other
+    tensor agrees to ~1e-6."""
+    import ctypes
+    import s2s_amd
+    from oracle import s2s_oracle as orc
+    from s2s_amd import _lib
+    from s2s_amd import profile as prof
+    S, A, Sc, O, kW, nF = 400, 256, 150, 62, 5, 16
+    rng = np.random.default_rng(B * 10 + T)
+    cfg, P = _timit_lstm_dec_case(rng, S, A, Sc, O, kW, nF)
+    cfg.penalty = pen
+    mlp = fe.Sequential(fe.Linear(S + A, 2 * O), fe.ReLU(), fe.Linear(2 * O, O), fe.LogSoftMax())
+    att, cell = _load_lstm_attention(s2s_amd, fe, P, cfg, mlp)
+    lins = [m for m in mlp.modules if isinstance(m, fe.Linear)]
+    layers = [("linear", _np(lins[0].weight), _np(lins[0].bias)), ("relu",),
+              ("linear", _np(lins[1].weight), _np(lins[1].bias)), ("logsoftmax",)]
+    h = rng.standard_normal((B, L, A)) * 0.5
+    labels = rng.integers(0, O, (B, T)).astype(np.int32)
+    dl = rng.standard_normal((B, T, O))
+    mode = _lib.lib.s2s_debug_dec_mode
+    mode.argtypes = [ctypes.c_int]
+
+    def run():
+        logp = att.forward([cu(h), cu(labels, torch.int32)]).clone()
+        ind = att.mono_ind().clone() if pen > 0 else None
+        att.zeroGradParameters()
+        dh = att.backward([cu(h), None], cu(dl), 1.0)[0].clone()
+        torch.cuda.synchronize()
+        grads = [t.clone() for t in list(att.own_grad.values()) + list(cell.named(grads=True).values())]
+        return logp, dh, grads, ind
+
+    _lib.check(_lib.lib.s2s_prof_enable(1))
+    try:
+        prof.collect()
+        logp, dh, grads, ind = run()
+        ran = prof.collect()
+    finally:
+        _lib.lib.s2s_prof_enable(0)
+    assert "dec_fwd_xcd_lstm" in ran and "dec_bwd_xcd_lstm" in ran, sorted(ran)
+    _, cache = orc.attention_fwd(h, labels, P, cfg)
+    if pen > 0:  # adopt the GPU's MonotonicAlignment decisions where the statistic is within fp32 noise of 0
+        gi = _np(ind)
+        a = cache["alpha"]
+        prev = np.concatenate([np.zeros_like(a[:, :1]), a[:, :-1]], 1)
+        stat = ((L - np.arange(L))[None, None, :] * (a - prev)).sum(-1)
+        clear = np.abs(stat) > 1e-4
+        assert np.array_equal(gi[clear], cache["mono_ind"][clear]), "MonotonicAlignment decisions differ"
+        cache["mono_ind"] = gi
+    lref, mc = fo.mlp_fwd(cache["v"].reshape(B * T, -1), layers)
+    assert_rel(_np(logp), lref.reshape(B, T, O), "logp")
+    mg = [(np.zeros_like(Lr[1]), np.zeros_like(Lr[2])) if Lr[0] == "linear" else None for Lr in layers]
+    dv = fo.mlp_bwd(layers, mc, dl.reshape(B * T, O), mg)
+    G = {k: np.zeros_like(v) for k, v in P.items()}
+    dhr = orc.attention_bwd(P, cfg, cache, None, G, dmlp_in=dv.reshape(B, T, -1))
+    names = list(att.own_grad.keys()) + ["dec." + n for n in cell.named(grads=True)]
+    pairs = [("dh", dh, dhr)] + [("d" + n, g, G[n]) for n, g in zip(names, grads) if n in G]
+    _assert_grads(pairs)
+    # the per-step launches on the same inputs
+    mode(1)
+    try:
+        logp_s, dh_s, grads_s, _ = run()
+    finally:
+        mode(-1)
+    diffs = {"logp": rel_err(_np(logp), _np(logp_s)), "dh": rel_err(_np(dh), _np(dh_s))}
+    diffs.update({"d" + n: rel_err(_np(g), _np(gs)) for n, g, gs in zip(names, grads, grads_s)})
+    print("XCD-local vs per-step launches, max rel diff:", {k: f"{v:.1e}" for k, v in diffs.items()})
+    bad = {k: f"{v:.2e}" for k, v in diffs.items() if not v <= 1e-4}
+    assert not bad, bad

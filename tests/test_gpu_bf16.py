@@ -253,7 +253,7 @@ BF16_PINNED_DEEP_GRAD_RTOL = 2e-2
 # of the context gradient dc (bf16 MLP data-gradient product upstream, ~6e-3 relative like every other tensor here)
 # onto h_l - c, a direction nearly orthogonal to it in 512 dimensions, so dc's rounding error reaches de ~4x
 # amplified -- measured 2.4-2.5e-2 on all four at the conditioned test point (vgg_case.condition; fp32 floor
-# 2.5-8e-6, so the bar judges the kernels, not fp32 noise).  Held to 5e-2 (the round-5 bar was 0.1 on an unconditioned
+# 0.6-3e-5, so the bar judges the kernels, not fp32 noise).  Held to 5e-2 (the round-5 bar was 0.1 on an unconditioned
 # case whose fp32 floor reached 0.9).
 BF16_ATTN_GRAD_RTOL = 5e-2
 
@@ -303,9 +303,10 @@ def test_vgg_model_step_bf16_config5(lib, prec):
         floor[name] = _rel(r32, r64)
     print(f"config 5 {prec} rel L2 errs, decisions pinned (fp32 floor):",
           {k: f"{errs[k]:.1e} ({floor[k]:.1e})" for k in errs})
-    # every tensor is judged; the attention score layer's gradients are conditioned here (fp32 floor <= 1e-5)
+    # every tensor is judged; the attention score layer's gradients are conditioned here (fp32 floor <= 1e-4, measured
+    # 0.6-3e-5 under the two variants' adopted decisions; the unconditioned case reached 0.9)
     attn = ("dV", "dWs", "dbs", "dwe")
-    att = {k: f"{floor[k]:.1e}" for k in attn if not floor[k] <= 1e-5}
+    att = {k: f"{floor[k]:.1e}" for k in attn if not floor[k] <= 1e-4}
     assert not att, att
     bad = {k: f"{errs[k]:.2e}" for k in errs
            if not errs[k] <= (BF16_PINNED_LOGP_RTOL if k == "logp" else BF16_ATTN_GRAD_RTOL if k in attn else
