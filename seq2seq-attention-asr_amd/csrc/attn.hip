@@ -129,7 +129,7 @@ struct XLArgs {
   float* sDG[4];  // [T][B][SP] da_q (chain-interleaved)                                 (bwd)
   float* sDC[2];  // [T][B][A] the two K halves of dc                                    (bwd)
   float* sDWS;    // [T][B][SCP] dws (chain-interleaved; columns past Sc published as 0)  (bwd)
-  granule_t *gS, *gE;                       // [2][B][SP], [2][B][L] scores (hybrid halo)       (inside fsync)
+  granule_t *gS, *gE, *gA;  // [2][B][SP], [2][B][L] scores and alpha (hybrid location features)   (inside fsync)
   granule_t *gDG[4], *gDC[2], *gDWS, *gQA;  // [2][B][SP] x 4, [2][B][A] x 2, [2][B][SCP], [2][B][L][kW] (bsync)
   float* PDG;     // [B NX][kW][Sc] dG partials per (utterance, chunk)                   (bwd scratch)
 };
@@ -302,6 +302,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   granule_t* xgQ = f.take<granule_t>(2 * B * S);
   granule_t* lgS = f.take<granule_t>(2 * B * SP);
   granule_t* lgE = f.take<granule_t>(v3 ? 2 * B * L : 0);
+  granule_t* lgA = f.take<granule_t>(v3 ? 2 * B * L : 0);
   unsigned* fcensus = f.take<unsigned>(kXChains * kXWG);
   const size_t fsync_bytes = f.off - (size_t)(fsync - scratch);
   float* lsS = f.take<float>(BT * SP);
@@ -376,7 +377,7 @@ Layout carve(const AttnDims& d, AttnK* k, char* saved, char* scratch, XArgs* x =
   if (y) {
     y->S = d.S; y->hk = (int)HK; y->pl = HK ? (HK % 2 ? (int)(HK - 1) / 2 : (int)HK / 2) : 0;
     y->WG = lWG; y->WXG = lWXG; y->WSP = lWSP; y->WUT = lWUT; y->WXGT = lWXGT; y->WSTP = lWSTP; y->WXD4 = lWXD4;
-    y->BQ = lBQ; y->KXG = lKXG; y->sS = lsS; y->gS = lgS; y->gE = lgE;
+    y->BQ = lBQ; y->KXG = lKXG; y->sS = lsS; y->gS = lgS; y->gE = lgE; y->gA = lgA;
     for (int q = 0; q < 4; ++q) { y->sDG[q] = lsDG[q]; y->gDG[q] = lgDG[q]; }
     for (int q = 0; q < 2; ++q) { y->sDC[q] = lsDC[q]; y->gDC[q] = lgDC[q]; }
     y->sDWS = lsDWS; y->gDWS = lgDWS; y->gQA = lgQA; y->PDG = lPDG;
