@@ -455,25 +455,31 @@ __device__ __forceinline__ float hyb_carry(const AttnK& k, int b, int l) {
 
 // weight gradients of the hybrid features from DGT = sum dG^T (kW x Sc) and DCU = sum dws (Sc):
 // G = U W, cu = U b  ->  dU = dG W^T + dcu b^T, dW = U^T dG, db = U^T dcu
-__global__ void dec_hyb_wgrad(AttnK k, AttnGrads G, float scale) {
-  const int nf = k.hf, kw = k.hk, Sc = k.Sc;
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+// one wave per output element: the dW / db sums run over Sc across the lanes (a thread-serial loop over Sc put ~160
+// dependent L2 loads behind each of those outputs: 33 us at the conv + BiLSTM model's Sc = 160)
+__global__ __launch_bounds__(256) void dec_hyb_wgrad(AttnK k, AttnGrads G, float scale) {
+  const int nf = k.hf, kw = k.hk, Sc = k.Sc, lane = threadIdx.x & 63;
+  const int idx = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (idx < Sc * nf) {
     const int j = idx / nf, f = idx % nf;
-    float v = 0.f;
-    for (int i = 0; i < kw; ++i) v += k.DGT[(long)i * Sc + j] * k.P.hybW[f * kw + i];
-    v += k.DCU[j] * k.P.hybb[f];
-    G.hybU[idx] += scale * v;
+    if (lane == 0) {
+      float v = 0.f;
+      for (int i = 0; i < kw; ++i) v += k.DGT[(long)i * Sc + j] * k.P.hybW[f * kw + i];
+      v += k.DCU[j] * k.P.hybb[f];
+      G.hybU[idx] += scale * v;
+    }
   } else if (idx < Sc * nf + nf * kw) {
     const int r = idx - Sc * nf, f = r / kw, i = r % kw;
     float v = 0.f;
-    for (int j = 0; j < Sc; ++j) v += k.P.hybU[(long)j * nf + f] * k.DGT[(long)i * Sc + j];
-    G.hybW[r] += scale * v;
+    for (int j = lane; j < Sc; j += 64) v += k.P.hybU[(long)j * nf + f] * k.DGT[(long)i * Sc + j];
+    v = wave_sum(v);
+    if (lane == 0) G.hybW[r] += scale * v;
   } else if (idx < Sc * nf + nf * kw + nf) {
     const int f = idx - Sc * nf - nf * kw;
     float v = 0.f;
-    for (int j = 0; j < Sc; ++j) v += k.P.hybU[(long)j * nf + f] * k.DCU[j];
-    G.hybb[f] += scale * v;
+    for (int j = lane; j < Sc; j += 64) v += k.P.hybU[(long)j * nf + f] * k.DCU[j];
+    v = wave_sum(v);
+    if (lane == 0) G.hybb[f] += scale * v;
   }
 }
 
@@ -1212,6 +1218,21 @@ __global__ __launch_bounds__(256) void dec_b8_ws(AttnK k) {
   else dec_gate_grads(k, b, t - 1, n, k.DV[((long)b * k.T + t - 1) * (S + k.A) + n] + carry);
 }
 
+// G.lstm[4 q] (Wqx) += LDW[q S + r][S + c], G.lstm[4 q + 2] (Wqh) += LDW[q S + r][c]  (LDW: (4S, 2S) gate-major)
+__global__ void lstm_dw_scatter(const float* __restrict__ ldw, int S, AttnGrads G) {
+  const long n = 8L * S * S;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const int h = (int)(i / (4L * S * S));  // 0: x half, 1: h half
+    const long e = i - h * 4L * S * S;
+    const int q = (int)(e / ((long)S * S));
+    const long rc = e - (long)q * S * S;
+    const int r = (int)(rc / S), c = (int)(rc - (long)r * S);
+    const float v = ldw[((long)q * S + r) * 2 * S + (h == 0 ? S + c : c)];
+    float* dst = G.lstm[4 * q + (h == 0 ? 0 : 2)] + rc;
+    *dst = *dst + v;
+  }
+}
+
 __global__ void dec_onehot_prev(AttnK k) {
   // YP[b][t] = onehot(y_{t-1}), zeros at t = 0 (RNNAttention.lua:172-176)
   const long n = (long)k.B * k.T * k.O;
@@ -1928,11 +1949,11 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
   S2S_TRY(colsum_f32(st, k.DD, S, rows, S, scale, 1.f, G.bd, cws));
   if (d.lstm) {
     ColsumOut outs[4];
-    for (int q = 0; q < 4; ++q) {  // LSTM.lua:25-29: Linear(S,S)(x) + Linear(S,S)(h), both with bias
-      S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S + S, 2L * S, G.lstm[4 * q], S, S, S, true));      // Wqx
-      S2S_TRY(copy2d_f32(st, k.LDW + (long)q * S * 2 * S, 2L * S, G.lstm[4 * q + 2], S, S, S, true));      // Wqh
-      outs[q] = ColsumOut{q * S, S, {G.lstm[4 * q + 1], G.lstm[4 * q + 3], nullptr}, 2};                   // bqx, bqh
-    }
+    // LSTM.lua:25-29: Linear(S,S)(x) + Linear(S,S)(h), both with bias: the four gates' Wqx / Wqh blocks of LDW added
+    // into their tensors in one launch (eight copy launches before)
+    hipLaunchKernelGGL(lstm_dw_scatter, dim3(1024), dim3(256), 0, st, k.LDW, S, G);
+    S2S_CHECK_HIP(hipGetLastError());
+    for (int q = 0; q < 4; ++q) outs[q] = ColsumOut{q * S, S, {G.lstm[4 * q + 1], G.lstm[4 * q + 3], nullptr}, 2};  // bqx, bqh
     S2S_TRY(colsum_scatter_f32(st, k.DGA, 4L * S, rows, 4 * S, scale, outs, 4, cws));
   }
   {
@@ -1949,7 +1970,7 @@ int attn_bwd_wgrad(hipStream_t st, const AttnDims& d, const float* h, const int*
       S2S_TRY(colsum_f32(st, k.PDG, (long)d.hk * Sc, B * k.NCH, d.hk * Sc, 1.f, 0.f, k.DGT, cws));
     S2S_TRY(colsum_f32(st, k.DWS, Sc, rows, Sc, 1.f, 0.f, k.DCU, cws));
     const int n = Sc * d.hf + d.hf * d.hk + d.hf;
-    hipLaunchKernelGGL(dec_hyb_wgrad, dim3((n + 255) / 256), dim3(256), 0, st, k, G, scale);
+    hipLaunchKernelGGL(dec_hyb_wgrad, dim3((n + 3) / 4), dim3(256), 0, st, k, G, scale);
     S2S_CHECK_HIP(hipGetLastError());
   }
   return 0;

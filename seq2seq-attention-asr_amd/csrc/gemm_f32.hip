@@ -559,8 +559,12 @@ __global__ void colsum_kernel(const float* __restrict__ X, long ldx, int M, int 
 }
 
 // two-stage column sums: part[p][col] = sum of row slice p (grid (N/64, parts), 64 columns x 4 row
-// groups per workgroup), then out[col] = beta*out + alpha * sum_p part[p][col] in slice order
+// groups per workgroup), then out[col] = beta*out + alpha * sum_p part[p][col] in slice order.  Slices of >= 64
+// rows (colsum_parts); a row group's rows go round-robin into four running sums (rows i, i + 4, i + 8, i + 12 into
+// sums 0..3), so four loads are in flight per thread instead of one add chain behind each load (a 1280 x 256 bias
+// gradient: 17 -> ~4 us), summed (s0 + s1) + (s2 + s3) -- one fixed order for a given M
 constexpr int kColParts = 64;
+__host__ __device__ inline int colsum_parts(int M) { return M < 128 ? 1 : (M + 63) / 64 < kColParts ? (M + 63) / 64 : kColParts; }
 __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restrict__ X, long ldx, int M, int N,
                                                           float* __restrict__ part) {
   __shared__ float red[4][65];
@@ -568,9 +572,20 @@ __global__ __launch_bounds__(256) void colsum_part_kernel(const float* __restric
   const int col = blockIdx.x * 64 + c;
   const int chunk = (M + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * chunk, r1 = min(M, r0 + chunk);
-  float s = 0.f;
-  if (col < N)
-    for (int i = r0 + g; i < r1; i += 4) s += X[(long)i * ldx + col];
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (col < N) {
+    const float* xc = X + col;
+    int i = r0 + g;
+    for (; i + 12 < r1; i += 16) {
+      const float a0 = xc[(long)i * ldx], a1 = xc[(long)(i + 4) * ldx], a2 = xc[(long)(i + 8) * ldx],
+                  a3 = xc[(long)(i + 12) * ldx];
+      s0 += a0; s1 += a1; s2 += a2; s3 += a3;
+    }
+    if (i < r1) s0 += xc[(long)i * ldx];
+    if (i + 4 < r1) s1 += xc[(long)(i + 4) * ldx];
+    if (i + 8 < r1) s2 += xc[(long)(i + 8) * ldx];
+  }
+  const float s = (s0 + s1) + (s2 + s3);
   red[g][c] = s;
   __syncthreads();
   if (g == 0 && col < N) part[(long)blockIdx.y * N + col] = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
@@ -833,9 +848,9 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
 int colsum_f32(hipStream_t st, const float* X, long ldx, int M, int N, float alpha, float beta, float* out,
                GemmWs ws) {
   if (N <= 0) return 0;
-  // row slices of >= 256 rows, at most kColParts; the fixed slice grid keeps the sum order
+  // row slices of >= 64 rows, at most kColParts; the fixed slice grid keeps the sum order
   // independent of the workspace size once the two-stage form is taken
-  const int parts = std::min(kColParts, (M + 255) / 256);
+  const int parts = colsum_parts(M);
   if (ws.p && parts > 1 && ws.n >= (size_t)kColParts * N) {
     hipLaunchKernelGGL(colsum_part_kernel, dim3((N + 63) / 64, parts), dim3(256), 0, st, X, ldx, M, N, ws.p);
     hipLaunchKernelGGL(colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, st, ws.p, parts, N, alpha, beta,
@@ -851,7 +866,7 @@ int colsum_scatter_f32(hipStream_t st, const float* X, long ldx, int M, int N, f
                        int nouts, GemmWs ws) {
   S2S_REQUIRE(nouts >= 0 && nouts <= kMaxColsumOuts, "colsum_scatter: too many output ranges");
   if (N <= 0 || nouts == 0) return 0;
-  const int parts = std::min(kColParts, (M + 255) / 256);
+  const int parts = colsum_parts(M);
   if (!(ws.p && parts > 1 && ws.n >= (size_t)kColParts * N)) {  // colsum_f32's one-stage form per destination
     for (int e = 0; e < nouts; ++e)
       for (int q = 0; q < outs[e].ndst; ++q)
