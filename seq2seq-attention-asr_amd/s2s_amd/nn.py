@@ -448,32 +448,39 @@ class Attention(Module):
 
     _PADDED = {"V": 0, "Ws": 0, "bs": 0, "we": 1, "hybU": 0}  # parameter -> score-channel axis
 
+    def _pad_bound(self):
+        return self._pad is not None and all(
+            self.own[n].data_ptr() == t.data_ptr() and self.own_grad[n].data_ptr() == self._pad[1][n].data_ptr()
+            for n, t in self._pad[0].items())
+
     def _sync_pad(self, grads_zero=False):
-        """Refresh the zero-padded score-channel copies the kernels read (scoreDepth % 16 != 0)."""
-        if self._scp == self.scoreDepth:
+        """The kernels read score channels zero-padded to a multiple of 16 (scoreDepth % 16 != 0).  The padded tensors
+        are the parameters' and gradients' own storage -- own[n] / own_grad[n] are narrow views of them, rebound here
+        whenever a parameter's storage was replaced (cuda(), a checkpoint load) -- so a step copies nothing (it used to
+        copy five parameters in and add five gradients back: ~20 launches a step).  The padded rows stay zero: a padded
+        channel has we_j = 0, so the kernels' gradients there are 0 too.  (grads_zero: kept for the call sites.)"""
+        if self._scp == self.scoreDepth or self._pad_bound():
             return
         Sc = self.scoreDepth
-        if self._pad is None or self._pad[0]["V"].device != self.own["V"].device:
-            mk = {}
-            for n, ax in self._PADDED.items():
-                if n in self.own:
-                    shp = list(self.own[n].shape)
-                    shp[ax] = self._scp
-                    mk[n] = torch.zeros(shp, dtype=torch.float32, device=self.own[n].device)
-            self._pad = (mk, {n: torch.zeros_like(t) for n, t in mk.items()})
+        mk, gk = {}, {}
         with torch.no_grad():
-            for n, t in self._pad[0].items():
-                t.narrow(self._PADDED[n], 0, Sc).copy_(self.own[n])
-            if grads_zero:
-                for t in self._pad[1].values():
-                    t.zero_()
+            for n, ax in self._PADDED.items():
+                if n not in self.own:
+                    continue
+                shp = list(self.own[n].shape)
+                shp[ax] = self._scp
+                dev = self.own[n].device
+                p = torch.zeros(shp, dtype=torch.float32, device=dev)
+                g = torch.zeros(shp, dtype=torch.float32, device=dev)
+                p.narrow(ax, 0, Sc).copy_(self.own[n])
+                g.narrow(ax, 0, Sc).copy_(self.own_grad[n])
+                self.own[n].data = p.narrow(ax, 0, Sc)
+                self.own_grad[n].data = g.narrow(ax, 0, Sc)
+                mk[n], gk[n] = p, g
+        self._pad = (mk, gk)
 
     def _unpad_grads(self):
-        if self._scp == self.scoreDepth:
-            return
-        with torch.no_grad():
-            for n, t in self._pad[1].items():
-                self.own_grad[n].add_(t.narrow(self._PADDED[n], 0, self.scoreDepth))
+        pass  # (the kernels accumulate into the gradients' padded storage directly, _sync_pad)
 
     def _tensors(self, grads=False, kernel=False):
         o = self.own_grad if grads else self.own
