@@ -105,6 +105,9 @@ struct s2s_ctx {
   hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
   unsigned long long* seed_dev = nullptr;  // dropout seed word read by this context's replayed graphs
   hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
+  // s2s_ctx_set_wgrad_overlap: the module-level backward calls fork their parameter gradients onto `side` (wev)
+  int wgrad_overlap = 0;
+  hipEvent_t wev = nullptr;
   // captured model steps, one per GraphKey (least recently used evicted past graph_cap): a caller
   // alternating shapes / buffers (a data loader's double buffers, length buckets) replays instead of
   // re-capturing every step
@@ -122,6 +125,17 @@ struct s2s_ctx {
 };
 
 namespace {
+
+// the stream a module-level backward issues its parameter gradients on: `st`, or the context's side stream forked
+// from `st` here when the caller set s2s_ctx_set_wgrad_overlap (joined by s2s_ctx_join_wgrad)
+int wgrad_stream(s2s_ctx* ctx, hipStream_t st, hipStream_t* out) {
+  *out = st;
+  if (!ctx->wgrad_overlap || !ctx->side || !ctx->wev || ctx->side == st) return 0;
+  S2S_CHECK_HIP(hipEventRecord(ctx->wev, st));
+  S2S_CHECK_HIP(hipStreamWaitEvent(ctx->side, ctx->wev, 0));
+  *out = ctx->side;
+  return 0;
+}
 
 // every compute entry point starts here: the device, the context's GEMM precision for this call, and the
 // context's failure status -- a persistent launch of an earlier call that timed out left wrong results, so
@@ -699,6 +713,7 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
       (void)hipStreamDestroy(c->side);
       c->side = nullptr;
     }
+  if (c->side && hipEventCreateWithFlags(&c->wev, hipEventDisableTiming) != hipSuccess) c->wev = nullptr;
   *out = c;
   return 0;
 }
@@ -715,6 +730,7 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
     if (e) (void)hipEventDestroy(e);
   for (auto& e : ctx->bev)
     if (e) (void)hipEventDestroy(e);
+  if (ctx->wev) (void)hipEventDestroy(ctx->wev);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->status_host) (void)hipHostFree(ctx->status_host);
   delete ctx;
@@ -725,6 +741,24 @@ int s2s_ctx_set_flags(s2s_ctx* ctx, int flags) {
   ctx->flags = flags;
   return 0;
 }
+
+int s2s_ctx_set_wgrad_overlap(s2s_ctx* ctx, int on) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  S2S_REQUIRE(!on || (ctx->side && ctx->wev), "ctx: no side stream for the parameter gradients");
+  ctx->wgrad_overlap = on ? 1 : 0;
+  return 0;
+}
+
+int s2s_ctx_join_wgrad(s2s_ctx* ctx, s2s_stream_t stream) {
+  S2S_REQUIRE(ctx != nullptr, "null context");
+  if (!ctx->side || !ctx->wev || static_cast<hipStream_t>(stream) == ctx->side) return 0;
+  S2S_CHECK_HIP(hipSetDevice(ctx->device));
+  S2S_CHECK_HIP(hipEventRecord(ctx->wev, ctx->side));
+  S2S_CHECK_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(stream), ctx->wev, 0));
+  return 0;
+}
+
+s2s_stream_t s2s_ctx_side_stream(s2s_ctx* ctx) { return ctx ? static_cast<s2s_stream_t>(ctx->side) : nullptr; }
 
 int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear) {
   S2S_REQUIRE(ctx != nullptr && status != nullptr, "null argument");
@@ -866,6 +900,10 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
       S2S_REQUIRE(dW[d * lstm_nparams(io.peep) + p], "lstm: null dW");
   }
   gr.lddy = lddy; gr.dx = dx; gr.lddx = lddx; gr.dx_accumulate = dx_accumulate; gr.dW = dW; gr.scale = scale;
+  if (ctx->wgrad_overlap) {  // the parameter gradients beside the caller's next launches, forked once dA is final
+    gr.wst = ctx->side;
+    gr.wev = ctx->wev;
+  }
   io.status = ctx->status_dev;
   return lstm_layer_bwd(static_cast<hipStream_t>(stream), io, gr, scratch, scratch_bytes);
 }
@@ -931,8 +969,12 @@ int s2s_attn_bwd(s2s_ctx* ctx, s2s_stream_t stream, const s2s_attn_dims* d, cons
     S2S_REQUIRE((pp[i] != nullptr && gp[i] != nullptr) || attn_param_optional(d, i), "attn: null parameter/grad");
   }
   const AttnDims ad = to_attn(d);
-  S2S_TRY(attn_bwd(static_cast<hipStream_t>(stream), ad, h, labels, ap, saved, dlogp, dh, dh_accumulate, ag, scale,
-                   scratch, scratch_bytes));
+  const hipStream_t st = static_cast<hipStream_t>(stream);
+  S2S_TRY(attn_bwd_core(st, ad, h, labels, ap, saved, dlogp, dh, dh_accumulate, scratch, scratch_bytes));
+  // accGradParameters beside the caller's next launches (s2s_ctx_set_wgrad_overlap): it reads only saved and scratch
+  hipStream_t wst;
+  S2S_TRY(wgrad_stream(ctx, st, &wst));
+  S2S_TRY(attn_bwd_wgrad(wst, ad, h, labels, ap, saved, ag, scale, scratch));
   return harvest_attn(ctx, stream, ad, const_cast<void*>(saved), scratch, 1);
 }
 
@@ -1033,7 +1075,7 @@ int s2s_tconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int 
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(x && W && dy && scratch, "TemporalConvolution: null argument");
   return tconv_bwd(static_cast<hipStream_t>(stream), B, L, Din, Dout, kW, relu, x, W, y, dy, dx, dx_accumulate, dW, db,
-                   scale, scratch, scratch_bytes);
+                   scale, scratch, scratch_bytes, ctx->wgrad_overlap ? ctx->side : nullptr, ctx->wev);
 }
 int s2s_tmaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const float* x, float* y,
                      int* idx) {

@@ -9,7 +9,7 @@ int tconv_fwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
               const float* b, float* y);
 int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W,
               const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db, float scale,
-              void* scratch, size_t scratch_bytes);
+              void* scratch, size_t scratch_bytes, hipStream_t wst = nullptr, hipEvent_t wev = nullptr);
 int tmaxpool_fwd(hipStream_t st, int B, int L, int D, int kW, int dW, const float* x, float* y, int* idx);
 int tmaxpool_bwd(hipStream_t st, int B, int L, int D, int kW, int dW, const int* idx, const float* dy, float* dx);
 size_t sconv_scratch_bytes(int B, int Cin, int H, int W, int Cout, int kH, int kW);

@@ -363,7 +363,7 @@ int tconv_fwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
 
 int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu, const float* x, const float* W,
               const float* y, const float* dy, float* dx, int dx_accumulate, float* dW, float* db, float scale,
-              void* scratch, size_t scratch_bytes) {
+              void* scratch, size_t scratch_bytes, hipStream_t wst, hipEvent_t wev) {
   S2S_REQUIRE(L >= kW && B > 0, "TemporalConvolution: bad sizes");
   S2S_REQUIRE(!relu || y, "TemporalConvolution: relu backward needs the forward output");
   S2S_REQUIRE(scratch_bytes >= tconv_scratch_bytes(B, L, Din, Dout, kW), "TemporalConvolution: scratch too small");
@@ -375,11 +375,19 @@ int tconv_bwd(hipStream_t st, int B, int L, int Din, int Dout, int kW, int relu,
                      dyp);
   S2S_CHECK_HIP(hipGetLastError());
   const long rows = (long)B * L - kW + 1;  // every window start of the flattened batch
+  // the parameter gradients on wst when the caller forks them (they read dyp and x; dx's GEMM below needs no
+  // split-K workspace)
+  hipStream_t pst = st;
+  if ((db || dW) && wst && wst != st && wev) {
+    S2S_CHECK_HIP(hipEventRecord(wev, st));
+    S2S_CHECK_HIP(hipStreamWaitEvent(wst, wev, 0));
+    pst = wst;
+  }
   // gradBias += scale * sum_t dY_t ; gradWeight += scale * dY^T [x_t | ... | x_{t+kW-1}]
-  if (db) S2S_TRY(colsum_f32(st, dyp, Dout, B * L, Dout, scale, 1.f, db, ws_of(scratch)));
+  if (db) S2S_TRY(colsum_f32(pst, dyp, Dout, B * L, Dout, scale, 1.f, db, ws_of(scratch)));
   if (dW) {
     WgradPrecision wp;  // weight gradient: fp32 under S2S_PREC_BF16_GEMM
-    S2S_TRY(big_gemm(st, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
+    S2S_TRY(big_gemm(pst, true, false, Dout, kW * Din, (int)rows, scale, dyp, Dout, x, Din, 1.f, dW, (long)kW * Din,
                      nullptr, 0, ws_of(scratch)));
   }
   if (dx) {

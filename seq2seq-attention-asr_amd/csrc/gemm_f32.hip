@@ -14,7 +14,7 @@
 // contiguous ([r][32 + 4]); MFMA step ks of a K-tile pairs k = ks (lanes 0-31) with
 // k = 16 + ks (lanes 32-63), so each lane's operands for the whole tile are 16 contiguous
 // floats = 4 ds_read_b128 per fragment (row stride 36 floats: conflict-free per 16-lane group).
-// Global reads are float4 whenever rows are 16-B aligned: k-contiguous operands go to LDS with
+// Global reads are float4 (any row length): k-contiguous operands go to LDS with
 // ds_write_b128, row-contiguous ones (A of TN, B of NN) are transposed by ds_write_b32 with
 // lanes running along k (conflict-free).
 // Batched problems are flattened into one 1-D grid; logical blocks are dealt XCD-contiguously
@@ -34,6 +34,9 @@ namespace s2s {
 namespace {
 
 constexpr int BK = 32, LDK = BK + 4;
+// the operand loaders' float4: rows of any length (a TemporalConvolution window over 123-float frames, the GRU weight
+// gradients' [h | x] rows) load as global_load_dwordx4 from 4-byte-aligned addresses (unaligned access mode)
+typedef float floatx4u __attribute__((ext_vector_type(4), aligned(4)));
 
 // Out-of-range lanes of the guarded operand loaders read this zero instead of branching around the
 // load: a conditional value (cond ? x : 0) let the compiler sink each load into an exec-masked block
@@ -46,7 +49,6 @@ struct GemmTile {
   float* part;  // split-K partial slabs (splits x M x N) or nullptr
   int tiles_n, tiles_m, splits, kslice;
   int base;  // first logical block of this problem
-  int vecA, vecB;
 };
 struct GemmLaunch {
   GemmTile q[kMaxGemmBatch];
@@ -54,7 +56,7 @@ struct GemmLaunch {
 };
 
 // k-contiguous operand (element (r, k) at X[r * ld + k]): f -> row f / 8, k quad f % 8.
-// FAST: interior tile, aligned rows -> unguarded float4.  Otherwise branch-free scalar loads
+// FAST: interior tile -> unguarded float4.  Otherwise branch-free scalar loads
 // from clamped addresses, zeroed outside the problem (no divergent waits between loads).
 template <int R, bool FAST>
 __device__ __forceinline__ void load_kc(floatx4 (&v)[R / 32], const float* X, long ld, int r0, int rmax, int k0,
@@ -64,7 +66,7 @@ __device__ __forceinline__ void load_kc(floatx4 (&v)[R / 32], const float* X, lo
     const int f = threadIdx.x + 256 * j;
     const int gr = r0 + (f >> 3), k = k0 + 4 * (f & 7);
     if (FAST) {
-      v[j] = *reinterpret_cast<const floatx4*>(X + (long)gr * ld + k);
+      v[j] = *reinterpret_cast<const floatx4u*>(X + (long)gr * ld + k);
     } else {
       const float* row = X + (long)min(gr, rmax - 1) * ld;
       float e[4];
@@ -93,7 +95,7 @@ __device__ __forceinline__ void load_rc(floatx4 (&v)[R / 32], const float* X, lo
     const int f = threadIdx.x + 256 * j;
     const int k = k0 + (f & 31), r = r0 + 4 * (f >> 5);
     if (FAST) {
-      v[j] = *reinterpret_cast<const floatx4*>(X + (long)k * ld + r);
+      v[j] = *reinterpret_cast<const floatx4u*>(X + (long)k * ld + r);
     } else {
       const float* row = X + (long)min(k, kend - 1) * ld;
       float e[4];
@@ -118,6 +120,21 @@ __device__ __forceinline__ void store_rc(float* Xs, const floatx4 (&v)[R / 32]) 
   }
 }
 
+// One K-tile's operand loads.  FAST (an interior tile): unguarded float4 loads while the K-tile is whole, the
+// guarded form for a K tail (K = 3 x 123 for the first convolution: every tile used to take the guarded form).
+template <bool TA, bool TB, int BM, int BN, bool FAST>
+__device__ __forceinline__ void load_tile(floatx4 (&ra)[BM / 32], floatx4 (&rb)[BN / 32], const float* A,
+                                          const float* Bm, long lda, long ldb, int m0, int n0, int M, int N, int k0,
+                                          int kend) {
+  if (FAST && k0 + BK <= kend) {
+    if (TA) load_rc<BM, true>(ra, A, lda, m0, M, k0, kend); else load_kc<BM, true>(ra, A, lda, m0, M, k0, kend);
+    if (TB) load_kc<BN, true>(rb, Bm, ldb, n0, N, k0, kend); else load_rc<BN, true>(rb, Bm, ldb, n0, N, k0, kend);
+  } else {
+    if (TA) load_rc<BM, false>(ra, A, lda, m0, M, k0, kend); else load_kc<BM, false>(ra, A, lda, m0, M, k0, kend);
+    if (TB) load_kc<BN, false>(rb, Bm, ldb, n0, N, k0, kend); else load_rc<BN, false>(rb, Bm, ldb, n0, N, k0, kend);
+  }
+}
+
 // Double-buffered K loop: the next K-tile's global loads are in flight (registers) while the
 // current tile's 16 x FM x FN MFMAs run; one barrier per K-tile.  No lambdas here: captured
 // prefetch arrays were left in scratch memory by the compiler.
@@ -128,8 +145,7 @@ __device__ __forceinline__ void gemm_mainloop(floatx16 (&acc)[BM / 64][BN / 64],
                                               int N, int kbeg, int kend, int nk, int wy, int wx, int li, int lk) {
   constexpr int WM = BM / 2, WN = BN / 2, FM = WM / 32, FN = WN / 32;
   floatx4 ra[BM / 32], rb[BN / 32];
-  if (TA) load_rc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend); else load_kc<BM, FAST>(ra, A, lda, m0, M, kbeg, kend);
-  if (TB) load_kc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend); else load_rc<BN, FAST>(rb, Bm, ldb, n0, N, kbeg, kend);
+  load_tile<TA, TB, BM, BN, FAST>(ra, rb, A, Bm, lda, ldb, m0, n0, M, N, kbeg, kend);
   if (TA) store_rc<BM>(As[0], ra); else store_kc<BM>(As[0], ra);
   if (TB) store_kc<BN>(Bs[0], rb); else store_rc<BN>(Bs[0], rb);
   __syncthreads();
@@ -137,9 +153,7 @@ __device__ __forceinline__ void gemm_mainloop(floatx16 (&acc)[BM / 64][BN / 64],
     const int buf = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      const int k0 = kbeg + (kt + 1) * BK;
-      if (TA) load_rc<BM, FAST>(ra, A, lda, m0, M, k0, kend); else load_kc<BM, FAST>(ra, A, lda, m0, M, k0, kend);
-      if (TB) load_kc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend); else load_rc<BN, FAST>(rb, Bm, ldb, n0, N, k0, kend);
+      load_tile<TA, TB, BM, BN, FAST>(ra, rb, A, Bm, lda, ldb, m0, n0, M, N, kbeg + (kt + 1) * BK, kend);
     }
     floatx4 a[FM][4], b[FN][4];
 #pragma unroll
@@ -196,7 +210,7 @@ __device__ __forceinline__ void hload_kc(floatx4 (&v)[R / 16], const float* X, l
     const int f = threadIdx.x + 256 * j;
     const int gr = r0 + (f >> 4), k = k0 + 4 * (f & 15);
     if (FAST) {
-      v[j] = *reinterpret_cast<const floatx4*>(X + (long)gr * ld + k);
+      v[j] = *reinterpret_cast<const floatx4u*>(X + (long)gr * ld + k);
     } else {
       const float* row = X + (long)min(gr, rmax - 1) * ld;
       float e[4];
@@ -229,7 +243,7 @@ __device__ __forceinline__ void hload_rc(floatx4 (&v)[R / 16], const float* X, l
     for (int c = 0; c < 4; ++c) {
       const int k = kb + c;
       if (FAST) {
-        v[4 * j + c] = *reinterpret_cast<const floatx4*>(X + (long)k * ld + r);
+        v[4 * j + c] = *reinterpret_cast<const floatx4u*>(X + (long)k * ld + r);
       } else {
         const float* row = X + (long)min(k, kend - 1) * ld;
         float e[4];
@@ -328,7 +342,7 @@ __global__ __launch_bounds__(256, 2) void gemm_bf16_kernel(GemmLaunch Lc) {
   const int nk = (kend - kbeg + HBK - 1) / HBK;
   if (nk > 0) {
     const int Mr = max(M, q.p.Mread), Nr = max(N, q.p.Nread);
-    const bool fast = q.vecA && q.vecB && m0 + BM <= Mr && n0 + BN <= Nr && (kend - kbeg) % HBK == 0;
+    const bool fast = m0 + BM <= Mr && n0 + BN <= Nr && (kend - kbeg) % HBK == 0;
     if (fast)
       gemm_mainloop_bf16<TA, TB, BM, BN, true>(acc, As, Bs, q.p.A, q.p.B, q.p.lda, q.p.ldb, m0, n0, M, N, kbeg, kend,
                                                nk, wy, wx, lane);
@@ -402,7 +416,7 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
 
   if (nk > 0) {
     const int Mr = max(M, q.p.Mread), Nr = max(N, q.p.Nread);
-    const bool fast = q.vecA && q.vecB && m0 + BM <= Mr && n0 + BN <= Nr && (kend - kbeg) % BK == 0;
+    const bool fast = m0 + BM <= Mr && n0 + BN <= Nr;
     if (fast)
       gemm_mainloop<TA, TB, BM, BN, true>(acc, As, Bs, A, Bm, lda, ldb, m0, n0, M, N, kbeg, kend, nk, wy, wx, li, lk);
     else
@@ -439,26 +453,34 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmLaunch Lc) {
 }
 
 // C = alpha * (sum of the split slabs in slice order) (+ bias) + beta * C; blockIdx.y = problem.
-// Four consecutive columns per thread (float4) when rows allow it.
-template <int S>
-__device__ __forceinline__ floatx4 slab_sum(const float* part, long mn, long e) {
-  floatx4 v[S];
+// Every slab's load of a group of up to 8 in flight before its adds (a runtime-bounded loop issued them one by one
+// behind each add: the 40-slice weight gradient of the 123-feature convolution took 42 us); the sum is the running
+// sum in slice order either way.
+template <typename V>
+__device__ __forceinline__ V slab_ld(const float* p) { return *reinterpret_cast<const V*>(p); }
+template <int S, typename V>
+__device__ __forceinline__ void slab_add(V& sum, const float* part, long mn, long e) {
+  V v[S];
 #pragma unroll
-  for (int s = 0; s < S; ++s) v[s] = *reinterpret_cast<const floatx4*>(part + s * mn + e);
-  floatx4 sum = {0.f, 0.f, 0.f, 0.f};
+  for (int s = 0; s < S; ++s) v[s] = slab_ld<V>(part + s * mn + e);
 #pragma unroll
   for (int s = 0; s < S; ++s) sum += v[s];
-  return sum;
 }
-
-template <int S>
-__device__ __forceinline__ float slab_sum1(const float* part, long mn, long e) {
-  float v[S];
-#pragma unroll
-  for (int s = 0; s < S; ++s) v[s] = part[s * mn + e];
-  float sum = 0.f;
-#pragma unroll
-  for (int s = 0; s < S; ++s) sum += v[s];
+template <typename V>
+__device__ __forceinline__ V slab_sum(const float* part, long mn, long e, int splits) {
+  V sum = V(0.f);
+  int s = 0;
+  for (; s + 8 <= splits; s += 8) slab_add<8>(sum, part + s * mn, mn, e);
+  switch (splits - s) {  // (the planner's fill rule picks any count, e.g. 7 for the encoder weight gradients)
+    case 1: slab_add<1>(sum, part + s * mn, mn, e); break;
+    case 2: slab_add<2>(sum, part + s * mn, mn, e); break;
+    case 3: slab_add<3>(sum, part + s * mn, mn, e); break;
+    case 4: slab_add<4>(sum, part + s * mn, mn, e); break;
+    case 5: slab_add<5>(sum, part + s * mn, mn, e); break;
+    case 6: slab_add<6>(sum, part + s * mn, mn, e); break;
+    case 7: slab_add<7>(sum, part + s * mn, mn, e); break;
+    default: break;
+  }
   return sum;
 }
 
@@ -469,33 +491,19 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
   const long mn = (long)M * N;
   const float alpha = q.p.alpha, beta = q.p.beta;
   const float* __restrict__ bias = q.p.bias;
-  // float4 slab reads whenever the slab rows allow them; float4 C writes only when C's rows do too (the GRU weight
-  // gradients' [H | D] rows of 379 floats take the scalar stores, their h-part slabs the float4 reads)
-  const bool vec = (N % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.part) & 15) == 0);
-  const bool vc = (q.p.ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.p.C) & 15) == 0);
+  // float4 slab reads whenever the slabs allow them (mn % 4 = 0); float4 C writes only when C's rows do too -- else
+  // the four outputs one by one (the GRU weight gradients' [H | D] rows of 379 floats, the convolution's 369)
+  const bool vec = (mn % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.part) & 15) == 0);
+  const bool vc = (N % 4 == 0) && (q.p.ldc % 4 == 0) && ((reinterpret_cast<uintptr_t>(q.p.C) & 15) == 0);
   if (vec) {
     for (long e = 4 * (blockIdx.x * 256L + threadIdx.x); e < mn; e += 4L * gridDim.x * 256) {
-      floatx4 sum = {0.f, 0.f, 0.f, 0.f};
-      // every slab's load in flight before the first add (a runtime-bounded loop issued them one by
-      // one behind each add); the sum order is the slice order either way
-      switch (q.splits) {  // (the planner's fill rule picks any count, e.g. 7 for the encoder weight gradients)
-        case 2: sum = slab_sum<2>(q.part, mn, e); break;
-        case 3: sum = slab_sum<3>(q.part, mn, e); break;
-        case 4: sum = slab_sum<4>(q.part, mn, e); break;
-        case 5: sum = slab_sum<5>(q.part, mn, e); break;
-        case 6: sum = slab_sum<6>(q.part, mn, e); break;
-        case 7: sum = slab_sum<7>(q.part, mn, e); break;
-        case 8: sum = slab_sum<8>(q.part, mn, e); break;
-        default:
-          for (int s = 0; s < q.splits; ++s) sum += *reinterpret_cast<const floatx4*>(q.part + s * mn + e);
-      }
-      const int row = (int)(e / N), col = (int)(e % N);
-      floatx4 v = alpha * sum;
-      if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
-      if (q.p.rbias) v += q.p.rbias[row];
-      float* cp = q.p.C + (long)row * q.p.ldc + col;
+      const floatx4 sum = slab_sum<floatx4>(q.part, mn, e, q.splits);
       if (vc) {
-        floatx4* c = reinterpret_cast<floatx4*>(cp);
+        const int row = (int)(e / N), col = (int)(e % N);
+        floatx4 v = alpha * sum;
+        if (bias) v += floatx4{bias[col], bias[col + 1], bias[col + 2], bias[col + 3]};
+        if (q.p.rbias) v += q.p.rbias[row];
+        floatx4* c = reinterpret_cast<floatx4*>(q.p.C + (long)row * q.p.ldc + col);
         if (beta != 0.f) v += beta * *c;
         if (q.p.relu)
 #pragma unroll
@@ -504,30 +512,21 @@ __global__ __launch_bounds__(256) void splitk_reduce_kernel(GemmLaunch Lc) {
       } else {
 #pragma unroll
         for (int e2 = 0; e2 < 4; ++e2) {
-          float w = v[e2];
-          if (beta != 0.f) w += beta * cp[e2];
+          const int row = (int)((e + e2) / N), col = (int)((e + e2) % N);
+          float w = alpha * sum[e2];
+          if (bias) w += bias[col];
+          if (q.p.rbias) w += q.p.rbias[row];
+          float* c = q.p.C + (long)row * q.p.ldc + col;
+          if (beta != 0.f) w += beta * *c;
           if (q.p.relu) w = fmaxf(w, 0.f);
-          cp[e2] = w;
+          *c = w;
         }
       }
     }
     return;
   }
   for (long e = blockIdx.x * 256L + threadIdx.x; e < mn; e += (long)gridDim.x * 256) {
-    // every slab's load in flight before the first add, as in the float4 form (the scalar form serves outputs
-    // whose rows are not 16-byte multiples, e.g. the GRU weight gradients' [H | D] rows); slice order either way
-    float sum = 0.f;
-    switch (q.splits) {
-      case 2: sum = slab_sum1<2>(q.part, mn, e); break;
-      case 3: sum = slab_sum1<3>(q.part, mn, e); break;
-      case 4: sum = slab_sum1<4>(q.part, mn, e); break;
-      case 5: sum = slab_sum1<5>(q.part, mn, e); break;
-      case 6: sum = slab_sum1<6>(q.part, mn, e); break;
-      case 7: sum = slab_sum1<7>(q.part, mn, e); break;
-      case 8: sum = slab_sum1<8>(q.part, mn, e); break;
-      default:
-        for (int s = 0; s < q.splits; ++s) sum += q.part[s * mn + e];
-    }
+    const float sum = slab_sum<float>(q.part, mn, e, q.splits);
     const int row = (int)(e / N), col = (int)(e % N);
     float v = alpha * sum;
     if (bias) v += bias[col];
@@ -816,8 +815,6 @@ int gemm_f32(hipStream_t st, const GemmProblem* probs, int nprob, bool transA, b
     }
     t.base = base;
     base += t.tiles_m * t.tiles_n * t.splits;
-    t.vecA = (t.p.lda % 4 == 0 && (reinterpret_cast<uintptr_t>(t.p.A) & 15) == 0) ? 1 : 0;
-    t.vecB = (t.p.ldb % 4 == 0 && (reinterpret_cast<uintptr_t>(t.p.B) & 15) == 0) ? 1 : 0;
     flops += 2.0 * t.p.M * t.p.N * t.p.K;
     bytes += 4.0 * ((double)t.p.M * t.p.K + (double)t.p.K * t.p.N + (double)t.p.M * t.p.N * (t.p.beta != 0.f ? 2 : 1));
   }

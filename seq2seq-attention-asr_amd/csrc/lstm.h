@@ -36,6 +36,10 @@ struct LstmLayerGrad {
   int dx_accumulate;
   float* const* dW;  // same layout as W; accumulated dW += scale * ...
   float scale;
+  // optional: the weight / bias gradients go to stream wst, forked from st by event wev once dA is final (the
+  // caller joins wst later; dx then runs its GEMM without the split-K workspace the gradients use)
+  hipStream_t wst = nullptr;
+  hipEvent_t wev = nullptr;
 };
 
 // Persistent recurrences (lstm_persist.hip): the whole sweep of a layer's directions in one launch (no peepholes)

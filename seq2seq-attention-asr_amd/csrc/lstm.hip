@@ -479,10 +479,20 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
     }
     S2S_CHECK_HIP(hipGetLastError());
   }
+  // weight gradients beside the caller's next launches when it forks them (LstmLayerGrad::wst); dx and the
+  // parameter gradients split the split-K workspace in halves either way (the same plans, bitwise the same sums)
+  const GemmWs wsx{c.ws.p, c.ws.n / 2}, wsw{c.ws.p + c.ws.n / 2, c.ws.n - c.ws.n / 2};
+  hipStream_t pst = st;
+  if (gr.wst && gr.wst != st && gr.wev) {
+    S2S_CHECK_HIP(hipEventRecord(gr.wev, st));
+    S2S_CHECK_HIP(hipStreamWaitEvent(gr.wst, gr.wev, 0));
+    pst = gr.wst;
+  }
   // dx (+)= dA (B*L, 4*nd*H) . Wx4 (4*nd*H, D): both directions summed (RNN.lua:196)
   if (gr.dx)
     S2S_TRY(gemm1(st, false, false, B * L, D, 4 * nd * H, 1.f, c.dA, ldA, c.Wx4, D, gr.dx_accumulate ? 1.f : 0.f,
-                  gr.dx, gr.lddx, nullptr, c.ws));
+                  gr.dx, gr.lddx, nullptr, wsx));
+  st = pst;
   // weight gradients over all B*L rows (Linear:accGradParameters per step, summed)
   for (int d = 0; d < nd; ++d) {
     float* const* G = gr.dW + d * np;
@@ -503,7 +513,7 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
     }
     {
     WgradPrecision wp;  // weight gradients: fp32 under S2S_PREC_BF16_GEMM
-    S2S_TRY(gemm_f32(st, pr, n, true, false, c.ws));
+    S2S_TRY(gemm_f32(st, pr, n, true, false, wsw));
   }
   }
   // every bias gradient (bqx = bqh = sum_rows da_q, + bqc with peepholes) of both directions: the column sums of
@@ -518,7 +528,7 @@ int lstm_layer_bwd(hipStream_t st, const LstmLayerIO& io, const LstmLayerGrad& g
       if (io.peep && q != 2) o.dst[o.ndst++] = G[kLstmParams + 2 * (q == 3 ? 2 : q) + 1];
     }
   }
-  S2S_TRY(colsum_scatter_f32(st, c.dA, ldA, B * L, (int)ldA, gr.scale, outs, no, c.ws));
+  S2S_TRY(colsum_scatter_f32(st, c.dA, ldA, B * L, (int)ldA, gr.scale, outs, no, wsw));
   return 0;
 }
 

@@ -21,6 +21,9 @@ void s2s_ctx_destroy(s2s_ctx* ctx);
 int s2s_ctx_set_flags(s2s_ctx* ctx, int flags);
 int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
 int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
+int s2s_ctx_set_wgrad_overlap(s2s_ctx* ctx, int on);
+int s2s_ctx_join_wgrad(s2s_ctx* ctx, s2s_stream_t stream);
+s2s_stream_t s2s_ctx_side_stream(s2s_ctx* ctx);
 int s2s_ctx_graph_stats(s2s_ctx* ctx, long* captures, long* replays, int* cached);
 int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear);
 size_t s2s_gru_saved_bytes(int B, int L, int H);

@@ -53,6 +53,9 @@ SIGNATURES = [
     ("s2s_ctx_set_flags", c_int, [c_void_p, c_int]),
     ("s2s_ctx_set_graph_cache", c_int, [c_void_p, c_int]),
     ("s2s_ctx_set_precision", c_int, [c_void_p, c_int]),
+    ("s2s_ctx_set_wgrad_overlap", c_int, [c_void_p, c_int]),
+    ("s2s_ctx_join_wgrad", c_int, [c_void_p, c_void_p]),
+    ("s2s_ctx_side_stream", c_void_p, [c_void_p]),
     ("s2s_ctx_graph_stats", c_int, [c_void_p, P(c_long), P(c_long), P(c_int)]),
     ("s2s_ctx_status", c_int, [c_void_p, c_void_p, P(c_int), c_int]),
     ("s2s_gru_saved_bytes", c_size_t, [c_int, c_int, c_int]),

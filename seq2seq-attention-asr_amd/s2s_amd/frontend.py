@@ -9,13 +9,14 @@ A convolution built with relu=True is the reference's `conv -> nn.ReLU()` pair f
 the GEMM epilogue; its backward masks by the conv output).  Gradients accumulate; backward returns
 gradInput (None for a module built with need_gradInput=False: the encoder input needs none).
 """
+import contextlib
 import math
 
 import torch
 
 from ._lib import check, lib
 from .nn import (LSTM, BiRNN, Module, S2SArgumentError, _bytes, _require_cuda_f32, _uniform, dptr, get_context,
-                 stream_ptr)
+                 overlap_param_grads, side_uses, stream_ptr)
 
 
 def _ctx(t):
@@ -65,6 +66,7 @@ class TemporalConvolution(Module):
         check(lib.s2s_tconv_bwd(_ctx(x), stream_ptr(), B, L, self.inputFrameSize, self.outputFrameSize, self.kW,
                                 int(self.relu), dptr(x), dptr(self.weight), dptr(y), dptr(go), dptr(dx), 0,
                                 dptr(self.gradWeight), dptr(self.gradBias), float(scale), dptr(scr), scr.numel()))
+        side_uses(x.device, scr)
         self.gradInput = None if dx is None else (dx if input.dim() == 3 else dx[0])
         return self.gradInput
 
@@ -470,6 +472,7 @@ class VGGAttentionModel(GraphStep, Module):
         # "bf16": every hoisted GEMM of the step (the VGG convolutions and 1x1 layers, Vh, decoder folds, the
         # decoder_mlp Linears, all weight gradients) on bf16 MFMA with fp32 accumulation (BASELINE config 5)
         self.precision = precision
+        self.overlap = True  # parameter gradients on the side stream during the backward (overlap_param_grads)
         g = generator
         S, A, M, O = stateDepth, outputFrameSize, mlpDepth, outputDepth
         self.encoder = VGGEncoder(inputFrameSize, outputFrameSize, hidden, generator=g)
@@ -493,8 +496,10 @@ class VGGAttentionModel(GraphStep, Module):
             lab = labels.to(torch.int32).contiguous()
             logp = self.decoder.forward([h, lab])
             nll, dlogp = nll_seed(logp, lab, normalizeNLL)
-            dh = self.decoder.backward([h, lab], dlogp, scale)[0]
-            self.encoder.backward(x, dh, scale)
+            # each module's parameter gradients beside the next module's backward (bitwise the serial sums)
+            with overlap_param_grads(x.device.index) if self.overlap else contextlib.nullcontext():
+                dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+                self.encoder.backward(x, dh, scale)
         return nll, logp
 
 class ConvBiLSTMAttentionModel(GraphStep, Module):
@@ -510,6 +515,7 @@ class ConvBiLSTMAttentionModel(GraphStep, Module):
         from .nn import Attention
         super().__init__()
         self.precision = precision  # "fp32" | "bf16" | "bf16-all" (s2s_amd.precision) for the step's GEMMs
+        self.overlap = True  # parameter gradients on the side stream during the backward (overlap_param_grads)
         g = generator
         S, A, O = stateDepth, 2 * outputFrameSize, numPhonemes
         self.encoder = ConvBiLSTMEncoder(inputFrameSize, hiddenFrameSize, outputFrameSize, 3, generator=g)
@@ -533,6 +539,8 @@ class ConvBiLSTMAttentionModel(GraphStep, Module):
             lab = labels.to(torch.int32).contiguous()
             logp = self.decoder.forward([h, lab])
             nll, dlogp = nll_seed(logp, lab, normalizeNLL)
-            dh = self.decoder.backward([h, lab], dlogp, scale)[0]
-            self.encoder.backward(x, dh, scale)
+            # each module's parameter gradients beside the next module's backward (bitwise the serial sums)
+            with overlap_param_grads(x.device.index) if self.overlap else contextlib.nullcontext():
+                dh = self.decoder.backward([h, lab], dlogp, scale)[0]
+                self.encoder.backward(x, dh, scale)
         return nll, logp

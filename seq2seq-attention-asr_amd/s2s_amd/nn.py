@@ -90,6 +90,61 @@ def precision(p: str, device=None):
         ctx.set_precision(prev)
 
 
+@contextlib.contextmanager
+def overlap_param_grads(device=None):
+    """with s2s_amd.overlap_param_grads(): inside the block the module backward calls (Attention, the LSTM layers,
+    TemporalConvolution) issue their parameter gradients on the context's side stream, beside the next module's
+    backward (s2s_ctx_set_wgrad_overlap: Torch's accGradParameters made asynchronous); leaving the block joins them
+    into the current stream, so from then on the gradients are final in its order.  The same kernels in the same
+    order per gradient: the results are bitwise those of the serial calls."""
+    ctx = get_context(device)
+    if getattr(ctx, "_wgrad_side", None) is not None:  # nested: the outer block joins
+        yield ctx
+        return
+    side = getattr(ctx, "_side_stream", None)
+    if side is None:
+        side = ctx._side_stream = torch.cuda.ExternalStream(lib.s2s_ctx_side_stream(ctx.handle),
+                                                            device=torch.device("cuda", ctx.device))
+    check(lib.s2s_ctx_set_wgrad_overlap(ctx.handle, 1))
+    ctx._wgrad_side = side
+    try:
+        yield ctx
+    finally:
+        ctx._wgrad_side = None
+        check(lib.s2s_ctx_set_wgrad_overlap(ctx.handle, 0))
+        check(lib.s2s_ctx_join_wgrad(ctx.handle, stream_ptr()))
+
+
+@contextlib.contextmanager
+def serial_param_grads(device=None):
+    """Inside overlap_param_grads: the block's parameter gradients stay on the call's stream (small products the
+    side stream would only queue behind a persistent launch that holds every CU)."""
+    ctx = _CTX.get(device)
+    side = getattr(ctx, "_wgrad_side", None) if ctx is not None else None
+    if side is None:
+        yield
+        return
+    check(lib.s2s_ctx_set_wgrad_overlap(ctx.handle, 0))
+    ctx._wgrad_side = None
+    try:
+        yield
+    finally:
+        check(lib.s2s_ctx_set_wgrad_overlap(ctx.handle, 1))
+        ctx._wgrad_side = side
+
+
+def side_uses(device, *tensors):
+    """Inside overlap_param_grads: the side stream reads these buffers after the call returns -- keep the caching
+    allocator from handing them out again before it has (record_stream; under graph capture the free is deferred to
+    the capture's end)."""
+    ctx = _CTX.get(device.index)
+    side = getattr(ctx, "_wgrad_side", None) if ctx is not None else None
+    if side is not None:
+        for t in tensors:
+            if t is not None:
+                t.record_stream(side)
+
+
 def get_context(device=None) -> Context:
     dev = torch.cuda.current_device() if device is None else int(device)
     if dev not in _CTX:
@@ -327,6 +382,7 @@ class _GruSeq(Module):
             check(lib.s2s_lstm_bwd(ctx, stream_ptr(), nd, B, L, D, H, self.peep, rev, dptr(input), D, W, sv, dy, nd * H,
                                    dptr(dx), D, 0, dW, float(scale), self._lengths_ptr(B, L, dev), dptr(scr),
                                    scr.numel()))
+            side_uses(dev, scr)
         else:
             scr = _bytes(lib.s2s_gru_scratch_bytes(nd, B, L, D, H), dev)
             check(lib.s2s_gru_bwd(ctx, stream_ptr(), nd, B, L, D, H, rev, dptr(input), D, W, sv, dy, nd * H, dptr(dx),
@@ -627,12 +683,14 @@ class Attention(Module):
         dh = torch.empty((d.B, d.L, self.annotationDepth), device=dev, dtype=torch.float32)
         scr = _bytes(lib.s2s_attn_scratch_bytes(ctypes.byref(d)), dev)
         if self.external_mlp:  # d[s_t; c_t] from the decoder_mlp backward replaces dlogp
-            go = self.decoder_mlp.backward(self._mlp_in, go.reshape(d.B * d.T, -1), scale)
+            with serial_param_grads(dev.index):  # (ahead of the decoder launch, which holds every CU)
+                go = self.decoder_mlp.backward(self._mlp_in, go.reshape(d.B * d.T, -1), scale)
             go = go.reshape(d.B, d.T, -1).contiguous()
         self._sync_pad(grads_zero=True)
         check(lib.s2s_attn_bwd(get_context(dev.index).handle, stream_ptr(), ctypes.byref(d), dptr(h),
                                dptr(self._labels), self._ptrs(False), dptr(self._saved), dptr(go), dptr(dh), 0,
                                self._ptrs(True), float(scale), dptr(scr), scr.numel()))
+        side_uses(dev, scr)
         self._unpad_grads()
         self.gradInput = [dh if h.dim() == 3 else dh[0], None]
         return self.gradInput

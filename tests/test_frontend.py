@@ -703,6 +703,49 @@ def test_conv_bilstm_graph_step_equals_eager(fe):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("model,graph", [("convlstm", False), ("convlstm", True), ("vgg", True)])
+def test_param_grads_beside_the_backward_are_bitwise_serial(fe, model, graph):
+    """overlap_param_grads (s2s_ctx_set_wgrad_overlap: the Attention, LSTM and TemporalConvolution parameter
+    gradients on the context's side stream beside the next module's backward -- the model steps' default) gives
+    bitwise the serial step's outputs and gradients, eager and captured: timit.lua's conv + BiLSTM model at its
+    widths (the XCD-local LSTM decoder) and a small VGG model (GRU decoder, external MLP)."""
+    import s2s_amd
+    rng = np.random.default_rng(21)
+    if model == "convlstm":
+        B, T, O = 8, 12, 62
+        shape = (B, 160, 123)
+
+        def make(ov):
+            m = s2s_amd.ConvBiLSTMAttentionModel(generator=torch.Generator().manual_seed(5), penalty=0.1).cuda()
+            m.overlap = ov
+            return m
+    else:
+        B, T, O = 2, 6, 29
+        shape = (B, 3, 40, 40)
+
+        def make(ov):
+            m = s2s_amd.VGGAttentionModel(40, outputFrameSize=128, hidden=128, scoreDepth=128, stateDepth=64,
+                                          outputDepth=O, mlpDepth=8, generator=torch.Generator().manual_seed(3)).cuda()
+            m.overlap = ov
+            return m
+    ser, ovl = make(False), make(True)
+    x = cu(rng.standard_normal(shape))
+    labels = cu(rng.integers(0, O, (B, T)), torch.int32)
+    for it in range(3):
+        ser.zeroGradParameters()
+        nll_s, logp_s = ser.step(x, labels)
+        if graph:
+            nll_o, logp_o = ovl.graph_step(x, labels)
+        else:
+            ovl.zeroGradParameters()
+            nll_o, logp_o = ovl.step(x, labels)
+        torch.cuda.synchronize()
+        assert torch.equal(logp_s, logp_o) and torch.equal(nll_s, nll_o), it
+        for i, (a, b) in enumerate(zip(ser.parameters()[1], ovl.parameters()[1])):
+            assert torch.equal(a, b), (it, i)
+
+
+@pytest.mark.gpu
 def test_lstm_fwd_bwd_one_graph_replays(fe):
     """BiRNN(LSTM) forward + backward captured in ONE graph equals the eager pair on every replay (the backward's
     carries used to be cleared by hipMemsetAsync, whose graph node left the previous replay's values in place from
