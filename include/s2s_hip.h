@@ -71,11 +71,11 @@ int s2s_ctx_set_graph_cache(s2s_ctx* ctx, int capacity);
 int s2s_ctx_set_precision(s2s_ctx* ctx, int precision);
 /* Parameter gradients beside the input gradients (Torch's backward = updateGradInput + accGradParameters, the
  * second made asynchronous).  With on = 1, s2s_attn_bwd, s2s_lstm_bwd and s2s_tconv_bwd issue their weight / bias
- * gradient work on the context's side stream, forked from the call's stream once its inputs are final, and order
- * only the input gradient on the call's stream, so the next module's backward overlaps them.  Until
- * s2s_ctx_join_wgrad(ctx, stream) the parameter gradients are not final on `stream`, and the buffers those calls
- * read (x, y, dy, saved, scratch) must stay untouched.  Captured inside a hipGraph the fork / join become graph
- * edges.  s2s_ctx_side_stream: that stream (for a caller's allocator to record buffer uses on it). */
+ * gradient work on a stream of the context's own (s2s_ctx_side_stream; not the model step's side stream), forked
+ * from the call's stream once its inputs are final, and order only the input gradient on the call's stream, so the
+ * next module's backward overlaps them.  Until s2s_ctx_join_wgrad(ctx, stream) the parameter gradients are not final
+ * on `stream`, and the buffers those calls read (x, y, dy, saved, scratch) must stay untouched (a caller's allocator
+ * records their uses on s2s_ctx_side_stream).  Captured inside a hipGraph the fork / join become graph edges. */
 int s2s_ctx_set_wgrad_overlap(s2s_ctx* ctx, int on);
 int s2s_ctx_join_wgrad(s2s_ctx* ctx, s2s_stream_t stream);
 s2s_stream_t s2s_ctx_side_stream(s2s_ctx* ctx);

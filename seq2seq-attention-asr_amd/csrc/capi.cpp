@@ -105,8 +105,10 @@ struct s2s_ctx {
   hipEvent_t ev[32] = {};  // model step: 0 / 1+l wgrad forks, 13-15 prologue + join, 16-20 decoder (attn_*)
   unsigned long long* seed_dev = nullptr;  // dropout seed word read by this context's replayed graphs
   hipEvent_t bev[kMaxBuckets] = {};  // S2S_BUCKET_EVENTS: gradient bucket i is final
-  // s2s_ctx_set_wgrad_overlap: the module-level backward calls fork their parameter gradients onto `side` (wev)
+  // s2s_ctx_set_wgrad_overlap: the module-level backward calls fork their parameter gradients onto a stream of their
+  // own (wside, event wev) -- not `side`, which the captured model steps' graphs hold
   int wgrad_overlap = 0;
+  hipStream_t wside = nullptr;
   hipEvent_t wev = nullptr;
   // captured model steps, one per GraphKey (least recently used evicted past graph_cap): a caller
   // alternating shapes / buffers (a data loader's double buffers, length buckets) replays instead of
@@ -130,10 +132,10 @@ namespace {
 // from `st` here when the caller set s2s_ctx_set_wgrad_overlap (joined by s2s_ctx_join_wgrad)
 int wgrad_stream(s2s_ctx* ctx, hipStream_t st, hipStream_t* out) {
   *out = st;
-  if (!ctx->wgrad_overlap || !ctx->side || !ctx->wev || ctx->side == st) return 0;
+  if (!ctx->wgrad_overlap || !ctx->wside || !ctx->wev || ctx->wside == st) return 0;
   S2S_CHECK_HIP(hipEventRecord(ctx->wev, st));
-  S2S_CHECK_HIP(hipStreamWaitEvent(ctx->side, ctx->wev, 0));
-  *out = ctx->side;
+  S2S_CHECK_HIP(hipStreamWaitEvent(ctx->wside, ctx->wev, 0));
+  *out = ctx->wside;
   return 0;
 }
 
@@ -713,7 +715,8 @@ int s2s_ctx_create(int device, s2s_ctx** out) {
       (void)hipStreamDestroy(c->side);
       c->side = nullptr;
     }
-  if (c->side && hipEventCreateWithFlags(&c->wev, hipEventDisableTiming) != hipSuccess) c->wev = nullptr;
+  if (hipStreamCreateWithFlags(&c->wside, hipStreamNonBlocking) != hipSuccess) c->wside = nullptr;
+  if (c->wside && hipEventCreateWithFlags(&c->wev, hipEventDisableTiming) != hipSuccess) c->wev = nullptr;
   *out = c;
   return 0;
 }
@@ -731,6 +734,7 @@ void s2s_ctx_destroy(s2s_ctx* ctx) {
   for (auto& e : ctx->bev)
     if (e) (void)hipEventDestroy(e);
   if (ctx->wev) (void)hipEventDestroy(ctx->wev);
+  if (ctx->wside) (void)hipStreamDestroy(ctx->wside);
   if (ctx->side) (void)hipStreamDestroy(ctx->side);
   if (ctx->status_host) (void)hipHostFree(ctx->status_host);
   delete ctx;
@@ -744,27 +748,28 @@ int s2s_ctx_set_flags(s2s_ctx* ctx, int flags) {
 
 int s2s_ctx_set_wgrad_overlap(s2s_ctx* ctx, int on) {
   S2S_REQUIRE(ctx != nullptr, "null context");
-  S2S_REQUIRE(!on || (ctx->side && ctx->wev), "ctx: no side stream for the parameter gradients");
+  S2S_REQUIRE(!on || (ctx->wside && ctx->wev), "ctx: no stream for the parameter gradients");
   ctx->wgrad_overlap = on ? 1 : 0;
   return 0;
 }
 
 int s2s_ctx_join_wgrad(s2s_ctx* ctx, s2s_stream_t stream) {
   S2S_REQUIRE(ctx != nullptr, "null context");
-  if (!ctx->side || !ctx->wev || static_cast<hipStream_t>(stream) == ctx->side) return 0;
+  if (!ctx->wside || !ctx->wev || static_cast<hipStream_t>(stream) == ctx->wside) return 0;
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
-  S2S_CHECK_HIP(hipEventRecord(ctx->wev, ctx->side));
+  S2S_CHECK_HIP(hipEventRecord(ctx->wev, ctx->wside));
   S2S_CHECK_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(stream), ctx->wev, 0));
   return 0;
 }
 
-s2s_stream_t s2s_ctx_side_stream(s2s_ctx* ctx) { return ctx ? static_cast<s2s_stream_t>(ctx->side) : nullptr; }
+s2s_stream_t s2s_ctx_side_stream(s2s_ctx* ctx) { return ctx ? static_cast<s2s_stream_t>(ctx->wside) : nullptr; }
 
 int s2s_ctx_status(s2s_ctx* ctx, s2s_stream_t stream, int* status, int clear) {
   S2S_REQUIRE(ctx != nullptr && status != nullptr, "null argument");
   S2S_CHECK_HIP(hipSetDevice(ctx->device));
   S2S_CHECK_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
   if (ctx->side) S2S_CHECK_HIP(hipStreamSynchronize(ctx->side));
+  if (ctx->wside) S2S_CHECK_HIP(hipStreamSynchronize(ctx->wside));
   *status = 0;
   if (!ctx->status_host) return 0;
   *status = (__atomic_load_n(ctx->status_host, __ATOMIC_ACQUIRE) ? S2S_STATUS_HANDOFF_TIMEOUT : 0) |
@@ -901,7 +906,7 @@ int s2s_lstm_bwd(s2s_ctx* ctx, s2s_stream_t stream, int ndir, int B, int L, int 
   }
   gr.lddy = lddy; gr.dx = dx; gr.lddx = lddx; gr.dx_accumulate = dx_accumulate; gr.dW = dW; gr.scale = scale;
   if (ctx->wgrad_overlap) {  // the parameter gradients beside the caller's next launches, forked once dA is final
-    gr.wst = ctx->side;
+    gr.wst = ctx->wside;
     gr.wev = ctx->wev;
   }
   io.status = ctx->status_dev;
@@ -1075,7 +1080,7 @@ int s2s_tconv_bwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int Din, int 
   S2S_TRY(set_device(ctx));
   S2S_REQUIRE(x && W && dy && scratch, "TemporalConvolution: null argument");
   return tconv_bwd(static_cast<hipStream_t>(stream), B, L, Din, Dout, kW, relu, x, W, y, dy, dx, dx_accumulate, dW, db,
-                   scale, scratch, scratch_bytes, ctx->wgrad_overlap ? ctx->side : nullptr, ctx->wev);
+                   scale, scratch, scratch_bytes, ctx->wgrad_overlap ? ctx->wside : nullptr, ctx->wev);
 }
 int s2s_tmaxpool_fwd(s2s_ctx* ctx, s2s_stream_t stream, int B, int L, int D, int kW, int dW, const float* x, float* y,
                      int* idx) {
