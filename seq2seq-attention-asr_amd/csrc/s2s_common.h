@@ -75,6 +75,27 @@ __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_f32<0x140>(v);  // row_mirror
   return (lane_f32(v, 0) + lane_f32(v, 16)) + (lane_f32(v, 32) + lane_f32(v, 48));
 }
+// Four wave sums at once, transposed: lane l ends with the wave's sum of value f(l) = 2 (l & 1) + ((l >> 1) & 1) of
+// {v0, v1, v2, v3} (lanes 0, 2, 1, 3 hold sums 0, 1, 2, 3).  Halving exchanges with the partners l ^ 1 and l ^ 2
+// (quad_perm: each lane keeps one value of the pair it shares with its partner), row rotations by 4 and 8 (the row's
+// four lanes of one value), then the rows by v_permlane32_swap / v_permlane16_swap: 7 lane moves and no v_readlane for
+// the four sums, instead of 4 x (4 DPP moves + 4 v_readlane + their wait states).  A fixed association (deterministic),
+// not wave_sum_dpp's.  Every lane of the wave must be active.
+__device__ __forceinline__ float wave_sum4_t(float v0, float v1, float v2, float v3, int lane) {
+  const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0;
+  const float qa = (b0 ? v2 : v0) + dpp_f32<0xB1>(b0 ? v0 : v2);  // quad_perm [1,0,3,2]: partner l ^ 1
+  const float qb = (b0 ? v3 : v1) + dpp_f32<0xB1>(b0 ? v1 : v3);
+  float r = (b1 ? qb : qa) + dpp_f32<0x4E>(b1 ? qa : qb);  // quad_perm [2,3,0,1]: partner l ^ 2
+  r += dpp_f32<0x124>(r);  // row_ror:4
+  r += dpp_f32<0x128>(r);  // row_ror:8
+  const unsigned u = __float_as_uint(r);
+  const auto p = __builtin_amdgcn_permlane32_swap(u, u, false, false);  // lanes l and l ^ 32
+  const unsigned y = __float_as_uint(__uint_as_float(p[0]) + __uint_as_float(p[1]));
+  const auto q = __builtin_amdgcn_permlane16_swap(y, y, false, false);  // rows 2k and 2k + 1
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+// the value index wave_sum4_t leaves in lane l (l < 4: 0 -> 0, 1 -> 2, 2 -> 1, 3 -> 3)
+__device__ __forceinline__ int wave_sum4_slot(int lane) { return 2 * (lane & 1) + ((lane >> 1) & 1); }
 __device__ __forceinline__ float wave_max_dpp(float v) {
   v = fmaxf(v, dpp_f32<0xB1>(v));
   v = fmaxf(v, dpp_f32<0x4E>(v));
