@@ -532,13 +532,25 @@ def main():
     # the optimizer (timit.lua:292-347: clip, adadelta, column-norm constraint) is outside t_step
     #  and reported on its own: device step on the flat buffers, HBM-bound
     opt = s2s_amd.optim.Adadelta(model, rho=0.95, eps=1e-8, colnormconstr=True)
+    flag = torch.zeros(1, dtype=torch.float32, device="cuda")
+
+    def opt_step():
+        # data parallel: a failed persistent launch on ANY rank skips the update on every rank (the failure flag's MAX
+        # over the ranks, s2s_amd.dist.reduce_failure_flag), or the replicas diverge; one rank: the plain update
+        if world > 1:
+            opt.failure_flag(stream, out=flag)
+            s2s_dist.reduce_failure_flag(flag)
+            opt.step(stream, skip_flag=flag)
+        else:
+            opt.step(stream)
+
     with torch.cuda.stream(stream):
         for _ in range(3):
-            opt.step(stream)
+            opt_step()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record(stream)
         for _ in range(20):
-            opt.step(stream)
+            opt_step()
         e1.record(stream)
     torch.cuda.synchronize()
     opt_us = 1000.0 * e0.elapsed_time(e1) / 20
@@ -566,7 +578,8 @@ def main():
                    "flop_per_step_per_gpu": flop_step},
         "step_tflops_per_gpu": round(flop_step / (ms / 1000.0) / 1e12, 3),
         "optimizer": {"us_per_step": round(opt_us, 2), "what": "adadelta (rho .95, eps 1e-8) + global-norm clip + "
-                      "column-norm constraint on the flat buffers (s2s_optim_adadelta_step), not in ms_per_step"},
+                      "column-norm constraint on the flat buffers (s2s_optim_adadelta_step), not in ms_per_step; N > 1: "
+                      "behind the failure flag's MAX over the ranks (skipped on every rank if any rank's step failed)"},
     }
     if ragged:
         out["config"]["ragged"] = {

@@ -138,3 +138,35 @@ def test_failure_flag_reduced_across_ranks(tmp_path, failing):
     mp.start_processes(_flag_worker, args=(world, _free_port(), out, failing), nprocs=world, start_method="spawn")
     got = [float(np.load(f"{out}.{r}.npy")[0]) for r in range(world)]
     assert got == [0.0 if failing < 0 else 1.0] * world
+
+
+def _flag_worker_rccl(rank, world, port, out_path, failing):
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(rank)
+    dist.init_process_group("nccl", rank=rank, world_size=world)
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "s2s_dist", os.path.join(ROOT, "seq2seq-attention-asr_amd", "s2s_amd", "dist.py"))
+    sd = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(sd)
+    flag = torch.tensor([1.0 if rank == failing else 0.0], dtype=torch.float32, device="cuda")
+    sd.reduce_failure_flag(flag)  # on the current stream (RCCL), the flag stays on the device
+    np.save(f"{out_path}.{rank}.npy", flag.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("failing", [-1, 1])
+def test_failure_flag_reduced_across_ranks_rccl(tmp_path, failing):
+    """the same MAX all-reduce of the failure flag on device tensors over RCCL (world size 2, one GPU per
+    rank) -- the form bench.py's data-parallel optimizer leg uses.  Needs two GPUs (skipped on one)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs")
+    world = 2
+    out = str(tmp_path / "g")
+    mp.start_processes(_flag_worker_rccl, args=(world, _free_port(), out, failing), nprocs=world, start_method="spawn")
+    got = [float(np.load(f"{out}.{r}.npy")[0]) for r in range(world)]
+    assert got == [0.0 if failing < 0 else 1.0] * world
