@@ -1828,7 +1828,8 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
       if (lds > 64 * 1024)
         S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(dec_xcd_dvh),
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-      hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 63) / 64, k.NCH, B), dim3(256), lds, side ? side : st, k, x);
+      hipLaunchKernelGGL(dec_xcd_dvh, dim3((Sc + 63) / 64, (L + kDvhF - 1) / kDvhF, B), dim3(256), lds, side ? side : st, k,
+                         x);
       S2S_CHECK_HIP(hipGetLastError());
     }
     if (side) S2S_CHECK_HIP(hipEventRecord(ev[4], side));
