@@ -358,10 +358,14 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
         from s2s_amd import profile as s2s_profile
         _lib.check(_lib.lib.s2s_prof_enable(1))
         s2s_profile.collect()
+        # the profiled steps keep the parameter gradients on the call's stream (model.overlap off): the timed steps run
+        # them beside the next module's backward, where a launch's events would also time the kernels beside it
+        overlap, model.overlap = model.overlap, False
         for _ in range(2):  # eager: the library brackets each launch with events
             model.zeroGradParameters()
             model.step(x, labels)
         torch.cuda.synchronize()
+        model.overlap = overlap
         agg = s2s_profile.collect()
         _lib.lib.s2s_prof_enable(0)
         bf16 = args.precision != "fp32"
@@ -386,7 +390,8 @@ def run_vgg(args, pmc, rank, world, torch, dist, s2s_amd, s2s_dist):
             r = dict(max(rows, key=lambda e: e["us_per_step"]))
             t, detail = traffic_of(pmc, SYMBOL_VGG.get(r["kernel"], r["kernel"]))
             r.update({"traffic": round(t) if t is not None else None, "traffic_detail": detail,
-                      "selection": "the MFMA-bound family with the largest live time (the others in mfma_families)",
+                      "selection": "the MFMA-bound family with the largest live time (the others in mfma_families); "
+                                   "live times from eager profiled steps with the parameter gradients serial",
                       "mfma_counters": mfma_of(pmc, SYMBOL_VGG.get(r["kernel"], r["kernel"]), r["avg_launch_us"])})
             out["roofline"] = r
             out["mfma_families"] = rows
