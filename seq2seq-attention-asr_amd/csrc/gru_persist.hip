@@ -1220,6 +1220,10 @@ __global__ __launch_bounds__(kBwdThreads) void gru_bwd_persist(PArgs a) {
       __syncthreads();  // [A]
       if (abort_lds) return;
       put(p + 2, ra);   // loaded during the previous step
+      // (progress for the row prefetchers, which only warm caches, and for the in-launch weight-gradient workers
+      // (s2s_debug_bptt_wgrad, off): those treat step p - 2 as final on the recurrence waves' dA stores having been
+      // acknowledged by the sweeps' vmcnt waits since -- not a release at agent scope; it would need one (vmcnt(0) in
+      // every storing wave before [A], an agent-scope release here) before that path could be turned on)
       if (prog && lane == 0) __hip_atomic_store(prog, (unsigned)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       // The next rows' loads are issued behind [A] and drained before [B] (the vmcnt(0) below): they are then in
       // this CU's memory queue only during the da_r hand-off -- whose consumers run the da_z half of their product
