@@ -1451,6 +1451,7 @@ static PersistLaunch pick_dec_bwd(int var, const AttnDims& d, int grid) {
 
 static int launch_persist(const PersistLaunch& p, int grid, hipStream_t st, AttnK& k) {
   void* args[] = {&k};
+  S2S_TRY(check_resident(p.fn, grid, 256, p.lds, "decoder persistent launch"));
   S2S_CHECK_HIP(hipLaunchKernel(p.fn, dim3(grid), dim3(256), args, p.lds, st));
   return 0;
 }
@@ -1475,6 +1476,7 @@ static int launch_xcd_t(bool fwd, int res, hipStream_t st, AttnK& k, XArgs& x) {
   const void* fn = x.U <= 4 && g_dec_r4.load() ? xcd_kernel<S, A, SC, true>(fwd, res) : xcd_kernel<S, A, SC, false>(fwd, res);
   if (lds) S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {&k, &x};
+  S2S_TRY(check_resident(fn, chain_grid(x.nchains, kXWG), 256, lds, fwd ? "dec_xcd_fwd" : "dec_xcd_bwd"));
   S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
   return 0;
 }
@@ -1489,6 +1491,7 @@ static int launch_xcd_lstm(bool fwd, hipStream_t st, AttnK& k, XArgs& x, XLArgs&
                        : (const void*)dec_xcd_lstm_bwd<kXlSP, 256, 160, kXlSCP, 5, true>;
   if (lds) S2S_CHECK_HIP(hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
   void* args[] = {&k, &x, &y};
+  S2S_TRY(check_resident(fn, chain_grid(x.nchains, kXWG), 256, lds, fwd ? "dec_xcd_lstm_fwd" : "dec_xcd_lstm_bwd"));
   S2S_CHECK_HIP(hipLaunchKernel(fn, dim3(chain_grid(x.nchains, kXWG)), dim3(256), args, lds, st));
   return 0;
 }

@@ -28,6 +28,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
 
 namespace s2s {
 
@@ -657,6 +661,35 @@ __global__ void axpby_kernel(const float* __restrict__ src, float* __restrict__ 
 #include "conv_bf16.inc"
 
 }  // namespace
+
+int check_resident(const void* fn, long grid, int block, size_t lds, const char* what) {
+  struct Key {
+    const void* fn;
+    int block, dev;
+    size_t lds;
+  };
+  static std::mutex mu;
+  static std::vector<std::pair<Key, long>> cache;  // key -> resident workgroups on the device
+  int dev = 0;
+  S2S_CHECK_HIP(hipGetDevice(&dev));
+  long cap = -1;
+  {
+    std::lock_guard<std::mutex> g(mu);
+    for (const auto& e : cache)
+      if (e.first.fn == fn && e.first.block == block && e.first.dev == dev && e.first.lds == lds) cap = e.second;
+  }
+  if (cap < 0) {
+    int per_cu = 0, cus = 0;
+    S2S_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, block, lds));
+    S2S_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    cap = (long)per_cu * cus;
+    std::lock_guard<std::mutex> g(mu);
+    cache.push_back({Key{fn, block, dev, lds}, cap});
+  }
+  S2S_REQUIRE(grid <= cap, std::string(what) + ": persistent grid of " + std::to_string(grid) +
+                               " workgroups exceeds the " + std::to_string(cap) + " the device holds at once");
+  return 0;
+}
 
 static thread_local int g_gemm_prec = kGemmF32;
 static thread_local GemmDeferred* g_gemm_defer = nullptr;

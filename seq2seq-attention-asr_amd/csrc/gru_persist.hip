@@ -1464,10 +1464,14 @@ int launch_nc(hipStream_t st, const PArgs& a, bool excl_req, bool fwd) {
   if (fwd) {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_fwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
+    S2S_TRY(check_resident(reinterpret_cast<const void*>(gru_fwd_persist<NC>), grid.x, kFwdThreads, shm,
+                           "gru_fwd_persist"));
     hipLaunchKernelGGL(gru_fwd_persist<NC>, grid, dim3(kFwdThreads), shm, st, a);
   } else {
     if (excl) S2S_CHECK_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(gru_bwd_persist<NC>),
                                                 hipFuncAttributeMaxDynamicSharedMemorySize, kExclLds));
+    S2S_TRY(check_resident(reinterpret_cast<const void*>(gru_bwd_persist<NC>), grid.x, kBwdThreads, shm,
+                           "gru_bwd_persist"));
     hipLaunchKernelGGL(gru_bwd_persist<NC>, grid, dim3(kBwdThreads), shm, st, a);
   }
   S2S_CHECK_HIP(hipGetLastError());

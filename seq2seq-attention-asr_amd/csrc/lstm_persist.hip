@@ -310,12 +310,16 @@ std::atomic<int> g_lstm_local{1};  // s2s_debug_lstm_local(0): tagged granules e
 
 template <int NC>
 int launch_fwd_nc(hipStream_t st, const LArgs& a) {
+  S2S_TRY(check_resident(reinterpret_cast<const void*>(lstm_fwd_persist<NC>), chain_grid(a.nchains, a.nmem), 256, 0,
+                         "lstm_fwd_persist"));
   hipLaunchKernelGGL(lstm_fwd_persist<NC>, dim3(chain_grid(a.nchains, a.nmem)), dim3(256), 0, st, a);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;
 }
 template <int NCB>
 int launch_bwd_nc(hipStream_t st, const LArgs& a) {
+  S2S_TRY(check_resident(reinterpret_cast<const void*>(lstm_bwd_persist<NCB>), chain_grid(a.nchains, a.nmem), 512, 0,
+                         "lstm_bwd_persist"));
   hipLaunchKernelGGL(lstm_bwd_persist<NCB>, dim3(chain_grid(a.nchains, a.nmem)), dim3(512), 0, st, a);
   S2S_CHECK_HIP(hipGetLastError());
   return 0;

@@ -142,6 +142,12 @@ struct WgradPrecision {
   }
   ~WgradPrecision() { set_gemm_precision(prev); }
 };
+// A persistent launch's workgroups hand data to each other, so all of them must be resident at once: checked before
+// the launch against the occupancy the runtime reports for the kernel, block size and LDS (cached per key) times the
+// device's CUs -- a shape or build past that fails loudly here instead of spinning until the hand-off timeout.  (The
+// runtime's answer can be one block per CU high at some SGPR counts, MI355X_MICROARCH.md; the grids here stay well
+// inside it: one or two workgroups per CU.)
+int check_resident(const void* fn, long grid, int block, size_t lds, const char* what);
 // A single-problem split-K GEMM issued while a GemmDeferReduce scope is live on this thread leaves its slabs
 // unreduced and describes them here (splits = 0: the GEMM wrote C itself); the consumer sums them in slice order
 // as splitk_reduce would (C = alpha * sum + bias; alpha = 1, beta = 0, no row bias, no ReLU only) -- the decoder
