@@ -67,6 +67,12 @@ template <int CTRL>
 __device__ __forceinline__ float dpp_f32(float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
 }
+// packed fp32 pair (v_pk_fma_f32 / v_pk_add_f32 / v_pk_mul_f32: two lanes' worth of fp32 per VALU instruction)
+typedef float floatx2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ floatx2 pk_fma(floatx2 a, floatx2 b, floatx2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ floatx2 rcp2(floatx2 a) {
+  return floatx2{__builtin_amdgcn_rcpf(a.x), __builtin_amdgcn_rcpf(a.y)};
+}
 __device__ __forceinline__ float lane_f32(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
 __device__ __forceinline__ float wave_sum_dpp(float v) {
   v += dpp_f32<0xB1>(v);   // quad_perm [1,0,3,2]
