@@ -41,6 +41,10 @@ struct AttnDims {
   // the XCD-local decoder's sync regions were prepared by attn_fwd_prologue (the model step runs it, and
   // joins it, before the decoder): attn_fwd / attn_bwd_core then launch no sync_prep of their own
   int syncs_in_prologue = 0;
+  // the loss seed dlogp (B*T, O) is final when attn_fwd runs (the model step's head writes it): the XCD-local
+  // forward's merged head launch then also runs the MLP head's backward (do, dm, the Maxout scatter into dU) and
+  // attn_bwd_core launches no dec_mlp_head_bwd (attn_head_bwd_fused); attn_bwd_core's dlogp must be this pointer
+  const float* dlogp_early = nullptr;
 };
 int set_device_u64(hipStream_t st, unsigned long long* p, unsigned long long v);
 constexpr int kMaxHybK = 8;  // largest hybrid filter served (the reference's fallback model uses 5)

@@ -795,14 +795,17 @@ __global__ void dec_init_fwd(AttnK k) {
   }
 }
 
-// MLP head (per row b*T+t, one wave each): maxout (first max wins), Linear(M,O), LogSoftMax.
+// MLP head (per row b*T+t, one wave each): maxout (first max wins), Linear(M,O), LogSoftMax; with k.dlogp set (the
+// seed is final before the forward, AttnDims::dlogp_early) also its backward, dec_mlp_head_bwd's per-row work with
+// the same sums: do = dlogp - exp(logp) sum(dlogp), dm = Wo^T do, dU = scatter(dm, argmax).  LDS: 4 M (+ 4 O) floats
 __device__ __forceinline__ void mlp_head_body(const AttnK& k, int rows, int blk) {
-  extern __shared__ float sm[];  // 4 * M
+  extern __shared__ float sm[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int r = blk * 4 + wave;
   const int M = k.M, Kw = k.K, O = k.O;
   float* mv = sm + wave * M;
-  if (r < rows) {
+  const bool live = r < rows;
+  if (live) {
     const float* u = k.U + (long)r * M * Kw;
     // U[r][c] from the MLP GEMM's slabs when it left them unreduced: splitk_reduce's expression (alpha = 1)
     auto uv = [&](int c) -> float {
@@ -825,24 +828,46 @@ __device__ __forceinline__ void mlp_head_body(const AttnK& k, int rows, int blk)
     }
   }
   __syncthreads();
-  if (r >= rows) return;
-  float mx = -INFINITY;
-  for (int n = lane; n < O; n += 64) {
-    float o = k.P.bo[n];
-    const float* w = k.P.Wo + (long)n * M;
-    for (int j = 0; j < M; ++j) o += w[j] * mv[j];
-    k.LOGP[(long)r * O + n] = o;
-    mx = fmaxf(mx, o);
+  if (live) {
+    float mx = -INFINITY;
+    for (int n = lane; n < O; n += 64) {
+      float o = k.P.bo[n];
+      const float* w = k.P.Wo + (long)n * M;
+      for (int j = 0; j < M; ++j) o += w[j] * mv[j];
+      k.LOGP[(long)r * O + n] = o;
+      mx = fmaxf(mx, o);
+    }
+    mx = wave_max(mx);
+    float se = 0.f;
+    for (int n = lane; n < O; n += 64) se += expf(k.LOGP[(long)r * O + n] - mx);
+    se = wave_sum(se);
+    const float lz = mx + logf(se);
+    for (int n = lane; n < O; n += 64) {
+      const float v = k.LOGP[(long)r * O + n] - lz;
+      k.LOGP[(long)r * O + n] = v;
+      if (k.logp) k.logp[(long)r * O + n] = v;
+    }
   }
-  mx = wave_max(mx);
-  float se = 0.f;
-  for (int n = lane; n < O; n += 64) se += expf(k.LOGP[(long)r * O + n] - mx);
-  se = wave_sum(se);
-  const float lz = mx + logf(se);
-  for (int n = lane; n < O; n += 64) {
-    const float v = k.LOGP[(long)r * O + n] - lz;
-    k.LOGP[(long)r * O + n] = v;
-    if (k.logp) k.logp[(long)r * O + n] = v;
+  if (!k.dlogp) return;
+  float* dov = sm + 4 * M + wave * O;
+  float sd = 0.f;
+  if (live)
+    for (int n = lane; n < O; n += 64) sd += k.dlogp[(long)r * O + n];
+  sd = wave_sum(sd);
+  if (live)
+    for (int n = lane; n < O; n += 64) {
+      const float v = k.dlogp[(long)r * O + n] - expf(k.LOGP[(long)r * O + n]) * sd;
+      dov[n] = v;
+      k.DO[(long)r * O + n] = v;
+    }
+  __syncthreads();
+  if (!live) return;
+  float* du = k.DU + (long)r * M * Kw;
+  for (int j = lane; j < M; j += 64) {
+    float dm = 0.f;
+    for (int n = 0; n < O; ++n) dm += k.P.Wo[(long)n * M + j] * dov[n];
+    const int am = k.AM[(long)r * M + j];
+    for (int i = 0; i < Kw; ++i) du[j * Kw + i] = i == am ? dm : 0.f;
   }
 }
 __global__ __launch_bounds__(256) void dec_mlp_head(AttnK k, int rows) { mlp_head_body(k, rows, blockIdx.x); }
@@ -1460,6 +1485,16 @@ static std::atomic<int> g_dec_allow_local{1};
 // s2s_debug_head_sums_slabs(0) (A/B): the decoder MLP GEMM's split-K reduce as its own launch in front of the MLP head
 static std::atomic<int> g_head_sums_slabs{1};
 static std::atomic<int> g_merge_alpha_head{1};  // s2s_debug_merge_alpha_head(0) (diagnostic): alpha / VBAR launched alone
+// attn_fwd's merged launch after the MLP GEMM: alpha / indicators, VBAR and the MLP head (the XCD-local path, no split
+// side stream, the in-library MLP)
+static bool merged_head(const AttnDims& d, const XPlan& xp, hipStream_t side) {
+  return xp.var && !side && !d.ext && g_merge_alpha_head;
+}
+// ... which also runs the head's backward when the seed is final before the forward (AttnDims::dlogp_early); the same
+// predicate in attn_bwd_core decides that dec_mlp_head_bwd is not launched there
+static bool attn_head_bwd_fused(const AttnDims& d) {
+  return d.dlogp_early && merged_head(d, dec_xcd_plan(d), nullptr);
+}
 
 // s2s_debug_dec_r4(0) (A/B): chains of <= 4 utterances keep the 16 x 16 x 4 skinny products
 static std::atomic<int> g_dec_r4{1};
@@ -1601,7 +1636,7 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
   const GemmWs gws = attn_gemm_ws(d, scratch);
   S2S_TRY(gemm1(st, false, true, B * L, d.Sc, d.A, 1.f, h, d.A, P.V, d.A, 0.f, k.Vh, d.Sc, nullptr, gws));
   const XPlan xp = dec_xcd_plan(d);
-  const bool merge_head = xp.var && !side && !d.ext && g_merge_alpha_head;  // dec_xcd_alpha_vbar_head
+  const bool merge_head = merged_head(d, xp, side);  // dec_xcd_alpha_vbar_head
   // s_0 = 0: the XCD-local path's prologue (dec_xcd_pack_ops) writes it
   if (!xp.var) hipLaunchKernelGGL(dec_init_fwd, dim3((B * S + 255) / 256), dim3(256), 0, st, k);
   const int pgrid = kDecWG * ((B + 15) / 16);
@@ -1702,9 +1737,12 @@ int attn_fwd(hipStream_t st, const AttnDims& d, const float* h, const int* label
       k.UPMN = dr.mn;
     }
   }
-  if (merge_head)
+  if (merge_head) {
+    const bool hb = attn_head_bwd_fused(d);
+    k.dlogp = hb ? d.dlogp_early : nullptr;
     hipLaunchKernelGGL(dec_xcd_alpha_vbar_head, dim3(T * B + ((d.Sc + 63) / 64) * B + (rows + 3) / 4), dim3(256),
-                       4 * d.M * sizeof(float), st, k, x, rows);
+                       4 * (d.M + (hb ? d.O : 0)) * sizeof(float), st, k, x, rows);
+  }
   else
     hipLaunchKernelGGL(dec_mlp_head, dim3((rows + 3) / 4), dim3(256), 4 * d.M * sizeof(float), st, k, rows);
   S2S_CHECK_HIP(hipGetLastError());
@@ -1789,9 +1827,13 @@ int attn_bwd_core(hipStream_t st, const AttnDims& d, const float* h, const int* 
   if (d.ext) {  // external decoder_mlp: dlogp holds d[s_t; c_t] (B*T, S+A)
     S2S_TRY(copy2d_f32(st, dlogp, S + A, k.DV, S + A, rows, S + A, false));
   } else {
-  // MLP backward for all rows (not on the recurrence)
-  hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
-  S2S_CHECK_HIP(hipGetLastError());
+  // MLP backward for all rows (not on the recurrence), unless the forward's head launch ran it
+  if (attn_head_bwd_fused(d)) {
+    S2S_REQUIRE(dlogp == d.dlogp_early, "attn: dlogp_early differs from the backward's dlogp");
+  } else {
+    hipLaunchKernelGGL(dec_mlp_head_bwd, dim3((rows + 3) / 4), dim3(256), 4 * O * sizeof(float), st, k, rows);
+    S2S_CHECK_HIP(hipGetLastError());
+  }
   // dV = dU Wm  ->  [ds_mlp | dc_mlp]
   S2S_TRY(gemm1(st, false, false, rows, S + A, Mk, 1.f, k.DU, Mk, P.Wm, S + A, 0.f, k.DV, S + A, nullptr, gws));
   }

@@ -370,6 +370,8 @@ int model_step_impl(hipStream_t st, hipStream_t side, hipEvent_t* ev, hipEvent_t
   AttnDims ad = model_attn(d);
   ad.dropout_seed_dev = seed_dev;
   ad.syncs_in_prologue = g_dec_sync_prologue;  // attn_fwd_prologue runs (and is joined) before the decoder
+  // the step head wrote the loss seed: the decoder forward's head launch runs the MLP head's backward too
+  if (head_seed) ad.dlogp_early = w.dlogp;
   AttnParams ap;
   AttnGrads ag;
   const float** pp = reinterpret_cast<const float**>(&ap);
