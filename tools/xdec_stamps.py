@@ -25,8 +25,23 @@ def report(name, st, nph, labels):
     m = lat[:, 1:].mean((0, 1))
     total = (ends[:, -1, nph - 1] - ends[:, 0, 0]).mean()
     print(f"{name}: {total:.1f} us over {T} steps = {total / T:.2f} us/step")
+    t0 = ends[:, 0, 0].min()
+    print("   per chain (start, end after the earliest loop start): " +
+          ", ".join(f"{a - t0:.0f}-{b - t0:.0f}" for a, b in zip(ends[:, 0, 0], ends[:, -1, nph - 1])))
     for lab, v in zip(labels, m):
         print(f"   {lab:24s} {v:7.2f} us")
+
+
+def prologue(name, st):
+    # slots 11-15 of the first processed step: entry (15), sentinel slots re-armed (13), chain census (12), chunk rows
+    # staged (11), loop start (14); times from the launch's first workgroup entry, latest workgroup per mark
+    p = st[:, :, 0, :]
+    if not (p[..., 15] > 0).all():
+        return
+    t0 = p[..., 15].min()
+    marks = [("entry", 15), ("re-armed", 13), ("census", 12), ("staged", 11), ("loop start", 14)]
+    print(f"{name} prologue (us after the first workgroup's entry, latest workgroup): " +
+          ", ".join(f"{lab} {(p[..., s].max() - t0) * 0.01:.1f}" for lab, s in marks))
 
 
 def main():
@@ -52,7 +67,9 @@ def main():
     nch = (B + U - 1) // U
     f = sf.cpu().numpy().reshape(8 * 32, T, 16)[: nch * 32].reshape(nch, 32, T, 16).astype(np.float64)
     b = sb.cpu().numpy().reshape(8 * 32, T, 16)[: nch * 32].reshape(nch, 32, T, 16)[:, :, ::-1].astype(np.float64)
+    prologue("decoder forward", f)
     report("decoder forward", f, 6, ["(loop)", "F1 ws,us", "F2 attention", "F3 combine", "F4 gx,z,r,q", "F5 hh,s"])
+    prologue("decoder backward", b)
     report("decoder backward", b, 7, ["(loop)", "G gate grads", "B2 dq,da_r", "B3 dc,us'", "B4 attention",
                                        "B45 dws", "B5 ds"])
 
