@@ -643,6 +643,34 @@ def test_mlp_head_summing_slabs_is_bitwise_the_reduce(s2s, B):
         assert torch.equal(a, b)
 
 
+@pytest.mark.parametrize("B", [32, 45])
+def test_mlp_head_backward_in_the_forward_head_launch_is_bitwise_separate(s2s, B):
+    """The model step writes the loss seed before the encoder, so the decoder forward's merged head launch also runs the
+    MLP head's backward row by row (AttnDims::dlogp_early; no dec_mlp_head_bwd launch between the decoder launches).
+    With the merged launch off (s2s_debug_merge_alpha_head(0): alpha / VBAR, the head and the head backward as separate
+    launches) the same per-row sums run in the same order: logp, nll and every gradient are bitwise equal."""
+    import ctypes
+    from s2s_amd import _lib
+    fn = _lib.lib.s2s_debug_merge_alpha_head
+    fn.argtypes = [ctypes.c_int]
+    cfg = s2s.ModelConfig()
+    model = s2s.ChorowskiBaseline(cfg, graph=False)
+    g = torch.Generator().manual_seed(17 + B)
+    x = torch.randn(B, 96, cfg.inputFrameSize, generator=g).cuda()
+    lab = torch.randint(0, cfg.outputDepth, (B, 40), generator=g).to(torch.int32).cuda()
+    outs = {}
+    try:
+        for arm, on in (("separate", 0), ("fused", 1)):
+            fn(on)
+            nll, logp = model.step(x, lab)
+            torch.cuda.synchronize()
+            outs[arm] = (nll.clone(), logp.clone(), model.grads.clone())
+    finally:
+        fn(1)
+    for a, b in zip(outs["separate"], outs["fused"]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("B", [32, 20, 9])
 def test_decoder_four_row_products_match_the_sixteen_row_form(s2s, B):
     """Chains of at most 4 utterances (B <= 32) run the XCD-local decoder's skinny products on
